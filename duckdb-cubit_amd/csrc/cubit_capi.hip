@@ -1,0 +1,1205 @@
+// C ABI of libcubitgpu.so (include/cubit_gpu.h) and the host-side planner that turns a
+// DuckDB-style predicate tree (TableFilter mirror) into bitvector programs for the
+// fused eval/decode kernel.
+//
+// Planner semantics (all exact; a leaf the index cannot answer exactly is built by K0 from
+// the raw column, never approximated):
+//   range index, L(k) = {valid & v < k}:  v<c = L(c'), v<=c = L(c+1), v>c = NN∖L(c+1),
+//     v>=c = NN∖L(c), v==c = L(c+1)∖L(c), v!=c = (NN∖L(c+1)) ∪ L(c); where L(c') is the
+//     bitvector of the smallest key ≥ c when the index holds every distinct value.
+//   equality index, E(k) = {v == k}: v==c = E(c), v!=c = NN∖E(c), ranges = ∪ E(k).
+//   NULLs never satisfy a comparison (TemplatedFilterSelection HAS_NULL path,
+//   column_segment.cpp:261-276) — NN is the column's validity bitvector.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/cubit_gpu.h"
+#include "cubit_internal.hpp"
+
+using namespace cubit;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_CHECK(expr)                                                                                  \
+    do {                                                                                                 \
+        hipError_t _e = (expr);                                                                          \
+        if (_e != hipSuccess) return fail(CUBIT_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                          __FILE__, __LINE__);                                           \
+    } while (0)
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+
+struct cubit_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    // one (start, stop) event pair per timed filter-kernel launch since the last reset
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    size_t n_timed = 0;
+    // look-back workspace: [counter, error, pad...] then tile status words
+    uint64_t* ws = nullptr;
+    uint64_t ws_tiles = 0;
+    int64_t* partials = nullptr;
+};
+
+namespace {
+
+int ensure_workspace(cubit_ctx* ctx, uint64_t tiles) {
+    if (tiles <= ctx->ws_tiles && ctx->ws) return CUBIT_OK;
+    if (ctx->ws) HIP_CHECK(hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    const uint64_t want = std::max<uint64_t>(tiles, 1024);
+    if (hipMalloc(&ctx->ws, (want + 2) * sizeof(uint64_t)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "workspace allocation of %llu tiles failed", (unsigned long long)want);
+    ctx->ws_tiles = want;
+    return CUBIT_OK;
+}
+
+int set_device(cubit_ctx* ctx) {
+    HIP_CHECK(hipSetDevice(ctx->device));
+    return CUBIT_OK;
+}
+
+// Launch eval over a compiled program. bits_only: write result words, no row ids.
+int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
+             uint64_t capacity, uint64_t* d_count, uint64_t* result_words, bool count_only, bool timed = false) {
+    const uint64_t nw = (n_rows + 63) / 64;
+    const uint64_t tiles = std::max<uint64_t>(1, padded_words(n_rows) / kTileWords);
+    if (int rc = ensure_workspace(ctx, tiles)) return rc;
+    EvalArgs a{};
+    a.prog = prog;
+    a.n_rows = n_rows;
+    a.n_words = nw;
+    a.row_base = row_base;
+    a.rowids = rowids;
+    a.capacity = rowids ? capacity : 0;
+    a.count = d_count;
+    a.result_words = result_words;
+    a.tile_counter = reinterpret_cast<uint32_t*>(ctx->ws);
+    a.error_flag = reinterpret_cast<uint32_t*>(ctx->ws) + 1;
+    a.tile_status = ctx->ws + 2;
+    a.num_tiles = (uint32_t)tiles;
+    HIP_CHECK(hipMemsetAsync(ctx->ws, 0, (tiles + 2) * sizeof(uint64_t), ctx->stream));
+    if (count_only) HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+    hipEvent_t stop = nullptr;
+    if (timed && ctx->timing) {
+        if (ctx->n_timed == ctx->evs.size()) {
+            hipEvent_t e0, e1;
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            ctx->evs.emplace_back(e0, e1);
+        }
+        HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed].first, ctx->stream));
+        stop = ctx->evs[ctx->n_timed].second;
+        ctx->n_timed++;
+    }
+    HIP_CHECK(launch_eval(a, count_only ? EvalMode::kCount : EvalMode::kDecode, ctx->stream));
+    if (stop) HIP_CHECK(hipEventRecord(stop, ctx->stream));
+    return CUBIT_OK;
+}
+
+int check_device_error(cubit_ctx* ctx) {
+    uint32_t flags[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(flags, ctx->ws, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (flags[1]) return fail(CUBIT_ERR_DEVICE, "look-back spin bound expired in the filter kernel");
+    return CUBIT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cubit_abi_version(void) { return 1; }
+int cubit_vector_size(void) { return (int)kVectorSize; }
+int cubit_row_group_size(void) { return (int)kRowGroupSize; }
+uint64_t cubit_padded_words(uint64_t n_rows) { return padded_words(n_rows); }
+const char* cubit_last_error(void) { return g_last_error.c_str(); }
+
+int cubit_ctx_create(int device, cubit_ctx** out) {
+    if (!out) return fail(CUBIT_ERR_INVALID, "out is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(CUBIT_ERR_HIP, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(CUBIT_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+    HIP_CHECK(hipSetDevice(device));
+    auto* ctx = new cubit_ctx();
+    ctx->device = device;
+    if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess) {
+        delete ctx;
+        return fail(CUBIT_ERR_OOM, "partials allocation failed");
+    }
+    *out = ctx;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_destroy(cubit_ctx* ctx) {
+    if (!ctx) return CUBIT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->partials) (void)hipFree(ctx->partials);
+    for (auto& e : ctx->evs) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    delete ctx;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_set_stream(cubit_ctx* ctx, void* stream) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    ctx->stream = static_cast<hipStream_t>(stream);
+    return CUBIT_OK;
+}
+
+int cubit_ctx_enable_timing(cubit_ctx* ctx, int on) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    ctx->timing = on != 0;
+    return CUBIT_OK;
+}
+
+int cubit_last_kernel_ms(cubit_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (ctx->n_timed == 0) return fail(CUBIT_ERR_INVALID, "no timed kernel recorded (enable timing first)");
+    const auto& e = ctx->evs[ctx->n_timed - 1];
+    HIP_CHECK(hipEventSynchronize(e.second));
+    HIP_CHECK(hipEventElapsedTime(ms, e.first, e.second));
+    return CUBIT_OK;
+}
+
+int cubit_ctx_timing_reset(cubit_ctx* ctx) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    ctx->n_timed = 0;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_kernel_times(cubit_ctx* ctx, float* ms, uint32_t cap, uint32_t* n) {
+    if (!ctx || !n) return fail(CUBIT_ERR_INVALID, "null argument");
+    const uint32_t m = (uint32_t)std::min<size_t>(cap, ctx->n_timed);
+    for (uint32_t i = 0; i < m; ++i) {
+        HIP_CHECK(hipEventSynchronize(ctx->evs[i].second));
+        HIP_CHECK(hipEventElapsedTime(&ms[i], ctx->evs[i].first, ctx->evs[i].second));
+    }
+    *n = (uint32_t)ctx->n_timed;
+    return CUBIT_OK;
+}
+
+int cubit_dev_alloc(cubit_ctx* ctx, uint64_t bytes, void** dptr) {
+    if (!ctx || !dptr) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    if (hipMalloc(dptr, std::max<uint64_t>(bytes, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "hipMalloc(%llu) failed", (unsigned long long)bytes);
+    return CUBIT_OK;
+}
+
+int cubit_dev_free(cubit_ctx* ctx, void* dptr) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (dptr) HIP_CHECK(hipFree(dptr));
+    return CUBIT_OK;
+}
+
+int cubit_memcpy_h2d(cubit_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return CUBIT_OK;
+}
+
+int cubit_memcpy_d2h(cubit_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return CUBIT_OK;
+}
+
+int cubit_memset_d(cubit_ctx* ctx, void* dst, int value, uint64_t bytes) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    HIP_CHECK(hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return CUBIT_OK;
+}
+
+int cubit_ctx_check(cubit_ctx* ctx) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (!ctx->ws) return CUBIT_OK;
+    return check_device_error(ctx);
+}
+
+int cubit_sync(cubit_ctx* ctx) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return CUBIT_OK;
+}
+
+int cubit_build_bitvector(cubit_ctx* ctx, const void* d_col, int type, const uint64_t* d_validity, uint64_t n_rows,
+                          int cmp, int64_t constant, uint64_t* d_words) {
+    if (!ctx || !d_col || !d_words) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (cmp < 0 || cmp > 5) return fail(CUBIT_ERR_INVALID, "cmp %d", cmp);
+    HIP_CHECK(launch_compare_bitvector(d_col, type, d_validity, n_rows, cmp, constant, d_words, ctx->stream));
+    return CUBIT_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ program compilation
+
+namespace {
+
+// Expression over bitvectors. Leaves carry the row predicate they encode so that MVCC
+// update patches can recompute a row's bit from its visible value.
+struct Leaf {
+    const uint64_t* bv = nullptr;
+    int column = -1;  // -1: not derived from a column value (visibility, temp)
+    int pred = 0;     // 0 = cmp (v CMP c), 1 = valid (NN)
+    int cmp = 0;
+    int64_t constant = 0;
+};
+
+struct Expr;
+using ExprP = std::shared_ptr<Expr>;
+struct Expr {
+    enum Kind { LEAF, AND, OR, ANDNOT, CONST_TRUE, CONST_FALSE } kind = CONST_FALSE;
+    Leaf leaf;
+    bool neg = false;  // LEAF only
+    ExprP a, b;
+};
+
+ExprP mk_true() {
+    auto e = std::make_shared<Expr>();
+    e->kind = Expr::CONST_TRUE;
+    return e;
+}
+ExprP mk_false() {
+    auto e = std::make_shared<Expr>();
+    e->kind = Expr::CONST_FALSE;
+    return e;
+}
+ExprP mk_leaf(const Leaf& l, bool neg = false) {
+    auto e = std::make_shared<Expr>();
+    e->kind = Expr::LEAF;
+    e->leaf = l;
+    e->neg = neg;
+    return e;
+}
+ExprP mk_not(const ExprP& x);
+ExprP mk_bin(Expr::Kind k, ExprP a, ExprP b) {
+    using K = Expr::Kind;
+    const bool at = a->kind == K::CONST_TRUE, af = a->kind == K::CONST_FALSE;
+    const bool bt = b->kind == K::CONST_TRUE, bf = b->kind == K::CONST_FALSE;
+    switch (k) {
+    case K::AND:
+        if (af || bf) return mk_false();
+        if (at) return b;
+        if (bt) return a;
+        break;
+    case K::OR:
+        if (at || bt) return mk_true();
+        if (af) return b;
+        if (bf) return a;
+        break;
+    case K::ANDNOT:
+        if (af || bt) return mk_false();
+        if (bf) return a;
+        if (at) return mk_not(b);
+        break;
+    default:
+        break;
+    }
+    auto e = std::make_shared<Expr>();
+    e->kind = k;
+    e->a = std::move(a);
+    e->b = std::move(b);
+    return e;
+}
+// NOT pushed to the leaves (De Morgan); ANDNOT(a,b) = a & ~b → ~a | b
+ExprP mk_not(const ExprP& x) {
+    using K = Expr::Kind;
+    switch (x->kind) {
+    case K::CONST_TRUE: return mk_false();
+    case K::CONST_FALSE: return mk_true();
+    case K::LEAF: return mk_leaf(x->leaf, !x->neg);
+    case K::AND: return mk_bin(K::OR, mk_not(x->a), mk_not(x->b));
+    case K::OR: return mk_bin(K::AND, mk_not(x->a), mk_not(x->b));
+    case K::ANDNOT: return mk_bin(K::OR, mk_not(x->a), x->b);
+    }
+    return mk_false();
+}
+
+int count_leaves(const ExprP& e) {
+    if (e->kind == Expr::LEAF) return 1;
+    if (e->kind == Expr::CONST_TRUE || e->kind == Expr::CONST_FALSE) return 0;
+    return count_leaves(e->a) + count_leaves(e->b);
+}
+
+// registers the expression needs (Sethi–Ullman / Strahler number)
+int need(const ExprP& e) {
+    if (e->kind == Expr::LEAF) return 1;
+    const int l = need(e->a), r = need(e->b);
+    return l == r ? l + 1 : std::max(l, r);
+}
+
+// Emit postfix. For AND/OR the heavier child goes first; ANDNOT with a heavier right child
+// is rewritten as AND(~b-side-first) via a reverse op: we keep a & ~b by emitting b first
+// and using AND with the complement pushed into b when b is a leaf, otherwise the order is
+// kept (depth checked by the caller).
+struct Emitter {
+    EvalProgram prog{};
+    int n_ops = 0;
+    int depth = 0, max_depth = 0;
+    bool ok = true;
+    void leaf(const Leaf& l, bool neg) {
+        if (prog.n_leaves >= (uint32_t)kMaxLeaves) {
+            ok = false;
+            return;
+        }
+        const uint32_t k = prog.n_leaves++;
+        prog.leaf[k] = l.bv;
+        if (neg) prog.negate |= 1u << k;
+        prog.nops[k] = 0;
+        max_depth = std::max(max_depth, ++depth);
+    }
+    void op(int8_t o) {
+        if (prog.n_leaves == 0 || n_ops >= kMaxOps) {
+            ok = false;
+            return;
+        }
+        prog.ops[n_ops++] = o;
+        prog.nops[prog.n_leaves - 1]++;
+        --depth;
+    }
+    void emit(const ExprP& e) {
+        switch (e->kind) {
+        case Expr::LEAF: leaf(e->leaf, e->neg); return;
+        case Expr::AND:
+        case Expr::OR: {
+            const int8_t o = e->kind == Expr::AND ? OP_AND : OP_OR;
+            if (need(e->b) > need(e->a)) {
+                emit(e->b);
+                emit(e->a);
+            } else {
+                emit(e->a);
+                emit(e->b);
+            }
+            op(o);
+            return;
+        }
+        case Expr::ANDNOT: {
+            if (need(e->b) > need(e->a) && e->b->kind == Expr::LEAF) {
+                // a & ~b == (~b) & a with b a leaf: emit complemented leaf first
+                leaf(e->b->leaf, !e->b->neg);
+                emit(e->a);
+                op(OP_AND);
+            } else {
+                emit(e->a);
+                emit(e->b);
+                op(OP_ANDNOT);
+            }
+            return;
+        }
+        default: ok = false; return;
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_leaves, uint32_t n_leaves,
+                                    uint32_t leaf_negate, const int32_t* prog, uint32_t n_prog, uint64_t n_rows,
+                                    int64_t row_base, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
+                                    uint64_t* d_result_words, uint32_t flags) {
+    if (!ctx || !d_leaves || !prog || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "n_rows is 0");
+    const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
+    if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
+    // postfix → expression (validates arity), then the emitter re-linearises it
+    std::vector<ExprP> st;
+    for (uint32_t i = 0; i < n_prog; ++i) {
+        const int32_t x = prog[i];
+        if (x >= 0) {
+            if ((uint32_t)x >= n_leaves) return fail(CUBIT_ERR_INVALID, "leaf %d out of range", x);
+            Leaf l;
+            l.bv = d_leaves[x];
+            st.push_back(mk_leaf(l, ((leaf_negate >> x) & 1u) != 0));
+        } else {
+            if (st.size() < 2) return fail(CUBIT_ERR_INVALID, "program underflow at %u", i);
+            ExprP b = st.back();
+            st.pop_back();
+            ExprP a = st.back();
+            st.pop_back();
+            Expr::Kind k = x == CUBIT_OP_AND ? Expr::AND : x == CUBIT_OP_OR ? Expr::OR : x == CUBIT_OP_ANDNOT
+                                                                                         ? Expr::ANDNOT
+                                                                                         : Expr::CONST_FALSE;
+            if (k == Expr::CONST_FALSE) return fail(CUBIT_ERR_INVALID, "bad opcode %d", x);
+            auto e = std::make_shared<Expr>();
+            e->kind = k;
+            e->a = a;
+            e->b = b;
+            st.push_back(e);
+        }
+    }
+    if (st.size() != 1) return fail(CUBIT_ERR_INVALID, "program leaves %zu values on the stack", st.size());
+    Emitter em;
+    em.emit(st[0]);
+    if (!em.ok || em.max_depth > 4)
+        return fail(CUBIT_ERR_UNSUPPORTED, "program needs %d leaves / depth %d (max %d / 4)", count_leaves(st[0]),
+                    em.max_depth, kMaxLeaves);
+    return run_eval(ctx, em.prog, n_rows, row_base, d_rowids, capacity, d_count, d_result_words, count_only, true);
+}
+
+extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const int64_t* d_rowids,
+                            const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* d_out) {
+    if (!ctx || !d_col || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    HIP_CHECK(launch_gather(d_col, type, d_rowids, d_count, max_n, row_base, d_out, ctx->stream));
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_gather_sum_product(cubit_ctx* ctx, const int64_t* d_a, const int64_t* d_b,
+                                        const int64_t* d_rowids, const uint64_t* d_count, uint64_t max_n,
+                                        int64_t row_base, int64_t* d_out) {
+    if (!ctx || !d_a || !d_b || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    HIP_CHECK(launch_gather_sum_product(d_a, d_b, d_rowids, d_count, max_n, row_base, ctx->partials, d_out,
+                                        ctx->stream));
+    return CUBIT_OK;
+}
+
+// ------------------------------------------------------------------ table partition
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Column {
+    int type = 0;
+    const void* data = nullptr;        // device
+    const uint64_t* validity = nullptr;  // device, padded (null = no NULLs)
+    std::vector<std::unique_ptr<DevBuf>> owned;
+    // value statistics (zonemap-like), computed at index build
+};
+
+struct Index {
+    int encoding = CUBIT_INDEX_RANGE;
+    bool exact_all = false;  // keys = every distinct value
+    int64_t vmin = 0, vmax = 0;
+    bool empty = true;       // no valid rows
+    std::vector<int64_t> keys;
+    std::vector<uint64_t*> bvs;  // parallel to keys
+    std::vector<std::unique_ptr<DevBuf>> owned;
+    uint64_t bytes = 0;
+};
+
+struct Updates {
+    std::unique_ptr<DevBuf> rows, values, versions;
+    std::vector<int64_t> h_rows, h_values;
+    std::vector<uint64_t> h_versions;
+    uint64_t n = 0;
+};
+
+}  // namespace
+
+struct cubit_table {
+    cubit_ctx* ctx = nullptr;
+    uint64_t n_rows = 0;
+    int64_t row_base = 0;
+    uint64_t nwp = 0;  // padded words
+    std::map<int, Column> cols;
+    std::map<int, Index> idx;
+    // MVCC delta
+    std::unique_ptr<DevBuf> del_rows, del_ids;
+    uint64_t n_del = 0;
+    std::map<int, Updates> upd;
+    // scratch bitvectors (reused across scans)
+    std::vector<std::unique_ptr<DevBuf>> scratch;
+    size_t scratch_used = 0;
+    std::unique_ptr<DevBuf> ones;  // all valid rows
+    uint32_t last_leaves = 0, last_passes = 0;
+    uint64_t* dummy_count = nullptr;
+    std::unique_ptr<DevBuf> dummy;
+};
+
+namespace {
+
+int scratch_bv(cubit_table* t, uint64_t** out) {
+    if (t->scratch_used < t->scratch.size()) {
+        *out = static_cast<uint64_t*>(t->scratch[t->scratch_used++]->p);
+        return CUBIT_OK;
+    }
+    auto b = std::make_unique<DevBuf>();
+    if (hipMalloc(&b->p, t->nwp * sizeof(uint64_t)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "scratch bitvector allocation failed");
+    *out = static_cast<uint64_t*>(b->p);
+    t->scratch.push_back(std::move(b));
+    t->scratch_used++;
+    return CUBIT_OK;
+}
+
+int ones_bv(cubit_table* t, const uint64_t** out) {
+    if (!t->ones) {
+        t->ones = std::make_unique<DevBuf>();
+        if (hipMalloc(&t->ones->p, t->nwp * sizeof(uint64_t)) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "ones bitvector allocation failed");
+        HIP_CHECK(launch_fill_valid(static_cast<uint64_t*>(t->ones->p), t->n_rows, t->ctx->stream));
+    }
+    *out = static_cast<const uint64_t*>(t->ones->p);
+    return CUBIT_OK;
+}
+
+int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
+    const uint64_t esz = type == CUBIT_TYPE_INT32 ? 4 : 8;
+    hipStream_t s = t->ctx->stream;
+    if (on_device) {
+        c.data = data;
+    } else {
+        auto b = std::make_unique<DevBuf>();
+        if (hipMalloc(&b->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "column allocation failed");
+        HIP_CHECK(hipMemcpyAsync(b->p, data, t->n_rows * esz, hipMemcpyHostToDevice, s));
+        c.data = b->p;
+        c.owned.push_back(std::move(b));
+    }
+    if (validity) {
+        // padded copy (the NN bitvector): kernels read whole tiles
+        auto b = std::make_unique<DevBuf>();
+        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "validity allocation failed");
+        HIP_CHECK(hipMemsetAsync(b->p, 0, t->nwp * 8, s));
+        const uint64_t nw = (t->n_rows + 63) / 64;
+        HIP_CHECK(hipMemcpyAsync(b->p, validity, nw * 8, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 s));
+        // clear bits past n_rows
+        if (t->n_rows & 63) {
+            uint64_t last = 0;
+            HIP_CHECK(hipMemcpyAsync(&last, static_cast<uint64_t*>(b->p) + nw - 1, 8, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            last &= (1ull << (t->n_rows & 63)) - 1;
+            HIP_CHECK(hipMemcpyAsync(static_cast<uint64_t*>(b->p) + nw - 1, &last, 8, hipMemcpyHostToDevice, s));
+        }
+        c.validity = static_cast<const uint64_t*>(b->p);
+        c.owned.push_back(std::move(b));
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    c.type = type;
+    return CUBIT_OK;
+}
+
+// distinct non-null values and min/max of a column (host pass over a D2H copy; index build
+// is setup work, not the scan path)
+int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct, bool want_distinct,
+                 int64_t& vmin, int64_t& vmax, bool& any) {
+    const uint64_t n = t->n_rows, esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
+    std::vector<unsigned char> host(n * esz);
+    std::vector<uint64_t> valid;
+    HIP_CHECK(hipMemcpy(host.data(), c.data, n * esz, hipMemcpyDeviceToHost));
+    if (c.validity) {
+        valid.resize((n + 63) / 64);
+        HIP_CHECK(hipMemcpy(valid.data(), c.validity, valid.size() * 8, hipMemcpyDeviceToHost));
+    }
+    any = false;
+    vmin = INT64_MAX;
+    vmax = INT64_MIN;
+    std::vector<int64_t> vals;
+    if (want_distinct) vals.reserve(n);
+    for (uint64_t r = 0; r < n; ++r) {
+        if (c.validity && !((valid[r >> 6] >> (r & 63)) & 1)) continue;
+        const int64_t v = c.type == CUBIT_TYPE_INT32 ? (int64_t) reinterpret_cast<const int32_t*>(host.data())[r]
+                                                     : reinterpret_cast<const int64_t*>(host.data())[r];
+        any = true;
+        vmin = std::min(vmin, v);
+        vmax = std::max(vmax, v);
+        if (want_distinct) vals.push_back(v);
+    }
+    if (want_distinct) {
+        if (any && (uint64_t)(vmax - vmin) < (1ull << 26)) {
+            std::vector<uint8_t> seen((size_t)(vmax - vmin) + 1, 0);
+            for (int64_t v : vals) seen[(size_t)(v - vmin)] = 1;
+            distinct.clear();
+            for (size_t i = 0; i < seen.size(); ++i)
+                if (seen[i]) distinct.push_back(vmin + (int64_t)i);
+        } else {
+            std::sort(vals.begin(), vals.end());
+            vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+            distinct = std::move(vals);
+        }
+    }
+    return CUBIT_OK;
+}
+
+}  // namespace
+
+extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_base, cubit_table** out) {
+    if (!ctx || !out) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "empty partition");
+    if (int rc = set_device(ctx)) return rc;
+    auto* t = new cubit_table();
+    t->ctx = ctx;
+    t->n_rows = n_rows;
+    t->row_base = row_base;
+    t->nwp = padded_words(n_rows);
+    t->dummy = std::make_unique<DevBuf>();
+    if (hipMalloc(&t->dummy->p, 64) != hipSuccess) {
+        delete t;
+        return fail(CUBIT_ERR_OOM, "allocation failed");
+    }
+    t->dummy_count = static_cast<uint64_t*>(t->dummy->p);
+    *out = t;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_destroy(cubit_table* t) {
+    if (!t) return CUBIT_OK;
+    (void)hipSetDevice(t->ctx->device);
+    (void)hipStreamSynchronize(t->ctx->stream);
+    delete t;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const void* data, const uint64_t* validity,
+                                      int on_device) {
+    if (!t || !data) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    Column c;
+    if (int rc = copy_column(t, c, type, data, validity, on_device)) return rc;
+    t->cols[col] = std::move(c);
+    t->idx.erase(col);
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, const int64_t* values, uint32_t n) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    auto it = t->cols.find(col);
+    if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (encoding != CUBIT_INDEX_RANGE && encoding != CUBIT_INDEX_EQUALITY)
+        return fail(CUBIT_ERR_INVALID, "encoding %d", encoding);
+    if (int rc = set_device(t->ctx)) return rc;
+    const Column& c = it->second;
+    Index ix;
+    ix.encoding = encoding;
+    std::vector<int64_t> distinct;
+    bool any = false;
+    if (int rc = column_stats(t, c, distinct, n == 0, ix.vmin, ix.vmax, any)) return rc;
+    ix.empty = !any;
+    if (n == 0) {
+        ix.exact_all = true;
+        ix.keys = distinct;
+        // range encoding: L(min) is empty, keep keys above the minimum
+        if (encoding == CUBIT_INDEX_RANGE && !ix.keys.empty()) ix.keys.erase(ix.keys.begin());
+    } else {
+        ix.keys.assign(values, values + n);
+        if (!std::is_sorted(ix.keys.begin(), ix.keys.end()))
+            return fail(CUBIT_ERR_INVALID, "index keys must be sorted ascending");
+        ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end()), ix.keys.end());
+    }
+    const int cmp = encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ;
+    for (int64_t k : ix.keys) {
+        auto b = std::make_unique<DevBuf>();
+        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(),
+                        ix.keys.size());
+        HIP_CHECK(launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows, cmp, k, static_cast<uint64_t*>(b->p),
+                                           t->ctx->stream));
+        ix.bvs.push_back(static_cast<uint64_t*>(b->p));
+        ix.owned.push_back(std::move(b));
+        ix.bytes += t->nwp * 8;
+    }
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    t->idx[col] = std::move(ix);
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_index_info(cubit_table* t, int col, uint32_t* n_bitvectors, uint64_t* bytes) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    auto it = t->idx.find(col);
+    const uint32_t nb = it == t->idx.end() ? 0 : (uint32_t)it->second.bvs.size();
+    const uint64_t by = it == t->idx.end() ? 0 : it->second.bytes;
+    if (n_bitvectors) *n_bitvectors = nb;
+    if (bytes) *bytes = by;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, const uint64_t* ids, uint64_t n) {
+    if (!t || (n && (!rows || !ids))) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(t->ctx)) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "delete row out of range");
+    t->del_rows = std::make_unique<DevBuf>();
+    t->del_ids = std::make_unique<DevBuf>();
+    if (hipMalloc(&t->del_rows->p, std::max<uint64_t>(n, 1) * 8) != hipSuccess ||
+        hipMalloc(&t->del_ids->p, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "delete list allocation failed");
+    if (n) {
+        HIP_CHECK(hipMemcpy(t->del_rows->p, rows, n * 8, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(t->del_ids->p, ids, n * 8, hipMemcpyHostToDevice));
+    }
+    t->n_del = n;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
+                                       const uint64_t* versions, uint64_t n) {
+    if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
+    // group records by row, keeping each row's records in chronological order
+    std::vector<uint64_t> order(n);
+    for (uint64_t i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
+    Updates u;
+    u.n = n;
+    for (uint64_t i : order) {
+        u.h_rows.push_back(rows[i]);
+        u.h_values.push_back(values[i]);
+        u.h_versions.push_back(versions[i]);
+    }
+    u.rows = std::make_unique<DevBuf>();
+    u.values = std::make_unique<DevBuf>();
+    u.versions = std::make_unique<DevBuf>();
+    if (hipMalloc(&u.rows->p, std::max<uint64_t>(n, 1) * 8) != hipSuccess ||
+        hipMalloc(&u.values->p, std::max<uint64_t>(n, 1) * 8) != hipSuccess ||
+        hipMalloc(&u.versions->p, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "update list allocation failed");
+    if (n) {
+        HIP_CHECK(hipMemcpy(u.rows->p, u.h_rows.data(), n * 8, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(u.values->p, u.h_values.data(), n * 8, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(u.versions->p, u.h_versions.data(), n * 8, hipMemcpyHostToDevice));
+    }
+    t->upd[col] = std::move(u);
+    return CUBIT_OK;
+}
+
+// ------------------------------------------------------------------ planner
+
+namespace {
+
+struct Planner {
+    cubit_table* t;
+    const cubit_filter_node* nodes;
+    uint32_t n_nodes;
+    int rc = CUBIT_OK;
+
+    int subtree_end(uint32_t i) {
+        if (i >= n_nodes) return -1;
+        uint32_t j = i + 1;
+        for (int k = 0; k < nodes[i].n_children; ++k) {
+            int e = subtree_end(j);
+            if (e < 0) return -1;
+            j = (uint32_t)e;
+        }
+        return (int)j;
+    }
+
+    ExprP nn(int col) {
+        const Column& c = t->cols.at(col);
+        if (!c.validity) return mk_true();
+        Leaf l;
+        l.bv = c.validity;
+        l.column = col;
+        l.pred = 1;
+        return mk_leaf(l);
+    }
+
+    // K0 fallback: build the comparison from the raw column into a scratch bitvector
+    ExprP raw_compare(int col, int cmp, int64_t c) {
+        const Column& cl = t->cols.at(col);
+        uint64_t* bv = nullptr;
+        if ((rc = scratch_bv(t, &bv))) return nullptr;
+        hipError_t e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, cmp, c, bv, t->ctx->stream);
+        if (e != hipSuccess) {
+            rc = fail(CUBIT_ERR_HIP, "compare kernel: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+        Leaf l;
+        l.bv = bv;
+        l.column = col;
+        l.cmp = cmp;
+        l.constant = c;
+        return mk_leaf(l);
+    }
+
+    // {v < c} from a range index; nullptr when the index cannot answer exactly
+    ExprP range_lt(int col, const Index& ix, int64_t c) {
+        if (ix.empty || c <= ix.vmin) return mk_false();
+        if (c > ix.vmax) return nn(col);
+        auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
+        if (it != ix.keys.end() && (*it == c || ix.exact_all)) {
+            Leaf l;
+            l.bv = ix.bvs[it - ix.keys.begin()];
+            l.column = col;
+            l.cmp = CUBIT_CMP_LT;
+            l.constant = *it;
+            return mk_leaf(l);
+        }
+        return nullptr;
+    }
+
+    ExprP eq_leaf(int col, const Index& ix, int64_t c, bool& exact) {
+        exact = true;
+        auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
+        if (it != ix.keys.end() && *it == c) {
+            Leaf l;
+            l.bv = ix.bvs[it - ix.keys.begin()];
+            l.column = col;
+            l.cmp = CUBIT_CMP_EQ;
+            l.constant = c;
+            return mk_leaf(l);
+        }
+        if (ix.exact_all || ix.empty || c < ix.vmin || c > ix.vmax) return mk_false();
+        exact = false;
+        return nullptr;
+    }
+
+    ExprP constant(int col, int cmp, int64_t c) {
+        auto ixit = t->idx.find(col);
+        if (ixit != t->idx.end()) {
+            const Index& ix = ixit->second;
+            const bool top = c == INT64_MAX;
+            if (ix.encoding == CUBIT_INDEX_RANGE) {
+                ExprP lt_c = range_lt(col, ix, c);
+                ExprP lt_c1 = top ? nn(col) : range_lt(col, ix, c + 1);
+                ExprP r;
+                switch (cmp) {
+                case CUBIT_CMP_LT: r = lt_c; break;
+                case CUBIT_CMP_LE: r = lt_c1; break;
+                case CUBIT_CMP_GT: r = lt_c1 ? mk_bin(Expr::ANDNOT, nn(col), lt_c1) : nullptr; break;
+                case CUBIT_CMP_GE: r = lt_c ? mk_bin(Expr::ANDNOT, nn(col), lt_c) : nullptr; break;
+                case CUBIT_CMP_EQ: r = (lt_c && lt_c1) ? mk_bin(Expr::ANDNOT, lt_c1, lt_c) : nullptr; break;
+                case CUBIT_CMP_NE:
+                    r = (lt_c && lt_c1) ? mk_bin(Expr::OR, mk_bin(Expr::ANDNOT, nn(col), lt_c1), lt_c) : nullptr;
+                    break;
+                default: break;
+                }
+                if (r) return r;
+            } else {
+                bool exact = true;
+                if (cmp == CUBIT_CMP_EQ) {
+                    ExprP e = eq_leaf(col, ix, c, exact);
+                    if (exact) return e;
+                } else if (cmp == CUBIT_CMP_NE) {
+                    ExprP e = eq_leaf(col, ix, c, exact);
+                    if (exact) return mk_bin(Expr::ANDNOT, nn(col), e);
+                } else if (ix.exact_all) {
+                    // union of the equality bitvectors in range; wide ranges go to K0
+                    std::vector<size_t> sel;
+                    for (size_t k = 0; k < ix.keys.size(); ++k) {
+                        const int64_t v = ix.keys[k];
+                        const bool in = cmp == CUBIT_CMP_LT ? v < c : cmp == CUBIT_CMP_LE ? v <= c
+                                        : cmp == CUBIT_CMP_GT ? v > c : v >= c;
+                        if (in) sel.push_back(k);
+                    }
+                    if (sel.size() <= 16) {
+                        ExprP acc = mk_false();
+                        for (size_t k : sel) {
+                            Leaf l;
+                            l.bv = ix.bvs[k];
+                            l.column = col;
+                            l.cmp = CUBIT_CMP_EQ;
+                            l.constant = ix.keys[k];
+                            acc = mk_bin(Expr::OR, acc, mk_leaf(l));
+                        }
+                        return acc;
+                    }
+                }
+            }
+        }
+        return raw_compare(col, cmp, c);
+    }
+
+    ExprP plan(uint32_t i) {
+        if (rc) return nullptr;
+        const cubit_filter_node& f = nodes[i];
+        switch (f.kind) {
+        case CUBIT_FILTER_AND:
+        case CUBIT_FILTER_OR: {
+            ExprP acc = f.kind == CUBIT_FILTER_AND ? mk_true() : mk_false();
+            uint32_t j = i + 1;
+            for (int k = 0; k < f.n_children; ++k) {
+                ExprP c = plan(j);
+                if (!c) return nullptr;
+                acc = mk_bin(f.kind == CUBIT_FILTER_AND ? Expr::AND : Expr::OR, acc, c);
+                j = (uint32_t)subtree_end(j);
+            }
+            return acc;
+        }
+        case CUBIT_FILTER_CONSTANT:
+        case CUBIT_FILTER_IS_NULL:
+        case CUBIT_FILTER_IS_NOT_NULL: {
+            if (!t->cols.count(f.column)) {
+                rc = fail(CUBIT_ERR_INVALID, "filter references unregistered column %d", f.column);
+                return nullptr;
+            }
+            if (f.kind == CUBIT_FILTER_IS_NOT_NULL) return nn(f.column);
+            if (f.kind == CUBIT_FILTER_IS_NULL) return mk_not(nn(f.column));
+            if (f.cmp < 0 || f.cmp > 5) {
+                rc = fail(CUBIT_ERR_INVALID, "comparison %d", f.cmp);
+                return nullptr;
+            }
+            return constant(f.column, f.cmp, f.constant);
+        }
+        default:
+            rc = fail(CUBIT_ERR_INVALID, "filter node kind %d", f.kind);
+            return nullptr;
+        }
+    }
+};
+
+// Materialise a subexpression into a scratch bitvector (bits-only pass).
+int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
+    Emitter em;
+    em.emit(e);
+    if (!em.ok || em.max_depth > 4) return fail(CUBIT_ERR_UNSUPPORTED, "subexpression too deep");
+    if (int rc = scratch_bv(t, out)) return rc;
+    t->last_passes++;
+    return run_eval(t->ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, *out, true);
+}
+
+bool fits(const ExprP& e) {
+    Emitter em;
+    em.emit(e);
+    return em.ok && em.max_depth <= 4;
+}
+
+// Reduce an expression until it fits one kernel pass (<= kMaxLeaves leaves, depth <= 4):
+// descend into a child that does not fit; when both children fit but not together,
+// materialise the larger one into a scratch bitvector (one bits-only pass).
+int fit(cubit_table* t, ExprP& e) {
+    for (int guard = 0; guard < 256; ++guard) {
+        if (fits(e)) return CUBIT_OK;
+        ExprP* cur = &e;
+        for (;;) {
+            if ((*cur)->kind == Expr::LEAF) return fail(CUBIT_ERR_UNSUPPORTED, "cannot split program");
+            ExprP& a = (*cur)->a;
+            ExprP& b = (*cur)->b;
+            if (!fits(a)) {
+                cur = &a;
+                continue;
+            }
+            if (!fits(b)) {
+                cur = &b;
+                continue;
+            }
+            ExprP* m = count_leaves(a) >= count_leaves(b) ? &a : &b;
+            if ((*m)->kind == Expr::LEAF) m = (m == &a) ? &b : &a;
+            uint64_t* bv = nullptr;
+            if (int rc = materialize(t, *m, &bv)) return rc;
+            Leaf l;
+            l.bv = bv;
+            *m = mk_leaf(l);
+            break;
+        }
+    }
+    return fail(CUBIT_ERR_UNSUPPORTED, "program too large");
+}
+
+// Copy-on-write patch of every leaf on an updated column: rows whose update is visible to
+// the transaction get the bit their visible value implies (UpdatesForTransaction,
+// update_info.hpp:44-55). Done on the device: copy the leaf, clear the updated rows, then
+// set the rows whose visible value passes the leaf predicate.
+__global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ values,
+                                  const uint64_t* __restrict__ versions, uint64_t n, uint64_t start_time,
+                                  uint64_t tid, int pred, int cmp, int64_t c, uint64_t* __restrict__ bv) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t ver = versions[i];
+        if (!(ver < start_time || ver == tid)) continue;
+        const int64_t r = rows[i];
+        // only the newest visible update of a row decides (records are chronological and
+        // grouped by row by the host)
+        bool newest = true;
+        for (uint64_t j = i + 1; j < n && rows[j] == r; ++j) {
+            const uint64_t vj = versions[j];
+            if (vj < start_time || vj == tid) {
+                newest = false;
+                break;
+            }
+        }
+        if (!newest) continue;
+        const int64_t v = values[i];
+        bool p;
+        if (pred == 1) p = true;
+        else if (cmp == 0) p = v == c;
+        else if (cmp == 1) p = v != c;
+        else if (cmp == 2) p = v < c;
+        else if (cmp == 3) p = v <= c;
+        else if (cmp == 4) p = v > c;
+        else p = v >= c;
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(&bv[r >> 6]);
+        const uint64_t bit = 1ull << (r & 63);
+        if (p) atomicOr(w, bit);
+        else atomicAnd(w, ~bit);
+    }
+}
+
+int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const uint64_t*, uint64_t*>& patched) {
+    if (e->kind == Expr::LEAF) {
+        auto uit = t->upd.find(e->leaf.column);
+        if (uit == t->upd.end() || uit->second.n == 0) return CUBIT_OK;
+        auto pit = patched.find(e->leaf.bv);
+        uint64_t* copy = nullptr;
+        if (pit != patched.end()) {
+            copy = pit->second;
+        } else {
+            if (int rc = scratch_bv(t, &copy)) return rc;
+            HIP_CHECK(hipMemcpyAsync(copy, e->leaf.bv, t->nwp * 8, hipMemcpyDeviceToDevice, t->ctx->stream));
+            const Updates& u = uit->second;
+            const unsigned grid = (unsigned)std::min<uint64_t>((u.n + 255) / 256, 4096);
+            hipLaunchKernelGGL(patch_leaf_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, t->ctx->stream,
+                               static_cast<const int64_t*>(u.rows->p), static_cast<const int64_t*>(u.values->p),
+                               static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time, txn->transaction_id,
+                               e->leaf.pred, e->leaf.cmp, e->leaf.constant, copy);
+            HIP_CHECK(hipGetLastError());
+            patched[e->leaf.bv] = copy;
+        }
+        Leaf l = e->leaf;
+        l.bv = copy;
+        e = mk_leaf(l, e->neg);
+        return CUBIT_OK;
+    }
+    if (e->kind == Expr::CONST_TRUE || e->kind == Expr::CONST_FALSE) return CUBIT_OK;
+    if (int rc = patch_updates(t, e->a, txn, patched)) return rc;
+    return patch_updates(t, e->b, txn, patched);
+}
+
+}  // namespace
+
+extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
+                                const cubit_txn* txn, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
+                                uint32_t flags) {
+    if (!t || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
+    const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
+    if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
+    if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
+    if (int rc = set_device(t->ctx)) return rc;
+    cubit_ctx* ctx = t->ctx;
+    t->scratch_used = 0;
+    t->last_passes = 0;
+    ExprP e;
+    if (n_nodes == 0) {
+        e = mk_true();
+    } else {
+        Planner p{t, nodes, n_nodes};
+        if (p.subtree_end(0) != (int)n_nodes) return fail(CUBIT_ERR_INVALID, "malformed filter tree");
+        e = p.plan(0);
+        if (!e) return p.rc ? p.rc : fail(CUBIT_ERR_INVALID, "planning failed");
+    }
+    if (txn) {
+        std::map<const uint64_t*, uint64_t*> patched;
+        if (!t->upd.empty()) {
+            if (int rc = patch_updates(t, e, txn, patched)) return rc;
+        }
+        if (t->n_del) {
+            uint64_t* vis = nullptr;
+            if (int rc = scratch_bv(t, &vis)) return rc;
+            HIP_CHECK(launch_visibility(static_cast<const int64_t*>(t->del_rows->p),
+                                        static_cast<const uint64_t*>(t->del_ids->p), t->n_del, t->n_rows,
+                                        txn->start_time, txn->transaction_id, vis, ctx->stream));
+            Leaf l;
+            l.bv = vis;
+            e = mk_bin(Expr::AND, e, mk_leaf(l));
+        }
+    }
+    if (e->kind == Expr::CONST_FALSE) {
+        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+        t->last_leaves = 0;
+        return CUBIT_OK;
+    }
+    if (e->kind == Expr::CONST_TRUE) {
+        const uint64_t* ones = nullptr;
+        if (int rc = ones_bv(t, &ones)) return rc;
+        Leaf l;
+        l.bv = ones;
+        e = mk_leaf(l);
+    }
+    if (int rc = fit(t, e)) return rc;
+    Emitter em;
+    em.emit(e);
+    t->last_leaves = em.prog.n_leaves;
+    t->last_passes++;
+    return run_eval(ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count, nullptr,
+                    count_only, true);
+}
+
+extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_t* n_passes) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    if (n_leaves) *n_leaves = t->last_leaves;
+    if (n_passes) *n_passes = t->last_passes;
+    return CUBIT_OK;
+}
+
+namespace {
+
+// visible value of updated rows for a probe: patch gathered values in place
+__global__ void patch_probe_kernel(const int64_t* __restrict__ rowids, const uint64_t* __restrict__ d_count,
+                                   uint64_t max_n, int64_t row_base, const int64_t* __restrict__ urows,
+                                   const int64_t* __restrict__ uvalues, const uint64_t* __restrict__ uversions,
+                                   uint64_t nu, uint64_t start_time, uint64_t tid, int64_t* __restrict__ out) {
+    const uint64_t n = min(*d_count, max_n);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t r = rowids[i] - row_base;
+        // binary search the first record of row r (records grouped by row, ascending)
+        uint64_t lo = 0, hi = nu;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (urows[mid] < r) lo = mid + 1;
+            else hi = mid;
+        }
+        for (uint64_t j = lo; j < nu && urows[j] == r; ++j) {
+            const uint64_t v = uversions[j];
+            if (v < start_time || v == tid) out[i] = uvalues[j];
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int cubit_table_probe(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_rowids,
+                                 const uint64_t* d_count, uint64_t max_n, int64_t* d_out) {
+    if (!t || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    auto it = t->cols.find(col);
+    if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    HIP_CHECK(launch_gather(it->second.data, it->second.type, d_rowids, d_count, max_n, t->row_base, d_out,
+                            t->ctx->stream));
+    auto uit = t->upd.find(col);
+    if (txn && uit != t->upd.end() && uit->second.n) {
+        const Updates& u = uit->second;
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((max_n + 255) / 256, 4096));
+        hipLaunchKernelGGL(patch_probe_kernel, dim3(grid), dim3(256), 0, t->ctx->stream, d_rowids, d_count, max_n,
+                           t->row_base, static_cast<const int64_t*>(u.rows->p),
+                           static_cast<const int64_t*>(u.values->p), static_cast<const uint64_t*>(u.versions->p), u.n,
+                           txn->start_time, txn->transaction_id, d_out);
+        HIP_CHECK(hipGetLastError());
+    }
+    return CUBIT_OK;
+}

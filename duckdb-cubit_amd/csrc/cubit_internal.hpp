@@ -1,0 +1,83 @@
+// Internal interfaces shared by the HIP kernels (cubit_kernels.hip) and the C ABI /
+// planner (cubit_capi.hip). Not installed; the public surface is include/cubit_gpu.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cubit {
+
+// DuckDB storage geometry (src/include/duckdb/common/vector_size.hpp:16-20,
+// src/include/duckdb/storage/storage_info.hpp:20). Both are whole 64-bit words, so vector
+// and row-group boundaries never split a bitvector word.
+constexpr uint64_t kVectorSize = 2048;
+constexpr uint64_t kRowGroupSize = 122880;
+static_assert(kVectorSize % 64 == 0 && kVectorSize / 64 == 32, "vector must be 32 words");
+static_assert(kRowGroupSize % 64 == 0 && kRowGroupSize / 64 == 1920, "row group must be 1920 words");
+
+// Filter kernel geometry: 256 threads, each owning two 16-byte word pairs per leaf
+// (one dwordx4 load per pair; a wave-instruction moves 1 KiB).
+constexpr int kThreads = 256;
+constexpr int kPairs = 2;
+constexpr int kWordsPerThread = 2 * kPairs;
+constexpr uint64_t kTileWords = (uint64_t)kThreads * kWordsPerThread;  // 1024 words = 65,536 rows
+constexpr int kStageCap = 2048;                                        // row ids staged in LDS per tile
+constexpr int kMaxLeaves = 8;
+constexpr int kMaxOps = 16;
+
+enum : int8_t { OP_AND = -1, OP_OR = -2, OP_ANDNOT = -3 };
+
+inline uint64_t padded_words(uint64_t n_rows) {
+    const uint64_t w = (n_rows + 63) / 64;
+    return ((w + kTileWords - 1) / kTileWords) * kTileWords;
+}
+
+// A postfix program whose leaves appear in order 0..n_leaves-1: leaf k is pushed
+// (complemented if bit k of `negate`), then nops[k] binary ops from `ops` are applied.
+struct EvalProgram {
+    const uint64_t* leaf[kMaxLeaves];
+    uint32_t negate;
+    uint32_t n_leaves;
+    uint8_t nops[kMaxLeaves];
+    int8_t ops[kMaxOps];
+};
+
+enum class EvalMode : int { kDecode = 0, kCount = 1 };
+
+struct EvalArgs {
+    EvalProgram prog;
+    uint64_t n_rows;
+    uint64_t n_words;  // ceil(n_rows / 64)
+    int64_t row_base;
+    int64_t* rowids;
+    uint64_t capacity;
+    uint64_t* count;
+    uint64_t* result_words;
+    uint64_t* tile_status;
+    uint32_t* tile_counter;
+    uint32_t* error_flag;
+    uint32_t num_tiles;
+};
+
+// launchers (cubit_kernels.hip); all asynchronous on `stream`
+hipError_t launch_eval(const EvalArgs& a, EvalMode mode, hipStream_t stream);
+hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
+                                    int64_t constant, uint64_t* out_words, hipStream_t stream);
+hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
+                         int64_t row_base, int64_t* out, hipStream_t stream);
+hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,
+                                     const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* partials,
+                                     int64_t* out, hipStream_t stream);
+constexpr int kSumBlocks = 1024;  // partials buffer holds 2 * kSumBlocks int64
+
+// MVCC (K4)
+// visibility: words = valid-row mask, then clear rows whose delete is visible to txn
+hipError_t launch_visibility(const int64_t* del_rows, const uint64_t* del_ids, uint64_t n_del, uint64_t n_rows,
+                             uint64_t start_time, uint64_t transaction_id, uint64_t* words, hipStream_t stream);
+// mark rows with an update visible to txn into `mask` (atomicOr)
+hipError_t launch_update_mask(const int64_t* upd_rows, const uint64_t* upd_versions, uint64_t n_upd,
+                              uint64_t start_time, uint64_t transaction_id, uint64_t* mask, hipStream_t stream);
+hipError_t launch_fill_valid(uint64_t* words, uint64_t n_rows, hipStream_t stream);
+
+}  // namespace cubit

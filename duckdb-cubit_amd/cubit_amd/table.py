@@ -1,0 +1,227 @@
+"""Python handle over the C ABI: device context, device buffers, table partitions.
+
+Everything here is a thin ctypes wrapper; the work happens in libcubitgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from .filters import Plan, Residual, TableFilterSet, serialize, to_ctypes
+
+
+class Context:
+    """cubit_ctx: one per device; optionally bound to an external HIP stream."""
+
+    def __init__(self, device: int = 0, stream: Optional[int] = None):
+        self.lib = L.gpu_lib()
+        h = C.c_void_p()
+        L.check(self.lib.cubit_ctx_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+        if stream is not None:
+            L.check(self.lib.cubit_ctx_set_stream(h, C.c_void_p(stream)))
+
+    def set_stream(self, stream: Optional[int]) -> None:
+        L.check(self.lib.cubit_ctx_set_stream(self.handle, C.c_void_p(stream or 0)))
+
+    def enable_timing(self, on: bool = True) -> None:
+        L.check(self.lib.cubit_ctx_enable_timing(self.handle, 1 if on else 0))
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        L.check(self.lib.cubit_last_kernel_ms(self.handle, C.byref(ms)))
+        return float(ms.value)
+
+    def timing_reset(self) -> None:
+        L.check(self.lib.cubit_ctx_timing_reset(self.handle))
+
+    def kernel_times_ms(self, cap: int = 4096):
+        arr = (C.c_float * cap)()
+        n = C.c_uint32()
+        L.check(self.lib.cubit_ctx_kernel_times(self.handle, arr, cap, C.byref(n)))
+        return [float(arr[i]) for i in range(min(cap, n.value))]
+
+    def sync(self) -> None:
+        L.check(self.lib.cubit_sync(self.handle))
+
+    def check(self) -> None:
+        L.check(self.lib.cubit_ctx_check(self.handle))
+
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, arr: np.ndarray) -> "DeviceBuffer":
+        arr = np.ascontiguousarray(arr)
+        buf = DeviceBuffer(self, max(arr.nbytes, 16))
+        if arr.nbytes:
+            L.check(self.lib.cubit_memcpy_h2d(self.handle, buf.ptr, arr.ctypes.data, arr.nbytes))
+        return buf
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.cubit_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        p = C.c_void_p()
+        L.check(ctx.lib.cubit_dev_alloc(ctx.handle, nbytes, C.byref(p)))
+        self.ptr = p
+
+    @property
+    def addr(self) -> int:
+        return int(self.ptr.value or 0)
+
+    def download(self, dtype, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if count:
+            L.check(self.ctx.lib.cubit_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def zero(self) -> None:
+        L.check(self.ctx.lib.cubit_memset_d(self.ctx.handle, self.ptr, 0, self.nbytes))
+
+    def free(self) -> None:
+        if self.ptr:
+            self.ctx.lib.cubit_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ctx.handle:
+                self.free()
+        except Exception:
+            pass
+
+
+def padded_words(n_rows: int) -> int:
+    return int(L.gpu_lib().cubit_padded_words(n_rows))
+
+
+class CubitTable:
+    """A row-range partition [row_base, row_base + n_rows) resident on one device."""
+
+    def __init__(self, ctx: Context, n_rows: int, row_base: int = 0):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        self.n_rows = int(n_rows)
+        self.row_base = int(row_base)
+        h = C.c_void_p()
+        L.check(self.lib.cubit_table_create(ctx.handle, self.n_rows, self.row_base, C.byref(h)))
+        self.handle = h
+        self.types: Dict[int, int] = {}
+        self._keep = []
+
+    def add_column(self, col: int, data: np.ndarray, validity: Optional[np.ndarray] = None) -> None:
+        data = np.ascontiguousarray(data)
+        if data.dtype == np.int32:
+            t = L.TYPE_INT32
+        elif data.dtype == np.int64:
+            t = L.TYPE_INT64
+        else:
+            raise TypeError(f"unsupported dtype {data.dtype}")
+        assert data.shape[0] == self.n_rows
+        vptr = None
+        if validity is not None:
+            validity = np.ascontiguousarray(validity, dtype=np.uint64)
+            vptr = validity.ctypes.data
+        L.check(self.lib.cubit_table_add_column(self.handle, col, t, data.ctypes.data, vptr, 0))
+        self.types[col] = t
+
+    def add_device_column(self, col: int, dptr: int, type_: int, validity_dptr: Optional[int] = None) -> None:
+        L.check(self.lib.cubit_table_add_column(self.handle, col, type_, C.c_void_p(dptr),
+                                                C.c_void_p(validity_dptr) if validity_dptr else None, 1))
+        self.types[col] = type_
+
+    def build_index(self, col: int, encoding: int = L.INDEX_RANGE, keys: Optional[Sequence[int]] = None) -> None:
+        if keys:
+            k = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+            L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, k.ctypes.data, len(k)))
+        else:
+            L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, None, 0))
+
+    def index_info(self, col: int):
+        n = C.c_uint32()
+        b = C.c_uint64()
+        L.check(self.lib.cubit_table_index_info(self.handle, col, C.byref(n), C.byref(b)))
+        return int(n.value), int(b.value)
+
+    def set_deletes(self, rows: np.ndarray, ids: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        L.check(self.lib.cubit_table_set_deletes(self.handle, rows.ctypes.data, ids.ctypes.data, len(rows)))
+
+    def set_updates(self, col: int, rows: np.ndarray, values: np.ndarray, versions: np.ndarray) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        values = np.ascontiguousarray(values, dtype=np.int64)
+        versions = np.ascontiguousarray(versions, dtype=np.uint64)
+        L.check(self.lib.cubit_table_set_updates(self.handle, col, rows.ctypes.data, values.ctypes.data,
+                                                 versions.ctypes.data, len(rows)))
+
+    # ------------------------------------------------------------------ scan
+    def scan_into(self, plan_nodes, rowids_dptr: int, capacity: int, count_dptr: int,
+                  txn: Optional[L.Txn] = None, count_only: bool = False) -> None:
+        """Asynchronous scan into caller-owned device buffers (the bench path)."""
+        arr = plan_nodes if isinstance(plan_nodes, C.Array) else to_ctypes(plan_nodes)
+        n = len(plan_nodes) if not isinstance(plan_nodes, C.Array) else len(arr)
+        L.check(self.lib.cubit_table_scan(self.handle, arr, n, C.byref(txn) if txn is not None else None,
+                                          C.c_void_p(rowids_dptr) if rowids_dptr else None, capacity,
+                                          C.c_void_p(count_dptr), L.SCAN_COUNT_ONLY if count_only else 0))
+
+    def scan(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
+             txn: Optional[L.Txn] = None, capacity: Optional[int] = None) -> np.ndarray:
+        """Synchronous scan returning the ascending global row ids as numpy int64."""
+        plan = serialize(filter_set, residual)
+        cap = self.n_rows if capacity is None else capacity
+        out = self.ctx.alloc(max(cap, 1) * 8)
+        cnt = self.ctx.alloc(16)
+        self.scan_into(plan.nodes, out.addr, cap, cnt.addr, txn)
+        self.ctx.check()
+        n = int(cnt.download(np.uint64, 1)[0])
+        if n > cap:
+            raise L.CubitError(L.ERR_CAPACITY, f"{n} rows qualify, capacity {cap}")
+        return out.download(np.int64, n)
+
+    def count(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
+              txn: Optional[L.Txn] = None) -> int:
+        plan = serialize(filter_set, residual)
+        cnt = self.ctx.alloc(16)
+        self.scan_into(plan.nodes, 0, 0, cnt.addr, txn, count_only=True)
+        self.ctx.check()
+        return int(cnt.download(np.uint64, 1)[0])
+
+    def probe(self, col: int, rowids_dptr: int, count_dptr: int, max_n: int, out_dptr: int,
+              txn: Optional[L.Txn] = None) -> None:
+        L.check(self.lib.cubit_table_probe(self.handle, col, C.byref(txn) if txn is not None else None,
+                                           C.c_void_p(rowids_dptr), C.c_void_p(count_dptr), max_n,
+                                           C.c_void_p(out_dptr)))
+
+    def last_plan(self):
+        k = C.c_uint32()
+        p = C.c_uint32()
+        L.check(self.lib.cubit_table_last_plan(self.handle, C.byref(k), C.byref(p)))
+        return int(k.value), int(p.value)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.cubit_table_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,188 @@
+/*
+ * cubit_gpu.h — C ABI of the MI355X bitmap-indexed table-scan filter (libcubitgpu.so).
+ *
+ * The reference (DuckDB v1.1.2, /root/reference) has no C ABI for this path: its drop-in
+ * boundary is the C++ `TableFunction` callback struct
+ * (src/include/duckdb/function/table_function.hpp:184-301) whose `seq_scan` implementation
+ * (src/function/table/table_scan.cpp:119-146, 405-442) drives
+ * RowGroup::TemplatedScan (src/storage/table/row_group.cpp:447-604). The entry points below
+ * are what a C++ DuckDB extension calls from its replacement table
+ * function; each cites the reference function whose work it takes over.
+ *
+ * Conventions: every call returns an int status (CUBIT_OK = 0), never
+ * throws across the ABI, and records a message readable with cubit_last_error() (thread
+ * local). Output buffers are caller-owned device buffers. One context per device; each
+ * calling thread may give the context its own HIP stream (cubit_ctx_set_stream).
+ * Row ids are int64 (DuckDB ROW_TYPE). Bitvectors are LSB-first 64-bit words, the layout
+ * of DuckDB's ValidityMask (src/include/duckdb/common/types/validity_mask.hpp:22,164-168).
+ */
+#ifndef CUBIT_GPU_H
+#define CUBIT_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes */
+#define CUBIT_OK 0
+#define CUBIT_ERR_INVALID 1      /* bad argument */
+#define CUBIT_ERR_HIP 2          /* HIP runtime error */
+#define CUBIT_ERR_OOM 3          /* device allocation failed */
+#define CUBIT_ERR_UNSUPPORTED 4  /* predicate shape / type not supported */
+#define CUBIT_ERR_CAPACITY 5     /* output buffer too small (count still reported) */
+#define CUBIT_ERR_DEVICE 6       /* in-kernel failure (bounded spin expired) */
+
+/* ---- physical types (DuckDB PhysicalType subset on the path: DATE = INT32,
+ *      DECIMAL(15,2) = INT64, BIGINT = INT64, INTEGER = INT32) */
+#define CUBIT_TYPE_INT32 0
+#define CUBIT_TYPE_INT64 1
+
+/* ---- comparison (ExpressionType COMPARE_* used by ConstantFilter,
+ *      src/planner/filter/constant_filter.cpp) */
+#define CUBIT_CMP_EQ 0
+#define CUBIT_CMP_NE 1
+#define CUBIT_CMP_LT 2
+#define CUBIT_CMP_LE 3
+#define CUBIT_CMP_GT 4
+#define CUBIT_CMP_GE 5
+
+/* ---- filter node kinds: mirror TableFilterType (src/include/duckdb/planner/table_filter.hpp:20-27) */
+#define CUBIT_FILTER_CONSTANT 0    /* ConstantFilter(cmp, constant) on `column` */
+#define CUBIT_FILTER_IS_NULL 1
+#define CUBIT_FILTER_IS_NOT_NULL 2
+#define CUBIT_FILTER_OR 3          /* ConjunctionOrFilter, n_children follow (prefix order) */
+#define CUBIT_FILTER_AND 4         /* ConjunctionAndFilter */
+
+/* ---- bitmap index encodings */
+#define CUBIT_INDEX_RANGE 0     /* L_j = {valid rows with v < edge_j}; exact for constants on edges */
+#define CUBIT_INDEX_EQUALITY 1  /* E_k = {rows with v == value_k} (CUBIT's equality encoding) */
+
+/* ---- bitvector program opcodes (operands >= 0 are leaf indices, postfix order) */
+#define CUBIT_OP_AND (-1)
+#define CUBIT_OP_OR (-2)
+#define CUBIT_OP_ANDNOT (-3) /* a AND NOT b */
+
+/* ---- scan flags */
+#define CUBIT_SCAN_COUNT_ONLY 1u /* do not materialise row ids */
+
+typedef struct cubit_ctx cubit_ctx;
+typedef struct cubit_table cubit_table;
+
+/* One node of a predicate tree in prefix order. A TableFilterSet (per-column AND,
+ * table_filter.hpp:67-101) is an AND root whose children each reference one column; a
+ * cross-column OR tree (the residual PhysicalFilter, execute_conjunction.cpp:56-142) uses
+ * the same nodes. */
+typedef struct {
+    int32_t kind;       /* CUBIT_FILTER_* */
+    int32_t cmp;        /* CUBIT_CMP_* (CONSTANT only) */
+    int32_t column;     /* table column index (leaf kinds) */
+    int32_t n_children; /* AND / OR */
+    int64_t constant;   /* CONSTANT: value in the column's physical representation */
+} cubit_filter_node;
+
+/* DuckDB TransactionData{start_time, transaction_id} (src/include/duckdb/transaction/transaction_data.hpp) */
+typedef struct {
+    uint64_t start_time;
+    uint64_t transaction_id;
+} cubit_txn;
+
+/* ------------------------------------------------------------------ context */
+int cubit_ctx_create(int device, cubit_ctx **out);
+int cubit_ctx_destroy(cubit_ctx *ctx);
+/* stream is a hipStream_t (NULL = the null stream). */
+int cubit_ctx_set_stream(cubit_ctx *ctx, void *stream);
+const char *cubit_last_error(void);
+/* Filter-kernel durations measured with HIP events recorded around each launch on the
+ * context stream (ms); requires cubit_ctx_enable_timing(ctx, 1). */
+int cubit_ctx_enable_timing(cubit_ctx *ctx, int on);
+int cubit_last_kernel_ms(cubit_ctx *ctx, float *ms);
+/* Every timed filter-kernel launch since the last reset: ms[i] for i < min(cap, *n). */
+int cubit_ctx_timing_reset(cubit_ctx *ctx);
+int cubit_ctx_kernel_times(cubit_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
+/* Compile-time contract checks (vector 2048 = 32 words, row group 122880 = 1920 words). */
+int cubit_abi_version(void);
+int cubit_vector_size(void);
+int cubit_row_group_size(void);
+
+/* ------------------------------------------------------------------ device memory helpers */
+int cubit_dev_alloc(cubit_ctx *ctx, uint64_t bytes, void **dptr);
+int cubit_dev_free(cubit_ctx *ctx, void *dptr);
+int cubit_memcpy_h2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int cubit_memcpy_d2h(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int cubit_memset_d(cubit_ctx *ctx, void *dst, int value, uint64_t bytes);
+int cubit_sync(cubit_ctx *ctx);
+/* Synchronise the stream and report an in-kernel failure of the last filter launch
+ * (CUBIT_ERR_DEVICE when a look-back spin bound expired). */
+int cubit_ctx_check(cubit_ctx *ctx);
+
+/* ------------------------------------------------------------------ low level (kernels) */
+
+/* K0 — predicate → bitvector over a raw column (TemplatedFilterSelection compare,
+ * column_segment.cpp:261-349; NULL never passes). words must hold
+ * cubit_padded_words(n_rows) words; padding is zeroed. */
+int cubit_build_bitvector(cubit_ctx *ctx, const void *d_col, int type, const uint64_t *d_validity, uint64_t n_rows,
+                          int cmp, int64_t constant, uint64_t *d_words);
+/* words per bitvector including tile padding */
+uint64_t cubit_padded_words(uint64_t n_rows);
+
+/* K1+K2 — evaluate a postfix program over `n_leaves` device bitvectors (each
+ * cubit_padded_words(n_rows) words; leaf_negate bit k complements leaf k before use) and
+ * write the ascending int64 row ids row_base + r of the set rows into d_rowids (capacity
+ * `capacity`), the count into *d_count (device). d_rowids may be NULL with
+ * CUBIT_SCAN_COUNT_ONLY; d_result_words (optional) receives the evaluated bitvector.
+ * Replaces the per-vector sel narrowing + row-id synthesis of RowGroup::TemplatedScan
+ * (row_group.cpp:537-580). */
+int cubit_bitvector_eval(cubit_ctx *ctx, const uint64_t *const *d_leaves, uint32_t n_leaves, uint32_t leaf_negate,
+                         const int32_t *prog, uint32_t n_prog, uint64_t n_rows, int64_t row_base, int64_t *d_rowids,
+                         uint64_t capacity, uint64_t *d_count, uint64_t *d_result_words, uint32_t flags);
+
+/* K3 — gather a column at row ids: out[i] = col[rowids[i] - row_base] as int64
+ * (ColumnData::FetchRow / FilterScan+Slice, column_data.cpp:305-309, 452-461). The number
+ * of ids is read from *d_count (device), at most max_n. */
+int cubit_gather(cubit_ctx *ctx, const void *d_col, int type, const int64_t *d_rowids, const uint64_t *d_count,
+                 uint64_t max_n, int64_t row_base, int64_t *d_out);
+/* Fused probe + reduce: sum over ids of a[r]*b[r] as a 128-bit integer (lo, hi int64 at
+ * d_out[0..1]) — Q6's sum(l_extendedprice*l_discount) (DECIMAL(38,4) storage). */
+int cubit_gather_sum_product(cubit_ctx *ctx, const int64_t *d_a, const int64_t *d_b, const int64_t *d_rowids,
+                             const uint64_t *d_count, uint64_t max_n, int64_t row_base, int64_t *d_out);
+
+/* ------------------------------------------------------------------ table partition API */
+
+/* A row-range partition of a table resident on one device: rows [row_base, row_base+n_rows). */
+int cubit_table_create(cubit_ctx *ctx, uint64_t n_rows, int64_t row_base, cubit_table **out);
+int cubit_table_destroy(cubit_table *t);
+/* Register column `col`. data/validity are host pointers unless on_device = 1 (then the
+ * table only references them). validity may be NULL (no NULLs). */
+int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
+                           int on_device);
+/* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
+ * distinct values of the column" (exact for every constant). */
+int cubit_table_build_index(cubit_table *t, int col, int encoding, const int64_t *values, uint32_t n);
+/* Number of bitvectors and bytes held by the index on col (0 if none). */
+int cubit_table_index_info(cubit_table *t, int col, uint32_t *n_bitvectors, uint64_t *bytes);
+
+/* MVCC delta. Deletes: rows with their delete ids (ChunkVectorInfo::deleted,
+ * chunk_info.cpp:181-202). Updates on `col`: rows, new values and version ids
+ * (UpdateSegment::Update, update_segment.cpp:1074-1199), chronological. Host arrays. */
+int cubit_table_set_deletes(cubit_table *t, const int64_t *rows, const uint64_t *ids, uint64_t n);
+int cubit_table_set_updates(cubit_table *t, int col, const int64_t *rows, const int64_t *values,
+                            const uint64_t *versions, uint64_t n);
+
+/* The scan: evaluate a predicate tree (prefix nodes) for transaction `txn` (NULL = see
+ * every committed row, no MVCC delta applied) and write ascending row ids into d_rowids,
+ * the count into *d_count (device). Replaces TableScanFunc → DataTable::Scan →
+ * RowGroup::TemplatedScan's filter + row-id materialisation (table_scan.cpp:119-146). */
+int cubit_table_scan(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
+                     int64_t *d_rowids, uint64_t capacity, uint64_t *d_count, uint32_t flags);
+/* Probe column `col` at the scan's row ids (visible values for txn). */
+int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64_t *d_rowids, const uint64_t *d_count,
+                      uint64_t max_n, int64_t *d_out);
+/* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
+int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CUBIT_GPU_H */

@@ -1,0 +1,202 @@
+"""ORACLE — test infrastructure only.
+
+ctypes handle on oracle/lib/libcubit_oracle.so (cpu_ref.c, the C restatement of the
+reference CPU scan path). Imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, always as the checker or the reported CPU baseline — never on the
+product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "lib" / "libcubit_oracle.so"
+
+OMAX_COLS = 16
+OTYPE_INT32, OTYPE_INT64 = 0, 1
+OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
+
+
+class OCol(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pad", C.c_int32), ("data", C.c_void_p), ("validity", C.c_void_p),
+                ("n_updates", C.c_uint64), ("upd_rows", C.c_void_p), ("upd_values", C.c_void_p),
+                ("upd_version", C.c_void_p)]
+
+
+class OMvcc(C.Structure):
+    _fields_ = [("inserted", C.c_void_p), ("deleted", C.c_void_p), ("start_time", C.c_uint64),
+                ("transaction_id", C.c_uint64)]
+
+
+class OFilter(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("cmp", C.c_int32), ("column", C.c_int32), ("n_children", C.c_int32),
+                ("constant", C.c_int64)]
+
+
+class OPushed(C.Structure):
+    _fields_ = [("column", C.c_int32), ("root", C.c_int32)]
+
+
+class OScan(C.Structure):
+    _fields_ = [("cols", C.POINTER(OCol)), ("n_cols", C.c_int32), ("n_pushed", C.c_int32),
+                ("pushed", C.POINTER(OPushed)), ("nodes", C.POINTER(OFilter)), ("residual_root", C.c_int32),
+                ("canonical", C.c_int32), ("n_rows", C.c_uint64), ("row_base", C.c_int64),
+                ("tx", C.POINTER(OMvcc))]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        l = C.CDLL(str(LIB))
+        l.oracle_table_scan.restype = C.c_int64
+        l.oracle_table_scan.argtypes = [C.POINTER(OScan), C.c_void_p, C.c_uint64]
+        l.oracle_table_scan_mt.restype = C.c_int64
+        l.oracle_table_scan_mt.argtypes = [C.POINTER(OScan), C.c_int, C.POINTER(C.c_uint64)]
+        l.oracle_fetch.restype = C.c_int
+        l.oracle_fetch.argtypes = [C.POINTER(OCol), C.POINTER(OMvcc), C.c_void_p, C.c_uint64, C.c_int64, C.c_void_p,
+                                   C.c_void_p]
+        l.oracle_sum_product.restype = None
+        l.oracle_sum_product.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int64,
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
+        l.oracle_bitmap_eval.restype = C.c_int64
+        l.oracle_bitmap_eval.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.c_int, C.c_uint64, C.c_int64,
+                                         C.c_void_p, C.c_uint64, C.c_void_p]
+        l.oracle_build_bitvector.restype = None
+        l.oracle_build_bitvector.argtypes = [C.POINTER(OCol), C.c_uint64, C.c_int, C.c_int64, C.c_void_p]
+        l.oracle_xor_hash.restype = C.c_uint64
+        l.oracle_xor_hash.argtypes = [C.c_void_p, C.c_uint64]
+        _lib = l
+    return _lib
+
+
+class Column:
+    """A column as the oracle sees it: base values, optional validity words and a
+    chronological update list (rows, values, version ids)."""
+
+    def __init__(self, data: np.ndarray, validity: Optional[np.ndarray] = None,
+                 updates: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None):
+        self.data = np.ascontiguousarray(data)
+        assert self.data.dtype in (np.int32, np.int64)
+        self.validity = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
+        if updates is None:
+            self.upd = None
+        else:
+            r, v, ver = updates
+            self.upd = (np.ascontiguousarray(r, dtype=np.int64), np.ascontiguousarray(v, dtype=np.int64),
+                        np.ascontiguousarray(ver, dtype=np.uint64))
+
+    def ocol(self) -> OCol:
+        c = OCol()
+        c.type = OTYPE_INT32 if self.data.dtype == np.int32 else OTYPE_INT64
+        c.data = self.data.ctypes.data
+        c.validity = self.validity.ctypes.data if self.validity is not None else None
+        if self.upd is not None:
+            c.n_updates = len(self.upd[0])
+            c.upd_rows, c.upd_values, c.upd_version = (a.ctypes.data for a in self.upd)
+        return c
+
+
+class Mvcc:
+    def __init__(self, start_time: int, transaction_id: int, inserted: Optional[np.ndarray] = None,
+                 deleted: Optional[np.ndarray] = None):
+        self.inserted = None if inserted is None else np.ascontiguousarray(inserted, dtype=np.uint64)
+        self.deleted = None if deleted is None else np.ascontiguousarray(deleted, dtype=np.uint64)
+        self.s = OMvcc(self.inserted.ctypes.data if self.inserted is not None else None,
+                       self.deleted.ctypes.data if self.deleted is not None else None, start_time, transaction_id)
+
+
+def _scan_struct(columns: Sequence[Column], plan, n_rows: int, row_base: int, tx: Optional[Mvcc], canonical: bool):
+    ocols = (OCol * len(columns))(*[c.ocol() for c in columns])
+    nodes = (OFilter * max(len(plan.nodes), 1))()
+    for i, (k, cmp, col, nc, const) in enumerate(plan.nodes):
+        nodes[i] = OFilter(k, cmp, col, nc, const)
+    pushed = (OPushed * max(len(plan.pushed), 1))(*[OPushed(c, r) for c, r in plan.pushed])
+    s = OScan()
+    s.cols = ocols
+    s.n_cols = len(columns)
+    s.n_pushed = len(plan.pushed)
+    s.pushed = pushed
+    s.nodes = nodes
+    s.residual_root = plan.residual_root
+    s.canonical = 1 if canonical else 0
+    s.n_rows = n_rows
+    s.row_base = row_base
+    s.tx = C.pointer(tx.s) if tx is not None else None
+    keep = (ocols, nodes, pushed, columns, tx)
+    return s, keep
+
+
+def table_scan(columns: Sequence[Column], plan, n_rows: int, row_base: int = 0, tx: Optional[Mvcc] = None,
+               canonical: bool = True) -> np.ndarray:
+    """RowGroup::TemplatedScan restatement → qualifying row ids (per-vector sel order; with
+    canonical=True each vector's ids are sorted, so the whole output is ascending)."""
+    s, keep = _scan_struct(columns, plan, n_rows, row_base, tx, canonical)
+    out = np.empty(max(n_rows, 1), dtype=np.int64)
+    n = lib().oracle_table_scan(C.byref(s), out.ctypes.data, n_rows)
+    assert n >= 0
+    return out[:n].copy()
+
+
+def table_scan_mt(columns: Sequence[Column], plan, n_rows: int, threads: int, row_base: int = 0,
+                  tx: Optional[Mvcc] = None) -> Tuple[int, int]:
+    """Morsel-driven multi-threaded scan (timing leg): returns (count, sum of row ids)."""
+    s, keep = _scan_struct(columns, plan, n_rows, row_base, tx, False)
+    sm = C.c_uint64()
+    n = lib().oracle_table_scan_mt(C.byref(s), threads, C.byref(sm))
+    return int(n), int(sm.value)
+
+
+def fetch(column: Column, rowids: np.ndarray, row_base: int = 0, tx: Optional[Mvcc] = None) -> np.ndarray:
+    rowids = np.ascontiguousarray(rowids, dtype=np.int64)
+    out = np.empty(max(len(rowids), 1), dtype=np.int64)
+    c = column.ocol()
+    lib().oracle_fetch(C.byref(c), C.pointer(tx.s) if tx is not None else None, rowids.ctypes.data, len(rowids),
+                       row_base, out.ctypes.data, None)
+    return out[: len(rowids)]
+
+
+def sum_product(a: np.ndarray, b: np.ndarray, rowids: np.ndarray, row_base: int = 0) -> int:
+    rowids = np.ascontiguousarray(rowids, dtype=np.int64)
+    lo = C.c_uint64()
+    hi = C.c_int64()
+    lib().oracle_sum_product(a.ctypes.data, b.ctypes.data, rowids.ctypes.data, len(rowids), row_base, C.byref(lo),
+                             C.byref(hi))
+    return (int(hi.value) << 64) + int(lo.value)
+
+
+def bitmap_eval(leaves: Sequence[np.ndarray], prog: Sequence[int], n_rows: int, row_base: int = 0):
+    """CPU bitmap evaluator: returns (row ids, result words)."""
+    arrs = [np.ascontiguousarray(x, dtype=np.uint64) for x in leaves]
+    ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    p = (C.c_int32 * len(prog))(*prog)
+    nw = (n_rows + 63) // 64
+    words = np.empty(nw, dtype=np.uint64)
+    out = np.empty(max(n_rows, 1), dtype=np.int64)
+    n = lib().oracle_bitmap_eval(ptrs, p, len(prog), n_rows, row_base, out.ctypes.data, n_rows, words.ctypes.data)
+    return out[:n].copy(), words
+
+
+def build_bitvector(column: Column, n_rows: int, cmp: int, constant: int) -> np.ndarray:
+    words = np.empty((n_rows + 63) // 64, dtype=np.uint64)
+    c = column.ocol()
+    lib().oracle_build_bitvector(C.byref(c), n_rows, cmp, constant, words.ctypes.data)
+    return words
+
+
+def xor_hash(rowids: np.ndarray) -> int:
+    rowids = np.ascontiguousarray(rowids, dtype=np.int64)
+    return int(lib().oracle_xor_hash(rowids.ctypes.data, len(rowids)))

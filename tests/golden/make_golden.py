@@ -1,0 +1,64 @@
+"""Regenerate tests/golden/*.json from the reference's own files (run in the build
+container, where /root/reference exists). The JSON it writes is data only: expected
+outputs quoted from the reference's answer files and tests, plus the fingerprints the
+survey measured by running the reference."""
+import json
+from pathlib import Path
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+
+def answer(sf):
+    p = REF / f"extension/tpch/dbgen/answers/sf{sf}/q06.csv"
+    lines = p.read_text().split()
+    assert lines[0] == "revenue"
+    return {"revenue": lines[1], "source": str(p.relative_to(REF))}
+
+
+def main():
+    tpch = {
+        "q6_revenue": {sf: answer(sf) for sf in ("0.01", "0.1", "1", "100")},
+        # SURVEY.md §8c "Golden vectors / known answers", measured with the reference
+        # (DuckDB v1.1.2 built from /root/reference) in the survey container.
+        "fingerprints": {
+            "sf1_q6": {"count": 114160, "sum_rowid": 341745978685, "min": 55, "max": 6001177,
+                       "xor_hash": 9778593094192572261},
+            "sf1_shipdate_eq_1995_03_15": {"count": 2528, "sum_rowid": 7563025794,
+                                            "xor_hash": 11097155983190906094},
+            "sf1_leaf_counts": {"shipdate_1994": 909455, "discount_005_007": 1637557, "quantity_lt_24": 2758822},
+            "sf100_q6": {"count": 11421368, "sum_rowid": 3427761320230477, "min": 55, "max": 600037873,
+                         "xor_hash": 11990059560084878909},
+            "sf100_shipdate_eq_1995_03_15": {"count": 249371},
+            "sf001_q6": {"count": 1191},
+            "sf001_mvcc": {"writer_view": 1267, "reader_view": 1191,
+                           "writer_txn": "UPDATE lineitem SET l_quantity=1 WHERE rowid%7=0; "
+                                         "DELETE FROM lineitem WHERE rowid%11=0 (uncommitted)"},
+            "source": "SURVEY.md §8c; BASELINE.md §3",
+        },
+    }
+    (OUT / "tpch.json").write_text(json.dumps(tpch, indent=1, sort_keys=True) + "\n")
+
+    # test/sql/filter/test_zonemap_segment.test: blocks of 65,534 rows with values 1..5,
+    # SUM(i) WHERE i=k
+    zm = {
+        "source": "test/sql/filter/test_zonemap_segment.test:13-111",
+        "block_rows": 65534,
+        "values": [1, 2, 3, 4, 5],
+        "expected_sum_eq": {"1": 65534, "2": 131068, "3": 196602, "4": 262136, "5": 327670, "6": None},
+    }
+    # test/sql/transactions/test_interleaved_versions.test: two rows, interleaved deletes
+    iv = {
+        "source": "test/sql/transactions/test_interleaved_versions.test:66-120",
+        "rows": [1, 2],
+        "steps": [
+            {"con1_deletes": "i=1", "con2_deletes": "i=2", "expect": {"con1": 2, "con2": 1, "con3": 3}},
+            {"after": "con1 COMMIT", "expect": {"con1": 2, "con2": 1}},
+        ],
+    }
+    (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv},
+                                                         indent=1, sort_keys=True) + "\n")
+
+
+if __name__ == "__main__":
+    main()

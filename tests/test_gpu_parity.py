@@ -1,0 +1,285 @@
+"""HIP path vs the oracle on identical inputs — bit-exact row-id sets (and probe values).
+
+Every test here calls libcubitgpu.so through the C ABI on the MI355X.
+"""
+import numpy as np
+import pytest
+
+from conftest import lineitem, revenue_from_answer
+from cubit_amd import _lib as L
+from cubit_amd import filters as F
+from cubit_amd.datagen import uniform_i32, validity_from_mask
+from cubit_amd.table import Context, CubitTable, padded_words
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TXN_START = 4611686018427388000
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def q6_table(ctx, li, index=True, encoding=L.INDEX_RANGE):
+    t = CubitTable(ctx, li.n_rows, li.row_base)
+    t.add_column(0, li.l_shipdate)
+    t.add_column(1, li.l_discount)
+    t.add_column(2, li.l_quantity)
+    t.add_column(3, li.l_extendedprice)
+    if index:
+        # shipdate binned at month starts (Q6's year bounds are month starts: exact);
+        # discount / quantity: every distinct value
+        months = [F.date(y, m, 1) for y in range(1992, 1999) for m in range(1, 13)] + [F.date(1999, 1, 1)]
+        t.build_index(0, L.INDEX_RANGE, months)
+        t.build_index(1, encoding)
+        t.build_index(2, encoding)
+    return t
+
+
+def oracle_q6(li):
+    cols = [O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity)]
+    return O.table_scan(cols, F.serialize(F.q6_filter_set()), li.n_rows, li.row_base)
+
+
+@pytest.mark.parametrize("sf", [0.01, 0.1])
+@pytest.mark.parametrize("index", [True, False])
+def test_q6_rowids_bit_exact(ctx, sf, index):
+    li = lineitem(sf)
+    t = q6_table(ctx, li, index=index)
+    got = t.scan(F.q6_filter_set())
+    assert np.array_equal(got, oracle_q6(li))
+    if index:
+        k, passes = t.last_plan()
+        assert k == 5 and passes == 1  # range-encoded Q6 = 5 bitvectors, one fused pass
+
+
+def test_q6_sf1_fingerprint_and_revenue(ctx, golden):
+    li = lineitem(1)
+    t = q6_table(ctx, li)
+    fp = golden["tpch"]["fingerprints"]["sf1_q6"]
+    rows = t.scan(F.q6_filter_set())
+    assert len(rows) == fp["count"] and int(rows.sum()) == fp["sum_rowid"]
+    assert O.xor_hash(rows) == fp["xor_hash"]
+    assert np.array_equal(rows, oracle_q6(li))
+    # K3: probe + fused sum on the device
+    d_rows = ctx.upload(rows)
+    d_cnt = ctx.upload(np.array([len(rows)], dtype=np.uint64))
+    out = ctx.alloc(16)
+    ep = ctx.upload(li.l_extendedprice)
+    di = ctx.upload(li.l_discount)
+    L.check(ctx.lib.cubit_gather_sum_product(ctx.handle, ep.ptr, di.ptr, d_rows.ptr, d_cnt.ptr, len(rows), 0,
+                                             out.ptr))
+    lo, hi = out.download(np.int64, 2)
+    rev = (int(hi) << 64) + (int(lo) & (2 ** 64 - 1))
+    assert rev == revenue_from_answer(golden["tpch"]["q6_revenue"]["1"]["revenue"])
+    probe = ctx.alloc(len(rows) * 8)
+    t.probe(3, d_rows.addr, d_cnt.addr, len(rows), probe.addr)
+    assert np.array_equal(probe.download(np.int64, len(rows)), li.l_extendedprice[rows])
+
+
+def test_sf1_equality_encoded_shipdate(ctx, golden):
+    li = lineitem(1)
+    t = CubitTable(ctx, li.n_rows)
+    t.add_column(0, li.l_shipdate)
+    t.build_index(0, L.INDEX_EQUALITY)
+    nbv, nbytes = t.index_info(0)
+    assert nbv == 2526
+    fp = golden["tpch"]["fingerprints"]["sf1_shipdate_eq_1995_03_15"]
+    fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter("=", F.date(1995, 3, 15)),
+                                                      F.IsNotNullFilter()])})
+    rows = t.scan(fs)
+    assert len(rows) == fp["count"] and int(rows.sum()) == fp["sum_rowid"]
+    assert O.xor_hash(rows) == fp["xor_hash"]
+    assert t.last_plan()[0] == 1
+
+
+def test_synthetic_range_config2_small(ctx):
+    n = 10_000_003
+    v = uniform_i32(42, n, 1_000_000)
+    t = CubitTable(ctx, n)
+    t.add_column(0, v)
+    t.build_index(0, L.INDEX_RANGE, [10_000])
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 10_000)})
+    got = t.scan(fs)
+    assert np.array_equal(got, np.nonzero(v < 10_000)[0])
+    assert t.last_plan() == (1, 1)
+
+
+def test_or_tree_config4_small(ctx):
+    n = 3_000_017
+    cols = [uniform_i32(s, n, 1_000_000) for s in (1, 2, 3, 4)]
+    t = CubitTable(ctx, n)
+    for i, c in enumerate(cols):
+        t.add_column(i, c)
+        t.build_index(i, L.INDEX_RANGE, [100_000])
+    tree = F.Or(F.And(F.Cmp(0, "<", 100_000), F.Cmp(1, "<", 100_000)),
+                F.And(F.Cmp(2, "<", 100_000), F.Cmp(3, "<", 100_000)))
+    got = t.scan(None, tree)
+    ref = O.table_scan([O.Column(c) for c in cols], F.serialize(None, tree), n)
+    assert np.array_equal(got, ref)
+    assert t.last_plan() == (4, 1)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4095, 65535, 65536, 65537, 200_001])
+def test_tails_and_dense_tiles(ctx, n):
+    """Tail words, tile boundaries and a dense result (> LDS stage capacity per tile)."""
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 10, n).astype(np.int64)
+    t = CubitTable(ctx, n, row_base=1000)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE)
+    for cmp, c in [("<", 9), (">=", 1), ("!=", 3), ("=", 0), (">", 100), ("<=", 9)]:
+        fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
+        ref = O.table_scan([O.Column(a)], F.serialize(fs), n, row_base=1000)
+        assert np.array_equal(t.scan(fs), ref), (cmp, c)
+
+
+def test_nulls_comparisons_and_null_filters(ctx):
+    n = 300_000
+    rng = np.random.default_rng(5)
+    a = rng.integers(-50, 50, n).astype(np.int32)
+    valid = rng.random(n) > 0.2
+    vw = validity_from_mask(valid)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a, vw)
+    t.add_column(1, a)  # no index, no nulls: K0 path
+    t.build_index(0, L.INDEX_RANGE)
+    oc = [O.Column(a, vw), O.Column(a)]
+    cases = [F.ConstantFilter("<", 0), F.ConstantFilter(">=", 10), F.ConstantFilter("!=", 3),
+             F.ConstantFilter("=", -50), F.IsNullFilter(), F.IsNotNullFilter(),
+             F.ConjunctionOrFilter([F.ConstantFilter("<", -40), F.IsNullFilter()]),
+             F.ConjunctionAndFilter([F.ConstantFilter(">", -10), F.ConstantFilter("<=", 10), F.IsNotNullFilter()])]
+    for f in cases:
+        for col in (0, 1):
+            fs = F.TableFilterSet({col: f})
+            ref = O.table_scan(oc, F.serialize(fs), n)
+            assert np.array_equal(t.scan(fs), ref), (f, col)
+
+
+def test_equality_index_ranges_and_wide_or(ctx):
+    n = 500_000
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 40, n).astype(np.int64)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_EQUALITY)
+    for f in [F.ConstantFilter("<", 5), F.ConstantFilter(">=", 30), F.ConstantFilter("<", 30),
+              F.ConjunctionOrFilter([F.ConstantFilter("=", k) for k in range(0, 40, 3)])]:
+        fs = F.TableFilterSet({0: f})
+        ref = O.table_scan([O.Column(a)], F.serialize(fs), n)
+        assert np.array_equal(t.scan(fs), ref), f
+
+
+def test_k0_compare_bitvector_matches_oracle(ctx):
+    n = 100_003
+    rng = np.random.default_rng(2)
+    for dt in (np.int32, np.int64):
+        a = rng.integers(-1000, 1000, n).astype(dt)
+        valid = rng.random(n) > 0.1
+        vw = validity_from_mask(valid)
+        da = ctx.upload(a)
+        dv = ctx.upload(np.concatenate([vw, np.zeros(padded_words(n) - len(vw), dtype=np.uint64)]))
+        out = ctx.alloc(padded_words(n) * 8)
+        for cmp in range(6):
+            L.check(ctx.lib.cubit_build_bitvector(ctx.handle, da.ptr, 0 if dt == np.int32 else 1, dv.ptr, n, cmp, 17,
+                                                  out.ptr))
+            got = out.download(np.uint64, padded_words(n))
+            ref = O.build_bitvector(O.Column(a, vw), n, cmp, 17)
+            assert np.array_equal(got[: len(ref)], ref)
+            assert not got[len(ref):].any()
+
+
+def test_low_level_eval_random_programs(ctx):
+    """cubit_bitvector_eval vs the oracle bitmap evaluator on random programs / negations."""
+    rng = np.random.default_rng(123)
+    n = 777_777
+    pw = padded_words(n)
+    nw = (n + 63) // 64
+    leaves = []
+    dleaves = []
+    for k in range(8):
+        dens = rng.choice([0.02, 0.3, 0.9])
+        w = validity_from_mask(rng.random(n) < dens)
+        leaves.append(w)
+        dleaves.append(ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])))
+    import ctypes as C
+
+    ptrs = (C.c_void_p * 8)(*[d.ptr.value for d in dleaves])
+    out = ctx.alloc(n * 8)
+    cnt = ctx.alloc(16)
+    words = ctx.alloc(pw * 8)
+    ops = [L.OP_AND, L.OP_OR, L.OP_ANDNOT]
+    for trial in range(40):
+        k = int(rng.integers(1, 9))
+        neg = int(rng.integers(0, 1 << k))
+        # random postfix over leaves 0..k-1
+        prog, depth = [], 0
+        leaf_i = 0
+        while leaf_i < k or depth > 1:
+            if leaf_i < k and (depth < 2 or rng.random() < 0.5):
+                prog.append(leaf_i)
+                leaf_i += 1
+                depth += 1
+            else:
+                prog.append(int(rng.choice(ops)))
+                depth -= 1
+        p = (C.c_int32 * len(prog))(*prog)
+        rc = ctx.lib.cubit_bitvector_eval(ctx.handle, ptrs, k, neg, p, len(prog), n, 5, out.ptr, n, cnt.ptr,
+                                          words.ptr, 0)
+        if rc == L.ERR_UNSUPPORTED:
+            continue  # stack deeper than 4
+        L.check(rc)
+        ctx.check()
+        c = int(cnt.download(np.uint64, 1)[0])
+        ol = [(~leaves[i] if (neg >> i) & 1 else leaves[i]) for i in range(k)]
+        ref_rows, ref_words = O.bitmap_eval(ol, prog, n, 5)
+        assert c == len(ref_rows)
+        assert np.array_equal(out.download(np.int64, c), ref_rows)
+        assert np.array_equal(words.download(np.uint64, nw), ref_words)
+
+
+def test_capacity_is_respected_and_count_reported(ctx):
+    n = 100_000
+    a = np.arange(n, dtype=np.int64)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a)
+    with pytest.raises(L.CubitError):
+        t.scan(F.TableFilterSet({0: F.ConstantFilter("<", 50_000)}), capacity=1000)
+    assert t.count(F.TableFilterSet({0: F.ConstantFilter("<", 50_000)})) == 50_000
+
+
+def test_mvcc_writer_reader_views_sf001(ctx, golden):
+    """SURVEY §3-E scenario on the GPU: visibility bitvector (deletes) + patched quantity
+    leaves (updates) → 1267 rows for the writer, 1191 for the concurrent reader."""
+    li = lineitem(0.01)
+    fp = golden["tpch"]["fingerprints"]["sf001_mvcc"]
+    n = li.n_rows
+    writer = TXN_START + 1
+    upd_rows = np.arange(0, n, 7, dtype=np.int64)
+    del_rows = np.arange(0, n, 11, dtype=np.int64)
+    for index in (True, False):
+        t = q6_table(ctx, li, index=index)
+        t.set_deletes(del_rows, np.full(len(del_rows), writer, dtype=np.uint64))
+        t.set_updates(2, upd_rows, np.full(len(upd_rows), 100), np.full(len(upd_rows), writer, dtype=np.uint64))
+        w = t.scan(F.q6_filter_set(), txn=L.Txn(2, writer))
+        r = t.scan(F.q6_filter_set(), txn=L.Txn(2, TXN_START + 2))
+        assert len(w) == fp["writer_view"] and len(r) == fp["reader_view"]
+        # exact sets vs the oracle
+        deleted = np.full(n, np.uint64(2 ** 64 - 2), dtype=np.uint64)
+        deleted[del_rows] = writer
+        qty = O.Column(li.l_quantity, updates=(upd_rows, np.full(len(upd_rows), 100, dtype=np.int64),
+                                               np.full(len(upd_rows), writer, dtype=np.uint64)))
+        cols = [O.Column(li.l_shipdate), O.Column(li.l_discount), qty]
+        plan = F.serialize(F.q6_filter_set())
+        assert np.array_equal(w, O.table_scan(cols, plan, n, tx=O.Mvcc(2, writer, deleted=deleted)))
+        assert np.array_equal(r, O.table_scan(cols, plan, n, tx=O.Mvcc(2, TXN_START + 2, deleted=deleted)))
+        # probe sees the writer's value
+        d_rows = ctx.upload(w)
+        d_cnt = ctx.upload(np.array([len(w)], dtype=np.uint64))
+        pr = ctx.alloc(len(w) * 8)
+        t.probe(2, d_rows.addr, d_cnt.addr, len(w), pr.addr, txn=L.Txn(2, writer))
+        assert np.array_equal(pr.download(np.int64, len(w)), O.fetch(qty, w, tx=O.Mvcc(2, writer)))

@@ -1,0 +1,170 @@
+"""Pin the oracle (oracle/cpu_ref.c) and the lineitem generator against the reference's
+own answers: extension/tpch/dbgen/answers/sf*/q06.csv and the fingerprints SURVEY.md §8c
+measured by running DuckDB v1.1.2 (tests/golden/tpch.json)."""
+import numpy as np
+import pytest
+
+from conftest import lineitem, revenue_from_answer
+from cubit_amd import filters as F
+from oracle import oracle as O
+
+
+def q6_columns(li):
+    return [O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity), O.Column(li.l_extendedprice)]
+
+
+def q6_rows(li, tx=None, cols=None):
+    plan = F.serialize(F.q6_filter_set(0, 1, 2))
+    return O.table_scan(cols or q6_columns(li), plan, li.n_rows, li.row_base, tx=tx)
+
+
+@pytest.mark.parametrize("sf", [0.01, 0.1, 1])
+def test_q6_revenue_matches_reference_answer(sf, golden):
+    li = lineitem(sf)
+    rows = q6_rows(li)
+    rev = O.sum_product(li.l_extendedprice, li.l_discount, rows)
+    key = {0.01: "0.01", 0.1: "0.1", 1: "1"}[sf]
+    assert rev == revenue_from_answer(golden["tpch"]["q6_revenue"][key]["revenue"])
+
+
+def test_sf001_q6_count(li001, golden):
+    assert len(q6_rows(li001)) == golden["tpch"]["fingerprints"]["sf001_q6"]["count"]
+
+
+def test_sf1_q6_fingerprint(li1, golden):
+    fp = golden["tpch"]["fingerprints"]["sf1_q6"]
+    rows = q6_rows(li1)
+    assert len(rows) == fp["count"]
+    assert int(rows.sum()) == fp["sum_rowid"]
+    assert int(rows.min()) == fp["min"] and int(rows.max()) == fp["max"]
+    assert O.xor_hash(rows) == fp["xor_hash"]
+    assert np.all(np.diff(rows) > 0)
+
+
+def test_sf1_shipdate_equality_fingerprint(li1, golden):
+    fp = golden["tpch"]["fingerprints"]["sf1_shipdate_eq_1995_03_15"]
+    fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter("=", F.date(1995, 3, 15)),
+                                                      F.IsNotNullFilter()])})
+    rows = O.table_scan(q6_columns(li1), F.serialize(fs), li1.n_rows)
+    assert len(rows) == fp["count"]
+    assert int(rows.sum()) == fp["sum_rowid"]
+    assert O.xor_hash(rows) == fp["xor_hash"]
+
+
+def test_sf1_leaf_counts(li1, golden):
+    fp = golden["tpch"]["fingerprints"]["sf1_leaf_counts"]
+    cols = q6_columns(li1)
+    ship = F.TableFilterSet()
+    ship.push_filter(0, F.ConstantFilter(">=", F.date(1994, 1, 1)))
+    ship.push_filter(0, F.ConstantFilter("<", F.date(1995, 1, 1)))
+    disc = F.TableFilterSet()
+    disc.push_filter(1, F.ConstantFilter(">=", 5))
+    disc.push_filter(1, F.ConstantFilter("<=", 7))
+    qty = F.TableFilterSet({2: F.ConstantFilter("<", 2400)})
+    assert len(O.table_scan(cols, F.serialize(ship), li1.n_rows)) == fp["shipdate_1994"]
+    assert len(O.table_scan(cols, F.serialize(disc), li1.n_rows)) == fp["discount_005_007"]
+    assert len(O.table_scan(cols, F.serialize(qty), li1.n_rows)) == fp["quantity_lt_24"]
+
+
+TXN_START = 4611686018427388000  # TRANSACTION_ID_START (src/common/constants.cpp:14)
+
+
+def mvcc_scenario(li):
+    """con1 (uncommitted) UPDATE l_quantity=1 WHERE rowid%7=0 and DELETE WHERE
+    rowid%11=0. Writer: start_time 2, transaction_id TXN_START+1; reader con2: start_time 2,
+    transaction_id TXN_START+2. Uncommitted versions carry the writer's transaction id."""
+    n = li.n_rows
+    writer = TXN_START + 1
+    upd_rows = np.arange(0, n, 7, dtype=np.int64)
+    del_rows = np.arange(0, n, 11, dtype=np.int64)
+    deleted = np.full(n, np.uint64(2 ** 64 - 2), dtype=np.uint64)  # NOT_DELETED_ID
+    deleted[del_rows] = writer
+    return upd_rows, del_rows, deleted, writer
+
+
+def test_sf001_mvcc_writer_and_reader_views(li001, golden):
+    fp = golden["tpch"]["fingerprints"]["sf001_mvcc"]
+    upd_rows, _, deleted, writer = mvcc_scenario(li001)
+    qty = O.Column(li001.l_quantity, updates=(upd_rows, np.full(len(upd_rows), 100, dtype=np.int64),
+                                              np.full(len(upd_rows), writer, dtype=np.uint64)))
+    cols = [O.Column(li001.l_shipdate), O.Column(li001.l_discount), qty, O.Column(li001.l_extendedprice)]
+    w = O.Mvcc(2, writer, deleted=deleted)
+    r = O.Mvcc(2, TXN_START + 2, deleted=deleted)
+    assert len(q6_rows(li001, tx=w, cols=cols)) == fp["writer_view"]
+    assert len(q6_rows(li001, tx=r, cols=cols)) == fp["reader_view"]
+
+
+def test_oracle_bitmap_evaluator_agrees_with_scan(li01):
+    """The CPU bitmap evaluator over range-encoded bitvectors equals the value scan."""
+    n = li01.n_rows
+    sd, di, qu = O.Column(li01.l_shipdate), O.Column(li01.l_discount), O.Column(li01.l_quantity)
+    leaves = [O.build_bitvector(sd, n, 2, F.date(1995, 1, 1)),   # shipdate < 1995-01-01
+              O.build_bitvector(sd, n, 2, F.date(1994, 1, 1)),   # shipdate < 1994-01-01
+              O.build_bitvector(di, n, 2, 8),                    # discount < 0.08
+              O.build_bitvector(di, n, 2, 5),                    # discount < 0.05
+              O.build_bitvector(qu, n, 2, 2400)]                 # quantity < 24
+    prog = [0, 1, O.OB_ANDNOT, 2, 3, O.OB_ANDNOT, O.OB_AND, 4, O.OB_AND]
+    rows, _ = O.bitmap_eval(leaves, prog, n)
+    assert np.array_equal(rows, q6_rows(li01))
+
+
+def test_per_column_or_is_a_set_union_in_child_order():
+    """ConjunctionOrFilter keeps child order (column_segment.cpp:381-409): the raw output is
+    not ascending, the canonical set equals the numpy predicate."""
+    rng = np.random.default_rng(7)
+    n = 10000
+    a = rng.integers(0, 100, n).astype(np.int32)
+    fs = F.TableFilterSet({0: F.ConjunctionOrFilter([F.ConstantFilter(">", 90), F.ConstantFilter("<", 5)])})
+    plan = F.serialize(fs)
+    raw = O.table_scan([O.Column(a)], plan, n, canonical=False)
+    canon = O.table_scan([O.Column(a)], plan, n, canonical=True)
+    expect = np.nonzero((a > 90) | (a < 5))[0]
+    assert np.array_equal(np.sort(raw), expect)
+    assert np.array_equal(canon, expect)
+    assert not np.all(np.diff(raw) > 0)
+
+
+def test_residual_or_tree_with_nulls():
+    rng = np.random.default_rng(11)
+    n = 5000
+    cols = [rng.integers(0, 100, n).astype(np.int32) for _ in range(4)]
+    valid = [rng.random(n) > 0.1 for _ in range(4)]
+    from cubit_amd.datagen import validity_from_mask
+
+    ocols = [O.Column(c, validity_from_mask(v)) for c, v in zip(cols, valid)]
+    tree = F.Or(F.And(F.Cmp(0, "<", 10), F.Cmp(1, "<", 10)), F.And(F.Cmp(2, "<", 10), F.Cmp(3, "<", 10)))
+    rows = O.table_scan(ocols, F.serialize(None, tree), n)
+    m = ((cols[0] < 10) & valid[0] & (cols[1] < 10) & valid[1]) | ((cols[2] < 10) & valid[2] & (cols[3] < 10) & valid[3])
+    assert np.array_equal(rows, np.nonzero(m)[0])
+
+
+def test_zonemap_segment_reference_case(golden):
+    """test/sql/filter/test_zonemap_segment.test: SUM(i) WHERE i=k over 5 blocks of 65,534."""
+    c = golden["cases"]["zonemap_segment"]
+    data = np.repeat(np.array(c["values"], dtype=np.int32), c["block_rows"])
+    for k, want in c["expected_sum_eq"].items():
+        fs = F.TableFilterSet({0: F.ConstantFilter("=", int(k))})
+        rows = O.table_scan([O.Column(data)], F.serialize(fs), len(data))
+        got = int(data[rows].astype(np.int64).sum()) if len(rows) else None
+        assert got == want
+
+
+def test_interleaved_versions_reference_case(golden):
+    """test/sql/transactions/test_interleaved_versions.test:66-120 (deletes by two txns)."""
+    data = np.array([1, 2], dtype=np.int32)
+    t1, t2 = TXN_START + 10, TXN_START + 11
+    deleted = np.array([t1, t2], dtype=np.uint64)  # con1 deletes i=1, con2 deletes i=2
+    plan = F.serialize(F.TableFilterSet())
+
+    def s(tx):
+        r = O.table_scan([O.Column(data)], plan, 2, tx=tx)
+        return int(data[r].sum()) if len(r) else None
+
+    exp = golden["cases"]["interleaved_versions"]["steps"]
+    assert s(O.Mvcc(5, t1, deleted=deleted)) == exp[0]["expect"]["con1"]
+    assert s(O.Mvcc(5, t2, deleted=deleted)) == exp[0]["expect"]["con2"]
+    assert s(O.Mvcc(5, TXN_START + 12, deleted=deleted)) == exp[0]["expect"]["con3"]
+    # con1 commits with commit id 6: the delete of i=1 now carries id 6; con2 (start 5) still sees it
+    deleted_c = np.array([6, t2], dtype=np.uint64)
+    assert s(O.Mvcc(5, t2, deleted=deleted_c)) == exp[1]["expect"]["con2"]
+    assert s(O.Mvcc(7, TXN_START + 13, deleted=deleted_c)) == 2
