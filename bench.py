@@ -247,8 +247,13 @@ def main():
 
     parity = None
     if rank == 0:
-        ids = rowids[:q].cpu().numpy()
-        parity = {"ascending_unique": bool(np.all(np.diff(ids) > 0)) if q > 1 else True}
+        from cubit_amd.table import runs_in_row_order
+
+        raw = rowids[:q].cpu().numpy()
+        directory, rows_per_tile = ctx.last_tiles()
+        ids = runs_in_row_order(raw, directory)
+        parity = {"tile_runs_cover_output": int(directory[:, 1].sum()) == q,
+                  "row_order_via_directory_ascending": bool(np.all(np.diff(ids) > 0)) if q > 1 else True}
         if world == 1 and abs(sf_total - 100.0) < 1e-9:
             fp = json.loads((ROOT / "tests" / "golden" / "tpch.json").read_text())["fingerprints"]["sf100_q6"]
             got = {"count": q, "sum_rowid": int(ids.sum()), "min": int(ids.min()), "max": int(ids.max()),
@@ -293,12 +298,13 @@ def main():
                 "index": "range-encoded: l_shipdate month edges (85), l_discount/l_quantity every distinct "
                          "value",
                 "concat": bool(args.concat and world > 1),
+                "output_order": "tile runs (131,072-row tiles, ascending within; directory gives row order)",
                 "parallelism": f"dp{world}",
             },
             "input_rows_per_sec": n_total * args.steps / t_max,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "eval_decode_kernel<5, kDecode>",
+                "kernel": "eval_decode_tiles<5, 2, 4096, 512>",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -53,27 +53,45 @@ int fail(int code, const char* fmt, ...) {
 
 struct cubit_ctx {
     int device = 0;
+    int n_cus = 256;
     hipStream_t stream = nullptr;
     bool timing = false;
     // one (start, stop) event pair per timed filter-kernel launch since the last reset
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
     size_t n_timed = 0;
-    // look-back workspace: [counter, error, pad...] then tile status words
-    uint64_t* ws = nullptr;
-    uint64_t ws_tiles = 0;
+    // tile directory of the last decode ({start, length} per tile) + ordered-pass scratch
+    uint64_t* dir = nullptr;
+    uint64_t* dst_off = nullptr;
+    uint64_t dir_tiles = 0;
+    uint32_t last_tiles = 0;
+    uint64_t last_tile_rows = 0;
+    int64_t* tmp_ids = nullptr;
+    uint64_t tmp_cap = 0;
     int64_t* partials = nullptr;
 };
 
 namespace {
 
-int ensure_workspace(cubit_ctx* ctx, uint64_t tiles) {
-    if (tiles <= ctx->ws_tiles && ctx->ws) return CUBIT_OK;
-    if (ctx->ws) HIP_CHECK(hipFree(ctx->ws));
-    ctx->ws = nullptr;
+int ensure_dir(cubit_ctx* ctx, uint64_t tiles) {
+    if (tiles <= ctx->dir_tiles && ctx->dir) return CUBIT_OK;
+    if (ctx->dir) HIP_CHECK(hipFree(ctx->dir));
+    if (ctx->dst_off) HIP_CHECK(hipFree(ctx->dst_off));
+    ctx->dir = ctx->dst_off = nullptr;
     const uint64_t want = std::max<uint64_t>(tiles, 1024);
-    if (hipMalloc(&ctx->ws, (want + 2) * sizeof(uint64_t)) != hipSuccess)
-        return fail(CUBIT_ERR_OOM, "workspace allocation of %llu tiles failed", (unsigned long long)want);
-    ctx->ws_tiles = want;
+    if (hipMalloc(&ctx->dir, 2 * want * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&ctx->dst_off, want * sizeof(uint64_t)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "tile directory allocation of %llu tiles failed", (unsigned long long)want);
+    ctx->dir_tiles = want;
+    return CUBIT_OK;
+}
+
+int ensure_tmp(cubit_ctx* ctx, uint64_t cap) {
+    if (cap <= ctx->tmp_cap && ctx->tmp_ids) return CUBIT_OK;
+    if (ctx->tmp_ids) HIP_CHECK(hipFree(ctx->tmp_ids));
+    ctx->tmp_ids = nullptr;
+    if (hipMalloc(&ctx->tmp_ids, std::max<uint64_t>(cap, 1) * sizeof(int64_t)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "ordered-pass scratch of %llu ids failed", (unsigned long long)cap);
+    ctx->tmp_cap = cap;
     return CUBIT_OK;
 }
 
@@ -82,27 +100,23 @@ int set_device(cubit_ctx* ctx) {
     return CUBIT_OK;
 }
 
-// Launch eval over a compiled program. bits_only: write result words, no row ids.
+enum class RunMode { kDecode, kCount };
+
+// Launch the evaluator over a compiled program (asynchronous on the context stream).
+//   kDecode: row ids as per-tile ascending runs + tile directory (ordered = lay them out in
+//            row order with one extra pass); kCount: count(*) and/or result words.
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
-             uint64_t capacity, uint64_t* d_count, uint64_t* result_words, bool count_only, bool timed = false) {
-    const uint64_t nw = (n_rows + 63) / 64;
-    const uint64_t tiles = std::max<uint64_t>(1, padded_words(n_rows) / kTileWords);
-    if (int rc = ensure_workspace(ctx, tiles)) return rc;
+             uint64_t capacity, uint64_t* d_count, uint64_t* result_words, RunMode mode, bool timed = false,
+             bool ordered = false) {
     EvalArgs a{};
     a.prog = prog;
     a.n_rows = n_rows;
-    a.n_words = nw;
+    a.n_words = (n_rows + 63) / 64;
     a.row_base = row_base;
-    a.rowids = rowids;
-    a.capacity = rowids ? capacity : 0;
     a.count = d_count;
     a.result_words = result_words;
-    a.tile_counter = reinterpret_cast<uint32_t*>(ctx->ws);
-    a.error_flag = reinterpret_cast<uint32_t*>(ctx->ws) + 1;
-    a.tile_status = ctx->ws + 2;
-    a.num_tiles = (uint32_t)tiles;
-    HIP_CHECK(hipMemsetAsync(ctx->ws, 0, (tiles + 2) * sizeof(uint64_t), ctx->stream));
-    if (count_only) HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+    const uint64_t pw = padded_words(n_rows);
+    HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
     hipEvent_t stop = nullptr;
     if (timed && ctx->timing) {
         if (ctx->n_timed == ctx->evs.size()) {
@@ -111,20 +125,32 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
             HIP_CHECK(hipEventCreate(&e1));
             ctx->evs.emplace_back(e0, e1);
         }
-        HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed].first, ctx->stream));
         stop = ctx->evs[ctx->n_timed].second;
-        ctx->n_timed++;
     }
-    HIP_CHECK(launch_eval(a, count_only ? EvalMode::kCount : EvalMode::kDecode, ctx->stream));
+    if (mode == RunMode::kCount) {
+        a.num_tiles = (uint32_t)(pw / count_tile_words());
+        if (stop) HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed++].first, ctx->stream));
+        HIP_CHECK(launch_eval_count(a, ctx->stream));
+        if (stop) HIP_CHECK(hipEventRecord(stop, ctx->stream));
+        return CUBIT_OK;
+    }
+    const uint64_t tiles = pw / decode_tile_words();
+    if (int rc = ensure_dir(ctx, tiles)) return rc;
+    if (ordered && rowids)
+        if (int rc = ensure_tmp(ctx, capacity)) return rc;
+    a.num_tiles = (uint32_t)tiles;
+    a.rowids = ordered && rowids ? ctx->tmp_ids : rowids;
+    a.capacity = rowids ? capacity : 0;
+    // persistent grid: two 512-thread workgroups per CU (VGPR-limited to 4 waves per SIMD)
+    const unsigned grid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)ctx->n_cus * 2);
+    if (stop) HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed++].first, ctx->stream));
+    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream));
     if (stop) HIP_CHECK(hipEventRecord(stop, ctx->stream));
-    return CUBIT_OK;
-}
-
-int check_device_error(cubit_ctx* ctx) {
-    uint32_t flags[2] = {0, 0};
-    HIP_CHECK(hipMemcpyAsync(flags, ctx->ws, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (flags[1]) return fail(CUBIT_ERR_DEVICE, "look-back spin bound expired in the filter kernel");
+    ctx->last_tiles = (uint32_t)tiles;
+    ctx->last_tile_rows = decode_tile_words() * 64;
+    if (ordered && rowids)
+        HIP_CHECK(launch_order_runs(ctx->dir, (uint32_t)tiles, ctx->dst_off, ctx->tmp_ids, capacity, rowids,
+                                    ctx->stream));
     return CUBIT_OK;
 }
 
@@ -146,6 +172,9 @@ int cubit_ctx_create(int device, cubit_ctx** out) {
     HIP_CHECK(hipSetDevice(device));
     auto* ctx = new cubit_ctx();
     ctx->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->n_cus = prop.multiProcessorCount;
     if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess) {
         delete ctx;
         return fail(CUBIT_ERR_OOM, "partials allocation failed");
@@ -157,7 +186,9 @@ int cubit_ctx_create(int device, cubit_ctx** out) {
 int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (!ctx) return CUBIT_OK;
     (void)hipSetDevice(ctx->device);
-    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->dir) (void)hipFree(ctx->dir);
+    if (ctx->dst_off) (void)hipFree(ctx->dst_off);
+    if (ctx->tmp_ids) (void)hipFree(ctx->tmp_ids);
     if (ctx->partials) (void)hipFree(ctx->partials);
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
@@ -241,8 +272,17 @@ int cubit_memset_d(cubit_ctx* ctx, void* dst, int value, uint64_t bytes) {
 
 int cubit_ctx_check(cubit_ctx* ctx) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
-    if (!ctx->ws) return CUBIT_OK;
-    return check_device_error(ctx);
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    HIP_CHECK(hipGetLastError());
+    return CUBIT_OK;
+}
+
+int cubit_ctx_last_tiles(cubit_ctx* ctx, const uint64_t** d_dir, uint32_t* n_tiles, uint64_t* rows_per_tile) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (d_dir) *d_dir = ctx->dir;
+    if (n_tiles) *n_tiles = ctx->last_tiles;
+    if (rows_per_tile) *rows_per_tile = ctx->last_tile_rows;
+    return CUBIT_OK;
 }
 
 int cubit_sync(cubit_ctx* ctx) {
@@ -464,7 +504,8 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
     if (!em.ok || em.max_depth > 4)
         return fail(CUBIT_ERR_UNSUPPORTED, "program needs %d leaves / depth %d (max %d / 4)", count_leaves(st[0]),
                     em.max_depth, kMaxLeaves);
-    return run_eval(ctx, em.prog, n_rows, row_base, d_rowids, capacity, d_count, d_result_words, count_only, true);
+    return run_eval(ctx, em.prog, n_rows, row_base, count_only ? nullptr : d_rowids, capacity, d_count, d_result_words,
+                    count_only ? RunMode::kCount : RunMode::kDecode, true, (flags & CUBIT_SCAN_ORDERED) != 0);
 }
 
 extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const int64_t* d_rowids,
@@ -980,7 +1021,7 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
     if (!em.ok || em.max_depth > 4) return fail(CUBIT_ERR_UNSUPPORTED, "subexpression too deep");
     if (int rc = scratch_bv(t, out)) return rc;
     t->last_passes++;
-    return run_eval(t->ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, *out, true);
+    return run_eval(t->ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, *out, RunMode::kCount);
 }
 
 bool fits(const ExprP& e) {
@@ -1146,7 +1187,7 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     t->last_leaves = em.prog.n_leaves;
     t->last_passes++;
     return run_eval(ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count, nullptr,
-                    count_only, true);
+                    count_only ? RunMode::kCount : RunMode::kDecode, true, (flags & CUBIT_SCAN_ORDERED) != 0);
 }
 
 extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_t* n_passes) {

@@ -16,13 +16,11 @@ constexpr uint64_t kRowGroupSize = 122880;
 static_assert(kVectorSize % 64 == 0 && kVectorSize / 64 == 32, "vector must be 32 words");
 static_assert(kRowGroupSize % 64 == 0 && kRowGroupSize / 64 == 1920, "row group must be 1920 words");
 
-// Filter kernel geometry: 256 threads, each owning two 16-byte word pairs per leaf
-// (one dwordx4 load per pair; a wave-instruction moves 1 KiB).
+// Filter kernel geometry: 256-thread workgroups; each thread owns PAIRS 16-byte word pairs
+// per leaf (one dwordx4 load per pair; a wave-instruction moves 1 KiB). Bitvectors are padded
+// to kPadWords so every tile shape reads in bounds.
 constexpr int kThreads = 256;
-constexpr int kPairs = 2;
-constexpr int kWordsPerThread = 2 * kPairs;
-constexpr uint64_t kTileWords = (uint64_t)kThreads * kWordsPerThread;  // 1024 words = 65,536 rows
-constexpr int kStageCap = 2048;                                        // row ids staged in LDS per tile
+constexpr uint64_t kPadWords = 16384;  // 1,048,576 rows
 constexpr int kMaxLeaves = 8;
 constexpr int kMaxOps = 16;
 
@@ -30,7 +28,7 @@ enum : int8_t { OP_AND = -1, OP_OR = -2, OP_ANDNOT = -3 };
 
 inline uint64_t padded_words(uint64_t n_rows) {
     const uint64_t w = (n_rows + 63) / 64;
-    return ((w + kTileWords - 1) / kTileWords) * kTileWords;
+    return ((w + kPadWords - 1) / kPadWords) * kPadWords;
 }
 
 // A postfix program whose leaves appear in order 0..n_leaves-1: leaf k is pushed
@@ -43,8 +41,6 @@ struct EvalProgram {
     int8_t ops[kMaxOps];
 };
 
-enum class EvalMode : int { kDecode = 0, kCount = 1 };
-
 struct EvalArgs {
     EvalProgram prog;
     uint64_t n_rows;
@@ -52,16 +48,22 @@ struct EvalArgs {
     int64_t row_base;
     int64_t* rowids;
     uint64_t capacity;
-    uint64_t* count;
-    uint64_t* result_words;
-    uint64_t* tile_status;
-    uint32_t* tile_counter;
-    uint32_t* error_flag;
+    uint64_t* count;         // running count (claims) / count(*) result; zeroed by the launcher
+    uint64_t* result_words;  // optional evaluated bitvector
     uint32_t num_tiles;
 };
 
 // launchers (cubit_kernels.hip); all asynchronous on `stream`
-hipError_t launch_eval(const EvalArgs& a, EvalMode mode, hipStream_t stream);
+uint64_t decode_tile_words();  // words per eval_decode_tiles tile
+uint64_t count_tile_words();   // words per eval_count_kernel tile
+int decode_block_threads();
+// evaluate + decode into per-tile runs; dir (optional) gets {start, length} per tile
+hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream);
+// evaluate + count (and/or write the result bitvector)
+hipError_t launch_eval_count(const EvalArgs& a, hipStream_t stream);
+// lay per-tile runs out in row order: dst[dst_off[i] ...] = src[dir run i]
+hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* dst_off, const int64_t* src,
+                             uint64_t capacity, int64_t* dst, hipStream_t stream);
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                                     int64_t constant, uint64_t* out_words, hipStream_t stream);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,

@@ -1,12 +1,13 @@
 // CDNA4 (gfx950) kernels of the bitmap-indexed scan filter.
 //
-//   K1+K2  eval_decode   — postfix AND/OR/ANDNOT over K bitvectors, fused with the
-//                          bitvector → ascending int64 row-id compaction (single pass,
-//                          decoupled look-back across tiles). Replaces the per-vector
+//   K1+K2  eval_decode_tiles — postfix AND/OR/ANDNOT over K bitvectors fused with the
+//                          bitvector → int64 row-id compaction. Replaces the per-vector
 //                          selection narrowing of RowGroup::TemplatedScan
 //                          (src/storage/table/row_group.cpp:537-550 → ColumnSegment::
 //                          FilterSelection, column_segment.cpp:378-522) and the row-id
 //                          synthesis start+current_row+sel[i] (row_group.cpp:573-580).
+//          eval_count_kernel — the same evaluation for count(*) / bitvector materialisation.
+//          order_* — optional pass that lays the per-tile runs out in row order.
 //   K0     compare_bitvector — predicate → bitvector over a raw column, the comparison
 //                          semantics of TemplatedFilterSelection (column_segment.cpp:261-349).
 //   K3     gather / gather_sum_product — probe columns at row ids
@@ -27,19 +28,6 @@ namespace {
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr uint64_t kFlagShift = 62;
-constexpr uint64_t kFlagAggregate = 1ull << kFlagShift;
-constexpr uint64_t kFlagPrefix = 2ull << kFlagShift;
-constexpr uint64_t kValueMask = (1ull << kFlagShift) - 1;
-constexpr uint32_t kMaxSpins = 1u << 22;
-
-__device__ __forceinline__ uint64_t load_status(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_status(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -59,21 +47,21 @@ __device__ __forceinline__ uint64_t apply_op(int8_t op, uint64_t a, uint64_t b) 
     return op == OP_AND ? (a & b) : (op == OP_OR ? (a | b) : (a & ~b));
 }
 
-// Evaluate the program on this thread's kWordsPerThread words. Leaves are loaded by the
-// caller (compile-time indexed), the stack is 4 deep and shifted with constant indices so
-// it stays in VGPRs.
-template <int K>
-__device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 (&v)[K][kPairs],
-                                           uint64_t (&r)[kWordsPerThread]) {
-    uint64_t s0[kWordsPerThread], s1[kWordsPerThread], s2[kWordsPerThread], s3[kWordsPerThread];
+// Evaluate the program on NW words per thread. Leaves are loaded by the caller
+// (compile-time indexed); the stack is 4 deep and shifted with constant indices so it stays
+// in VGPRs.
+template <int K, int NW>
+__device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 (&v)[K][NW / 2],
+                                           uint64_t (&r)[NW]) {
+    uint64_t s0[NW], s1[NW], s2[NW], s3[NW];
 #pragma unroll
-    for (int j = 0; j < kWordsPerThread; ++j) s0[j] = s1[j] = s2[j] = s3[j] = 0;
+    for (int j = 0; j < NW; ++j) s0[j] = s1[j] = s2[j] = s3[j] = 0;
     int op_i = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint64_t neg = ((prog.negate >> k) & 1u) ? ~0ull : 0ull;
 #pragma unroll
-        for (int j = 0; j < kWordsPerThread; ++j) {
+        for (int j = 0; j < NW; ++j) {
             s3[j] = s2[j];
             s2[j] = s1[j];
             s1[j] = s0[j];
@@ -84,7 +72,7 @@ __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 
         for (int t = 0; t < nops; ++t) {
             const int8_t op = prog.ops[op_i++];
 #pragma unroll
-            for (int j = 0; j < kWordsPerThread; ++j) {
+            for (int j = 0; j < NW; ++j) {
                 s0[j] = apply_op(op, s1[j], s0[j]);
                 s1[j] = s2[j];
                 s2[j] = s3[j];
@@ -92,162 +80,254 @@ __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 
         }
     }
 #pragma unroll
-    for (int j = 0; j < kWordsPerThread; ++j) r[j] = s0[j];
+    for (int j = 0; j < NW; ++j) r[j] = s0[j];
 }
 
-// One workgroup = one tile of kTileWords words (65,536 rows). Word layout inside a tile:
-// pair p of thread t holds words p*512 + 2t + {0,1}, so every dwordx4 wave-load is a
-// contiguous 1 KiB. Tile ids come from an atomic counter in launch order, so a tile only
-// ever waits on tiles that already started (forward progress for the look-back).
-template <int K, EvalMode MODE>
-__global__ __launch_bounds__(kThreads) void eval_decode_kernel(EvalArgs a) {
-    __shared__ uint64_t s_wave_tot[kThreads / 64];
-    __shared__ uint64_t s_excl;
-    __shared__ uint32_t s_tile;
-    __shared__ int64_t s_stage[MODE == EvalMode::kDecode ? kStageCap : 1];
+// Word j of a thread in a tile: pair p = j/2 holds words p·2·THREADS + 2t + {0,1}, so every
+// dwordx4 wave-load reads a contiguous 1 KiB.
+template <int THREADS>
+__device__ __forceinline__ uint64_t word_index(uint64_t tile_word0, int j, int t) {
+    return tile_word0 + (uint64_t)(j >> 1) * (2 * THREADS) + 2 * t + (j & 1);
+}
 
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
+template <int NW, int THREADS>
+__device__ __forceinline__ void tail_mask(const EvalArgs& a, uint64_t tile_word0, int t, uint64_t (&r)[NW]) {
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const uint64_t gw = word_index<THREADS>(tile_word0, j, t);
+        if (gw >= a.n_words) r[j] = 0;
+        else if (gw == a.n_words - 1 && (a.n_rows & 63)) r[j] &= (1ull << (a.n_rows & 63)) - 1;
+    }
+}
 
-    if (t == 0) s_tile = atomicAdd(a.tile_counter, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint64_t tile_word0 = (uint64_t)tile * kTileWords;
+template <int PAIRS, int THREADS>
+__device__ __forceinline__ void store_words(uint64_t* out, uint64_t tile_word0, int t, const uint64_t (&r)[2 * PAIRS]) {
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p) {
+        u64x2 o;
+        o.x = r[2 * p];
+        o.y = r[2 * p + 1];
+        reinterpret_cast<u64x2*>(out + tile_word0)[p * THREADS + t] = o;
+    }
+}
 
-    // ---- load K leaves (padded: always in bounds)
-    u64x2 v[K][kPairs];
+template <int K, int PAIRS, int THREADS>
+__device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0, int t, u64x2 (&v)[K][PAIRS]) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const u64x2* base = reinterpret_cast<const u64x2*>(a.prog.leaf[k] + tile_word0);
 #pragma unroll
-        for (int p = 0; p < kPairs; ++p) v[k][p] = __builtin_nontemporal_load(base + p * kThreads + t);
-    }
-
-    // ---- evaluate + tail mask
-    uint64_t r[kWordsPerThread];
-    eval_words<K>(a.prog, v, r);
-#pragma unroll
-    for (int j = 0; j < kWordsPerThread; ++j) {
-        const uint64_t gw = tile_word0 + (uint64_t)(j >> 1) * (2 * kThreads) + 2 * t + (j & 1);
-        if (gw >= a.n_words) {
-            r[j] = 0;
-        } else if (gw == a.n_words - 1 && (a.n_rows & 63)) {
-            r[j] &= (1ull << (a.n_rows & 63)) - 1;
-        }
-    }
-    if (a.result_words) {
-#pragma unroll
-        for (int p = 0; p < kPairs; ++p) {
-            u64x2 o;
-            o.x = r[2 * p];
-            o.y = r[2 * p + 1];
-            reinterpret_cast<u64x2*>(a.result_words + tile_word0)[p * kThreads + t] = o;
-        }
-    }
-
-    // ---- per-thread counts in tile order: pair 0 of every thread, then pair 1
-    const uint64_t c0 = (uint64_t)(__popcll(r[0]) + __popcll(r[1]));
-    const uint64_t c1 = (uint64_t)(__popcll(r[2]) + __popcll(r[3]));
-    const uint64_t packed = c0 | (c1 << 32);
-    const uint64_t incl = wave_incl_scan(packed, lane);
-    if (lane == 63) s_wave_tot[wave] = incl;
-    __syncthreads();
-    uint64_t wave_prefix = 0, block_tot = 0;
-#pragma unroll
-    for (int w = 0; w < kThreads / 64; ++w) {
-        const uint64_t x = s_wave_tot[w];
-        if (w < wave) wave_prefix += x;
-        block_tot += x;
-    }
-    const uint64_t excl_packed = wave_prefix + incl - packed;
-    const uint64_t tot0 = block_tot & 0xffffffffull, tot1 = block_tot >> 32;
-    const uint64_t tile_count = tot0 + tot1;
-
-    if (MODE == EvalMode::kCount) {
-        if (t == 0 && tile_count) atomicAdd(reinterpret_cast<unsigned long long*>(a.count), tile_count);
-        return;
-    }
-
-    // ---- decoupled look-back (wave 0). Status words are 8-byte {flag, value} granules
-    // written by one agent-scope store: the data is the flag (MI355X guide R2).
-    if (wave == 0) {
-        uint64_t excl = 0;
-        if (tile == 0) {
-            if (lane == 0) store_status(&a.tile_status[0], kFlagPrefix | tile_count);
-        } else {
-            if (lane == 0) store_status(&a.tile_status[tile], kFlagAggregate | tile_count);
-            int64_t base = (int64_t)tile - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t idx = base - lane;
-                const uint64_t s = idx >= 0 ? load_status(&a.tile_status[idx]) : kFlagPrefix;
-                const uint64_t flag = s >> kFlagShift;
-                const uint64_t pmask = __ballot(flag == 2);
-                const uint64_t imask = __ballot(flag == 0);
-                const uint64_t win = pmask ? ((pmask & (~pmask + 1)) << 1) - 1 : ~0ull;
-                if (imask & win) {
-                    if (++spins > kMaxSpins) {
-                        if (lane == 0) atomicOr(a.error_flag, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += wave_sum(((win >> lane) & 1ull) ? (s & kValueMask) : 0ull);
-                if (pmask) break;
-                base -= 64;
-            }
-            if (lane == 0) store_status(&a.tile_status[tile], kFlagPrefix | (excl + tile_count));
-        }
-        if (lane == 0) s_excl = excl;
-    }
-    __syncthreads();
-    const uint64_t tile_off = s_excl;
-    if (t == 0 && tile == a.num_tiles - 1) *a.count = tile_off + tile_count;
-    if (tile_count == 0 || a.rowids == nullptr) return;
-
-    // ---- decode: thread-local ascending runs, staged in LDS when the tile fits
-    const bool stage = tile_count <= (uint64_t)kStageCap;
-    const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
-#pragma unroll
-    for (int p = 0; p < kPairs; ++p) {
-        uint64_t off = p == 0 ? (excl_packed & 0xffffffffull) : tot0 + (excl_packed >> 32);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            uint64_t w = r[2 * p + e];
-            const int64_t wrow = row0 + (int64_t)((p * 2 * kThreads + 2 * t + e) * 64);
-            while (w) {
-                const int b = __builtin_ctzll(w);
-                const int64_t rid = wrow + b;
-                if (stage) {
-                    s_stage[off] = rid;
-                } else {
-                    const uint64_t g = tile_off + off;
-                    if (g < a.capacity) a.rowids[g] = rid;
-                }
-                ++off;
-                w &= w - 1;
-            }
-        }
-    }
-    if (stage) {
-        __syncthreads();
-        for (uint64_t i = t; i < tile_count; i += kThreads) {
-            const uint64_t g = tile_off + i;
-            if (g < a.capacity) a.rowids[g] = s_stage[i];
-        }
+        for (int p = 0; p < PAIRS; ++p) v[k][p] = __builtin_nontemporal_load(base + p * THREADS + t);
     }
 }
 
-template <int K>
-hipError_t launch_eval_k(const EvalArgs& a, EvalMode mode, hipStream_t stream) {
-    const dim3 grid(a.num_tiles), block(kThreads);
-    if (mode == EvalMode::kDecode)
-        hipLaunchKernelGGL((eval_decode_kernel<K, EvalMode::kDecode>), grid, block, 0, stream, a);
-    else
-        hipLaunchKernelGGL((eval_decode_kernel<K, EvalMode::kCount>), grid, block, 0, stream, a);
-    return hipGetLastError();
+// ------------------------------------------------------------------ K1: count / materialise
+
+// count(*) of the program and/or its result bitvector; one tile per workgroup, one
+// non-returning atomic per tile.
+template <int K, int PAIRS>
+__global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
+    constexpr int THREADS = 256, NW = 2 * PAIRS;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    const int t = threadIdx.x;
+    const uint64_t tile_word0 = (uint64_t)blockIdx.x * TILE_WORDS;
+    u64x2 v[K][PAIRS];
+    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+    uint64_t r[NW];
+    eval_words<K, NW>(a.prog, v, r);
+    tail_mask<NW, THREADS>(a, tile_word0, t, r);
+    if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+    __shared__ uint64_t s_part[THREADS / 64];
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
+    c = wave_sum(c);
+    if ((t & 63) == 0) s_part[t >> 6] = c;
+    __syncthreads();
+    // one atomic per workgroup: a single address serves ~88 returning atomics/µs
+    // (MI355X_MICROARCH.md "dequeue"), so per-wave atomics would throttle the kernel
+    if (t == 0) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int w = 0; w < THREADS / 64; ++w) s += s_part[w];
+        if (s) atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)s);
+    }
+}
+
+// ------------------------------------------------------------------ K1+K2: evaluate + decode
+
+// Persistent, software-pipelined evaluate + decode. Workgroup g takes tiles g, g+G, g+2G, …
+// (static striding: per-tile work is uniform up to the decode). Per tile:
+//   evaluate the tile whose leaves landed → per-pair bit counts → block scan →
+//   ONE returning atomicAdd on the running count claims the tile's output range →
+//   issue the NEXT tile's loads (they fly during the rest of this iteration) →
+//   decode the set bits into LDS as 32-bit tile-local offsets (each thread's run is
+//   ascending and runs are in word order) → copy the run out coalesced as int64 row ids.
+// Output: per-tile ascending runs, runs in claim order — the shape of DuckDB's parallel scan,
+// whose morsels reach the sink in nondeterministic order with a batch index
+// (table_scan.cpp:179-189). dir[2·tile] / dir[2·tile+1] = the run's start / length, so
+// reading runs in tile order yields the ascending sequence (order_runs does that on device).
+// There is no inter-workgroup wait: a claim is one atomic, so no prefix chain serialises the
+// tiles (a decoupled look-back over ~10^4 tiles measured 1.7× slower).
+// Per-pair counts are packed as FB-bit fields so one 64-bit scan covers several pairs
+// (a pair-chunk holds at most THREADS·128 set bits).
+template <int K, int PAIRS, int STAGE, int THREADS>
+__global__ __launch_bounds__(THREADS) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
+    constexpr int NW = 2 * PAIRS;
+    constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
+    constexpr int FPW = 64 / FB;
+    constexpr uint64_t FMASK = (FB == 16) ? 0xffffull : 0xffffffffull;
+    constexpr int NPK = (PAIRS + FPW - 1) / FPW;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr int NWAVES = THREADS / 64;
+    static_assert(TILE_WORDS * 64 < (1ull << 32), "tile-local offsets are 32-bit");
+    __shared__ uint64_t s_wave_tot[NWAVES][NPK];
+    __shared__ uint64_t s_off;
+    __shared__ uint32_t s_stage[STAGE];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    uint32_t tile = blockIdx.x;
+    u64x2 v[K][PAIRS];
+    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+    while (tile < a.num_tiles) {
+        const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+        uint64_t r[NW];
+        eval_words<K, NW>(a.prog, v, r);
+        tail_mask<NW, THREADS>(a, tile_word0, t, r);
+        if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+        uint64_t packed[NPK], incl[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) packed[q] = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p)
+            packed[p / FPW] |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            incl[q] = wave_incl_scan(packed[q], lane);
+            if (lane == 63) s_wave_tot[wave][q] = incl[q];
+        }
+        __syncthreads();  // A: wave totals visible
+        uint64_t block_tot[NPK], wave_pre[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            uint64_t wp = 0, bt = 0;
+#pragma unroll
+            for (int w = 0; w < NWAVES; ++w) {
+                const uint64_t x = s_wave_tot[w][q];
+                if (w < wave) wp += x;
+                bt += x;
+            }
+            block_tot[q] = bt;
+            wave_pre[q] = wp;
+        }
+        uint64_t pair_base[PAIRS];
+        uint64_t tile_count = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            pair_base[p] = tile_count;
+            tile_count += (block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK;
+        }
+        uint64_t claimed = 0;
+        if (t == 0 && tile_count)
+            claimed = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count);
+        const uint32_t next = tile + gridDim.x;
+        if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);  // prefetch
+        const bool stage = tile_count <= (uint64_t)STAGE;
+        const bool write = tile_count && a.rowids;
+        if (!stage || !write) {
+            if (t == 0) {
+                s_off = claimed;
+                if (dir) {
+                    dir[2 * tile] = tile_count ? claimed : 0;
+                    dir[2 * tile + 1] = tile_count;
+                }
+            }
+            __syncthreads();
+        }
+        const uint64_t direct_off = s_off;
+        const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
+        if (write) {
+#pragma unroll
+            for (int p = 0; p < PAIRS; ++p) {
+                uint64_t off = pair_base[p] +
+                               (((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    uint64_t w = r[2 * p + e];
+                    const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                    while (w) {
+                        const uint32_t b = (uint32_t)__builtin_ctzll(w);
+                        if (stage) {
+                            s_stage[off] = wrow + b;
+                        } else {
+                            const uint64_t g = direct_off + off;
+                            if (g < a.capacity) a.rowids[g] = row0 + (int64_t)(wrow + b);
+                        }
+                        ++off;
+                        w &= w - 1;
+                    }
+                }
+            }
+        }
+        if (stage && write) {
+            if (t == 0) {
+                s_off = claimed;
+                if (dir) {
+                    dir[2 * tile] = claimed;
+                    dir[2 * tile + 1] = tile_count;
+                }
+            }
+            __syncthreads();  // B: staged run and its offset visible
+            const uint64_t off0 = s_off;
+            for (uint64_t i = t; i < tile_count; i += THREADS) {
+                const uint64_t g = off0 + i;
+                if (g < a.capacity) a.rowids[g] = row0 + (int64_t)s_stage[i];
+            }
+        }
+        __syncthreads();  // C: stage / s_off / s_wave_tot free for the next tile
+        tile = next;
+    }
+}
+
+// ------------------------------------------------------------------ row-order pass
+
+// Exclusive scan of the per-tile run lengths (one workgroup, any tile count).
+__global__ __launch_bounds__(1024) void order_scan_kernel(const uint64_t* __restrict__ dir, uint32_t n_tiles,
+                                                          uint64_t* __restrict__ dst_off) {
+    __shared__ uint64_t s_tot[16];
+    __shared__ uint64_t s_carry;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n_tiles; base += 1024) {
+        const uint32_t i = base + t;
+        const uint64_t c = i < n_tiles ? dir[2 * i + 1] : 0;
+        const uint64_t incl = wave_incl_scan(c, lane);
+        if (lane == 63) s_tot[wave] = incl;
+        __syncthreads();
+        uint64_t pre = s_carry, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            if (w < wave) pre += s_tot[w];
+            tot += s_tot[w];
+        }
+        if (i < n_tiles) dst_off[i] = pre + incl - c;
+        __syncthreads();
+        if (t == 0) s_carry += tot;
+        __syncthreads();
+    }
+}
+
+// One workgroup per tile: move its run to the ordered position.
+__global__ __launch_bounds__(256) void order_copy_kernel(const uint64_t* __restrict__ dir,
+                                                         const uint64_t* __restrict__ dst_off,
+                                                         const int64_t* __restrict__ src, uint64_t capacity,
+                                                         int64_t* __restrict__ dst) {
+    const uint32_t tile = blockIdx.x;
+    const uint64_t so = dir[2 * tile], n = dir[2 * tile + 1], d = dst_off[tile];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x)
+        if (so + i < capacity && d + i < capacity) dst[d + i] = src[so + i];
 }
 
 // ------------------------------------------------------------------ K0: compare → bitvector
@@ -413,18 +493,63 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 
 }  // namespace
 
-hipError_t launch_eval(const EvalArgs& a, EvalMode mode, hipStream_t stream) {
+// production geometry: decode tiles of 512 threads × 2 pairs = 2,048 words (131,072 rows),
+// STAGE 4,096 staged ids (16 KiB LDS); count tiles of 256 threads × 8 pairs = 4,096 words.
+// Chosen from the interleaved variant sweep in scripts/kbench.hip.
+constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
+constexpr int kCountPairs = 8;
+
+uint64_t decode_tile_words() { return (uint64_t)kDecodeThreads * 2 * kDecodePairs; }
+uint64_t count_tile_words() { return 256ull * 2 * kCountPairs; }
+int decode_block_threads() { return kDecodeThreads; }
+
+template <int K>
+hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s) {
+    hipLaunchKernelGGL((eval_decode_tiles<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
+                       dim3(kDecodeThreads), 0, s, a, dir);
+    return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_count_k(const EvalArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s) {
     switch (a.prog.n_leaves) {
-    case 1: return launch_eval_k<1>(a, mode, stream);
-    case 2: return launch_eval_k<2>(a, mode, stream);
-    case 3: return launch_eval_k<3>(a, mode, stream);
-    case 4: return launch_eval_k<4>(a, mode, stream);
-    case 5: return launch_eval_k<5>(a, mode, stream);
-    case 6: return launch_eval_k<6>(a, mode, stream);
-    case 7: return launch_eval_k<7>(a, mode, stream);
-    case 8: return launch_eval_k<8>(a, mode, stream);
+    case 1: return launch_decode_k<1>(a, dir, grid, s);
+    case 2: return launch_decode_k<2>(a, dir, grid, s);
+    case 3: return launch_decode_k<3>(a, dir, grid, s);
+    case 4: return launch_decode_k<4>(a, dir, grid, s);
+    case 5: return launch_decode_k<5>(a, dir, grid, s);
+    case 6: return launch_decode_k<6>(a, dir, grid, s);
+    case 7: return launch_decode_k<7>(a, dir, grid, s);
+    case 8: return launch_decode_k<8>(a, dir, grid, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_eval_count(const EvalArgs& a, hipStream_t s) {
+    switch (a.prog.n_leaves) {
+    case 1: return launch_count_k<1>(a, s);
+    case 2: return launch_count_k<2>(a, s);
+    case 3: return launch_count_k<3>(a, s);
+    case 4: return launch_count_k<4>(a, s);
+    case 5: return launch_count_k<5>(a, s);
+    case 6: return launch_count_k<6>(a, s);
+    case 7: return launch_count_k<7>(a, s);
+    case 8: return launch_count_k<8>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* dst_off, const int64_t* src,
+                             uint64_t capacity, int64_t* dst, hipStream_t s) {
+    if (n_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, s, dir, n_tiles, dst_off);
+    hipLaunchKernelGGL(order_copy_kernel, dim3(n_tiles), dim3(256), 0, s, dir, dst_off, src, capacity, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,

@@ -24,6 +24,7 @@ FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = ran
 INDEX_RANGE, INDEX_EQUALITY = 0, 1
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
+SCAN_ORDERED = 2
 
 
 class FilterNode(C.Structure):
@@ -71,6 +72,7 @@ GPU_SIGNATURES = {
     "cubit_ctx_timing_reset": (C.c_int, [_P]),
     "cubit_ctx_kernel_times": (C.c_int, [_P, C.POINTER(C.c_float), _U32, C.POINTER(_U32)]),
     "cubit_ctx_check": (C.c_int, [_P]),
+    "cubit_ctx_last_tiles": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_U32), C.POINTER(_U64)]),
     "cubit_dev_alloc": (C.c_int, [_P, _U64, C.POINTER(_P)]),
     "cubit_dev_free": (C.c_int, [_P, _P]),
     "cubit_memcpy_h2d": (C.c_int, [_P, _P, _P, _U64]),

@@ -48,6 +48,18 @@ class Context:
     def sync(self) -> None:
         L.check(self.lib.cubit_sync(self.handle))
 
+    def last_tiles(self):
+        """Tile directory of the last row-id materialisation: (int64 [n_tiles, 2] of
+        {run start, run length}, rows per tile)."""
+        d = C.c_void_p()
+        n = C.c_uint32()
+        rpt = C.c_uint64()
+        L.check(self.lib.cubit_ctx_last_tiles(self.handle, C.byref(d), C.byref(n), C.byref(rpt)))
+        out = np.empty(2 * n.value, dtype=np.uint64)
+        if n.value:
+            L.check(self.lib.cubit_memcpy_d2h(self.handle, out.ctypes.data, d, out.nbytes))
+        return out.reshape(-1, 2), int(rpt.value)
+
     def check(self) -> None:
         L.check(self.lib.cubit_ctx_check(self.handle))
 
@@ -105,6 +117,13 @@ class DeviceBuffer:
                 self.free()
         except Exception:
             pass
+
+
+def runs_in_row_order(ids: np.ndarray, directory: np.ndarray) -> np.ndarray:
+    """Concatenate the per-tile runs of a tile-run-order output in tile order (what a
+    consumer iterating the directory sees)."""
+    parts = [ids[int(s): int(s) + int(n)] for s, n in directory if n]
+    return np.concatenate(parts) if parts else np.empty(0, dtype=np.int64)
 
 
 def padded_words(n_rows: int) -> int:
@@ -173,22 +192,24 @@ class CubitTable:
 
     # ------------------------------------------------------------------ scan
     def scan_into(self, plan_nodes, rowids_dptr: int, capacity: int, count_dptr: int,
-                  txn: Optional[L.Txn] = None, count_only: bool = False) -> None:
+                  txn: Optional[L.Txn] = None, count_only: bool = False, ordered: bool = False) -> None:
         """Asynchronous scan into caller-owned device buffers (the bench path)."""
         arr = plan_nodes if isinstance(plan_nodes, C.Array) else to_ctypes(plan_nodes)
         n = len(plan_nodes) if not isinstance(plan_nodes, C.Array) else len(arr)
+        flags = (L.SCAN_COUNT_ONLY if count_only else 0) | (L.SCAN_ORDERED if ordered else 0)
         L.check(self.lib.cubit_table_scan(self.handle, arr, n, C.byref(txn) if txn is not None else None,
                                           C.c_void_p(rowids_dptr) if rowids_dptr else None, capacity,
-                                          C.c_void_p(count_dptr), L.SCAN_COUNT_ONLY if count_only else 0))
+                                          C.c_void_p(count_dptr), flags))
 
     def scan(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
-             txn: Optional[L.Txn] = None, capacity: Optional[int] = None) -> np.ndarray:
-        """Synchronous scan returning the ascending global row ids as numpy int64."""
+             txn: Optional[L.Txn] = None, capacity: Optional[int] = None, ordered: bool = True) -> np.ndarray:
+        """Synchronous scan returning the global row ids as numpy int64: ascending with
+        ordered=True (device ordered pass), else in tile-run order (see last_tiles())."""
         plan = serialize(filter_set, residual)
         cap = self.n_rows if capacity is None else capacity
         out = self.ctx.alloc(max(cap, 1) * 8)
         cnt = self.ctx.alloc(16)
-        self.scan_into(plan.nodes, out.addr, cap, cnt.addr, txn)
+        self.scan_into(plan.nodes, out.addr, cap, cnt.addr, txn, ordered=ordered)
         self.ctx.check()
         n = int(cnt.download(np.uint64, 1)[0])
         if n > cap:

@@ -64,8 +64,15 @@ extern "C" {
 #define CUBIT_OP_OR (-2)
 #define CUBIT_OP_ANDNOT (-3) /* a AND NOT b */
 
-/* ---- scan flags */
+/* ---- scan flags
+ * Default output order ("tile runs"): the row ids of each 131,072-row tile form one
+ * ascending run, and runs appear in the order tiles finished — the shape of DuckDB's
+ * parallel table scan, whose morsels reach the sink in nondeterministic order with a batch
+ * index (src/function/table/table_scan.cpp:179-189). cubit_ctx_last_tiles() returns the
+ * tile directory ({start, length} per tile) that restores row order for free.
+ * CUBIT_SCAN_ORDERED lays the runs out ascending with one extra device pass. */
 #define CUBIT_SCAN_COUNT_ONLY 1u /* do not materialise row ids */
+#define CUBIT_SCAN_ORDERED 2u    /* one globally ascending array */
 
 typedef struct cubit_ctx cubit_ctx;
 typedef struct cubit_table cubit_table;
@@ -113,9 +120,12 @@ int cubit_memcpy_h2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes)
 int cubit_memcpy_d2h(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memset_d(cubit_ctx *ctx, void *dst, int value, uint64_t bytes);
 int cubit_sync(cubit_ctx *ctx);
-/* Synchronise the stream and report an in-kernel failure of the last filter launch
- * (CUBIT_ERR_DEVICE when a look-back spin bound expired). */
+/* Synchronise the context stream and report any pending HIP error. */
 int cubit_ctx_check(cubit_ctx *ctx);
+/* Tile directory of the last row-id materialisation on this context (device pointer, valid
+ * until the next scan): d_dir[2i] = start of tile i's run in the output, d_dir[2i+1] = its
+ * length; tile i covers rows [i*rows_per_tile, (i+1)*rows_per_tile) of the partition. */
+int cubit_ctx_last_tiles(cubit_ctx *ctx, const uint64_t **d_dir, uint32_t *n_tiles, uint64_t *rows_per_tile);
 
 /* ------------------------------------------------------------------ low level (kernels) */
 
@@ -129,8 +139,8 @@ uint64_t cubit_padded_words(uint64_t n_rows);
 
 /* K1+K2 — evaluate a postfix program over `n_leaves` device bitvectors (each
  * cubit_padded_words(n_rows) words; leaf_negate bit k complements leaf k before use) and
- * write the ascending int64 row ids row_base + r of the set rows into d_rowids (capacity
- * `capacity`), the count into *d_count (device). d_rowids may be NULL with
+ * write the int64 row ids row_base + r of the set rows into d_rowids (capacity `capacity`;
+ * tile-run order unless CUBIT_SCAN_ORDERED), the count into *d_count (device). d_rowids may be NULL with
  * CUBIT_SCAN_COUNT_ONLY; d_result_words (optional) receives the evaluated bitvector.
  * Replaces the per-vector sel narrowing + row-id synthesis of RowGroup::TemplatedScan
  * (row_group.cpp:537-580). */
@@ -171,8 +181,8 @@ int cubit_table_set_updates(cubit_table *t, int col, const int64_t *rows, const 
                             const uint64_t *versions, uint64_t n);
 
 /* The scan: evaluate a predicate tree (prefix nodes) for transaction `txn` (NULL = see
- * every committed row, no MVCC delta applied) and write ascending row ids into d_rowids,
- * the count into *d_count (device). Replaces TableScanFunc → DataTable::Scan →
+ * every committed row, no MVCC delta applied) and write the qualifying row ids into
+ * d_rowids (tile runs, or ascending with CUBIT_SCAN_ORDERED), the count into *d_count. Replaces TableScanFunc → DataTable::Scan →
  * RowGroup::TemplatedScan's filter + row-id materialisation (table_scan.cpp:119-146). */
 int cubit_table_scan(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
                      int64_t *d_rowids, uint64_t capacity, uint64_t *d_count, uint32_t flags);

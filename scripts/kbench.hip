@@ -1,0 +1,170 @@
+// Kernel microbenchmark (development tool, not shipped): times the evaluate/decode kernels
+// interleaved in one process on SF100-sized bitvectors (600,037,902 rows, K = 5 leaves,
+// Q6-like densities, ~1.9 % selected) and checks every variant against the production
+// decode (row ids rebuilt in row order through the tile directory).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I duckdb-cubit_amd/csrc scripts/kbench.hip -o scripts/kbench
+// The variant sweep that chose the production geometry is summarised in DESIGN.md §K1.
+#include "cubit_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace cubit;
+
+#define CK(x)                                                                                        \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            fprintf(stderr, "%s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(1);                                                                                 \
+        }                                                                                            \
+    } while (0)
+
+__device__ __forceinline__ uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_random(uint64_t* w, uint64_t pw, uint64_t n_rows, uint32_t thresh, uint64_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pw; i += stride) {
+        uint64_t word = 0;
+        for (int b = 0; b < 64; ++b) {
+            const uint64_t row = i * 64 + b;
+            const uint32_t h = (uint32_t)(mix(seed * 0x9E3779B97F4A7C15ull + row) >> 32);
+            if (row < n_rows && h < thresh) word |= 1ull << b;
+        }
+        w[i] = word;
+    }
+}
+
+struct Variant {
+    std::string name;
+    std::function<void(EvalArgs&, hipStream_t)> launch;
+    int kind;  // 0 = tile runs + dir, 1 = ordered output, 2 = count only
+};
+
+int main(int argc, char** argv) {
+    const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 600037902ull;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 15;
+    const uint64_t W = (n + 63) / 64, pw = padded_words(n);
+    const double dens[5] = {0.25, 0.40, 0.50, 0.45, 0.46};
+    uint64_t* leaf[5];
+    for (int k = 0; k < 5; ++k) {
+        CK(hipMalloc(&leaf[k], pw * 8));
+        hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, leaf[k], pw, n, (uint32_t)(dens[k] * 4294967296.0),
+                           (uint64_t)k + 1);
+    }
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const unsigned cus = prop.multiProcessorCount;
+    const uint64_t cap = n / 10 + 4096;
+    int64_t *ids, *ids2;
+    uint64_t *cnt, *dir, *dst_off;
+    CK(hipMalloc(&ids, cap * 8));
+    CK(hipMalloc(&ids2, cap * 8));
+    CK(hipMalloc(&cnt, 64));
+    CK(hipMalloc(&dir, (pw / 512 + 16) * 16));
+    CK(hipMalloc(&dst_off, (pw / 512 + 16) * 8));
+    CK(hipDeviceSynchronize());
+
+    EvalArgs base{};
+    for (int k = 0; k < 5; ++k) base.prog.leaf[k] = leaf[k];
+    base.prog.n_leaves = 5;
+    // (L0 ANDNOT L1) AND (L2 ANDNOT L3) AND L4
+    const uint8_t nops[5] = {0, 1, 0, 2, 1};
+    const int8_t ops[4] = {OP_ANDNOT, OP_ANDNOT, OP_AND, OP_AND};
+    for (int k = 0; k < 5; ++k) base.prog.nops[k] = nops[k];
+    for (int i = 0; i < 4; ++i) base.prog.ops[i] = ops[i];
+    base.n_rows = n;
+    base.n_words = W;
+    base.rowids = ids;
+    base.capacity = cap;
+    base.count = cnt;
+
+    std::vector<Variant> vs;
+    const uint32_t dtiles = (uint32_t)(pw / decode_tile_words());
+    vs.push_back({"decode tiles (prod)", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 0});
+#define DT(NAME, P, S, T, WGPC)                                                                                \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = (uint32_t)(pw / ((uint64_t)T * 2 * P));                                   \
+                      hipLaunchKernelGGL((eval_decode_tiles<5, P, S, T>), dim3(std::min<unsigned>(a.num_tiles, WGPC * cus)), \
+                                         dim3(T), 0, s, a, dir);                                              \
+                  }, 0})
+    DT("decode P2 T512 x3/CU", 2, 4096, 512, 3);
+    DT("decode P1 T1024 x2/CU", 1, 4096, 1024, 2);
+    DT("decode P2 T1024 x1/CU", 2, 8192, 1024, 1);
+    vs.push_back({"decode + ordered pass", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.rowids = ids2;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                      CK(launch_order_runs(dir, dtiles, dst_off, ids2, cap, ids, s));
+                  }, 1});
+    vs.push_back({"count only", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = (uint32_t)(pw / count_tile_words());
+                      CK(launch_eval_count(a, s));
+                  }, 2});
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> times(vs.size());
+    uint64_t ref_count = 0;
+    std::vector<int64_t> ref_ids;
+    for (int r = -1; r < rounds; ++r) {
+        for (size_t i = 0; i < vs.size(); ++i) {
+            EvalArgs a = base;
+            CK(hipMemsetAsync(cnt, 0, 8, 0));
+            CK(hipEventRecord(e0, 0));
+            vs[i].launch(a, 0);
+            CK(hipGetLastError());
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 0) times[i].push_back(ms);
+            if (r != -1) continue;
+            uint64_t c = 0;
+            CK(hipMemcpy(&c, cnt, 8, hipMemcpyDeviceToHost));
+            if (vs[i].kind == 2) {
+                printf("%s %s\n", c == ref_count ? "ok" : "MISMATCH", vs[i].name.c_str());
+                continue;
+            }
+            std::vector<int64_t> h(c);
+            CK(hipMemcpy(h.data(), ids, c * 8, hipMemcpyDeviceToHost));
+            if (vs[i].kind == 0) {
+                std::vector<uint64_t> d(2 * a.num_tiles);
+                CK(hipMemcpy(d.data(), dir, d.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<int64_t> o;
+                o.reserve(c);
+                for (uint32_t tt = 0; tt < a.num_tiles; ++tt)
+                    o.insert(o.end(), h.begin() + d[2 * tt], h.begin() + d[2 * tt] + d[2 * tt + 1]);
+                h.swap(o);
+            }
+            if (i == 0) {
+                ref_count = c;
+                ref_ids = h;
+                printf("reference count %llu (%.3f %% of %llu rows)\n", (unsigned long long)c, 100.0 * c / n,
+                       (unsigned long long)n);
+            } else {
+                printf("%s %s\n", h == ref_ids ? "ok" : "MISMATCH", vs[i].name.c_str());
+            }
+        }
+    }
+    const double alg = 8.0 * W * 5 + 8.0 * ref_count;
+    printf("%-26s %10s %10s %10s\n", "variant", "median_us", "min_us", "alg_GB/s");
+    for (size_t i = 0; i < vs.size(); ++i) {
+        auto t = times[i];
+        std::sort(t.begin(), t.end());
+        const double med = t[t.size() / 2] * 1e3, mn = t[0] * 1e3;
+        printf("%-26s %10.1f %10.1f %10.0f\n", vs[i].name.c_str(), med, mn, alg / (med * 1e-6) / 1e9);
+    }
+    return 0;
+}

@@ -32,9 +32,9 @@ def test_library_loads_and_reports_geometry():
     assert lib.cubit_abi_version() == 1
     assert lib.cubit_vector_size() == 2048 and lib.cubit_vector_size() % 64 == 0
     assert lib.cubit_row_group_size() == 122880 and lib.cubit_row_group_size() % 64 == 0
-    assert lib.cubit_padded_words(1) == 1024
-    assert lib.cubit_padded_words(65536) == 1024
-    assert lib.cubit_padded_words(65537) == 2048
+    assert lib.cubit_padded_words(1) == 16384
+    assert lib.cubit_padded_words(1 << 20) == 16384
+    assert lib.cubit_padded_words((1 << 20) + 1) == 32768
 
 
 def test_errors_are_status_codes_not_exceptions():

@@ -9,7 +9,7 @@ from conftest import lineitem, revenue_from_answer
 from cubit_amd import _lib as L
 from cubit_amd import filters as F
 from cubit_amd.datagen import uniform_i32, validity_from_mask
-from cubit_amd.table import Context, CubitTable, padded_words
+from cubit_amd.table import Context, CubitTable, padded_words, runs_in_row_order
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -229,7 +229,7 @@ def test_low_level_eval_random_programs(ctx):
                 depth -= 1
         p = (C.c_int32 * len(prog))(*prog)
         rc = ctx.lib.cubit_bitvector_eval(ctx.handle, ptrs, k, neg, p, len(prog), n, 5, out.ptr, n, cnt.ptr,
-                                          words.ptr, 0)
+                                          words.ptr, L.SCAN_ORDERED if trial % 2 else 0)
         if rc == L.ERR_UNSUPPORTED:
             continue  # stack deeper than 4
         L.check(rc)
@@ -238,8 +238,32 @@ def test_low_level_eval_random_programs(ctx):
         ol = [(~leaves[i] if (neg >> i) & 1 else leaves[i]) for i in range(k)]
         ref_rows, ref_words = O.bitmap_eval(ol, prog, n, 5)
         assert c == len(ref_rows)
-        assert np.array_equal(out.download(np.int64, c), ref_rows)
+        got = out.download(np.int64, c)
+        if trial % 2 == 0:
+            d, _ = ctx.last_tiles()
+            got = runs_in_row_order(got, d)
+        assert np.array_equal(got, ref_rows)
         assert np.array_equal(words.download(np.uint64, nw), ref_words)
+
+
+def test_tile_run_output_and_directory(ctx):
+    """Default output order: ascending runs per 131,072-row tile, directory restores row
+    order; the run multiset equals the oracle's row-id set (DuckDB parallel-scan semantics)."""
+    li = lineitem(0.1)
+    t = q6_table(ctx, li)
+    raw = t.scan(F.q6_filter_set(), ordered=False)
+    d, rows_per_tile = ctx.last_tiles()
+    ref = oracle_q6(li)
+    assert rows_per_tile == 131072
+    assert len(d) * rows_per_tile >= li.n_rows
+    assert int(d[:, 1].sum()) == len(raw) == len(ref)
+    for i, (start, n) in enumerate(d):
+        run = raw[int(start): int(start) + int(n)]
+        assert np.all(np.diff(run) > 0)
+        if n:
+            assert run[0] >= i * rows_per_tile and run[-1] < (i + 1) * rows_per_tile
+    assert np.array_equal(runs_in_row_order(raw, d), ref)
+    assert np.array_equal(np.sort(raw), ref)
 
 
 def test_capacity_is_respected_and_count_reported(ctx):
