@@ -416,16 +416,16 @@ struct Emitter {
         const uint32_t k = prog.n_leaves++;
         prog.leaf[k] = l.bv;
         if (neg) prog.negate |= 1u << k;
-        prog.nops[k] = 0;
         max_depth = std::max(max_depth, ++depth);
     }
-    void op(int8_t o) {
-        if (prog.n_leaves == 0 || n_ops >= kMaxOps) {
+    void op(uint32_t o) {
+        const uint32_t k = prog.n_leaves - 1;
+        if (prog.n_leaves == 0 || n_ops >= kMaxOps || prog_nops(prog, (int)k) == 15) {
             ok = false;
             return;
         }
-        prog.ops[n_ops++] = o;
-        prog.nops[prog.n_leaves - 1]++;
+        prog.ops |= o << (2 * n_ops++);
+        prog.nops += 1u << (4 * k);
         --depth;
     }
     void emit(const ExprP& e) {
@@ -433,7 +433,7 @@ struct Emitter {
         case Expr::LEAF: leaf(e->leaf, e->neg); return;
         case Expr::AND:
         case Expr::OR: {
-            const int8_t o = e->kind == Expr::AND ? OP_AND : OP_OR;
+            const uint32_t o = e->kind == Expr::AND ? OP_AND : OP_OR;
             if (need(e->b) > need(e->a)) {
                 emit(e->b);
                 emit(e->a);

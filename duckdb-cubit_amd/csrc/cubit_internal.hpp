@@ -22,24 +22,29 @@ static_assert(kRowGroupSize % 64 == 0 && kRowGroupSize / 64 == 1920, "row group 
 constexpr int kThreads = 256;
 constexpr uint64_t kPadWords = 16384;  // 1,048,576 rows
 constexpr int kMaxLeaves = 8;
-constexpr int kMaxOps = 16;
+constexpr int kMaxOps = 16;  // 2 bits each in EvalProgram::ops
 
-enum : int8_t { OP_AND = -1, OP_OR = -2, OP_ANDNOT = -3 };
+enum : uint32_t { OP_AND = 1, OP_OR = 2, OP_ANDNOT = 3 };
+
+// A postfix program whose leaves appear in order 0..n_leaves-1: leaf k is pushed
+// (complemented if bit k of `negate`), then nops(k) binary ops are applied. The op counts
+// (4 bits per leaf) and opcodes (2 bits per op) are packed into words so the kernel decodes
+// them with scalar shifts (a runtime-indexed byte array in the kernel arguments compiles to
+// vector loads, each followed by an s_waitcnt vmcnt(0) that drains every outstanding load).
+struct EvalProgram {
+    const uint64_t* leaf[kMaxLeaves];
+    uint32_t negate;
+    uint32_t n_leaves;
+    uint32_t nops;  // 4 bits per leaf
+    uint32_t ops;   // 2 bits per op
+};
+
+inline uint32_t prog_nops(const EvalProgram& p, int k) { return (p.nops >> (4 * k)) & 15u; }
 
 inline uint64_t padded_words(uint64_t n_rows) {
     const uint64_t w = (n_rows + 63) / 64;
     return ((w + kPadWords - 1) / kPadWords) * kPadWords;
 }
-
-// A postfix program whose leaves appear in order 0..n_leaves-1: leaf k is pushed
-// (complemented if bit k of `negate`), then nops[k] binary ops from `ops` are applied.
-struct EvalProgram {
-    const uint64_t* leaf[kMaxLeaves];
-    uint32_t negate;
-    uint32_t n_leaves;
-    uint8_t nops[kMaxLeaves];
-    int8_t ops[kMaxOps];
-};
 
 struct EvalArgs {
     EvalProgram prog;

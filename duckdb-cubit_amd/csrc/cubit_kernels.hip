@@ -43,7 +43,7 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint64_t apply_op(int8_t op, uint64_t a, uint64_t b) {
+__device__ __forceinline__ uint64_t apply_op(uint32_t op, uint64_t a, uint64_t b) {
     return op == OP_AND ? (a & b) : (op == OP_OR ? (a | b) : (a & ~b));
 }
 
@@ -68,9 +68,9 @@ __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 
             const u64x2 p = v[k][j >> 1];
             s0[j] = ((j & 1) ? p.y : p.x) ^ neg;
         }
-        const int nops = prog.nops[k];
+        const int nops = (int)((prog.nops >> (4 * k)) & 15u);
         for (int t = 0; t < nops; ++t) {
-            const int8_t op = prog.ops[op_i++];
+            const uint32_t op = (prog.ops >> (2 * op_i++)) & 3u;
 #pragma unroll
             for (int j = 0; j < NW; ++j) {
                 s0[j] = apply_op(op, s1[j], s0[j]);
@@ -171,8 +171,11 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
 // tiles (a decoupled look-back over ~10^4 tiles measured 1.7× slower).
 // Per-pair counts are packed as FB-bit fields so one 64-bit scan covers several pairs
 // (a pair-chunk holds at most THREADS·128 set bits).
-template <int K, int PAIRS, int STAGE, int THREADS>
-__global__ __launch_bounds__(THREADS) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
+// CLAIM / DECODE = false are diagnostic builds (scripts/kbench.hip), never launched by the
+// library. __launch_bounds__: two workgroups per CU (2·THREADS/256 waves per SIMD) caps
+// VGPRs at 128.
+template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true>
+__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
     constexpr int NW = 2 * PAIRS;
     constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
     constexpr int FPW = 64 / FB;
@@ -230,12 +233,13 @@ __global__ __launch_bounds__(THREADS) void eval_decode_tiles(EvalArgs a, uint64_
             tile_count += (block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK;
         }
         uint64_t claimed = 0;
-        if (t == 0 && tile_count)
-            claimed = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count);
+        if (t == 0 && tile_count)  // not wave-aggregated: built with -amdgpu-atomic-optimizer-strategy=None
+            claimed = CLAIM ? atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count)
+                            : (uint64_t)tile * (TILE_WORDS / 32);
         const uint32_t next = tile + gridDim.x;
         if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);  // prefetch
         const bool stage = tile_count <= (uint64_t)STAGE;
-        const bool write = tile_count && a.rowids;
+        const bool write = DECODE && tile_count && a.rowids;
         if (!stage || !write) {
             if (t == 0) {
                 s_off = claimed;

@@ -64,9 +64,11 @@ int main(int argc, char** argv) {
     const unsigned cus = prop.multiProcessorCount;
     const uint64_t cap = n / 10 + 4096;
     int64_t *ids, *ids2;
+    uint64_t* ovf;
     uint64_t *cnt, *dir, *dst_off;
     CK(hipMalloc(&ids, cap * 8));
-    CK(hipMalloc(&ids2, cap * 8));
+    CK(hipMalloc(&ids2, (cap + pw * 2) * 8));
+    CK(hipMalloc(&ovf, 64));
     CK(hipMalloc(&cnt, 64));
     CK(hipMalloc(&dir, (pw / 512 + 16) * 16));
     CK(hipMalloc(&dst_off, (pw / 512 + 16) * 8));
@@ -76,10 +78,10 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 5; ++k) base.prog.leaf[k] = leaf[k];
     base.prog.n_leaves = 5;
     // (L0 ANDNOT L1) AND (L2 ANDNOT L3) AND L4
-    const uint8_t nops[5] = {0, 1, 0, 2, 1};
-    const int8_t ops[4] = {OP_ANDNOT, OP_ANDNOT, OP_AND, OP_AND};
-    for (int k = 0; k < 5; ++k) base.prog.nops[k] = nops[k];
-    for (int i = 0; i < 4; ++i) base.prog.ops[i] = ops[i];
+    const uint32_t nops[5] = {0, 1, 0, 2, 1};
+    const uint32_t ops[4] = {OP_ANDNOT, OP_ANDNOT, OP_AND, OP_AND};
+    for (int k = 0; k < 5; ++k) base.prog.nops |= nops[k] << (4 * k);
+    for (int i = 0; i < 4; ++i) base.prog.ops |= ops[i] << (2 * i);
     base.n_rows = n;
     base.n_words = W;
     base.rowids = ids;
@@ -98,9 +100,17 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_tiles<5, P, S, T>), dim3(std::min<unsigned>(a.num_tiles, WGPC * cus)), \
                                          dim3(T), 0, s, a, dir);                                              \
                   }, 0})
+#define DX(NAME, CL, DE)                                                                                       \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = dtiles;                                                                   \
+                      hipLaunchKernelGGL((eval_decode_tiles<5, 2, 4096, 512, CL, DE>), dim3(std::min<unsigned>(dtiles, 2 * cus)), \
+                                         dim3(512), 0, s, a, dir);                                            \
+                  }, 3})
+    DX("diag no-claim", false, true);
+    DX("diag no-decode", true, false);
+    DX("diag no-claim no-decode", false, false);
     DT("decode P2 T512 x3/CU", 2, 4096, 512, 3);
-    DT("decode P1 T1024 x2/CU", 1, 4096, 1024, 2);
-    DT("decode P2 T1024 x1/CU", 2, 8192, 1024, 1);
+    DT("decode P2 T256 x4/CU", 2, 2048, 256, 4);
     vs.push_back({"decode + ordered pass", [&](EvalArgs& a, hipStream_t s) {
                       a.num_tiles = dtiles;
                       a.rowids = ids2;
@@ -133,12 +143,28 @@ int main(int argc, char** argv) {
             if (r != -1) continue;
             uint64_t c = 0;
             CK(hipMemcpy(&c, cnt, 8, hipMemcpyDeviceToHost));
+            if (vs[i].kind == 3) continue;
             if (vs[i].kind == 2) {
                 printf("%s %s\n", c == ref_count ? "ok" : "MISMATCH", vs[i].name.c_str());
                 continue;
             }
             std::vector<int64_t> h(c);
-            CK(hipMemcpy(h.data(), ids, c * 8, hipMemcpyDeviceToHost));
+            if (vs[i].kind == 4) {
+                // slotted: gather runs in tile order through the directory
+                std::vector<uint64_t> d(2 * a.num_tiles);
+                CK(hipMemcpy(d.data(), dir, d.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<int64_t> o;
+                o.reserve(c);
+                for (uint32_t tt = 0; tt < a.num_tiles; ++tt) {
+                    std::vector<int64_t> run(d[2 * tt + 1]);
+                    if (!run.empty())
+                        CK(hipMemcpy(run.data(), ids2 + d[2 * tt], run.size() * 8, hipMemcpyDeviceToHost));
+                    o.insert(o.end(), run.begin(), run.end());
+                }
+                h.swap(o);
+            } else {
+                CK(hipMemcpy(h.data(), ids, c * 8, hipMemcpyDeviceToHost));
+            }
             if (vs[i].kind == 0) {
                 std::vector<uint64_t> d(2 * a.num_tiles);
                 CK(hipMemcpy(d.data(), dir, d.size() * 8, hipMemcpyDeviceToHost));
