@@ -562,7 +562,16 @@ struct Updates {
     std::unique_ptr<DevBuf> rows, values, versions;
     std::vector<int64_t> h_rows, h_values;
     std::vector<uint64_t> h_versions;
+    std::vector<uint64_t> distinct_versions;  // sorted
     uint64_t n = 0;
+    // does any record pass TransactionVersionOperator::UseInsertedVersion for this
+    // transaction (id < start_time || id == transaction_id)? If not, the transaction sees
+    // the base values and no patch is needed.
+    bool any_visible(const cubit_txn* txn) const {
+        if (!txn || distinct_versions.empty()) return false;
+        if (distinct_versions.front() < txn->start_time) return true;
+        return std::binary_search(distinct_versions.begin(), distinct_versions.end(), txn->transaction_id);
+    }
 };
 
 }  // namespace
@@ -823,6 +832,10 @@ extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* r
         u.h_values.push_back(values[i]);
         u.h_versions.push_back(versions[i]);
     }
+    u.distinct_versions = u.h_versions;
+    std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
+    u.distinct_versions.erase(std::unique(u.distinct_versions.begin(), u.distinct_versions.end()),
+                              u.distinct_versions.end());
     u.rows = std::make_unique<DevBuf>();
     u.values = std::make_unique<DevBuf>();
     u.versions = std::make_unique<DevBuf>();
@@ -1104,7 +1117,7 @@ __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_
 int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const uint64_t*, uint64_t*>& patched) {
     if (e->kind == Expr::LEAF) {
         auto uit = t->upd.find(e->leaf.column);
-        if (uit == t->upd.end() || uit->second.n == 0) return CUBIT_OK;
+        if (uit == t->upd.end() || !uit->second.any_visible(txn)) return CUBIT_OK;
         auto pit = patched.find(e->leaf.bv);
         uint64_t* copy = nullptr;
         if (pit != patched.end()) {
@@ -1233,7 +1246,7 @@ extern "C" int cubit_table_probe(cubit_table* t, int col, const cubit_txn* txn, 
     HIP_CHECK(launch_gather(it->second.data, it->second.type, d_rowids, d_count, max_n, t->row_base, d_out,
                             t->ctx->stream));
     auto uit = t->upd.find(col);
-    if (txn && uit != t->upd.end() && uit->second.n) {
+    if (txn && uit != t->upd.end() && uit->second.any_visible(txn)) {
         const Updates& u = uit->second;
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((max_n + 255) / 256, 4096));
         hipLaunchKernelGGL(patch_probe_kernel, dim3(grid), dim3(256), 0, t->ctx->stream, d_rowids, d_count, max_n,
@@ -1242,5 +1255,13 @@ extern "C" int cubit_table_probe(cubit_table* t, int col, const cubit_txn* txn, 
                            txn->start_time, txn->transaction_id, d_out);
         HIP_CHECK(hipGetLastError());
     }
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_info(cubit_table* t, uint64_t* n_rows, int64_t* row_base, cubit_ctx** ctx) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    if (n_rows) *n_rows = t->n_rows;
+    if (row_base) *row_base = t->row_base;
+    if (ctx) *ctx = t->ctx;
     return CUBIT_OK;
 }

@@ -14,6 +14,7 @@ PKG_ROOT = Path(__file__).resolve().parent.parent          # duckdb-cubit_amd/
 LIB_DIR = PKG_ROOT / "lib"
 GPU_LIB = LIB_DIR / "libcubitgpu.so"
 GEN_LIB = LIB_DIR / "libcubit_datagen.so"
+SCAN_LIB = LIB_DIR / "libcubit_scan.so"
 
 # status codes / constants (include/cubit_gpu.h)
 OK = 0
@@ -88,6 +89,7 @@ GPU_SIGNATURES = {
     "cubit_gather_sum_product": (C.c_int, [_P, _P, _P, _P, _P, _U64, _I64, _P]),
     "cubit_table_create": (C.c_int, [_P, _U64, _I64, C.POINTER(_P)]),
     "cubit_table_destroy": (C.c_int, [_P]),
+    "cubit_table_info": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_I64), C.POINTER(_P)]),
     "cubit_table_add_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _P, C.c_int]),
     "cubit_table_build_index": (C.c_int, [_P, C.c_int, C.c_int, _P, _U32]),
     "cubit_table_index_info": (C.c_int, [_P, C.c_int, C.POINTER(_U32), C.POINTER(_U64)]),
@@ -109,8 +111,22 @@ GEN_SIGNATURES = {
     "cubit_synth_uniform_i32": (C.c_int, [_U64, _U64, _U64, _U32, _P, C.c_int]),
 }
 
+SCAN_SIGNATURES = {
+    "cubit_scan_last_error": (C.c_char_p, []),
+    "cubit_scan_init_global": (C.c_int, [_P, C.POINTER(_U64), _U32, C.POINTER(_U64), _U32, C.POINTER(FilterNode),
+                                         _U32, C.POINTER(Txn), C.POINTER(_P)]),
+    "cubit_scan_max_threads": (C.c_int, [_P, C.POINTER(_U64)]),
+    "cubit_scan_init_local": (C.c_int, [_P, C.POINTER(_P)]),
+    "cubit_scan_function": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_U64)]),
+    "cubit_scan_batch_index": (C.c_int, [_P, _P, C.POINTER(_U64)]),
+    "cubit_scan_progress": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "cubit_scan_local_destroy": (C.c_int, [_P]),
+    "cubit_scan_destroy": (C.c_int, [_P]),
+}
+
 _gpu = None
 _gen = None
+_scan = None
 
 
 def _bind(lib, sigs):
@@ -139,6 +155,23 @@ def gen_lib():
             raise RuntimeError(f"{GEN_LIB} is missing: build it with `make -C {PKG_ROOT}`")
         _gen = _bind(C.CDLL(str(GEN_LIB)), GEN_SIGNATURES)
     return _gen
+
+
+def scan_lib():
+    """libcubit_scan.so: the TableFunction mirror (loads libcubitgpu.so first)."""
+    global _scan
+    if _scan is None:
+        gpu_lib()
+        if not SCAN_LIB.exists():
+            raise RuntimeError(f"{SCAN_LIB} is missing: build it with `make -C {PKG_ROOT}`")
+        _scan = _bind(C.CDLL(str(SCAN_LIB)), SCAN_SIGNATURES)
+    return _scan
+
+
+def check_scan(rc: int) -> None:
+    if rc != OK:
+        msg = scan_lib().cubit_scan_last_error()
+        raise CubitError(rc, msg.decode() if msg else "")
 
 
 def check(rc: int) -> None:

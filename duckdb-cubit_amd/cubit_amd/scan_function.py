@@ -1,0 +1,90 @@
+"""Python handle on libcubit_scan.so — the TableFunction mirror (include/cubit_scan.h).
+
+CubitScanFunction.init_global / init_local / function / get_batch_index / progress follow
+DuckDB's seq_scan callbacks (src/function/table/table_scan.cpp); `function` returns the
+next DataChunk as a list of int64 numpy columns, empty when the scan is finished.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+from .filters import Residual, TableFilterSet, serialize, to_ctypes
+
+ROW_ID = 2 ** 64 - 1  # COLUMN_IDENTIFIER_ROW_ID
+VECTOR_SIZE = 2048
+
+
+class LocalState:
+    def __init__(self, scan: "CubitScanFunction"):
+        self.scan = scan
+        h = C.c_void_p()
+        L.check_scan(scan.lib.cubit_scan_init_local(scan.handle, C.byref(h)))
+        self.handle = h
+        self.bufs = [np.empty(VECTOR_SIZE, dtype=np.int64) for _ in range(scan.n_out)]
+        self.ptrs = (C.c_void_p * max(scan.n_out, 1))(*[b.ctypes.data for b in self.bufs])
+
+    def __del__(self):
+        try:
+            self.scan.lib.cubit_scan_local_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class CubitScanFunction:
+    """init_global: run the GPU scan (+ probes) for the given column_ids / projection_ids /
+    filters; then any number of local states drain it chunk by chunk."""
+
+    def __init__(self, table, column_ids: Sequence[int], projection_ids: Optional[Sequence[int]] = None,
+                 filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
+                 txn: Optional[L.Txn] = None):
+        self.lib = L.scan_lib()
+        self.table = table
+        cols = (C.c_uint64 * max(len(column_ids), 1))(*column_ids)
+        proj = list(projection_ids or [])
+        projc = (C.c_uint64 * max(len(proj), 1))(*proj)
+        nodes = serialize(filter_set, residual).nodes if (filter_set or residual) else []
+        arr = to_ctypes(nodes)
+        h = C.c_void_p()
+        L.check_scan(self.lib.cubit_scan_init_global(table.handle, cols, len(column_ids), projc if proj else None,
+                                                      len(proj), arr if nodes else None, len(nodes),
+                                                      C.byref(txn) if txn is not None else None, C.byref(h)))
+        self.handle = h
+        self.n_out = len(proj) if proj else len(column_ids)
+
+    def max_threads(self) -> int:
+        v = C.c_uint64()
+        L.check_scan(self.lib.cubit_scan_max_threads(self.handle, C.byref(v)))
+        return int(v.value)
+
+    def init_local(self) -> LocalState:
+        return LocalState(self)
+
+    def function(self, local: LocalState) -> List[np.ndarray]:
+        n = C.c_uint64()
+        L.check_scan(self.lib.cubit_scan_function(self.handle, local.handle, local.ptrs, C.byref(n)))
+        return [b[: n.value].copy() for b in local.bufs]
+
+    def get_batch_index(self, local: LocalState) -> int:
+        v = C.c_uint64()
+        L.check_scan(self.lib.cubit_scan_batch_index(self.handle, local.handle, C.byref(v)))
+        return int(v.value)
+
+    def progress(self) -> float:
+        v = C.c_double()
+        L.check_scan(self.lib.cubit_scan_progress(self.handle, C.byref(v)))
+        return float(v.value)
+
+    def close(self):
+        if self.handle:
+            self.lib.cubit_scan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

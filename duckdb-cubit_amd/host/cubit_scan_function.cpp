@@ -1,0 +1,290 @@
+// cubit_scan: DuckDB TableFunction callbacks over libcubitgpu (see cubit_scan_function.hpp)
+// plus the extern "C" surface of include/cubit_scan.h.
+#include "cubit_scan_function.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "../../include/cubit_scan.h"
+
+namespace cubit {
+namespace duck {
+
+namespace {
+
+struct ScanError : public std::runtime_error {
+    int code;
+    ScanError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void check(int rc, const char* what) {
+    if (rc != CUBIT_OK) throw ScanError(rc, std::string(what) + ": " + cubit_last_error());
+}
+
+// Device result of one scan, copied to host once (the GPU work is one fused launch plus one
+// gather per emitted column; DataChunks are then served from host memory).
+struct CubitScanGlobalState : public GlobalTableFunctionState {
+    std::vector<column_t> column_ids;
+    std::vector<idx_t> emit;  // positions of column_ids that reach the output
+    idx_t count = 0;
+    idx_t rows_per_tile = 0;
+    std::vector<int64_t> rowids;                // tile-run order
+    std::vector<std::vector<int64_t>> columns;  // per emitted position (row ids or probed values)
+    std::vector<uint32_t> tiles;                // non-empty tiles, ascending
+    std::vector<uint64_t> dir;                  // {start, length} per tile
+    std::atomic<uint32_t> next{0};
+    std::atomic<idx_t> emitted{0};
+    idx_t MaxThreads() const override {
+        const idx_t hw = std::max<unsigned>(1, std::thread::hardware_concurrency());
+        return std::max<idx_t>(1, std::min<idx_t>(tiles.size(), hw));
+    }
+};
+
+struct CubitScanLocalState : public LocalTableFunctionState {
+    int64_t tile_slot = -1;  // index into tiles, -1 = none yet
+    idx_t pos = 0;           // next row of the tile's run to emit
+};
+
+struct DeviceBuffer {
+    cubit_ctx* ctx;
+    void* p = nullptr;
+    DeviceBuffer(cubit_ctx* c, uint64_t bytes) : ctx(c) { check(cubit_dev_alloc(c, bytes, &p), "cubit_dev_alloc"); }
+    ~DeviceBuffer() {
+        if (p) cubit_dev_free(ctx, p);
+    }
+};
+
+std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
+    auto& bind = static_cast<const CubitScanBindData&>(*input.bind_data);
+    auto g = std::make_unique<CubitScanGlobalState>();
+    g->column_ids = input.column_ids;
+    if (input.CanRemoveFilterColumns()) {
+        g->emit = input.projection_ids;
+    } else {
+        for (idx_t i = 0; i < input.column_ids.size(); ++i) g->emit.push_back(i);
+    }
+    cubit_ctx* ctx = bind.ctx;
+    const uint64_t cap = std::max<uint64_t>(bind.n_rows, 1);
+    DeviceBuffer d_ids(ctx, cap * 8), d_cnt(ctx, 16);
+    const cubit_txn* txn = bind.has_txn ? &bind.txn : nullptr;
+    const auto& nodes = input.filters ? input.filters->nodes : std::vector<cubit_filter_node>{};
+    check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
+                           static_cast<int64_t*>(d_ids.p), cap, static_cast<uint64_t*>(d_cnt.p), 0),
+          "cubit_table_scan");
+    check(cubit_ctx_check(ctx), "scan kernel");
+    check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
+    const uint64_t* d_dir = nullptr;
+    uint32_t n_tiles = 0;
+    check(cubit_ctx_last_tiles(ctx, &d_dir, &n_tiles, &g->rows_per_tile), "tiles");
+    g->dir.resize(2 * (size_t)n_tiles);
+    if (n_tiles) check(cubit_memcpy_d2h(ctx, g->dir.data(), d_dir, g->dir.size() * 8), "directory");
+    g->rowids.resize(g->count);
+    if (g->count) check(cubit_memcpy_d2h(ctx, g->rowids.data(), d_ids.p, g->count * 8), "row ids");
+    for (uint32_t t = 0; t < n_tiles; ++t)
+        if (g->dir[2 * t + 1]) g->tiles.push_back(t);
+    // probe every emitted storage column at the row ids (ColumnData::FilterScan semantics)
+    g->columns.resize(g->emit.size());
+    for (size_t e = 0; e < g->emit.size(); ++e) {
+        const column_t col = g->column_ids[g->emit[e]];
+        if (col == COLUMN_IDENTIFIER_ROW_ID || g->count == 0) continue;
+        DeviceBuffer d_vals(ctx, g->count * 8);
+        check(cubit_table_probe(bind.table, (int)col, txn, static_cast<int64_t*>(d_ids.p),
+                                static_cast<uint64_t*>(d_cnt.p), g->count, static_cast<int64_t*>(d_vals.p)),
+              "cubit_table_probe");
+        g->columns[e].resize(g->count);
+        check(cubit_memcpy_d2h(ctx, g->columns[e].data(), d_vals.p, g->count * 8), "probe values");
+    }
+    return g;
+}
+
+std::unique_ptr<LocalTableFunctionState> CubitScanInitLocal(TableFunctionInitInput&, GlobalTableFunctionState*) {
+    return std::make_unique<CubitScanLocalState>();
+}
+
+// TableScanParallelStateNext analogue: take the next non-empty tile (row_group_collection.cpp
+// hands out row groups under a mutex; one atomic suffices here).
+bool NextTile(CubitScanGlobalState& g, CubitScanLocalState& l) {
+    const uint32_t s = g.next.fetch_add(1);
+    if (s >= g.tiles.size()) {
+        l.tile_slot = (int64_t)g.tiles.size();
+        return false;
+    }
+    l.tile_slot = s;
+    l.pos = 0;
+    return true;
+}
+
+void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
+    auto& g = static_cast<CubitScanGlobalState&>(*data.global_state);
+    auto& l = static_cast<CubitScanLocalState&>(*data.local_state);
+    output.Reset();
+    for (;;) {
+        if (l.tile_slot < 0 && !NextTile(g, l)) return;
+        if ((size_t)l.tile_slot >= g.tiles.size()) return;
+        const uint32_t tile = g.tiles[l.tile_slot];
+        const uint64_t start = g.dir[2 * tile], len = g.dir[2 * tile + 1];
+        if (l.pos < len) {
+            const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
+            for (size_t e = 0; e < g.emit.size(); ++e) {
+                const column_t col = g.column_ids[g.emit[e]];
+                const int64_t* src = col == COLUMN_IDENTIFIER_ROW_ID ? g.rowids.data() : g.columns[e].data();
+                std::memcpy(output.data[e].data(), src + start + l.pos, n * sizeof(int64_t));
+            }
+            l.pos += n;
+            output.SetCardinality(n);
+            g.emitted.fetch_add(n);
+            return;
+        }
+        if (!NextTile(g, l)) return;
+    }
+}
+
+idx_t CubitScanGetBatchIndex(const FunctionData*, LocalTableFunctionState* lstate, GlobalTableFunctionState* gstate) {
+    auto& g = static_cast<CubitScanGlobalState&>(*gstate);
+    auto& l = static_cast<CubitScanLocalState&>(*lstate);
+    if (l.tile_slot < 0 || (size_t)l.tile_slot >= g.tiles.size()) return 0;
+    return g.tiles[l.tile_slot];
+}
+
+double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gstate) {
+    auto& g = static_cast<const CubitScanGlobalState&>(*gstate);
+    if (g.count == 0) return 100.0;
+    return 100.0 * (double)g.emitted.load() / (double)g.count;
+}
+
+}  // namespace
+
+TableFunction GetCubitScanFunction() {
+    TableFunction f;
+    f.name = "cubit_scan";
+    f.function = CubitScanFunc;
+    f.init_global = CubitScanInitGlobal;
+    f.init_local = CubitScanInitLocal;
+    f.get_batch_index = CubitScanGetBatchIndex;
+    f.table_scan_progress = CubitScanProgress;
+    f.projection_pushdown = true;  // as seq_scan (table_scan.cpp:436-438)
+    f.filter_pushdown = true;
+    f.filter_prune = true;
+    return f;
+}
+
+}  // namespace duck
+}  // namespace cubit
+
+// ------------------------------------------------------------------ C surface (include/cubit_scan.h)
+
+using namespace cubit::duck;
+
+struct cubit_scan {
+    CubitScanBindData bind;
+    TableFilterSet filters;
+    TableFunctionInitInput input;
+    TableFunction fn;
+    std::unique_ptr<GlobalTableFunctionState> gstate;
+    std::string error;
+};
+
+struct cubit_scan_local {
+    std::unique_ptr<LocalTableFunctionState> lstate;
+    DataChunk chunk;
+};
+
+namespace {
+thread_local std::string g_scan_error;
+int scan_fail(int code, const std::string& m) {
+    g_scan_error = m;
+    return code;
+}
+}  // namespace
+
+extern "C" {
+
+const char* cubit_scan_last_error(void) { return g_scan_error.c_str(); }
+
+int cubit_scan_init_global(cubit_table* table, const uint64_t* column_ids, uint32_t n_column_ids,
+                           const uint64_t* projection_ids, uint32_t n_projection_ids, const cubit_filter_node* nodes,
+                           uint32_t n_nodes, const cubit_txn* txn, cubit_scan** out) {
+    if (!table || !out || (n_column_ids && !column_ids)) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    try {
+        auto s = std::make_unique<cubit_scan>();
+        s->fn = GetCubitScanFunction();
+        uint64_t n = 0;
+        int64_t base = 0;
+        check(cubit_table_info(table, &n, &base, &s->bind.ctx), "cubit_table_info");
+        s->bind.table = table;
+        s->bind.n_rows = n;
+        s->bind.row_base = base;
+        if (txn) {
+            s->bind.has_txn = true;
+            s->bind.txn = *txn;
+        }
+        s->filters.nodes.assign(nodes, nodes + n_nodes);
+        s->input.bind_data = &s->bind;
+        s->input.column_ids.assign(column_ids, column_ids + n_column_ids);
+        if (projection_ids) s->input.projection_ids.assign(projection_ids, projection_ids + n_projection_ids);
+        for (idx_t p : s->input.projection_ids)
+            if (p >= n_column_ids) return scan_fail(CUBIT_ERR_INVALID, "projection id out of range");
+        s->input.filters = &s->filters;
+        s->gstate = s->fn.init_global(s->input);
+        *out = s.release();
+        return CUBIT_OK;
+    } catch (const ScanError& e) {
+        return scan_fail(e.code, e.what());
+    } catch (const std::exception& e) {
+        return scan_fail(CUBIT_ERR_INVALID, e.what());
+    }
+}
+
+int cubit_scan_max_threads(cubit_scan* s, uint64_t* out) {
+    if (!s || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    *out = s->gstate->MaxThreads();
+    return CUBIT_OK;
+}
+
+int cubit_scan_init_local(cubit_scan* s, cubit_scan_local** out) {
+    if (!s || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    auto l = std::make_unique<cubit_scan_local>();
+    l->lstate = s->fn.init_local(s->input, s->gstate.get());
+    const size_t n_out = s->input.CanRemoveFilterColumns() ? s->input.projection_ids.size() : s->input.column_ids.size();
+    l->chunk.Initialize(n_out);
+    *out = l.release();
+    return CUBIT_OK;
+}
+
+int cubit_scan_function(cubit_scan* s, cubit_scan_local* l, int64_t* const* out_columns, uint64_t* out_count) {
+    if (!s || !l || !out_count) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    TableFunctionInput in{&s->bind, l->lstate.get(), s->gstate.get()};
+    s->fn.function(in, l->chunk);
+    const idx_t n = l->chunk.size();
+    if (out_columns)
+        for (size_t c = 0; c < l->chunk.data.size(); ++c)
+            if (out_columns[c]) std::memcpy(out_columns[c], l->chunk.data[c].data(), n * sizeof(int64_t));
+    *out_count = n;
+    return CUBIT_OK;
+}
+
+int cubit_scan_batch_index(cubit_scan* s, cubit_scan_local* l, uint64_t* out) {
+    if (!s || !l || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    *out = s->fn.get_batch_index(&s->bind, l->lstate.get(), s->gstate.get());
+    return CUBIT_OK;
+}
+
+int cubit_scan_progress(cubit_scan* s, double* out) {
+    if (!s || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    *out = s->fn.table_scan_progress(&s->bind, s->gstate.get());
+    return CUBIT_OK;
+}
+
+int cubit_scan_local_destroy(cubit_scan_local* l) {
+    delete l;
+    return CUBIT_OK;
+}
+
+int cubit_scan_destroy(cubit_scan* s) {
+    delete s;
+    return CUBIT_OK;
+}
+
+}  // extern "C"

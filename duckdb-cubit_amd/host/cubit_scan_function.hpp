@@ -1,0 +1,118 @@
+// Host-side mirror of DuckDB's TableFunction interface for the bitmap-indexed scan.
+//
+// DuckDB v1.1.2 drives a table scan through the callback struct TableFunction
+// (src/include/duckdb/function/table_function.hpp:184-301): bind → init_global →
+// init_local (per pipeline task) → function (one DataChunk of ≤ STANDARD_VECTOR_SIZE rows per
+// call, size 0 = finished; PhysicalTableScan::GetData, physical_table_scan.cpp:82-103), with
+// get_batch_index for order-preserving sinks (table_scan.cpp:179-189) and
+// table_scan_progress. `seq_scan` sets projection_pushdown / filter_pushdown /
+// filter_prune (table_scan.cpp:422-442).
+//
+// cubit_scan is the drop-in replacement of seq_scan's callbacks for a table partition held
+// by libcubitgpu (include/cubit_gpu.h): init_global runs the GPU scan once (fused evaluate +
+// decode, then the probe of every projected column, K1–K3) — the way index_scan
+// materialises its row-id list at plan time (table_scan.cpp:296-370) — and `function` hands
+// the result out as DataChunks, one 131,072-row tile per morsel, so N pipeline tasks drain
+// it concurrently and batch index = tile index restores row order.
+//
+// The types below reproduce the shape of the DuckDB ones this path touches, without the
+// DuckDB headers (the shim in INTEGRATION.md maps them 1:1 onto the real classes).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cubit_gpu.h"
+
+namespace cubit {
+namespace duck {
+
+using idx_t = uint64_t;
+using column_t = uint64_t;
+constexpr column_t COLUMN_IDENTIFIER_ROW_ID = (column_t)-1;  // src/include/duckdb/common/constants.hpp
+constexpr idx_t STANDARD_VECTOR_SIZE = 2048;                  // common/vector_size.hpp:16-20
+
+// DataChunk with flat int64 vectors (ROW_TYPE row ids; DATE / DECIMAL(15,2) physical values
+// widened to int64). size() == 0 signals the end of the scan.
+struct DataChunk {
+    std::vector<std::vector<int64_t>> data;
+    idx_t count = 0;
+    void Initialize(idx_t n_columns) {
+        data.assign(n_columns, std::vector<int64_t>(STANDARD_VECTOR_SIZE));
+        count = 0;
+    }
+    void Reset() { count = 0; }
+    idx_t size() const { return count; }
+    void SetCardinality(idx_t n) { count = n; }
+};
+
+struct FunctionData {
+    virtual ~FunctionData() = default;
+};
+struct GlobalTableFunctionState {
+    virtual ~GlobalTableFunctionState() = default;
+    virtual idx_t MaxThreads() const { return 1; }
+};
+struct LocalTableFunctionState {
+    virtual ~LocalTableFunctionState() = default;
+};
+
+// TableFilterSet as prefix-order cubit_filter_node trees (kind/cmp/column/constant mirror
+// ConstantFilter / IsNull / IsNotNull / ConjunctionAnd / ConjunctionOr); the root ANDs the
+// per-column filters exactly like TableFilterSet::filters (table_filter.hpp:67-101).
+struct TableFilterSet {
+    std::vector<cubit_filter_node> nodes;
+};
+
+struct TableFunctionInitInput {
+    const FunctionData* bind_data = nullptr;
+    std::vector<column_t> column_ids;   // storage columns to scan (or ROW_ID)
+    std::vector<idx_t> projection_ids;  // positions of column_ids to emit (filter_prune)
+    const TableFilterSet* filters = nullptr;
+    bool CanRemoveFilterColumns() const { return !projection_ids.empty(); }
+};
+
+struct TableFunctionInput {
+    const FunctionData* bind_data;
+    LocalTableFunctionState* local_state;
+    GlobalTableFunctionState* global_state;
+};
+
+using table_function_init_global_t = std::unique_ptr<GlobalTableFunctionState> (*)(TableFunctionInitInput& input);
+using table_function_init_local_t = std::unique_ptr<LocalTableFunctionState> (*)(TableFunctionInitInput& input,
+                                                                                  GlobalTableFunctionState* gstate);
+using table_function_t = void (*)(TableFunctionInput& data, DataChunk& output);
+using table_function_get_batch_index_t = idx_t (*)(const FunctionData* bind_data, LocalTableFunctionState* lstate,
+                                                   GlobalTableFunctionState* gstate);
+using table_function_progress_t = double (*)(const FunctionData* bind_data, const GlobalTableFunctionState* gstate);
+
+struct TableFunction {
+    std::string name;
+    table_function_t function = nullptr;
+    table_function_init_global_t init_global = nullptr;
+    table_function_init_local_t init_local = nullptr;
+    table_function_get_batch_index_t get_batch_index = nullptr;
+    table_function_progress_t table_scan_progress = nullptr;
+    bool projection_pushdown = false;
+    bool filter_pushdown = false;
+    bool filter_prune = false;
+};
+
+// bind data: the partition and the reading transaction (TransactionData{start_time, id})
+struct CubitScanBindData : public FunctionData {
+    cubit_table* table = nullptr;
+    cubit_ctx* ctx = nullptr;
+    idx_t n_rows = 0;
+    int64_t row_base = 0;
+    bool has_txn = false;
+    cubit_txn txn{};
+};
+
+TableFunction GetCubitScanFunction();
+
+}  // namespace duck
+}  // namespace cubit

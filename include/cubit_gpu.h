@@ -163,6 +163,8 @@ int cubit_gather_sum_product(cubit_ctx *ctx, const int64_t *d_a, const int64_t *
 /* A row-range partition of a table resident on one device: rows [row_base, row_base+n_rows). */
 int cubit_table_create(cubit_ctx *ctx, uint64_t n_rows, int64_t row_base, cubit_table **out);
 int cubit_table_destroy(cubit_table *t);
+/* rows, row base and owning context of a partition */
+int cubit_table_info(cubit_table *t, uint64_t *n_rows, int64_t *row_base, cubit_ctx **ctx);
 /* Register column `col`. data/validity are host pointers unless on_device = 1 (then the
  * table only references them). validity may be NULL (no NULLs). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,

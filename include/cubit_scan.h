@@ -1,0 +1,56 @@
+/*
+ * cubit_scan.h — C surface of libcubit_scan.so, the host-side mirror of DuckDB's
+ * TableFunction callbacks for the bitmap-indexed scan (duckdb-cubit_amd/host/).
+ *
+ * Each entry point replaces one seq_scan callback (src/function/table/table_scan.cpp) and
+ * keeps its contract:
+ *   cubit_scan_init_global  ← TableScanInitGlobal   (table_scan.cpp:88-106)
+ *                             (bind data = table partition + TransactionData)
+ *   cubit_scan_max_threads  ← GlobalTableFunctionState::MaxThreads (DataTable::MaxThreads,
+ *                             data_table.cpp:247-254)
+ *   cubit_scan_init_local   ← TableScanInitLocal    (table_scan.cpp:67-86)
+ *   cubit_scan_function     ← TableScanFunc         (table_scan.cpp:119-146): ≤ 2,048 rows per
+ *                             call, 0 rows = finished (PhysicalTableScan::GetData,
+ *                             physical_table_scan.cpp:82-103)
+ *   cubit_scan_batch_index  ← TableScanGetBatchIndex (table_scan.cpp:179-189)
+ *   cubit_scan_progress     ← TableScanProgress     (table_scan.cpp:158-177)
+ * column_ids / projection_ids / filters mean what TableFunctionInitInput's members mean
+ * (table_function.hpp:103-126): column_ids are storage columns (UINT64_MAX = row id), the
+ * output holds column_ids[projection_ids[i]] (or every column_id when projection_ids is
+ * empty), and filter columns need not be projected (filter_prune). Errors are status codes
+ * with a message from cubit_scan_last_error(). cubit_scan_function may be called
+ * concurrently with distinct local states (one per pipeline task).
+ */
+#ifndef CUBIT_SCAN_H
+#define CUBIT_SCAN_H
+
+#include <stdint.h>
+
+#include "cubit_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CUBIT_COLUMN_ROW_ID UINT64_MAX /* COLUMN_IDENTIFIER_ROW_ID */
+
+typedef struct cubit_scan cubit_scan;
+typedef struct cubit_scan_local cubit_scan_local;
+
+const char *cubit_scan_last_error(void);
+int cubit_scan_init_global(cubit_table *table, const uint64_t *column_ids, uint32_t n_column_ids,
+                           const uint64_t *projection_ids, uint32_t n_projection_ids, const cubit_filter_node *nodes,
+                           uint32_t n_nodes, const cubit_txn *txn, cubit_scan **out);
+int cubit_scan_max_threads(cubit_scan *scan, uint64_t *out);
+int cubit_scan_init_local(cubit_scan *scan, cubit_scan_local **out);
+/* out_columns[i] receives output column i (capacity 2,048 int64 each); *out_count the rows */
+int cubit_scan_function(cubit_scan *scan, cubit_scan_local *local, int64_t *const *out_columns, uint64_t *out_count);
+int cubit_scan_batch_index(cubit_scan *scan, cubit_scan_local *local, uint64_t *out);
+int cubit_scan_progress(cubit_scan *scan, double *out);
+int cubit_scan_local_destroy(cubit_scan_local *local);
+int cubit_scan_destroy(cubit_scan *scan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CUBIT_SCAN_H */

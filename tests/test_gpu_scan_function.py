@@ -1,0 +1,127 @@
+"""The TableFunction mirror (include/cubit_scan.h) driven the way DuckDB's pipeline drives
+seq_scan: N tasks with their own local state call `function` until it returns an empty
+chunk (PhysicalTableScan::GetData, physical_table_scan.cpp:82-103); an order-preserving sink
+sorts chunks by batch index (table_scan.cpp:179-189)."""
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import lineitem, revenue_from_answer
+from cubit_amd import _lib as L
+from cubit_amd import filters as F
+from cubit_amd.scan_function import ROW_ID, CubitScanFunction
+from cubit_amd.table import Context, CubitTable
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TXN_START = 4611686018427388000
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def q6_table(ctx, li):
+    t = CubitTable(ctx, li.n_rows, li.row_base)
+    for c, arr in enumerate((li.l_shipdate, li.l_discount, li.l_quantity, li.l_extendedprice)):
+        t.add_column(c, arr)
+    months = [F.date(y, m, 1) for y in range(1992, 1999) for m in range(1, 13)] + [F.date(1999, 1, 1)]
+    t.build_index(0, L.INDEX_RANGE, months)
+    t.build_index(1, L.INDEX_RANGE)
+    t.build_index(2, L.INDEX_RANGE)
+    return t
+
+
+def drain(fn, n_tasks):
+    """Run n_tasks pipeline tasks; returns [(batch_index, chunk columns)]."""
+    out, lock = [], threading.Lock()
+
+    def task():
+        local = fn.init_local()
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                return
+            assert len(cols[0]) <= 2048
+            b = fn.get_batch_index(local)
+            with lock:
+                out.append((b, cols))
+
+    th = [threading.Thread(target=task) for _ in range(n_tasks)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    return out
+
+
+def ordered(chunks, col):
+    chunks = sorted(chunks, key=lambda bc: (bc[0], bc[1][0][0] if len(bc[1][0]) else 0))
+    return np.concatenate([c[col] for _, c in chunks]) if chunks else np.empty(0, np.int64)
+
+
+@pytest.mark.parametrize("tasks", [1, 4])
+def test_q6_through_table_function(ctx, golden, tasks):
+    li = lineitem(0.1)
+    t = q6_table(ctx, li)
+    # SELECT rowid, l_extendedprice, l_discount ... WHERE <Q6>: column_ids include the filter
+    # columns, projection_ids drop them (filter_prune)
+    column_ids = [0, 1, 2, 3, ROW_ID]
+    projection_ids = [4, 3, 1]
+    fn = CubitScanFunction(t, column_ids, projection_ids, F.q6_filter_set(0, 1, 2))
+    assert fn.max_threads() >= 1
+    chunks = drain(fn, tasks)
+    rows = ordered(chunks, 0)
+    ref = O.table_scan([O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity)],
+                       F.serialize(F.q6_filter_set()), li.n_rows)
+    assert np.array_equal(rows, ref)
+    assert np.array_equal(ordered(chunks, 1), li.l_extendedprice[ref])
+    assert np.array_equal(ordered(chunks, 2), li.l_discount[ref])
+    rev = int((ordered(chunks, 1).astype(object) * ordered(chunks, 2).astype(object)).sum())
+    assert rev == revenue_from_answer(golden["tpch"]["q6_revenue"]["0.1"]["revenue"])
+    assert fn.progress() == pytest.approx(100.0)
+    # batch indexes are tiles: rows of batch b lie in tile b
+    for b, cols in chunks:
+        assert np.all(cols[0] // 131072 == b)
+
+
+def test_no_filter_full_scan_and_empty_result(ctx):
+    n = 300_000
+    a = np.arange(n, dtype=np.int64) % 1000
+    t = CubitTable(ctx, n, row_base=7)
+    t.add_column(0, a)
+    fn = CubitScanFunction(t, [ROW_ID, 0])
+    chunks = drain(fn, 3)
+    assert np.array_equal(ordered(chunks, 0), np.arange(n) + 7)
+    assert np.array_equal(ordered(chunks, 1), a)
+    fn2 = CubitScanFunction(t, [0], None, F.TableFilterSet({0: F.ConstantFilter(">", 5000)}))
+    local = fn2.init_local()
+    assert len(fn2.function(local)[0]) == 0
+    assert fn2.progress() == 100.0
+
+
+def test_mvcc_views_through_table_function(ctx, golden):
+    li = lineitem(0.01)
+    t = q6_table(ctx, li)
+    n = li.n_rows
+    writer = TXN_START + 1
+    t.set_deletes(np.arange(0, n, 11), np.full(len(range(0, n, 11)), writer, dtype=np.uint64))
+    upd = np.arange(0, n, 7)
+    t.set_updates(2, upd, np.full(len(upd), 100), np.full(len(upd), writer, dtype=np.uint64))
+    fp = golden["tpch"]["fingerprints"]["sf001_mvcc"]
+    for txn, want in ((L.Txn(2, writer), fp["writer_view"]), (L.Txn(2, TXN_START + 2), fp["reader_view"])):
+        fn = CubitScanFunction(t, [0, 1, 2, ROW_ID], [3, 2], F.q6_filter_set(), txn=txn)
+        chunks = drain(fn, 2)
+        assert len(ordered(chunks, 0)) == want
+        # the probed l_quantity is the version the transaction sees
+        q = ordered(chunks, 1)
+        rows = ordered(chunks, 0)
+        exp = li.l_quantity[rows].copy()
+        if txn.transaction_id == writer:
+            exp[rows % 7 == 0] = 100
+        assert np.array_equal(q, exp)
