@@ -586,6 +586,14 @@ struct cubit_table {
     // MVCC delta
     std::unique_ptr<DevBuf> del_rows, del_ids;
     uint64_t n_del = 0;
+    // Committed-delete visibility bitvector, kept across scans (CUBIT keeps deletions as a
+    // maintained bitvector rather than re-deriving them per query). For a transaction with no
+    // deletes of its own, the deletes in effect are exactly those with id < start_time — a
+    // prefix of the id-sorted list — so the bitvector is reused while that prefix length is
+    // unchanged. vis_prefix = -1: not built.
+    std::vector<uint64_t> del_ids_sorted;
+    std::unique_ptr<DevBuf> vis_cache;
+    int64_t vis_prefix = -1;
     std::map<int, Updates> upd;
     // scratch bitvectors (reused across scans)
     std::vector<std::unique_ptr<DevBuf>> scratch;
@@ -811,6 +819,9 @@ extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, cons
         HIP_CHECK(hipMemcpy(t->del_ids->p, ids, n * 8, hipMemcpyHostToDevice));
     }
     t->n_del = n;
+    t->del_ids_sorted.assign(ids, ids + n);
+    std::sort(t->del_ids_sorted.begin(), t->del_ids_sorted.end());
+    t->vis_prefix = -1;
     return CUBIT_OK;
 }
 
@@ -1172,11 +1183,28 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
             if (int rc = patch_updates(t, e, txn, patched)) return rc;
         }
         if (t->n_del) {
+            const auto& ids = t->del_ids_sorted;
+            const int64_t prefix = std::lower_bound(ids.begin(), ids.end(), txn->start_time) - ids.begin();
+            const bool own = std::binary_search(ids.begin(), ids.end(), txn->transaction_id) &&
+                             txn->transaction_id >= txn->start_time;
             uint64_t* vis = nullptr;
-            if (int rc = scratch_bv(t, &vis)) return rc;
-            HIP_CHECK(launch_visibility(static_cast<const int64_t*>(t->del_rows->p),
-                                        static_cast<const uint64_t*>(t->del_ids->p), t->n_del, t->n_rows,
-                                        txn->start_time, txn->transaction_id, vis, ctx->stream));
+            if (!own) {
+                if (!t->vis_cache) {
+                    auto b = std::make_unique<DevBuf>();
+                    if (hipMalloc(&b->p, t->nwp * sizeof(uint64_t)) != hipSuccess)
+                        return fail(CUBIT_ERR_OOM, "visibility bitvector allocation failed");
+                    t->vis_cache = std::move(b);
+                }
+                vis = static_cast<uint64_t*>(t->vis_cache->p);
+            } else if (int rc = scratch_bv(t, &vis)) {
+                return rc;
+            }
+            if (own || prefix != t->vis_prefix) {
+                HIP_CHECK(launch_visibility(static_cast<const int64_t*>(t->del_rows->p),
+                                            static_cast<const uint64_t*>(t->del_ids->p), t->n_del, t->n_rows,
+                                            txn->start_time, txn->transaction_id, vis, ctx->stream));
+                if (!own) t->vis_prefix = prefix;
+            }
             Leaf l;
             l.bv = vis;
             e = mk_bin(Expr::AND, e, mk_leaf(l));

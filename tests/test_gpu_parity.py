@@ -124,7 +124,7 @@ def test_or_tree_config4_small(ctx):
     assert t.last_plan() == (4, 1)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 4095, 65535, 65536, 65537, 200_001])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4095, 65535, 65536, 65537, 131_071, 131_072, 131_073, 200_001, 262_145])
 def test_tails_and_dense_tiles(ctx, n):
     """Tail words, tile boundaries and a dense result (> LDS stage capacity per tile)."""
     rng = np.random.default_rng(n)
@@ -307,3 +307,36 @@ def test_mvcc_writer_reader_views_sf001(ctx, golden):
         pr = ctx.alloc(len(w) * 8)
         t.probe(2, d_rows.addr, d_cnt.addr, len(w), pr.addr, txn=L.Txn(2, writer))
         assert np.array_equal(pr.download(np.int64, len(w)), O.fetch(qty, w, tx=O.Mvcc(2, writer)))
+
+
+def test_visibility_bitvector_cache_across_snapshots(ctx):
+    """Committed deletes at ids 5 / 20 / 40 and one uncommitted (writer) delete set; a
+    sequence of snapshots that reuses, rebuilds and bypasses the cached visibility bitvector
+    must match the oracle at every step (chunk_info.cpp:11-19 visibility rule)."""
+    n = 400_000
+    a = uniform_i32(7, n, 1000)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE, [100, 500])
+    rng = np.random.default_rng(3)
+    rows = rng.choice(n, size=40_000, replace=False).astype(np.int64)
+    writer = TXN_START + 9
+    ids = np.array([5, 20, 40, writer], dtype=np.uint64)[rng.integers(0, 4, len(rows))]
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 500)})
+    plan = F.serialize(fs)
+
+    def check(start, tid):
+        got = t.scan(fs, txn=L.Txn(start, tid))
+        deleted = np.full(n, np.uint64(2 ** 64 - 2), dtype=np.uint64)
+        deleted[rows] = ids
+        ref = O.table_scan([O.Column(a)], plan, n, tx=O.Mvcc(start, tid, deleted=deleted))
+        assert np.array_equal(got, ref), (start, tid)
+
+    t.set_deletes(rows, ids)
+    for start, tid in ((10, TXN_START + 1), (10, TXN_START + 2), (30, TXN_START + 3), (3, TXN_START + 4),
+                       (50, writer), (50, TXN_START + 5), (10, TXN_START + 6)):
+        check(start, tid)
+    # replacing the delete list invalidates the cached bitvector
+    ids = np.full(len(rows), 5, dtype=np.uint64)
+    t.set_deletes(rows, ids)
+    check(10, TXN_START + 7)
