@@ -235,7 +235,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
         uint64_t claimed = 0;
         if (t == 0 && tile_count)  // not wave-aggregated: built with -amdgpu-atomic-optimizer-strategy=None
             claimed = CLAIM ? atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count)
-                            : (uint64_t)tile * (TILE_WORDS / 32);
+                            : (uint64_t)tile * (TILE_WORDS * 64 / 50);  // diag: ~2 % density, disjoint runs
         const uint32_t next = tile + gridDim.x;
         if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);  // prefetch
         const bool stage = tile_count <= (uint64_t)STAGE;
@@ -293,6 +293,227 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
         __syncthreads();  // C: stage / s_off / s_wave_tot free for the next tile
         tile = next;
     }
+}
+
+// Pair-claimed evaluate + decode: one returning atomic per PAIR of tiles, issued one unit
+// before its result is needed, so the claim latency is covered by the next tile's work.
+// Per pair (tiles A = u, B = u + G of this workgroup's walk):
+//   unit A: wait A's leaves → eval → block scan → copy out the PREVIOUS pair (its claim
+//           returned meanwhile) → prefetch B → decode A into the pair's stage
+//   unit B: wait B's leaves → eval → block scan → claim cnt(A)+cnt(B) → prefetch the next A →
+//           decode B into the stage right after A's run
+// Stage entries are 32-bit row offsets from tile A's first row (tile B sits G·TILE_ROWS
+// further), so the pair's output is ONE contiguous run of cnt(A)+cnt(B) ids, copied out with
+// 16-byte stores (measured: 16 B/lane stores cut this read/write mix's floor from 81 to 77 µs).
+// Copy-out stores are issued before the prefetch they precede, so the wait for the prefetched
+// leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
+// STAGE hits claims on its own and writes straight to the output (dense path).
+template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0>
+__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(EvalArgs a, uint64_t* __restrict__ dir) {
+    // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
+    // fake decode (same LDS traffic, no per-bit loop)
+    constexpr int NW = 2 * PAIRS;
+    constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
+    constexpr int FPW = 64 / FB;
+    constexpr uint64_t FMASK = (FB == 16) ? 0xffffull : 0xffffffffull;
+    constexpr int NPK = (PAIRS + FPW - 1) / FPW;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
+    constexpr int NWAVES = THREADS / 64;
+    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+    __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
+    __shared__ uint64_t s_off;
+    __shared__ uint32_t s_stage[2][2 * STAGE];
+    __shared__ uint32_t s_tile_a[2], s_tile_b[2], s_cnt_a[2], s_cnt_b[2];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const uint32_t G = gridDim.x;
+    // B's rows as offsets from A's first row must fit 32 bits
+    if ((uint64_t)G * TILE_ROWS + TILE_ROWS >= (1ull << 32)) __builtin_trap();
+    const bool write_ids = a.rowids != nullptr;
+    uint64_t pend_claim = 0;  // thread 0: the previous pair's claimed base
+
+    u64x2 v[K][PAIRS];
+    uint32_t tile = blockIdx.x;
+    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+
+    // evaluate the tile in v → r, block scan → per-pair offsets within the tile, tile count
+    auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS]) -> uint64_t {
+        const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
+        eval_words<K, NW>(a.prog, v, r);
+        tail_mask<NW, THREADS>(a, tile_word0, t, r);
+        if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+        uint64_t packed[NPK], incl[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) packed[q] = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p)
+            packed[p / FPW] |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            incl[q] = wave_incl_scan(packed[q], lane);
+            if (lane == 63) s_wave_tot[par][wave][q] = incl[q];
+        }
+        __syncthreads();
+        uint64_t block_tot[NPK], wave_pre[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            uint64_t wp = 0, bt = 0;
+#pragma unroll
+            for (int w = 0; w < NWAVES; ++w) {
+                const uint64_t x = s_wave_tot[par][w][q];
+                if (w < wave) wp += x;
+                bt += x;
+            }
+            block_tot[q] = bt;
+            wave_pre[q] = wp;
+        }
+        uint64_t tile_count = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            pair_off[p] = tile_count +
+                          (((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
+            tile_count += (block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK;
+        }
+        return tile_count;
+    };
+
+    // decode r into stage sp at stage_base with row offsets + delta; dense tiles go direct.
+    // Returns the staged count (0 for a dense tile).
+    auto decode = [&](uint32_t tl, int sp, uint32_t stage_base, uint32_t delta, const uint64_t (&r)[NW],
+                      const uint64_t (&pair_off)[PAIRS], uint64_t tile_count) -> uint32_t {
+        if (tile_count <= (uint64_t)STAGE) {
+            if (DIAG & 2) {
+                for (uint32_t i = t; i < (uint32_t)tile_count; i += THREADS) s_stage[sp][stage_base + i] = delta + i * 53;
+            } else if (write_ids) {
+#pragma unroll
+                for (int p = 0; p < PAIRS; ++p) {
+                    uint32_t off = stage_base + (uint32_t)pair_off[p];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        uint64_t w = r[2 * p + e];
+                        const uint32_t wrow = delta + (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                        while (w) {
+                            s_stage[sp][off++] = wrow + (uint32_t)__builtin_ctzll(w);
+                            w &= w - 1;
+                        }
+                    }
+                }
+            }
+            return (uint32_t)tile_count;
+        }
+        // dense tile: its own claim, direct writes
+        const int64_t row0 = a.row_base + (int64_t)((uint64_t)tl * TILE_ROWS);
+        if (t == 0) {
+            const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count);
+            s_off = c;
+            if (dir) {
+                dir[2 * tl] = c;
+                dir[2 * tl + 1] = tile_count;
+            }
+        }
+        __syncthreads();
+        const uint64_t base = s_off;
+        if (write_ids) {
+#pragma unroll
+            for (int p = 0; p < PAIRS; ++p) {
+                uint64_t off = base + pair_off[p];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    uint64_t w = r[2 * p + e];
+                    const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                    while (w) {
+                        if (off < a.capacity) a.rowids[off] = row0 + (int64_t)(wrow + (uint32_t)__builtin_ctzll(w));
+                        ++off;
+                        w &= w - 1;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // s_off free again
+        return 0;
+    };
+
+    // copy out stage sp (one contiguous run of cnt_a + cnt_b ids) at the claimed base
+    auto copy_out = [&](int sp) {
+        if (t == 0) {
+            s_off = pend_claim;
+            if (dir) {
+                const uint32_t ca = s_cnt_a[sp], cb = s_cnt_b[sp];
+                if (ca) {
+                    dir[2 * s_tile_a[sp]] = pend_claim;
+                    dir[2 * s_tile_a[sp] + 1] = ca;
+                }
+                if (cb) {
+                    dir[2 * s_tile_b[sp]] = pend_claim + ca;
+                    dir[2 * s_tile_b[sp] + 1] = cb;
+                }
+            }
+        }
+        __syncthreads();
+        const uint64_t base = s_off;
+        const uint32_t n = s_cnt_a[sp] + s_cnt_b[sp];
+        if (write_ids && n) {
+            const int64_t row0 = a.row_base + (int64_t)((uint64_t)s_tile_a[sp] * TILE_ROWS);
+            int64_t* out = a.rowids + base;
+            // a leading element when the run starts off a 16-byte boundary
+            const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
+            if (t == 0 && head && base < a.capacity) out[0] = row0 + (int64_t)s_stage[sp][0];
+            const uint64_t room = a.capacity > base ? a.capacity - base : 0;
+            for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
+                if (i + 1 < n && i + 1 < room) {
+                    i64x2 val;
+                    val.x = row0 + (int64_t)s_stage[sp][i];
+                    val.y = row0 + (int64_t)s_stage[sp][i + 1];
+                    *reinterpret_cast<i64x2*>(out + i) = val;
+                } else if (i < room) {
+                    out[i] = row0 + (int64_t)s_stage[sp][i];
+                }
+            }
+        }
+        __syncthreads();  // stage and s_off reusable
+    };
+
+    bool pending = false;  // a claimed pair waits for copy-out (uniform)
+    uint32_t pair = 0;
+    while (tile < a.num_tiles) {
+        const int sp = (int)(pair & 1);
+        // ---- unit A
+        uint64_t r[NW], off[PAIRS];
+        const uint64_t cnt_a_all = eval_scan(tile, 0, r, off);
+        if (pending) copy_out(sp ^ 1);
+        const uint32_t tile_b = tile + G;
+        if (tile_b < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile_b * TILE_WORDS, t, v);
+        const uint32_t ca = decode(tile, sp, 0, 0, r, off, cnt_a_all);
+        // ---- unit B
+        uint32_t cb = 0;
+        uint32_t next = tile_b;
+        if (tile_b < a.num_tiles) {
+            const uint64_t cnt_b_all = eval_scan(tile_b, 1, r, off);
+            next = tile_b + G;
+            const uint32_t staged_b = cnt_b_all <= (uint64_t)STAGE ? (uint32_t)cnt_b_all : 0;
+            if (t == 0 && (ca + staged_b))
+                pend_claim = (DIAG & 1) ? (uint64_t)tile * 5400
+                                        : atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)(ca + staged_b));
+            if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+            cb = decode(tile_b, sp, ca, G * (uint32_t)TILE_ROWS, r, off, cnt_b_all);
+        } else if (t == 0 && ca) {
+            pend_claim = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)ca);
+        }
+        if (t == 0) {
+            s_tile_a[sp] = tile;
+            s_tile_b[sp] = tile_b;
+            s_cnt_a[sp] = ca;
+            s_cnt_b[sp] = cb;
+        }
+        __syncthreads();  // this pair's stage and counts complete
+        pending = true;
+        tile = next;
+        ++pair;
+    }
+    if (pending) copy_out((int)((pair - 1) & 1));
 }
 
 // ------------------------------------------------------------------ row-order pass

@@ -42,6 +42,71 @@ __global__ void fill_random(uint64_t* w, uint64_t pw, uint64_t n_rows, uint32_t 
     }
 }
 
+// Bandwidth floor for this read/write mix: the same persistent tile walk and leaf loads,
+// then WR int64 written per tile as one contiguous coalesced run (no eval / LDS / atomics).
+template <int K, int WR, int MODE = 0>
+__global__ __launch_bounds__(512, 4) void stream_floor(EvalArgs a, int64_t* out) {
+    constexpr int THREADS = 512, PAIRS = 2;
+    constexpr uint64_t TILE_WORDS = THREADS * 2 * PAIRS;
+    const int t = threadIdx.x;
+    u64x2 v[K][PAIRS];
+    __shared__ uint32_t s_st[4096];
+    uint32_t tile = blockIdx.x;
+    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+    while (tile < a.num_tiles) {
+        if (MODE >= 3) __syncthreads();
+        uint64_t x = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int p = 0; p < PAIRS; ++p) x ^= v[k][p].x ^ v[k][p].y;
+        const uint32_t next = tile + gridDim.x;
+        if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        if (WR > 0) {
+            if (MODE == 0) {
+                for (int i = t; i < WR; i += THREADS) out[(uint64_t)tile * WR + i] = (int64_t)(x + i);
+            } else if (MODE == 1) {
+                for (int i = t; i < WR; i += THREADS) __builtin_nontemporal_store((int64_t)(x + i), out + (uint64_t)tile * WR + i);
+            } else if (MODE == 3) {
+                // one block barrier per tile, 16 B stores from registers
+                typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+                i64x2* o = reinterpret_cast<i64x2*>(out + (uint64_t)tile * (WR + 6));
+                for (int i = t; i < (WR + 1) / 2; i += THREADS) {
+                    i64x2 val;
+                    val.x = (int64_t)(x + 2 * i);
+                    val.y = (int64_t)(x + 2 * i + 1);
+                    o[i] = val;
+                }
+            } else if (MODE == 4) {
+                // LDS staging: every thread writes ~WR/THREADS u32, barrier, 16 B stores from LDS
+                for (int i = t; i < WR; i += THREADS) s_st[(i * 5) % WR] = (uint32_t)(x + i);
+                __syncthreads();
+                typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+                i64x2* o = reinterpret_cast<i64x2*>(out + (uint64_t)tile * (WR + 6));
+                for (int i = t; i < (WR + 1) / 2; i += THREADS) {
+                    i64x2 val;
+                    val.x = (int64_t)s_st[2 * i];
+                    val.y = (int64_t)s_st[2 * i + 1];
+                    o[i] = val;
+                }
+            } else {
+                // 16 B per lane
+                typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+                i64x2* o = reinterpret_cast<i64x2*>(out + (uint64_t)tile * (WR + 6));
+                for (int i = t; i < (WR + 1) / 2; i += THREADS) {
+                    i64x2 val;
+                    val.x = (int64_t)(x + 2 * i);
+                    val.y = (int64_t)(x + 2 * i + 1);
+                    o[i] = val;
+                }
+            }
+        } else if (x == 0x123456789ull) {
+            out[tile] = 1;  // keep the loads
+        }
+        tile = next;
+    }
+}
+
 struct Variant {
     std::string name;
     std::function<void(EvalArgs&, hipStream_t)> launch;
@@ -62,7 +127,7 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const unsigned cus = prop.multiProcessorCount;
-    const uint64_t cap = n / 10 + 4096;
+    const uint64_t cap = n / 10 + 4096;  // diag no-claim writes up to n/50 + a tile
     int64_t *ids, *ids2;
     uint64_t* ovf;
     uint64_t *cnt, *dir, *dst_off;
@@ -106,11 +171,50 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_tiles<5, 2, 4096, 512, CL, DE>), dim3(std::min<unsigned>(dtiles, 2 * cus)), \
                                          dim3(512), 0, s, a, dir);                                            \
                   }, 3})
+#define DP(NAME, P, S, T, WGPC)                                                                                \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = (uint32_t)(pw / ((uint64_t)T * 2 * P));                                   \
+                      hipLaunchKernelGGL((eval_decode_pairs<5, P, S, T>), dim3(std::min<unsigned>(a.num_tiles, WGPC * cus)), \
+                                         dim3(T), 0, s, a, dir);                                              \
+                  }, 0})
+    DP("pairs P2 T512 x2/CU", 2, 4096, 512, 2);
+#define DPD(NAME, D)                                                                                           \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = dtiles;                                                                   \
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, D>), dim3(std::min<unsigned>(dtiles, 2 * cus)), \
+                                         dim3(512), 0, s, a, dir);                                            \
+                  }, 3})
+    DPD("pairs diag no-claim", 1);
+    DPD("pairs diag fake-decode", 2);
+    DPD("pairs diag no-claim fake-decode", 3);
+    vs.push_back({"floor: reads only", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 0>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"floor: + ids nt store", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 2490, 1>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"floor: + ids 16B/lane", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 2490, 2>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"floor: 16B + 1 barrier", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 2490, 3>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"floor: 16B + LDS stage", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 2490, 4>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"floor: reads + 2490 ids/tile", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<5, 2490>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
     DX("diag no-claim", false, true);
     DX("diag no-decode", true, false);
     DX("diag no-claim no-decode", false, false);
-    DT("decode P2 T512 x3/CU", 2, 4096, 512, 3);
-    DT("decode P2 T256 x4/CU", 2, 2048, 256, 4);
+
     vs.push_back({"decode + ordered pass", [&](EvalArgs& a, hipStream_t s) {
                       a.num_tiles = dtiles;
                       a.rowids = ids2;
