@@ -311,9 +311,10 @@ namespace {
 struct Leaf {
     const uint64_t* bv = nullptr;
     int column = -1;  // -1: not derived from a column value (visibility, temp)
-    int pred = 0;     // 0 = cmp (v CMP c), 1 = valid (NN)
+    int pred = 0;     // 0 = cmp (v CMP c), 1 = valid (NN), 2 = bin (c <= v < constant2)
     int cmp = 0;
     int64_t constant = 0;
+    int64_t constant2 = 0;
 };
 
 struct Expr;
@@ -583,6 +584,7 @@ struct cubit_table {
     uint64_t nwp = 0;  // padded words
     std::map<int, Column> cols;
     std::map<int, Index> idx;
+    std::map<int, Index> bins;  // CUBIT_INDEX_BINS (secondary)
     // MVCC delta
     std::unique_ptr<DevBuf> del_rows, del_ids;
     uint64_t n_del = 0;
@@ -749,6 +751,7 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     if (int rc = copy_column(t, c, type, data, validity, on_device)) return rc;
     t->cols[col] = std::move(c);
     t->idx.erase(col);
+    t->bins.erase(col);
     return CUBIT_OK;
 }
 
@@ -756,8 +759,10 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     auto it = t->cols.find(col);
     if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
-    if (encoding != CUBIT_INDEX_RANGE && encoding != CUBIT_INDEX_EQUALITY)
+    if (encoding != CUBIT_INDEX_RANGE && encoding != CUBIT_INDEX_EQUALITY && encoding != CUBIT_INDEX_BINS)
         return fail(CUBIT_ERR_INVALID, "encoding %d", encoding);
+    if (encoding == CUBIT_INDEX_BINS && (n < 2 || !values)) return fail(CUBIT_ERR_INVALID, "bins need >= 2 edges");
+    if (n && !values) return fail(CUBIT_ERR_INVALID, "values is null");
     if (int rc = set_device(t->ctx)) return rc;
     const Column& c = it->second;
     Index ix;
@@ -776,29 +781,43 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
         if (!std::is_sorted(ix.keys.begin(), ix.keys.end()))
             return fail(CUBIT_ERR_INVALID, "index keys must be sorted ascending");
         ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end()), ix.keys.end());
+        if (encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) return fail(CUBIT_ERR_INVALID, "bins need >= 2 edges");
     }
-    const int cmp = encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ;
-    for (int64_t k : ix.keys) {
+    const size_t n_bv = encoding == CUBIT_INDEX_BINS ? ix.keys.size() - 1 : ix.keys.size();
+    for (size_t k = 0; k < n_bv; ++k) {
         auto b = std::make_unique<DevBuf>();
         if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
-            return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(),
-                        ix.keys.size());
-        HIP_CHECK(launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows, cmp, k, static_cast<uint64_t*>(b->p),
-                                           t->ctx->stream));
+            return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(), n_bv);
+        hipError_t e;
+        if (encoding == CUBIT_INDEX_BINS)
+            e = launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows, kCmpBetween, ix.keys[k],
+                                         static_cast<uint64_t*>(b->p), t->ctx->stream, ix.keys[k + 1]);
+        else
+            e = launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows,
+                                         encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ, ix.keys[k],
+                                         static_cast<uint64_t*>(b->p), t->ctx->stream);
+        HIP_CHECK(e);
         ix.bvs.push_back(static_cast<uint64_t*>(b->p));
         ix.owned.push_back(std::move(b));
         ix.bytes += t->nwp * 8;
     }
     HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
-    t->idx[col] = std::move(ix);
+    if (encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
+    else t->idx[col] = std::move(ix);
     return CUBIT_OK;
 }
 
 extern "C" int cubit_table_index_info(cubit_table* t, int col, uint32_t* n_bitvectors, uint64_t* bytes) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
-    auto it = t->idx.find(col);
-    const uint32_t nb = it == t->idx.end() ? 0 : (uint32_t)it->second.bvs.size();
-    const uint64_t by = it == t->idx.end() ? 0 : it->second.bytes;
+    uint32_t nb = 0;
+    uint64_t by = 0;
+    for (auto* m : {&t->idx, &t->bins}) {
+        auto it = m->find(col);
+        if (it != m->end()) {
+            nb += (uint32_t)it->second.bvs.size();
+            by += it->second.bytes;
+        }
+    }
     if (n_bitvectors) *n_bitvectors = nb;
     if (bytes) *bytes = by;
     return CUBIT_OK;
@@ -1000,18 +1019,119 @@ struct Planner {
         return raw_compare(col, cmp, c);
     }
 
+    // Cheapest exact plan of lo <= v < hi (half-open, from folded constant filters) out of
+    // the column's binned index, or nullptr when the bins cannot answer it in fewer leaves than
+    // the range index would (2, or 1 for a one-sided bound).
+    ExprP interval_from_bins(int col, int64_t lo, int64_t hi, bool has_lo, bool has_hi) {
+        auto bit = t->bins.find(col);
+        if (bit == t->bins.end()) return nullptr;
+        const Index& b = bit->second;
+        if (b.empty) return mk_false();
+        const std::vector<int64_t>& e = b.keys;
+        const size_t nb = e.size() - 1;
+        size_t first, last;  // bins [first, last)
+        if (!has_lo || lo <= b.vmin) {
+            if (e.front() > b.vmin) return nullptr;  // rows below the first edge are in no bin
+            first = 0;
+        } else {
+            auto it = std::lower_bound(e.begin(), e.end(), lo);
+            if (it == e.end() || *it != lo) return nullptr;
+            first = (size_t)(it - e.begin());
+        }
+        if (!has_hi || hi > b.vmax) {
+            if (e.back() <= b.vmax) return nullptr;  // rows at or above the last edge
+            last = nb;
+        } else {
+            auto it = std::lower_bound(e.begin(), e.end(), hi);
+            if (it == e.end() || *it != hi) return nullptr;
+            last = (size_t)(it - e.begin());
+        }
+        if (last <= first) return mk_false();
+        const size_t range_cost = (has_lo && lo > b.vmin ? 1 : 0) + (has_hi && hi <= b.vmax ? 1 : 0);
+        if (last - first >= std::max<size_t>(range_cost, 1) && t->idx.count(col)) return nullptr;
+        if (last - first > 16) return nullptr;
+        ExprP acc = mk_false();
+        for (size_t k = first; k < last; ++k) {
+            Leaf l;
+            l.bv = b.bvs[k];
+            l.column = col;
+            l.pred = 2;
+            l.constant = e[k];
+            l.constant2 = e[k + 1];
+            acc = mk_bin(Expr::OR, acc, mk_leaf(l));
+        }
+        return acc;
+    }
+
+    // AND node: constant comparisons on one column fold into an interval first (DuckDB
+    // pushes "a <= x AND x < b" as one ConjunctionAndFilter on x, table_filter.cpp:20-40).
+    ExprP plan_and(uint32_t i) {
+        const cubit_filter_node& f = nodes[i];
+        struct Bounds {
+            int64_t lo = INT64_MIN, hi = INT64_MAX;
+            bool has_lo = false, has_hi = false, empty = false;
+            std::vector<uint32_t> members;
+        };
+        std::map<int, Bounds> by_col;
+        std::vector<uint32_t> kids;
+        uint32_t j = i + 1;
+        for (int k = 0; k < f.n_children; ++k) {
+            kids.push_back(j);
+            const cubit_filter_node& c = nodes[j];
+            if (c.kind == CUBIT_FILTER_CONSTANT && c.n_children == 0 && c.cmp != CUBIT_CMP_NE && c.cmp >= 0 &&
+                c.cmp <= 5 && t->bins.count(c.column)) {
+                Bounds& bd = by_col[c.column];
+                const int64_t v = c.constant;
+                auto lower = [&](int64_t x) { bd.lo = bd.has_lo ? std::max(bd.lo, x) : x; bd.has_lo = true; };
+                auto upper = [&](int64_t x) { bd.hi = bd.has_hi ? std::min(bd.hi, x) : x; bd.has_hi = true; };
+                switch (c.cmp) {
+                case CUBIT_CMP_GE: lower(v); break;
+                case CUBIT_CMP_GT: if (v == INT64_MAX) bd.empty = true; else lower(v + 1); break;
+                case CUBIT_CMP_LT: upper(v); break;
+                case CUBIT_CMP_LE: if (v != INT64_MAX) upper(v + 1); break;
+                case CUBIT_CMP_EQ:
+                    lower(v);
+                    if (v == INT64_MAX) bd.empty = true; else upper(v + 1);
+                    break;
+                default: break;
+                }
+                bd.members.push_back(j);
+            }
+            j = (uint32_t)subtree_end(j);
+        }
+        std::vector<char> done(n_nodes, 0);
+        ExprP acc = mk_true();
+        for (auto& [col, bd] : by_col) {
+            ExprP e;
+            if (bd.empty || (bd.has_lo && bd.has_hi && bd.hi <= bd.lo)) e = mk_false();
+            else e = interval_from_bins(col, bd.lo, bd.hi, bd.has_lo, bd.has_hi);
+            if (rc) return nullptr;
+            if (!e) continue;
+            for (uint32_t m : bd.members) done[m] = 1;
+            acc = mk_bin(Expr::AND, acc, e);
+        }
+        for (uint32_t k : kids) {
+            if (done[k]) continue;
+            ExprP c = plan(k);
+            if (!c) return nullptr;
+            acc = mk_bin(Expr::AND, acc, c);
+        }
+        return acc;
+    }
+
     ExprP plan(uint32_t i) {
         if (rc) return nullptr;
         const cubit_filter_node& f = nodes[i];
         switch (f.kind) {
         case CUBIT_FILTER_AND:
+            return plan_and(i);
         case CUBIT_FILTER_OR: {
-            ExprP acc = f.kind == CUBIT_FILTER_AND ? mk_true() : mk_false();
+            ExprP acc = mk_false();
             uint32_t j = i + 1;
             for (int k = 0; k < f.n_children; ++k) {
                 ExprP c = plan(j);
                 if (!c) return nullptr;
-                acc = mk_bin(f.kind == CUBIT_FILTER_AND ? Expr::AND : Expr::OR, acc, c);
+                acc = mk_bin(Expr::OR, acc, c);
                 j = (uint32_t)subtree_end(j);
             }
             return acc;
@@ -1092,7 +1212,7 @@ int fit(cubit_table* t, ExprP& e) {
 // set the rows whose visible value passes the leaf predicate.
 __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ values,
                                   const uint64_t* __restrict__ versions, uint64_t n, uint64_t start_time,
-                                  uint64_t tid, int pred, int cmp, int64_t c, uint64_t* __restrict__ bv) {
+                                  uint64_t tid, int pred, int cmp, int64_t c, int64_t c2, uint64_t* __restrict__ bv) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t ver = versions[i];
@@ -1112,6 +1232,7 @@ __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_
         const int64_t v = values[i];
         bool p;
         if (pred == 1) p = true;
+        else if (pred == 2) p = v >= c && v < c2;
         else if (cmp == 0) p = v == c;
         else if (cmp == 1) p = v != c;
         else if (cmp == 2) p = v < c;
@@ -1141,7 +1262,7 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
             hipLaunchKernelGGL(patch_leaf_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, t->ctx->stream,
                                static_cast<const int64_t*>(u.rows->p), static_cast<const int64_t*>(u.values->p),
                                static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time, txn->transaction_id,
-                               e->leaf.pred, e->leaf.cmp, e->leaf.constant, copy);
+                               e->leaf.pred, e->leaf.cmp, e->leaf.constant, e->leaf.constant2, copy);
             HIP_CHECK(hipGetLastError());
             patched[e->leaf.bv] = copy;
         }

@@ -69,8 +69,10 @@ hipError_t launch_eval_count(const EvalArgs& a, hipStream_t stream);
 // lay per-tile runs out in row order: dst[dst_off[i] ...] = src[dir run i]
 hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* dst_off, const int64_t* src,
                              uint64_t capacity, int64_t* dst, hipStream_t stream);
+// cmp = CUBIT_CMP_* (0..5) or kCmpBetween (constant <= v < constant2)
+constexpr int kCmpBetween = 6;
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
-                                    int64_t constant, uint64_t* out_words, hipStream_t stream);
+                                    int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2 = 0);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,

@@ -557,14 +557,16 @@ __global__ __launch_bounds__(256) void order_copy_kernel(const uint64_t* __restr
 
 // ------------------------------------------------------------------ K0: compare → bitvector
 
+// CMP 0..5 = EQ NE LT LE GT GE (CUBIT_CMP_*); 6 = c <= v < c2 (bin of a CUBIT_INDEX_BINS index)
 template <int CMP>
-__device__ __forceinline__ bool cmp_op(int64_t v, int64_t c) {
+__device__ __forceinline__ bool cmp_op(int64_t v, int64_t c, int64_t c2) {
     if (CMP == 0) return v == c;
     if (CMP == 1) return v != c;
     if (CMP == 2) return v < c;
     if (CMP == 3) return v <= c;
     if (CMP == 4) return v > c;
-    return v >= c;
+    if (CMP == 5) return v >= c;
+    return v >= c && v < c2;
 }
 
 // Each wave produces 64 consecutive words: for word j every lane tests one row and the
@@ -573,7 +575,7 @@ template <typename T, int CMP>
 __global__ __launch_bounds__(256) void compare_bitvector_kernel(const T* __restrict__ col,
                                                                 const uint64_t* __restrict__ validity,
                                                                 uint64_t n_rows, uint64_t n_words_padded,
-                                                                int64_t c, uint64_t* __restrict__ out) {
+                                                                int64_t c, int64_t c2, uint64_t* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(256) void compare_bitvector_kernel(const T* __restr
             bool p = false;
             if (row < n_rows) {
                 const bool valid = validity ? ((validity[w0 + j] >> lane) & 1ull) : true;
-                p = valid && cmp_op<CMP>((int64_t)col[row], c);
+                p = valid && cmp_op<CMP>((int64_t)col[row], c, c2);
             }
             const uint64_t b = __ballot(p);
             if (lane == j) mine = b;
@@ -594,21 +596,27 @@ __global__ __launch_bounds__(256) void compare_bitvector_kernel(const T* __restr
 }
 
 template <typename T>
-hipError_t launch_compare_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp, int64_t c,
+hipError_t launch_compare_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp, int64_t c, int64_t c2,
                             uint64_t* out, hipStream_t stream) {
     const uint64_t nw = padded_words(n_rows);
     const uint64_t waves = nw / 64;
     const uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
     const dim3 grid((unsigned)std::max<uint64_t>(blocks, 1)), block(256);
+#define CUBIT_CMP_CASE(C)                                                                                       \
+    case C:                                                                                                     \
+        hipLaunchKernelGGL((compare_bitvector_kernel<T, C>), grid, block, 0, stream, col, validity, n_rows, nw, c, c2, out); \
+        break;
     switch (cmp) {
-    case 0: hipLaunchKernelGGL((compare_bitvector_kernel<T, 0>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
-    case 1: hipLaunchKernelGGL((compare_bitvector_kernel<T, 1>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
-    case 2: hipLaunchKernelGGL((compare_bitvector_kernel<T, 2>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
-    case 3: hipLaunchKernelGGL((compare_bitvector_kernel<T, 3>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
-    case 4: hipLaunchKernelGGL((compare_bitvector_kernel<T, 4>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
-    case 5: hipLaunchKernelGGL((compare_bitvector_kernel<T, 5>), grid, block, 0, stream, col, validity, n_rows, nw, c, out); break;
+        CUBIT_CMP_CASE(0)
+        CUBIT_CMP_CASE(1)
+        CUBIT_CMP_CASE(2)
+        CUBIT_CMP_CASE(3)
+        CUBIT_CMP_CASE(4)
+        CUBIT_CMP_CASE(5)
+        CUBIT_CMP_CASE(6)
     default: return hipErrorInvalidValue;
     }
+#undef CUBIT_CMP_CASE
     return hipGetLastError();
 }
 
@@ -778,12 +786,12 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
 }
 
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
-                                    int64_t constant, uint64_t* out_words, hipStream_t stream) {
+                                    int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2) {
     if (type == 0)
-        return launch_compare_t<int32_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, constant, out_words,
-                                         stream);
-    return launch_compare_t<int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, constant, out_words,
-                                     stream);
+        return launch_compare_t<int32_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, constant, constant2,
+                                         out_words, stream);
+    return launch_compare_t<int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, constant, constant2,
+                                     out_words, stream);
 }
 
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,

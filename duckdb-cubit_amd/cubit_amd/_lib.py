@@ -22,7 +22,7 @@ ERR_INVALID, ERR_HIP, ERR_OOM, ERR_UNSUPPORTED, ERR_CAPACITY, ERR_DEVICE = 1, 2,
 TYPE_INT32, TYPE_INT64 = 0, 1
 CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
 FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = range(5)
-INDEX_RANGE, INDEX_EQUALITY = 0, 1
+INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2

@@ -58,6 +58,9 @@ extern "C" {
 /* ---- bitmap index encodings */
 #define CUBIT_INDEX_RANGE 0     /* L_j = {valid rows with v < edge_j}; exact for constants on edges */
 #define CUBIT_INDEX_EQUALITY 1  /* E_k = {rows with v == value_k} (CUBIT's equality encoding) */
+#define CUBIT_INDEX_BINS 2      /* B_i = {valid rows with edge_i <= v < edge_i+1}: kept beside a range or
+                                   equality index on the same column; a range whose bounds are bin
+                                   edges reads its bins instead of two range bitvectors when fewer */
 
 /* ---- bitvector program opcodes (operands >= 0 are leaf indices, postfix order) */
 #define CUBIT_OP_AND (-1)
@@ -170,9 +173,10 @@ int cubit_table_info(cubit_table *t, uint64_t *n_rows, int64_t *row_base, cubit_
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
 /* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
- * distinct values of the column" (exact for every constant). */
+ * distinct values of the column" (exact for every constant). RANGE / EQUALITY replace the
+ * column's primary index; BINS (n >= 2 edges) adds a secondary binned index. */
 int cubit_table_build_index(cubit_table *t, int col, int encoding, const int64_t *values, uint32_t n);
-/* Number of bitvectors and bytes held by the index on col (0 if none). */
+/* Number of bitvectors and bytes held by the indexes on col, all encodings (0 if none). */
 int cubit_table_index_info(cubit_table *t, int col, uint32_t *n_bitvectors, uint64_t *bytes);
 
 /* MVCC delta. Deletes: rows with their delete ids (ChunkVectorInfo::deleted,

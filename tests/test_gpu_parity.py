@@ -340,3 +340,48 @@ def test_visibility_bitvector_cache_across_snapshots(ctx):
     ids = np.full(len(rows), 5, dtype=np.uint64)
     t.set_deletes(rows, ids)
     check(10, TXN_START + 7)
+
+
+def test_q6_with_year_bins_reads_four_bitvectors(ctx, golden):
+    """A binned index (year edges) beside the month range index: Q6's one-year shipdate range
+    reads one bin instead of two range bitvectors (K 5 → 4); rows identical."""
+    li = lineitem(0.1)
+    t = q6_table(ctx, li)
+    years = [F.date(y, 1, 1) for y in range(1992, 2000)]
+    t.build_index(0, L.INDEX_BINS, years)
+    got = t.scan(F.q6_filter_set())
+    assert np.array_equal(got, oracle_q6(li))
+    k, passes = t.last_plan()
+    assert k == 4 and passes == 1
+
+
+@pytest.mark.parametrize("with_range", [True, False])
+def test_bins_index_intervals_vs_oracle(ctx, with_range):
+    n = 300_007
+    a = uniform_i32(11, n, 1000).astype(np.int64)
+    valid = np.random.default_rng(5).random(n) > 0.05
+    t = CubitTable(ctx, n)
+    t.add_column(0, a, validity_from_mask(valid))
+    if with_range:
+        t.build_index(0, L.INDEX_RANGE, [100, 200, 500, 900])
+    edges = [0, 100, 200, 300, 500, 700, 1000]
+    t.build_index(0, L.INDEX_BINS, edges)
+    col = O.Column(a, validity_from_mask(valid))
+    cases = [((">=", 100), ("<", 200)), ((">=", 200), ("<", 700)), ((">", 99), ("<=", 299)), ((">=", 150), ("<", 300)),
+             ((">=", 0), ("<", 1000)), ((">=", 500),), (("<", 300),), (("=", 5),), ((">=", 700), ("<", 100)),
+             ((">=", 300), ("<", 500), ("<", 400))]
+    for c in cases:
+        filt = F.ConstantFilter(*c[0]) if len(c) == 1 else F.ConjunctionAndFilter([F.ConstantFilter(*x) for x in c])
+        fs = F.TableFilterSet({0: filt})
+        got = t.scan(fs)
+        ref = O.table_scan([col], F.serialize(fs), n)
+        assert np.array_equal(got, ref), c
+    # a bin leaf patched for an update the transaction sees
+    rows = np.arange(0, n, 13, dtype=np.int64)
+    t.set_updates(0, rows, np.full(len(rows), 150), np.full(len(rows), TXN_START + 1, dtype=np.uint64))
+    fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 100), F.ConstantFilter("<", 200)])})
+    got = t.scan(fs, txn=L.Txn(2, TXN_START + 1))
+    colu = O.Column(a, validity_from_mask(valid), updates=(rows, np.full(len(rows), 150, dtype=np.int64),
+                                                           np.full(len(rows), TXN_START + 1, dtype=np.uint64)))
+    ref = O.table_scan([colu], F.serialize(fs), n, tx=O.Mvcc(2, TXN_START + 1))
+    assert np.array_equal(got, ref)
