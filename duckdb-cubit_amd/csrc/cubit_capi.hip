@@ -429,6 +429,33 @@ struct Emitter {
         prog.nops += 1u << (4 * k);
         --depth;
     }
+    // a conjunction of (possibly complemented) leaves: AND nodes, ANDNOT with a leaf on the right
+    static bool conj_leaves(const ExprP& e, std::vector<std::pair<Leaf, bool>>& out) {
+        switch (e->kind) {
+        case Expr::LEAF: out.push_back({e->leaf, e->neg}); return true;
+        case Expr::AND: return conj_leaves(e->a, out) && conj_leaves(e->b, out);
+        case Expr::ANDNOT:
+            if (e->b->kind != Expr::LEAF) return false;
+            if (!conj_leaves(e->a, out)) return false;
+            out.push_back({e->b->leaf, !e->b->neg});
+            return true;
+        default: return false;
+        }
+    }
+    // top level: a pure conjunction is emitted as a left-deep AND chain, which the kernels
+    // evaluate branch-free (is_conjunction, cubit_kernels.hip)
+    void emit_top(const ExprP& e) {
+        std::vector<std::pair<Leaf, bool>> c;
+        if (e->kind != Expr::LEAF && conj_leaves(e, c)) {
+            leaf(c[0].first, c[0].second);
+            for (size_t i = 1; i < c.size(); ++i) {
+                leaf(c[i].first, c[i].second);
+                op(OP_AND);
+            }
+            return;
+        }
+        emit(e);
+    }
     void emit(const ExprP& e) {
         switch (e->kind) {
         case Expr::LEAF: leaf(e->leaf, e->neg); return;
@@ -501,7 +528,7 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
     }
     if (st.size() != 1) return fail(CUBIT_ERR_INVALID, "program leaves %zu values on the stack", st.size());
     Emitter em;
-    em.emit(st[0]);
+    em.emit_top(st[0]);
     if (!em.ok || em.max_depth > 4)
         return fail(CUBIT_ERR_UNSUPPORTED, "program needs %d leaves / depth %d (max %d / 4)", count_leaves(st[0]),
                     em.max_depth, kMaxLeaves);
@@ -1161,7 +1188,7 @@ struct Planner {
 // Materialise a subexpression into a scratch bitvector (bits-only pass).
 int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
     Emitter em;
-    em.emit(e);
+    em.emit_top(e);
     if (!em.ok || em.max_depth > 4) return fail(CUBIT_ERR_UNSUPPORTED, "subexpression too deep");
     if (int rc = scratch_bv(t, out)) return rc;
     t->last_passes++;
@@ -1170,7 +1197,7 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
 
 bool fits(const ExprP& e) {
     Emitter em;
-    em.emit(e);
+    em.emit_top(e);
     return em.ok && em.max_depth <= 4;
 }
 
@@ -1345,7 +1372,7 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     }
     if (int rc = fit(t, e)) return rc;
     Emitter em;
-    em.emit(e);
+    em.emit_top(e);
     t->last_leaves = em.prog.n_leaves;
     t->last_passes++;
     return run_eval(ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count, nullptr,

@@ -50,9 +50,25 @@ __device__ __forceinline__ uint64_t apply_op(uint32_t op, uint64_t a, uint64_t b
 // Evaluate the program on NW words per thread. Leaves are loaded by the caller
 // (compile-time indexed); the stack is 4 deep and shifted with constant indices so it stays
 // in VGPRs.
-template <int K, int NW>
+// CONJ: the program is a left-deep chain of ANDs (launch_eval_* detects it), evaluated
+// branch-free as the AND of the (possibly complemented) leaves.
+template <int K, int NW, bool CONJ = false>
 __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 (&v)[K][NW / 2],
                                            uint64_t (&r)[NW]) {
+    if (CONJ) {
+#pragma unroll
+        for (int j = 0; j < NW; ++j) r[j] = ~0ull;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t neg = ((prog.negate >> k) & 1u) ? ~0ull : 0ull;
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const u64x2 p = v[k][j >> 1];
+                r[j] &= ((j & 1) ? p.y : p.x) ^ neg;
+            }
+        }
+        return;
+    }
     uint64_t s0[NW], s1[NW], s2[NW], s3[NW];
 #pragma unroll
     for (int j = 0; j < NW; ++j) s0[j] = s1[j] = s2[j] = s3[j] = 0;
@@ -125,7 +141,7 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
 
 // count(*) of the program and/or its result bitvector; one tile per workgroup, one
 // non-returning atomic per tile.
-template <int K, int PAIRS>
+template <int K, int PAIRS, bool CONJ = false>
 __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
     constexpr int THREADS = 256, NW = 2 * PAIRS;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
@@ -134,7 +150,7 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
     u64x2 v[K][PAIRS];
     load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
     uint64_t r[NW];
-    eval_words<K, NW>(a.prog, v, r);
+    eval_words<K, NW, CONJ>(a.prog, v, r);
     tail_mask<NW, THREADS>(a, tile_word0, t, r);
     if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
     __shared__ uint64_t s_part[THREADS / 64];
@@ -174,7 +190,7 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
 // CLAIM / DECODE = false are diagnostic builds (scripts/kbench.hip), never launched by the
 // library. __launch_bounds__: two workgroups per CU (2·THREADS/256 waves per SIMD) caps
 // VGPRs at 128.
-template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true>
+template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true, bool CONJ = false>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
     constexpr int NW = 2 * PAIRS;
     constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
@@ -197,7 +213,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
     while (tile < a.num_tiles) {
         const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
         uint64_t r[NW];
-        eval_words<K, NW>(a.prog, v, r);
+        eval_words<K, NW, CONJ>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
         uint64_t packed[NPK], incl[NPK];
@@ -285,9 +301,23 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
             }
             __syncthreads();  // B: staged run and its offset visible
             const uint64_t off0 = s_off;
-            for (uint64_t i = t; i < tile_count; i += THREADS) {
-                const uint64_t g = off0 + i;
-                if (g < a.capacity) a.rowids[g] = row0 + (int64_t)s_stage[i];
+            // 16-byte stores (a wave writes 1 KiB per instruction); one leading 8-byte element
+            // when the run starts off a 16-byte boundary
+            typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+            int64_t* out = a.rowids + off0;
+            const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
+            const uint64_t room = a.capacity > off0 ? a.capacity - off0 : 0;
+            const uint32_t n = (uint32_t)tile_count;
+            if (t == 0 && head && room) out[0] = row0 + (int64_t)s_stage[0];
+            for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
+                if (i + 1 < n && i + 1 < room) {
+                    i64x2 val;
+                    val.x = row0 + (int64_t)s_stage[i];
+                    val.y = row0 + (int64_t)s_stage[i + 1];
+                    *reinterpret_cast<i64x2*>(out + i) = val;
+                } else if (i < room) {
+                    out[i] = row0 + (int64_t)s_stage[i];
+                }
             }
         }
         __syncthreads();  // C: stage / s_off / s_wave_tot free for the next tile
@@ -308,7 +338,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
 // Copy-out stores are issued before the prefetch they precede, so the wait for the prefetched
 // leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
 // STAGE hits claims on its own and writes straight to the output (dense path).
-template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0>
+template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, bool CONJ = false>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(EvalArgs a, uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
     // fake decode (same LDS traffic, no per-bit loop)
@@ -324,7 +354,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
     __shared__ uint64_t s_off;
     __shared__ uint32_t s_stage[2][2 * STAGE];
-    __shared__ uint32_t s_tile_a[2], s_tile_b[2], s_cnt_a[2], s_cnt_b[2];
+    __shared__ uint32_t s_tile_a[2], s_tile_b[2], s_cnt_a[2], s_cnt_b[2], s_dense[2];
 
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -342,7 +372,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     // evaluate the tile in v → r, block scan → per-pair offsets within the tile, tile count
     auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS]) -> uint64_t {
         const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
-        eval_words<K, NW>(a.prog, v, r);
+        eval_words<K, NW, CONJ>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
         uint64_t packed[NPK], incl[NPK];
@@ -441,13 +471,14 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         if (t == 0) {
             s_off = pend_claim;
             if (dir) {
+                // staged tiles (dense ones wrote their own entry); empty tiles get {0, 0}
                 const uint32_t ca = s_cnt_a[sp], cb = s_cnt_b[sp];
-                if (ca) {
-                    dir[2 * s_tile_a[sp]] = pend_claim;
+                if (!(s_dense[sp] & 1)) {
+                    dir[2 * s_tile_a[sp]] = ca ? pend_claim : 0;
                     dir[2 * s_tile_a[sp] + 1] = ca;
                 }
-                if (cb) {
-                    dir[2 * s_tile_b[sp]] = pend_claim + ca;
+                if (!(s_dense[sp] & 2) && s_tile_b[sp] < a.num_tiles) {
+                    dir[2 * s_tile_b[sp]] = cb ? pend_claim + ca : 0;
                     dir[2 * s_tile_b[sp] + 1] = cb;
                 }
             }
@@ -490,8 +521,10 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         // ---- unit B
         uint32_t cb = 0;
         uint32_t next = tile_b;
+        bool dense_b = false;
         if (tile_b < a.num_tiles) {
             const uint64_t cnt_b_all = eval_scan(tile_b, 1, r, off);
+            dense_b = cnt_b_all > (uint64_t)STAGE;
             next = tile_b + G;
             const uint32_t staged_b = cnt_b_all <= (uint64_t)STAGE ? (uint32_t)cnt_b_all : 0;
             if (t == 0 && (ca + staged_b))
@@ -507,6 +540,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
             s_tile_b[sp] = tile_b;
             s_cnt_a[sp] = ca;
             s_cnt_b[sp] = cb;
+            s_dense[sp] = (cnt_a_all > (uint64_t)STAGE ? 1u : 0u) | (dense_b ? 2u : 0u);
         }
         __syncthreads();  // this pair's stage and counts complete
         pending = true;
@@ -736,16 +770,33 @@ uint64_t decode_tile_words() { return (uint64_t)kDecodeThreads * 2 * kDecodePair
 uint64_t count_tile_words() { return 256ull * 2 * kCountPairs; }
 int decode_block_threads() { return kDecodeThreads; }
 
+// A left-deep chain of ANDs (nops = 0,1,1,…; every op AND) evaluates as a plain conjunction.
+bool is_conjunction(const EvalProgram& p) {
+    if (p.n_leaves == 0 || prog_nops(p, 0) != 0) return false;
+    for (uint32_t k = 1; k < p.n_leaves; ++k)
+        if (prog_nops(p, (int)k) != 1 || ((p.ops >> (2 * (k - 1))) & 3u) != OP_AND) return false;
+    return true;
+}
+
+// production decode: the pair-claimed kernel (scripts/kbench.hip: 83 µs vs 94 µs for the
+// per-tile claim kernel on SF100 Q6-shaped leaves)
 template <int K>
 hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s) {
-    hipLaunchKernelGGL((eval_decode_tiles<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
-                       dim3(kDecodeThreads), 0, s, a, dir);
+    if (is_conjunction(a.prog))
+        hipLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, true>), dim3(grid),
+                           dim3(kDecodeThreads), 0, s, a, dir);
+    else
+        hipLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
+                           dim3(kDecodeThreads), 0, s, a, dir);
     return hipGetLastError();
 }
 
 template <int K>
 hipError_t launch_count_k(const EvalArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, a);
+    if (is_conjunction(a.prog))
+        hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs, true>), dim3(a.num_tiles), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -155,8 +155,23 @@ int main(int argc, char** argv) {
 
     std::vector<Variant> vs;
     const uint32_t dtiles = (uint32_t)(pw / decode_tile_words());
-    vs.push_back({"decode tiles (prod)", [&](EvalArgs& a, hipStream_t s) {
+    vs.push_back({"decode (prod, interpreted)", [&](EvalArgs& a, hipStream_t s) {
                       a.num_tiles = dtiles;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 0});
+    vs.push_back({"tiles kernel (r01 prod)", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((eval_decode_tiles<5, 2, 4096, 512>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
+                                         dim3(512), 0, s, a, dir);
+                  }, 0});
+    // the same predicate as a left-deep AND chain with complemented leaves → branch-free CONJ path
+    vs.push_back({"decode conj (prod)", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.negate = 0b01010;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      for (int i = 0; i < 4; ++i) a.prog.ops |= (uint32_t)OP_AND << (2 * i);
                       CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
                   }, 0});
 #define DT(NAME, P, S, T, WGPC)                                                                                \
@@ -184,6 +199,15 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, D>), dim3(std::min<unsigned>(dtiles, 2 * cus)), \
                                          dim3(512), 0, s, a, dir);                                            \
                   }, 3})
+    vs.push_back({"pairs conj", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.negate = 0b01010;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, 0, true>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
+                                         dim3(512), 0, s, a, dir);
+                  }, 0});
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);
