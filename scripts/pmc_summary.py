@@ -13,7 +13,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 ROUND = sys.argv[1] if len(sys.argv) > 1 else "r01"
-KERNEL = "eval_decode_tiles"
+KERNEL = "eval_decode_pairs"
 
 
 def rows(pattern):
