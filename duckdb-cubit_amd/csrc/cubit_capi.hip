@@ -127,11 +127,11 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         }
         stop = ctx->evs[ctx->n_timed].second;
     }
+    hipEvent_t start = stop ? ctx->evs[ctx->n_timed].first : nullptr;
+    if (stop) ctx->n_timed++;
     if (mode == RunMode::kCount) {
         a.num_tiles = (uint32_t)(pw / count_tile_words());
-        if (stop) HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed++].first, ctx->stream));
-        HIP_CHECK(launch_eval_count(a, ctx->stream));
-        if (stop) HIP_CHECK(hipEventRecord(stop, ctx->stream));
+        HIP_CHECK(launch_eval_count(a, ctx->stream, start, stop));
         return CUBIT_OK;
     }
     const uint64_t tiles = pw / decode_tile_words();
@@ -143,9 +143,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.capacity = rowids ? capacity : 0;
     // persistent grid: two 512-thread workgroups per CU (VGPR-limited to 4 waves per SIMD)
     const unsigned grid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)ctx->n_cus * 2);
-    if (stop) HIP_CHECK(hipEventRecord(ctx->evs[ctx->n_timed++].first, ctx->stream));
-    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream));
-    if (stop) HIP_CHECK(hipEventRecord(stop, ctx->stream));
+    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop));
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (ordered && rowids)

@@ -63,9 +63,13 @@ uint64_t decode_tile_words();  // words per eval_decode_tiles tile
 uint64_t count_tile_words();   // words per eval_count_kernel tile
 int decode_block_threads();
 // evaluate + decode into per-tile runs; dir (optional) gets {start, length} per tile
-hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream);
+// ev0 / ev1 (optional): events stamped by the kernel dispatch itself (hipExtLaunchKernel), so
+// their elapsed time is the kernel's execution, as rocprofv3's kernel trace reports it
+hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream,
+                              hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // evaluate + count (and/or write the result bitvector)
-hipError_t launch_eval_count(const EvalArgs& a, hipStream_t stream);
+hipError_t launch_eval_count(const EvalArgs& a, hipStream_t stream, hipEvent_t ev0 = nullptr,
+                             hipEvent_t ev1 = nullptr);
 // lay per-tile runs out in row order: dst[dst_off[i] ...] = src[dir run i]
 hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* dst_off, const int64_t* src,
                              uint64_t capacity, int64_t* dst, hipStream_t stream);

@@ -18,6 +18,7 @@
 //
 // Bandwidth-bound integer work: no MFMA. Loads are 16 B per lane (dwordx4), a wave moves
 // 1 KiB per load instruction; row ids are staged in LDS and written as contiguous runs.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "cubit_internal.hpp"
@@ -781,49 +782,52 @@ bool is_conjunction(const EvalProgram& p) {
 // production decode: the pair-claimed kernel (scripts/kbench.hip: 83 µs vs 94 µs for the
 // per-tile claim kernel on SF100 Q6-shaped leaves)
 template <int K>
-hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s) {
+hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
+                           hipEvent_t e1) {
     if (is_conjunction(a.prog))
-        hipLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, true>), dim3(grid),
-                           dim3(kDecodeThreads), 0, s, a, dir);
+        hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, true>), dim3(grid),
+                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
     else
-        hipLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
-                           dim3(kDecodeThreads), 0, s, a, dir);
+        hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
+                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
     return hipGetLastError();
 }
 
 template <int K>
-hipError_t launch_count_k(const EvalArgs& a, hipStream_t s) {
+hipError_t launch_count_k(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (is_conjunction(a.prog))
-        hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs, true>), dim3(a.num_tiles), dim3(256), 0, s, a);
+        hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, true>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0,
+                              a);
     else
-        hipLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, a);
+        hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0, a);
     return hipGetLastError();
 }
 
-hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s) {
+hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1) {
     switch (a.prog.n_leaves) {
-    case 1: return launch_decode_k<1>(a, dir, grid, s);
-    case 2: return launch_decode_k<2>(a, dir, grid, s);
-    case 3: return launch_decode_k<3>(a, dir, grid, s);
-    case 4: return launch_decode_k<4>(a, dir, grid, s);
-    case 5: return launch_decode_k<5>(a, dir, grid, s);
-    case 6: return launch_decode_k<6>(a, dir, grid, s);
-    case 7: return launch_decode_k<7>(a, dir, grid, s);
-    case 8: return launch_decode_k<8>(a, dir, grid, s);
+    case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1);
+    case 2: return launch_decode_k<2>(a, dir, grid, s, e0, e1);
+    case 3: return launch_decode_k<3>(a, dir, grid, s, e0, e1);
+    case 4: return launch_decode_k<4>(a, dir, grid, s, e0, e1);
+    case 5: return launch_decode_k<5>(a, dir, grid, s, e0, e1);
+    case 6: return launch_decode_k<6>(a, dir, grid, s, e0, e1);
+    case 7: return launch_decode_k<7>(a, dir, grid, s, e0, e1);
+    case 8: return launch_decode_k<8>(a, dir, grid, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_eval_count(const EvalArgs& a, hipStream_t s) {
+hipError_t launch_eval_count(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (a.prog.n_leaves) {
-    case 1: return launch_count_k<1>(a, s);
-    case 2: return launch_count_k<2>(a, s);
-    case 3: return launch_count_k<3>(a, s);
-    case 4: return launch_count_k<4>(a, s);
-    case 5: return launch_count_k<5>(a, s);
-    case 6: return launch_count_k<6>(a, s);
-    case 7: return launch_count_k<7>(a, s);
-    case 8: return launch_count_k<8>(a, s);
+    case 1: return launch_count_k<1>(a, s, e0, e1);
+    case 2: return launch_count_k<2>(a, s, e0, e1);
+    case 3: return launch_count_k<3>(a, s, e0, e1);
+    case 4: return launch_count_k<4>(a, s, e0, e1);
+    case 5: return launch_count_k<5>(a, s, e0, e1);
+    case 6: return launch_count_k<6>(a, s, e0, e1);
+    case 7: return launch_count_k<7>(a, s, e0, e1);
+    case 8: return launch_count_k<8>(a, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
 }
