@@ -68,6 +68,7 @@ struct cubit_ctx {
     int64_t* tmp_ids = nullptr;
     uint64_t tmp_cap = 0;
     int64_t* partials = nullptr;
+    uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
 };
 
 namespace {
@@ -115,8 +116,8 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.row_base = row_base;
     a.count = d_count;
     a.result_words = result_words;
+    a.ticket = ctx->ticket;
     const uint64_t pw = padded_words(n_rows);
-    HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
     hipEvent_t stop = nullptr;
     if (timed && ctx->timing) {
         if (ctx->n_timed == ctx->evs.size()) {
@@ -173,9 +174,13 @@ int cubit_ctx_create(int device, cubit_ctx** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->n_cus = prop.multiProcessorCount;
-    if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess) {
+    if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&ctx->ticket, 2 * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(ctx->ticket, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (ctx->partials) (void)hipFree(ctx->partials);
+        if (ctx->ticket) (void)hipFree(ctx->ticket);
         delete ctx;
-        return fail(CUBIT_ERR_OOM, "partials allocation failed");
+        return fail(CUBIT_ERR_OOM, "context workspace allocation failed");
     }
     *out = ctx;
     return CUBIT_OK;
@@ -188,6 +193,7 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (ctx->dst_off) (void)hipFree(ctx->dst_off);
     if (ctx->tmp_ids) (void)hipFree(ctx->tmp_ids);
     if (ctx->partials) (void)hipFree(ctx->partials);
+    if (ctx->ticket) (void)hipFree(ctx->ticket);
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);

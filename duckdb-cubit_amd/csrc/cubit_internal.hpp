@@ -53,9 +53,13 @@ struct EvalArgs {
     int64_t row_base;
     int64_t* rowids;
     uint64_t capacity;
-    uint64_t* count;         // running count (claims) / count(*) result; zeroed by the launcher
+    uint64_t* count;         // result: the number of qualifying rows (written at kernel end)
     uint64_t* result_words;  // optional evaluated bitvector
     uint32_t num_tiles;
+    // claim ticket (context-owned, 2 words, zero between launches): [0] running claim
+    // counter, [1] finished workgroups. The last workgroup to finish publishes *count and
+    // re-zeroes both words, so no memset launch precedes a scan (finish_ticket).
+    uint64_t* ticket;
 };
 
 // launchers (cubit_kernels.hip); all asynchronous on `stream`

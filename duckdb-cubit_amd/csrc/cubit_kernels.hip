@@ -44,6 +44,21 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     return x;
 }
 
+// Called by thread 0 of every workgroup after its last claim: the last workgroup to arrive
+// publishes the claim total to *count and re-arms the ticket for the next launch on the
+// stream (stream order guarantees that launch sees the zeroes).
+__device__ __forceinline__ void finish_ticket(uint64_t* ticket, uint64_t* count) {
+    __threadfence();
+    const unsigned long long arrived = atomicAdd(reinterpret_cast<unsigned long long*>(ticket + 1), 1ull);
+    if (arrived == (unsigned long long)(gridDim.x - 1)) {
+        __threadfence();
+        const unsigned long long total = atomicAdd(reinterpret_cast<unsigned long long*>(ticket), 0ull);
+        *count = total;
+        atomicExch(reinterpret_cast<unsigned long long*>(ticket), 0ull);
+        atomicExch(reinterpret_cast<unsigned long long*>(ticket + 1), 0ull);
+    }
+}
+
 __device__ __forceinline__ uint64_t apply_op(uint32_t op, uint64_t a, uint64_t b) {
     return op == OP_AND ? (a & b) : (op == OP_OR ? (a | b) : (a & ~b));
 }
@@ -167,7 +182,8 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
         uint64_t s = 0;
 #pragma unroll
         for (int w = 0; w < THREADS / 64; ++w) s += s_part[w];
-        if (s) atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)s);
+        if (s) atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)s);
+        finish_ticket(a.ticket, a.count);
     }
 }
 
@@ -438,7 +454,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         // dense tile: its own claim, direct writes
         const int64_t row0 = a.row_base + (int64_t)((uint64_t)tl * TILE_ROWS);
         if (t == 0) {
-            const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count);
+            const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)tile_count);
             s_off = c;
             if (dir) {
                 dir[2 * tl] = c;
@@ -530,11 +546,11 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
             const uint32_t staged_b = cnt_b_all <= (uint64_t)STAGE ? (uint32_t)cnt_b_all : 0;
             if (t == 0 && (ca + staged_b))
                 pend_claim = (DIAG & 1) ? (uint64_t)tile * 5400
-                                        : atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)(ca + staged_b));
+                                        : atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)(ca + staged_b));
             if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
             cb = decode(tile_b, sp, ca, G * (uint32_t)TILE_ROWS, r, off, cnt_b_all);
         } else if (t == 0 && ca) {
-            pend_claim = atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)ca);
+            pend_claim = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)ca);
         }
         if (t == 0) {
             s_tile_a[sp] = tile;
@@ -549,6 +565,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         ++pair;
     }
     if (pending) copy_out((int)((pair - 1) & 1));
+    if (t == 0) finish_ticket(a.ticket, a.count);
 }
 
 // ------------------------------------------------------------------ row-order pass

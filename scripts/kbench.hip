@@ -130,7 +130,9 @@ int main(int argc, char** argv) {
     const uint64_t cap = n / 10 + 4096;  // diag no-claim writes up to n/50 + a tile
     int64_t *ids, *ids2;
     uint64_t* ovf;
-    uint64_t *cnt, *dir, *dst_off;
+    uint64_t *cnt, *dir, *dst_off, *ticket;
+    CK(hipMalloc(&ticket, 16));
+    CK(hipMemset(ticket, 0, 16));
     CK(hipMalloc(&ids, cap * 8));
     CK(hipMalloc(&ids2, (cap + pw * 2) * 8));
     CK(hipMalloc(&ovf, 64));
@@ -152,6 +154,7 @@ int main(int argc, char** argv) {
     base.rowids = ids;
     base.capacity = cap;
     base.count = cnt;
+    base.ticket = ticket;
 
     std::vector<Variant> vs;
     const uint32_t dtiles = (uint32_t)(pw / decode_tile_words());
