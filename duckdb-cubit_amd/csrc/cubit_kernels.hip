@@ -44,14 +44,16 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     return x;
 }
 
-// Called by thread 0 of every workgroup after its last claim: the last workgroup to arrive
-// publishes the claim total to *count and re-arms the ticket for the next launch on the
-// stream (stream order guarantees that launch sees the zeroes).
+// Called by thread 0 of every workgroup after its last claim has RETURNED (every claim is a
+// returning atomic whose value the caller consumed, so it is performed before this arrival
+// is issued): the last workgroup to arrive publishes the claim total to *count and re-arms
+// the ticket for the next launch on the stream (stream order guarantees that launch sees
+// the zeroes). No __threadfence(): an agent-scope release on gfx950 writes back L2 (measured
+// +18 µs on the decode, +88 µs on the count kernel); only the atomics need ordering, and
+// they are coherent on their own.
 __device__ __forceinline__ void finish_ticket(uint64_t* ticket, uint64_t* count) {
-    __threadfence();
     const unsigned long long arrived = atomicAdd(reinterpret_cast<unsigned long long*>(ticket + 1), 1ull);
     if (arrived == (unsigned long long)(gridDim.x - 1)) {
-        __threadfence();
         const unsigned long long total = atomicAdd(reinterpret_cast<unsigned long long*>(ticket), 0ull);
         *count = total;
         atomicExch(reinterpret_cast<unsigned long long*>(ticket), 0ull);
@@ -182,7 +184,10 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
         uint64_t s = 0;
 #pragma unroll
         for (int w = 0; w < THREADS / 64; ++w) s += s_part[w];
-        if (s) atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)s);
+        // returning claim, consumed below, so it is performed before the arrival atomic
+        const unsigned long long before =
+            s ? atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)s) : 0ull;
+        if (before == ~0ull) __builtin_trap();
         finish_ticket(a.ticket, a.count);
     }
 }
