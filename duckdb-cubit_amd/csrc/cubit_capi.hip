@@ -446,10 +446,61 @@ struct Emitter {
         default: return false;
         }
     }
-    // top level: a pure conjunction is emitted as a left-deep AND chain, which the kernels
-    // evaluate branch-free (is_conjunction, cubit_kernels.hip)
+    using Lits = std::vector<std::pair<Leaf, bool>>;
+    static bool or_literals(const ExprP& e, Lits& out) {
+        if (e->kind == Expr::LEAF) {
+            out.push_back({e->leaf, e->neg});
+            return true;
+        }
+        if (e->kind == Expr::OR) return or_literals(e->a, out) && or_literals(e->b, out);
+        return false;
+    }
+    static void or_parts(const ExprP& e, std::vector<ExprP>& out) {
+        if (e->kind == Expr::OR) {
+            or_parts(e->a, out);
+            or_parts(e->b, out);
+        } else {
+            out.push_back(e);
+        }
+    }
+    // AND-ed parts; a & ~leaf contributes the complemented leaf as a part of its own
+    static bool and_parts(const ExprP& e, std::vector<Lits>& groups) {
+        if (e->kind == Expr::AND) return and_parts(e->a, groups) && and_parts(e->b, groups);
+        if (e->kind == Expr::ANDNOT) {
+            if (e->b->kind != Expr::LEAF) return false;
+            if (!and_parts(e->a, groups)) return false;
+            groups.push_back({{e->b->leaf, !e->b->neg}});
+            return true;
+        }
+        Lits g;
+        if (!or_literals(e, g)) return false;
+        groups.push_back(std::move(g));
+        return true;
+    }
+    // two-level program: groups of literals combined by `inner`, groups combined by `outer`;
+    // the postfix encoding of the same program is emitted alongside (interpreter fallback)
+    bool emit_groups(const std::vector<Lits>& groups, uint32_t inner, uint32_t outer, uint32_t form) {
+        size_t total = 0;
+        for (const auto& g : groups) total += g.size();
+        if (groups.empty() || total > (size_t)kMaxLeaves) return false;
+        uint32_t gstart = 0;
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
+            gstart |= 1u << prog.n_leaves;
+            for (size_t i = 0; i < groups[gi].size(); ++i) {
+                leaf(groups[gi][i].first, groups[gi][i].second);
+                if (i) op(inner);
+            }
+            if (gi) op(outer);
+        }
+        prog.form = form;
+        prog.gstart = gstart;
+        return ok;
+    }
+    // top level: a pure conjunction is emitted as a left-deep AND chain (branch-free CONJ
+    // form, is_conjunction in cubit_kernels.hip); an OR of conjunctions (DNF) or an AND of
+    // ORs of literals (CNF) as a branch-free two-level program; anything else as postfix
     void emit_top(const ExprP& e) {
-        std::vector<std::pair<Leaf, bool>> c;
+        Lits c;
         if (e->kind != Expr::LEAF && conj_leaves(e, c)) {
             leaf(c[0].first, c[0].second);
             for (size_t i = 1; i < c.size(); ++i) {
@@ -457,6 +508,37 @@ struct Emitter {
                 op(OP_AND);
             }
             return;
+        }
+        if (e->kind == Expr::OR) {
+            std::vector<ExprP> parts;
+            or_parts(e, parts);
+            std::vector<Lits> groups;
+            bool dnf = true;
+            for (const auto& p : parts) {
+                Lits g;
+                if (!conj_leaves(p, g)) {
+                    dnf = false;
+                    break;
+                }
+                groups.push_back(std::move(g));
+            }
+            if (dnf) {
+                Emitter trial;
+                if (trial.emit_groups(groups, OP_AND, OP_OR, FORM_DNF)) {
+                    *this = trial;
+                    return;
+                }
+            }
+        }
+        if (e->kind == Expr::AND || e->kind == Expr::ANDNOT) {
+            std::vector<Lits> groups;
+            if (and_parts(e, groups)) {
+                Emitter trial;
+                if (trial.emit_groups(groups, OP_OR, OP_AND, FORM_CNF)) {
+                    *this = trial;
+                    return;
+                }
+            }
         }
         emit(e);
     }

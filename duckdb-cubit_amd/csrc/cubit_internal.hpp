@@ -31,12 +31,18 @@ enum : uint32_t { OP_AND = 1, OP_OR = 2, OP_ANDNOT = 3 };
 // (4 bits per leaf) and opcodes (2 bits per op) are packed into words so the kernel decodes
 // them with scalar shifts (a runtime-indexed byte array in the kernel arguments compiles to
 // vector loads, each followed by an s_waitcnt vmcnt(0) that drains every outstanding load).
+// Evaluation forms: the general postfix interpreter, or a branch-free two-level form chosen
+// by the planner's emitter (leaves ordered by group, gstart bit k = leaf k opens a group).
+enum : uint32_t { FORM_POSTFIX = 0, FORM_CONJ = 1, FORM_DNF = 2, FORM_CNF = 3 };
+
 struct EvalProgram {
     const uint64_t* leaf[kMaxLeaves];
     uint32_t negate;
     uint32_t n_leaves;
-    uint32_t nops;  // 4 bits per leaf
-    uint32_t ops;   // 2 bits per op
+    uint32_t nops;    // 4 bits per leaf
+    uint32_t ops;     // 2 bits per op
+    uint32_t form;    // FORM_*; FORM_POSTFIX runs the postfix program (is_conjunction upgrades)
+    uint32_t gstart;  // FORM_DNF / FORM_CNF group starts
 };
 
 inline uint32_t prog_nops(const EvalProgram& p, int k) { return (p.nops >> (4 * k)) & 15u; }

@@ -68,12 +68,13 @@ __device__ __forceinline__ uint64_t apply_op(uint32_t op, uint64_t a, uint64_t b
 // Evaluate the program on NW words per thread. Leaves are loaded by the caller
 // (compile-time indexed); the stack is 4 deep and shifted with constant indices so it stays
 // in VGPRs.
-// CONJ: the program is a left-deep chain of ANDs (launch_eval_* detects it), evaluated
-// branch-free as the AND of the (possibly complemented) leaves.
-template <int K, int NW, bool CONJ = false>
+// FORM (template): FORM_POSTFIX interprets the postfix program; FORM_CONJ = AND of the
+// (possibly complemented) leaves; FORM_DNF = OR over groups of AND-ed literals; FORM_CNF =
+// AND over groups of OR-ed literals. The last three are branch-free on the data.
+template <int K, int NW, int FORM = FORM_POSTFIX>
 __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 (&v)[K][NW / 2],
                                            uint64_t (&r)[NW]) {
-    if (CONJ) {
+    if (FORM == FORM_CONJ) {
 #pragma unroll
         for (int j = 0; j < NW; ++j) r[j] = ~0ull;
 #pragma unroll
@@ -85,6 +86,33 @@ __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 
                 r[j] &= ((j & 1) ? p.y : p.x) ^ neg;
             }
         }
+        return;
+    }
+    if (FORM == FORM_DNF || FORM == FORM_CNF) {
+        constexpr bool DNF = FORM == FORM_DNF;
+        uint64_t cur[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) r[j] = DNF ? 0ull : ~0ull;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t neg = ((prog.negate >> k) & 1u) ? ~0ull : 0ull;
+            const bool opens = k == 0 || ((prog.gstart >> k) & 1u);
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const u64x2 p = v[k][j >> 1];
+                const uint64_t x = ((j & 1) ? p.y : p.x) ^ neg;
+                if (k == 0) {
+                    cur[j] = x;
+                } else if (opens) {
+                    r[j] = DNF ? (r[j] | cur[j]) : (r[j] & cur[j]);
+                    cur[j] = x;
+                } else {
+                    cur[j] = DNF ? (cur[j] & x) : (cur[j] | x);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NW; ++j) r[j] = DNF ? (r[j] | cur[j]) : (r[j] & cur[j]);
         return;
     }
     uint64_t s0[NW], s1[NW], s2[NW], s3[NW];
@@ -159,7 +187,7 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
 
 // count(*) of the program and/or its result bitvector; one tile per workgroup, one
 // non-returning atomic per tile.
-template <int K, int PAIRS, bool CONJ = false>
+template <int K, int PAIRS, int FORM = FORM_POSTFIX>
 __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
     constexpr int THREADS = 256, NW = 2 * PAIRS;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
@@ -168,7 +196,7 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
     u64x2 v[K][PAIRS];
     load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
     uint64_t r[NW];
-    eval_words<K, NW, CONJ>(a.prog, v, r);
+    eval_words<K, NW, FORM>(a.prog, v, r);
     tail_mask<NW, THREADS>(a, tile_word0, t, r);
     if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
     __shared__ uint64_t s_part[THREADS / 64];
@@ -212,7 +240,7 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
 // CLAIM / DECODE = false are diagnostic builds (scripts/kbench.hip), never launched by the
 // library. __launch_bounds__: two workgroups per CU (2·THREADS/256 waves per SIMD) caps
 // VGPRs at 128.
-template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true, bool CONJ = false>
+template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true, int FORM = FORM_POSTFIX>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
     constexpr int NW = 2 * PAIRS;
     constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
@@ -235,7 +263,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
     while (tile < a.num_tiles) {
         const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
         uint64_t r[NW];
-        eval_words<K, NW, CONJ>(a.prog, v, r);
+        eval_words<K, NW, FORM>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
         uint64_t packed[NPK], incl[NPK];
@@ -360,7 +388,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
 // Copy-out stores are issued before the prefetch they precede, so the wait for the prefetched
 // leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
 // STAGE hits claims on its own and writes straight to the output (dense path).
-template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, bool CONJ = false>
+template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(EvalArgs a, uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
     // fake decode (same LDS traffic, no per-bit loop)
@@ -394,7 +422,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     // evaluate the tile in v → r, block scan → per-pair offsets within the tile, tile count
     auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS]) -> uint64_t {
         const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
-        eval_words<K, NW, CONJ>(a.prog, v, r);
+        eval_words<K, NW, FORM>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
         uint64_t packed[NPK], incl[NPK];
@@ -801,27 +829,44 @@ bool is_conjunction(const EvalProgram& p) {
     return true;
 }
 
+uint32_t eval_form(const EvalProgram& p) {
+    if (p.form == FORM_DNF || p.form == FORM_CNF || p.form == FORM_CONJ) return p.form;
+    return is_conjunction(p) ? FORM_CONJ : FORM_POSTFIX;
+}
+
 // production decode: the pair-claimed kernel (scripts/kbench.hip: 83 µs vs 94 µs for the
 // per-tile claim kernel on SF100 Q6-shaped leaves)
+template <int K, int FORM>
+void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, FORM>), dim3(grid),
+                          dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
+}
+
 template <int K>
 hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
                            hipEvent_t e1) {
-    if (is_conjunction(a.prog))
-        hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, true>), dim3(grid),
-                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
-    else
-        hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads>), dim3(grid),
-                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
+    switch (eval_form(a.prog)) {
+    case FORM_CONJ: launch_decode_kf<K, FORM_CONJ>(a, dir, grid, s, e0, e1); break;
+    case FORM_DNF: launch_decode_kf<K, FORM_DNF>(a, dir, grid, s, e0, e1); break;
+    case FORM_CNF: launch_decode_kf<K, FORM_CNF>(a, dir, grid, s, e0, e1); break;
+    default: launch_decode_kf<K, FORM_POSTFIX>(a, dir, grid, s, e0, e1); break;
+    }
     return hipGetLastError();
+}
+
+template <int K, int FORM>
+void launch_count_kf(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, FORM>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0, a);
 }
 
 template <int K>
 hipError_t launch_count_k(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (is_conjunction(a.prog))
-        hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, true>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0,
-                              a);
-    else
-        hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0, a);
+    switch (eval_form(a.prog)) {
+    case FORM_CONJ: launch_count_kf<K, FORM_CONJ>(a, s, e0, e1); break;
+    case FORM_DNF: launch_count_kf<K, FORM_DNF>(a, s, e0, e1); break;
+    case FORM_CNF: launch_count_kf<K, FORM_CNF>(a, s, e0, e1); break;
+    default: launch_count_kf<K, FORM_POSTFIX>(a, s, e0, e1); break;
+    }
     return hipGetLastError();
 }
 

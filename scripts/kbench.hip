@@ -208,7 +208,7 @@ int main(int argc, char** argv) {
                       a.prog.nops = 0;
                       for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
                       a.prog.ops = 0;
-                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, 0, true>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, 0, FORM_CONJ>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
                                          dim3(512), 0, s, a, dir);
                   }, 0});
     DPD("pairs diag no-claim", 1);
