@@ -175,8 +175,8 @@ int cubit_ctx_create(int device, cubit_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->n_cus = prop.multiProcessorCount;
     if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess ||
-        hipMalloc(&ctx->ticket, 2 * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(ctx->ticket, 0, 2 * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        hipMalloc(&ctx->ticket, kTicketWords * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(ctx->ticket, 0, kTicketWords * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         if (ctx->partials) (void)hipFree(ctx->partials);
         if (ctx->ticket) (void)hipFree(ctx->ticket);
         delete ctx;

@@ -62,11 +62,14 @@ struct EvalArgs {
     uint64_t* count;         // result: the number of qualifying rows (written at kernel end)
     uint64_t* result_words;  // optional evaluated bitvector
     uint32_t num_tiles;
-    // claim ticket (context-owned, 2 words, zero between launches): [0] running claim
-    // counter, [1] finished workgroups. The last workgroup to finish publishes *count and
-    // re-zeroes both words, so no memset launch precedes a scan (finish_ticket).
+    // claim ticket (context-owned, kTicketWords words, zero between launches): running claim
+    // counter + arrival counters. The last workgroup to finish publishes *count and re-zeroes
+    // the ticket, so no memset launch precedes a scan (finish_ticket, cubit_kernels.hip).
     uint64_t* ticket;
 };
+constexpr uint32_t kTicketStride = 64;  // words (512 B) between ticket counters
+constexpr uint32_t kTicketGroups = 8;
+constexpr uint32_t kTicketWords = kTicketStride * (kTicketGroups + 2);
 
 // launchers (cubit_kernels.hip); all asynchronous on `stream`
 uint64_t decode_tile_words();  // words per eval_decode_tiles tile

@@ -44,21 +44,35 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
     return x;
 }
 
-// Called by thread 0 of every workgroup after its last claim has RETURNED (every claim is a
-// returning atomic whose value the caller consumed, so it is performed before this arrival
-// is issued): the last workgroup to arrive publishes the claim total to *count and re-arms
-// the ticket for the next launch on the stream (stream order guarantees that launch sees
-// the zeroes). No __threadfence(): an agent-scope release on gfx950 writes back L2 (measured
-// +18 µs on the decode, +88 µs on the count kernel); only the atomics need ordering, and
-// they are coherent on their own.
+// Claim-ticket layout (kTicketWords words, context-owned, zero between launches): word 0 =
+// running claim counter; word kTicketStride·(1+g) = arrivals of workgroup group g
+// (blockIdx % 8, one group per XCD under round-robin dispatch); word kTicketStride·9 =
+// arrived groups. Counters sit 512 B apart: atomics on one line serialise (≈88/µs,
+// MI355X_MICROARCH.md "dequeue"), and a flat arrival counter put a 512-atomic tail on
+// every launch.
+//
+// finish_ticket is called by thread 0 of every workgroup after its last claim has RETURNED
+// (every claim is a returning atomic whose value the caller consumed, so it is performed
+// before the arrival is issued). The last workgroup of a group arrives at the group counter;
+// the last group publishes the claim total to *count and re-arms the ticket for the next
+// launch on the stream (stream order guarantees that launch sees the zeroes).
+// No __threadfence(): an agent-scope release on gfx950 writes back L2 (measured +18 µs on
+// the decode); only the atomics need ordering, and they are coherent on their own.
 __device__ __forceinline__ void finish_ticket(uint64_t* ticket, uint64_t* count) {
-    const unsigned long long arrived = atomicAdd(reinterpret_cast<unsigned long long*>(ticket + 1), 1ull);
-    if (arrived == (unsigned long long)(gridDim.x - 1)) {
-        const unsigned long long total = atomicAdd(reinterpret_cast<unsigned long long*>(ticket), 0ull);
-        *count = total;
-        atomicExch(reinterpret_cast<unsigned long long*>(ticket), 0ull);
-        atomicExch(reinterpret_cast<unsigned long long*>(ticket + 1), 0ull);
-    }
+    const uint32_t G = gridDim.x;
+    const uint32_t groups = G < kTicketGroups ? G : kTicketGroups;
+    const uint32_t g = blockIdx.x % groups;
+    const uint32_t members = G / groups + (g < G % groups ? 1u : 0u);
+    unsigned long long* gc = reinterpret_cast<unsigned long long*>(ticket + kTicketStride * (1 + g));
+    if (atomicAdd(gc, 1ull) != (unsigned long long)(members - 1)) return;
+    unsigned long long* top = reinterpret_cast<unsigned long long*>(ticket + kTicketStride * (1 + kTicketGroups));
+    if (atomicAdd(top, 1ull) != (unsigned long long)(groups - 1)) return;
+    const unsigned long long total = atomicAdd(reinterpret_cast<unsigned long long*>(ticket), 0ull);
+    *count = total;
+    atomicExch(reinterpret_cast<unsigned long long*>(ticket), 0ull);
+    for (uint32_t i = 0; i < groups; ++i)
+        atomicExch(reinterpret_cast<unsigned long long*>(ticket + kTicketStride * (1 + i)), 0ull);
+    atomicExch(top, 0ull);
 }
 
 __device__ __forceinline__ uint64_t apply_op(uint32_t op, uint64_t a, uint64_t b) {
@@ -185,29 +199,30 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
 
 // ------------------------------------------------------------------ K1: count / materialise
 
-// count(*) of the program and/or its result bitvector; one tile per workgroup, one
-// non-returning atomic per tile.
+// count(*) of the program and/or its result bitvector. Persistent: workgroup g takes tiles
+// g, g+G, …, keeps its count in registers, and claims once at the end (one returning atomic
+// per workgroup instead of one per tile).
 template <int K, int PAIRS, int FORM = FORM_POSTFIX>
 __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
     constexpr int THREADS = 256, NW = 2 * PAIRS;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     const int t = threadIdx.x;
-    const uint64_t tile_word0 = (uint64_t)blockIdx.x * TILE_WORDS;
-    u64x2 v[K][PAIRS];
-    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
-    uint64_t r[NW];
-    eval_words<K, NW, FORM>(a.prog, v, r);
-    tail_mask<NW, THREADS>(a, tile_word0, t, r);
-    if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
-    __shared__ uint64_t s_part[THREADS / 64];
     uint64_t c = 0;
+    for (uint32_t tile = blockIdx.x; tile < a.num_tiles; tile += gridDim.x) {
+        const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+        u64x2 v[K][PAIRS];
+        load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+        uint64_t r[NW];
+        eval_words<K, NW, FORM>(a.prog, v, r);
+        tail_mask<NW, THREADS>(a, tile_word0, t, r);
+        if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
 #pragma unroll
-    for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
+        for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
+    }
+    __shared__ uint64_t s_part[THREADS / 64];
     c = wave_sum(c);
     if ((t & 63) == 0) s_part[t >> 6] = c;
     __syncthreads();
-    // one atomic per workgroup: a single address serves ~88 returning atomics/µs
-    // (MI355X_MICROARCH.md "dequeue"), so per-wave atomics would throttle the kernel
     if (t == 0) {
         uint64_t s = 0;
 #pragma unroll
@@ -300,7 +315,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
         }
         uint64_t claimed = 0;
         if (t == 0 && tile_count)  // not wave-aggregated: built with -amdgpu-atomic-optimizer-strategy=None
-            claimed = CLAIM ? atomicAdd(reinterpret_cast<unsigned long long*>(a.count), (unsigned long long)tile_count)
+            claimed = CLAIM ? atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)tile_count)
                             : (uint64_t)tile * (TILE_WORDS * 64 / 50);  // diag: ~2 % density, disjoint runs
         const uint32_t next = tile + gridDim.x;
         if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);  // prefetch
@@ -373,6 +388,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
         __syncthreads();  // C: stage / s_off / s_wave_tot free for the next tile
         tile = next;
     }
+    if (t == 0) finish_ticket(a.ticket, a.count);
 }
 
 // Pair-claimed evaluate + decode: one returning atomic per PAIR of tiles, issued one unit
@@ -816,6 +832,7 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 // Chosen from the interleaved variant sweep in scripts/kbench.hip.
 constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
 constexpr int kCountPairs = 8;
+constexpr int kCountGrid = 1024;  // persistent count grid: 4 workgroups per CU
 
 uint64_t decode_tile_words() { return (uint64_t)kDecodeThreads * 2 * kDecodePairs; }
 uint64_t count_tile_words() { return 256ull * 2 * kCountPairs; }
@@ -856,7 +873,8 @@ hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipS
 
 template <int K, int FORM>
 void launch_count_kf(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, FORM>), dim3(a.num_tiles), dim3(256), 0, s, e0, e1, 0, a);
+    const unsigned grid = std::min<unsigned>(a.num_tiles, (unsigned)kCountGrid);
+    hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, FORM>), dim3(grid), dim3(256), 0, s, e0, e1, 0, a);
 }
 
 template <int K>

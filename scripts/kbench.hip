@@ -131,8 +131,8 @@ int main(int argc, char** argv) {
     int64_t *ids, *ids2;
     uint64_t* ovf;
     uint64_t *cnt, *dir, *dst_off, *ticket;
-    CK(hipMalloc(&ticket, 16));
-    CK(hipMemset(ticket, 0, 16));
+    CK(hipMalloc(&ticket, kTicketWords * 8));
+    CK(hipMemset(ticket, 0, kTicketWords * 8));
     CK(hipMalloc(&ids, cap * 8));
     CK(hipMalloc(&ids2, (cap + pw * 2) * 8));
     CK(hipMalloc(&ovf, 64));
@@ -211,6 +211,12 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, 0, FORM_CONJ>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
                                          dim3(512), 0, s, a, dir);
                   }, 0});
+    DT("tiles P2 T512 x2/CU", 2, 4096, 512, 2);
+    DT("tiles P1 T512 x2/CU", 1, 2048, 512, 2);
+    DT("tiles P1 T256 x4/CU", 1, 1024, 256, 4);
+    DT("tiles P2 T256 x4/CU", 2, 2048, 256, 4);
+    DP("pairs P1 T512 x2/CU", 1, 2048, 512, 2);
+    DP("pairs P1 T256 x4/CU", 1, 1024, 256, 4);
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);
