@@ -1,6 +1,6 @@
 // CDNA4 (gfx950) kernels of the bitmap-indexed scan filter.
 //
-//   K1+K2  eval_decode_tiles — postfix AND/OR/ANDNOT over K bitvectors fused with the
+//   K1+K2  eval_decode_pairs — AND/OR/ANDNOT over K bitvectors fused with the
 //                          bitvector → int64 row-id compaction. Replaces the per-vector
 //                          selection narrowing of RowGroup::TemplatedScan
 //                          (src/storage/table/row_group.cpp:537-550 → ColumnSegment::
@@ -237,6 +237,8 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
 
 // ------------------------------------------------------------------ K1+K2: evaluate + decode
 
+// Per-tile-claim evaluate + decode (round-1 production kernel, now kept as the reference
+// variant in scripts/kbench.hip; the library launches eval_decode_pairs below).
 // Persistent, software-pipelined evaluate + decode. Workgroup g takes tiles g, g+G, g+2G, …
 // (static striding: per-tile work is uniform up to the decode). Per tile:
 //   evaluate the tile whose leaves landed → per-pair bit counts → block scan →
@@ -249,11 +251,10 @@ __global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
 // (table_scan.cpp:179-189). dir[2·tile] / dir[2·tile+1] = the run's start / length, so
 // reading runs in tile order yields the ascending sequence (order_runs does that on device).
 // There is no inter-workgroup wait: a claim is one atomic, so no prefix chain serialises the
-// tiles (a decoupled look-back over ~10^4 tiles measured 1.7× slower, DESIGN.md §K1).
+// tiles (a decoupled look-back over ~10^4 tiles measured 1.7× slower, DESIGN.md §3).
 // Per-pair counts are packed as FB-bit fields so one 64-bit scan covers several pairs
 // (a pair-chunk holds at most THREADS·128 set bits).
-// CLAIM / DECODE = false are diagnostic builds (scripts/kbench.hip), never launched by the
-// library. __launch_bounds__: two workgroups per CU (2·THREADS/256 waves per SIMD) caps
+// CLAIM / DECODE = false are diagnostic builds (scripts/kbench.hip). __launch_bounds__: two workgroups per CU (2·THREADS/256 waves per SIMD) caps
 // VGPRs at 128.
 template <int K, int PAIRS, int STAGE, int THREADS, bool CLAIM = true, bool DECODE = true, int FORM = FORM_POSTFIX>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(EvalArgs a, uint64_t* __restrict__ dir) {
@@ -829,7 +830,7 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 
 // production geometry: decode tiles of 512 threads × 2 pairs = 2,048 words (131,072 rows),
 // STAGE 4,096 staged ids (16 KiB LDS); count tiles of 256 threads × 8 pairs = 4,096 words.
-// Chosen from the interleaved variant sweep in scripts/kbench.hip (DESIGN.md §K1).
+// Chosen from the interleaved variant sweep in scripts/kbench.hip (DESIGN.md §3).
 constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
 constexpr int kCountPairs = 8;
 constexpr int kCountGrid = 1024;  // persistent count grid: 4 workgroups per CU

@@ -3,7 +3,7 @@
 // Q6-like densities, ~1.9 % selected) and checks every variant against the production
 // decode (row ids rebuilt in row order through the tile directory).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I duckdb-cubit_amd/csrc scripts/kbench.hip -o scripts/kbench
-// The variant sweep that chose the production geometry is summarised in DESIGN.md §K1.
+// The variant sweep that chose the production geometry is summarised in DESIGN.md §3.
 #include "cubit_kernels.hip"
 
 #include <algorithm>
