@@ -785,43 +785,40 @@ int copy_column(cubit_table* t, Column& c, int type, const void* data, const uin
 
 // distinct non-null values and min/max of a column (host pass over a D2H copy; index build
 // is setup work, not the scan path)
+// Index-build statistics on the device: min / max / any valid, and (want_distinct) the
+// distinct valid values through a presence bitmap of vmax - vmin + 1 bits (≤ 2^32 values;
+// an index with more distinct keys than that is not a bitmap index anyone should build).
 int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct, bool want_distinct,
                  int64_t& vmin, int64_t& vmax, bool& any) {
-    const uint64_t n = t->n_rows, esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
-    std::vector<unsigned char> host(n * esz);
-    std::vector<uint64_t> valid;
-    HIP_CHECK(hipMemcpy(host.data(), c.data, n * esz, hipMemcpyDeviceToHost));
-    if (c.validity) {
-        valid.resize((n + 63) / 64);
-        HIP_CHECK(hipMemcpy(valid.data(), c.validity, valid.size() * 8, hipMemcpyDeviceToHost));
-    }
-    any = false;
-    vmin = INT64_MAX;
-    vmax = INT64_MIN;
-    std::vector<int64_t> vals;
-    if (want_distinct) vals.reserve(n);
-    for (uint64_t r = 0; r < n; ++r) {
-        if (c.validity && !((valid[r >> 6] >> (r & 63)) & 1)) continue;
-        const int64_t v = c.type == CUBIT_TYPE_INT32 ? (int64_t) reinterpret_cast<const int32_t*>(host.data())[r]
-                                                     : reinterpret_cast<const int64_t*>(host.data())[r];
-        any = true;
-        vmin = std::min(vmin, v);
-        vmax = std::max(vmax, v);
-        if (want_distinct) vals.push_back(v);
-    }
-    if (want_distinct) {
-        if (any && (uint64_t)(vmax - vmin) < (1ull << 26)) {
-            std::vector<uint8_t> seen((size_t)(vmax - vmin) + 1, 0);
-            for (int64_t v : vals) seen[(size_t)(v - vmin)] = 1;
-            distinct.clear();
-            for (size_t i = 0; i < seen.size(); ++i)
-                if (seen[i]) distinct.push_back(vmin + (int64_t)i);
-        } else {
-            std::sort(vals.begin(), vals.end());
-            vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
-            distinct = std::move(vals);
-        }
-    }
+    const uint64_t n = t->n_rows;
+    DevBuf stats;
+    if (hipMalloc(&stats.p, 3 * sizeof(int64_t)) != hipSuccess) return fail(CUBIT_ERR_OOM, "stats allocation failed");
+    int64_t h[3] = {INT64_MAX, INT64_MIN, 0};
+    HIP_CHECK(hipMemcpyAsync(stats.p, h, sizeof(h), hipMemcpyHostToDevice, t->ctx->stream));
+    HIP_CHECK(launch_column_minmax(c.data, c.type, c.validity, n, static_cast<int64_t*>(stats.p), t->ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(h, stats.p, sizeof(h), hipMemcpyDeviceToHost, t->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    any = h[2] > 0;
+    vmin = h[0];
+    vmax = h[1];
+    if (!want_distinct) return CUBIT_OK;
+    distinct.clear();
+    if (!any) return CUBIT_OK;
+    const uint64_t span = (uint64_t)vmax - (uint64_t)vmin;  // no signed overflow
+    if (span >= (1ull << 32))
+        return fail(CUBIT_ERR_UNSUPPORTED, "value range too wide for an all-distinct-values index; give keys");
+    const uint64_t range = span + 1;
+    const uint64_t nw = (range + 63) / 64;
+    DevBuf bits;
+    if (hipMalloc(&bits.p, nw * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "presence bitmap allocation failed");
+    HIP_CHECK(hipMemsetAsync(bits.p, 0, nw * 8, t->ctx->stream));
+    HIP_CHECK(launch_presence(c.data, c.type, c.validity, n, vmin, range, static_cast<uint64_t*>(bits.p),
+                              t->ctx->stream));
+    std::vector<uint64_t> hb(nw);
+    HIP_CHECK(hipMemcpyAsync(hb.data(), bits.p, nw * 8, hipMemcpyDeviceToHost, t->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    for (uint64_t w = 0; w < nw; ++w)
+        for (uint64_t x = hb[w]; x; x &= x - 1) distinct.push_back(vmin + (int64_t)(w * 64 + __builtin_ctzll(x)));
     return CUBIT_OK;
 }
 

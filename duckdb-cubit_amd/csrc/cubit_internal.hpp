@@ -90,6 +90,12 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
 constexpr int kCmpBetween = 6;
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                                     int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2 = 0);
+// index-build statistics (out3 = {min, max, valid count}, pre-set by the caller) and the
+// presence bitmap of the valid values (bit v - vmin, `range` bits, zeroed by the caller)
+hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,
+                                hipStream_t stream);
+hipError_t launch_presence(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t vmin,
+                           uint64_t range, uint64_t* bits, hipStream_t stream);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,

@@ -722,6 +722,69 @@ hipError_t launch_compare_t(const T* col, const uint64_t* validity, uint64_t n_r
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ index build: column stats
+
+// min / max / any-valid of a column (the statistics an index build needs; the reference
+// keeps them per segment as BaseStatistics, used by CheckZonemap, row_group.cpp:361-371).
+// out[0] = min, out[1] = max (pre-set to INT64_MAX / INT64_MIN), out[2] = valid rows.
+template <typename T>
+__global__ __launch_bounds__(256) void column_minmax_kernel(const T* __restrict__ col,
+                                                            const uint64_t* __restrict__ validity, uint64_t n,
+                                                            int64_t* __restrict__ out) {
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    uint64_t cnt = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) continue;
+        const int64_t v = (int64_t)col[i];
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+        ++cnt;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+        cnt += __shfl_xor(cnt, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && cnt) {
+        atomicMin(reinterpret_cast<long long*>(out), (long long)mn);
+        atomicMax(reinterpret_cast<long long*>(out + 1), (long long)mx);
+        atomicAdd(reinterpret_cast<unsigned long long*>(out + 2), (unsigned long long)cnt);
+    }
+}
+
+// presence bitmap of the valid values: bit (v - vmin) of `bits`. Narrow ranges (≤ 2^16
+// values) collect in LDS first so the few global words are OR-ed once per workgroup.
+template <typename T, bool LDS>
+__global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col, const uint64_t* __restrict__ validity,
+                                                       uint64_t n, int64_t vmin, uint64_t range,
+                                                       uint64_t* __restrict__ bits) {
+    __shared__ uint64_t s_bits[LDS ? 1024 : 1];
+    const uint64_t nw = (range + 63) / 64;
+    if (LDS) {
+        for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x) s_bits[w] = 0;
+        __syncthreads();
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) continue;
+        const uint64_t off = (uint64_t)((int64_t)col[i] - vmin);
+        const uint64_t bit = 1ull << (off & 63);
+        if (LDS) {
+            if (!(s_bits[off >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[off >> 6]), bit);
+        } else {
+            atomicOr(reinterpret_cast<unsigned long long*>(&bits[off >> 6]), bit);
+        }
+    }
+    if (LDS) {
+        __syncthreads();
+        for (uint64_t w = threadIdx.x; w < nw; w += blockDim.x)
+            if (s_bits[w]) atomicOr(reinterpret_cast<unsigned long long*>(&bits[w]), s_bits[w]);
+    }
+}
+
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -933,6 +996,36 @@ hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* v
                                          out_words, stream);
     return launch_compare_t<int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, constant, constant2,
                                      out_words, stream);
+}
+
+hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,
+                                hipStream_t stream) {
+    const dim3 grid(grid_for(n_rows, 2048)), block(256);
+    if (type == 0)
+        hipLaunchKernelGGL(column_minmax_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
+                           validity, n_rows, out3);
+    else
+        hipLaunchKernelGGL(column_minmax_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, n_rows, out3);
+    return hipGetLastError();
+}
+
+hipError_t launch_presence(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t vmin,
+                           uint64_t range, uint64_t* bits, hipStream_t stream) {
+    const dim3 grid(grid_for(n_rows, 2048)), block(256);
+    const bool lds = range <= 65536;
+#define CUBIT_PRESENCE(T, L)                                                                                   \
+    hipLaunchKernelGGL((presence_kernel<T, L>), grid, block, 0, stream, static_cast<const T*>(col), validity, \
+                       n_rows, vmin, range, bits)
+    if (type == 0) {
+        if (lds) CUBIT_PRESENCE(int32_t, true);
+        else CUBIT_PRESENCE(int32_t, false);
+    } else {
+        if (lds) CUBIT_PRESENCE(int64_t, true);
+        else CUBIT_PRESENCE(int64_t, false);
+    }
+#undef CUBIT_PRESENCE
+    return hipGetLastError();
 }
 
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,

@@ -56,7 +56,29 @@ def main():
             {"after": "con1 COMMIT", "expect": {"con1": 2, "con2": 1}},
         ],
     }
-    (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv},
+    # test/optimizer/pushdown/table_or_pushdown.test: integers(a, b) = (1,1) … (5,5); the
+    # integer queries' expected rows (a values). The trees use the repo's residual syntax:
+    # ["or"|"and", children…] / [column, cmp, constant], column 0 = a, 1 = b.
+    orp = {
+        "source": "test/optimizer/pushdown/table_or_pushdown.test:11-57",
+        "rows": [1, 2, 3, 4, 5],
+        "queries": [
+            {"sql": "a=1 OR b=2 AND (a>3 OR b<5)",
+             "tree": ["or", [0, "=", 1], ["and", [1, "=", 2], ["or", [0, ">", 3], [1, "<", 5]]]],
+             "expect": [1, 2]},
+            {"sql": "a=1 OR a=2 AND (a>3 OR b<5)",
+             "tree": ["or", [0, "=", 1], ["and", [0, "=", 2], ["or", [0, ">", 3], [1, "<", 5]]]],
+             "expect": [1, 2]},
+            {"sql": "a=1 OR (a>3 AND a<5)",
+             "tree": ["or", [0, "=", 1], ["and", [0, ">", 3], [0, "<", 5]]],
+             "expect": [1, 4]},
+            {"sql": "a=1 OR a>3 OR a<5",
+             "tree": ["or", [0, "=", 1], [0, ">", 3], [0, "<", 5]],
+             "expect": [1, 2, 3, 4, 5]},
+        ],
+    }
+    (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
+                                                          "table_or_pushdown": orp},
                                                          indent=1, sort_keys=True) + "\n")
 
 

@@ -385,3 +385,33 @@ def test_bins_index_intervals_vs_oracle(ctx, with_range):
                                                            np.full(len(rows), TXN_START + 1, dtype=np.uint64)))
     ref = O.table_scan([colu], F.serialize(fs), n, tx=O.Mvcc(2, TXN_START + 1))
     assert np.array_equal(got, ref)
+
+
+def test_index_build_statistics_on_device(ctx):
+    """Distinct keys come from the device presence bitmap: negative values, NULLs ignored,
+    one bitvector per distinct value (range drops the minimum); too-wide ranges refuse."""
+    n = 200_003
+    rng = np.random.default_rng(21)
+    a = rng.choice(np.array([-70000, -3, 0, 5, 9, 123456], dtype=np.int64), n)
+    valid = rng.random(n) > 0.3
+    a_null_only = a.copy()
+    a_null_only[~valid] = 777  # a value present only under NULLs must not become a key
+    t = CubitTable(ctx, n)
+    t.add_column(0, a_null_only, validity_from_mask(valid))
+    t.build_index(0, L.INDEX_EQUALITY)
+    assert t.index_info(0)[0] == 6
+    t.build_index(0, L.INDEX_RANGE)
+    assert t.index_info(0)[0] == 5
+    col = O.Column(a_null_only, validity_from_mask(valid))
+    for c in (-70000, -3, 0, 5, 9, 123456, 777):
+        for cmp in ("<", "=", ">="):
+            fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
+            assert np.array_equal(t.scan(fs), O.table_scan([col], F.serialize(fs), n)), (cmp, c)
+    wide = np.array([-(2 ** 62), 2 ** 62] * 10, dtype=np.int64)
+    t2 = CubitTable(ctx, len(wide))
+    t2.add_column(0, wide)
+    with pytest.raises(Exception, match="too wide"):
+        t2.build_index(0, L.INDEX_RANGE)
+    t2.build_index(0, L.INDEX_RANGE, [0])  # explicit keys are fine
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 0)})
+    assert np.array_equal(t2.scan(fs), np.arange(0, 20, 2))

@@ -168,3 +168,22 @@ def test_interleaved_versions_reference_case(golden):
     deleted_c = np.array([6, t2], dtype=np.uint64)
     assert s(O.Mvcc(5, t2, deleted=deleted_c)) == exp[1]["expect"]["con2"]
     assert s(O.Mvcc(7, TXN_START + 13, deleted=deleted_c)) == 2
+
+
+def residual_from_json(node):
+    """["or"|"and", children…] / [column, cmp, constant] → residual filter tree."""
+    if node[0] in ("or", "and"):
+        kids = [residual_from_json(c) for c in node[1:]]
+        return F.Or(*kids) if node[0] == "or" else F.And(*kids)
+    col, cmp, c = node
+    return F.Cmp(col, cmp, c)
+
+
+def test_table_or_pushdown_reference_case(golden):
+    """test/optimizer/pushdown/table_or_pushdown.test: cross-column OR/AND trees on (a, b)."""
+    c = golden["cases"]["table_or_pushdown"]
+    data = np.array(c["rows"], dtype=np.int32)
+    cols = [O.Column(data), O.Column(data.copy())]
+    for q in c["queries"]:
+        rows = O.table_scan(cols, F.serialize(None, residual_from_json(q["tree"])), len(data))
+        assert data[rows].tolist() == q["expect"], q["sql"]
