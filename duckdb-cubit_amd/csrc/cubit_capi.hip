@@ -715,6 +715,7 @@ struct cubit_table {
     size_t scratch_used = 0;
     std::unique_ptr<DevBuf> ones;  // all valid rows
     uint32_t last_leaves = 0, last_passes = 0;
+    uint32_t last_decoded = 0;  // sum_product: values of b decoded from its index (0 = gathered)
     uint64_t* dummy_count = nullptr;
     std::unique_ptr<DevBuf> dummy;
 };
@@ -1388,14 +1389,14 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
 
 }  // namespace
 
-extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
-                                const cubit_txn* txn, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
-                                uint32_t flags) {
-    if (!t || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
-    const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
-    if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
-    if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
-    if (int rc = set_device(t->ctx)) return rc;
+namespace {
+
+// Plan a pushed filter tree for a transaction into one program (front half of every scan):
+// planner → MVCC update patches → visibility leaf → constant folding → split until it fits
+// one pass → emit. *empty = the filter is FALSE (no kernel needed).
+int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes, const cubit_txn* txn,
+                 Emitter& em, bool* empty) {
+    *empty = false;
     cubit_ctx* ctx = t->ctx;
     t->scratch_used = 0;
     t->last_passes = 0;
@@ -1442,7 +1443,7 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
         }
     }
     if (e->kind == Expr::CONST_FALSE) {
-        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+        *empty = true;
         t->last_leaves = 0;
         return CUBIT_OK;
     }
@@ -1454,18 +1455,170 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
         e = mk_leaf(l);
     }
     if (int rc = fit(t, e)) return rc;
-    Emitter em;
     em.emit_top(e);
+    if (!em.ok) return fail(CUBIT_ERR_UNSUPPORTED, "program does not fit one pass");
     t->last_leaves = em.prog.n_leaves;
     t->last_passes++;
-    return run_eval(ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count, nullptr,
-                    count_only ? RunMode::kCount : RunMode::kDecode, true, (flags & CUBIT_SCAN_ORDERED) != 0);
+    return CUBIT_OK;
+}
+
+// The values `col` can take among the rows the filter keeps, when its constant filters in the
+// top-level AND pin it to a short list that the column's exact range index can decode:
+// v0 < v1 < … with leaves L(v_j). Returns false when it cannot (the kernel then gathers b).
+bool decodable_values(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes, int col,
+                      std::vector<int64_t>& vals, std::vector<const uint64_t*>& leaves) {
+    auto ixit = t->idx.find(col);
+    if (ixit == t->idx.end() || ixit->second.encoding != CUBIT_INDEX_RANGE || !ixit->second.exact_all ||
+        ixit->second.empty || n_nodes == 0)
+        return false;
+    const Index& ix = ixit->second;
+    int64_t lo = ix.vmin, hi = ix.vmax;  // inclusive bounds
+    bool bounded = false;
+    // constants on col reachable through AND nodes only
+    std::vector<uint32_t> stack{0};
+    Planner pl{t, nodes, n_nodes};
+    while (!stack.empty()) {
+        const uint32_t i = stack.back();
+        stack.pop_back();
+        const cubit_filter_node& f = nodes[i];
+        if (f.kind == CUBIT_FILTER_AND) {
+            uint32_t j = i + 1;
+            for (int k = 0; k < f.n_children; ++k) {
+                stack.push_back(j);
+                j = (uint32_t)pl.subtree_end(j);
+            }
+        } else if (f.kind == CUBIT_FILTER_CONSTANT && f.column == col) {
+            const int64_t c = f.constant;
+            switch (f.cmp) {
+            case CUBIT_CMP_EQ: lo = std::max(lo, c); hi = std::min(hi, c); break;
+            case CUBIT_CMP_LT: if (c == INT64_MIN) return false; hi = std::min(hi, c - 1); break;
+            case CUBIT_CMP_LE: hi = std::min(hi, c); break;
+            case CUBIT_CMP_GT: if (c == INT64_MAX) return false; lo = std::max(lo, c + 1); break;
+            case CUBIT_CMP_GE: lo = std::max(lo, c); break;
+            default: continue;
+            }
+            bounded = true;
+        }
+    }
+    if (!bounded || lo > hi) return false;
+    vals.clear();
+    leaves.clear();
+    if (ix.vmin >= lo && ix.vmin <= hi) vals.push_back(ix.vmin);
+    for (size_t k = 0; k < ix.keys.size(); ++k) {
+        if (ix.keys[k] < lo || ix.keys[k] > hi) continue;
+        if (!vals.empty()) leaves.push_back(ix.bvs[k]);  // L(v_j) for j >= 1
+        vals.push_back(ix.keys[k]);
+        if (vals.size() > (size_t)kMaxDecode + 1) return false;
+    }
+    return !vals.empty();
+}
+
+}  // namespace
+
+extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
+                                const cubit_txn* txn, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
+                                uint32_t flags) {
+    if (!t || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
+    const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
+    if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
+    if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
+    if (int rc = set_device(t->ctx)) return rc;
+    Emitter em;
+    bool empty = false;
+    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
+    if (empty) {
+        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
+        return CUBIT_OK;
+    }
+    return run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
+                    nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
+                    (flags & CUBIT_SCAN_ORDERED) != 0);
+}
+
+extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
+                                       const cubit_txn* txn, int col_a, int col_b, int64_t* d_out,
+                                       uint64_t* d_count, uint32_t flags) {
+    if (!t || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
+    auto ait = t->cols.find(col_a), bit = t->cols.find(col_b);
+    if (ait == t->cols.end() || bit == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column not registered");
+    if (ait->second.type != CUBIT_TYPE_INT64 || bit->second.type != CUBIT_TYPE_INT64)
+        return fail(CUBIT_ERR_UNSUPPORTED, "sum_product needs INT64 (DECIMAL storage) columns");
+    if (int rc = set_device(t->ctx)) return rc;
+    cubit_ctx* ctx = t->ctx;
+    uint64_t* count = d_count ? d_count : t->dummy_count;
+    auto visible_updates = [&](int col) {
+        auto u = t->upd.find(col);
+        return txn && u != t->upd.end() && u->second.any_visible(txn);
+    };
+    if (visible_updates(col_a) || visible_updates(col_b)) {
+        // MVCC fallback: row ids, then the probe (which applies the visible updates), then
+        // a plain sum over the two value arrays
+        if (ait->second.validity || bit->second.validity)
+            return fail(CUBIT_ERR_UNSUPPORTED, "sum_product with visible updates on nullable columns");
+        const uint64_t cap = t->n_rows;
+        if (int rc = ensure_tmp(ctx, 3 * cap)) return rc;
+        int64_t* ids = ctx->tmp_ids + 0;
+        int64_t* xa = ctx->tmp_ids + cap;
+        int64_t* xb = ctx->tmp_ids + 2 * cap;
+        // the scan's own decode must not use tmp_ids (ordered flag off)
+        if (int rc = cubit_table_scan(t, nodes, n_nodes, txn, ids, cap, count, 0)) return rc;
+        if (int rc = cubit_table_probe(t, col_a, txn, ids, count, cap, xa)) return rc;
+        if (int rc = cubit_table_probe(t, col_b, txn, ids, count, cap, xb)) return rc;
+        HIP_CHECK(launch_sum_product_arrays(xa, xb, count, cap, ctx->partials, d_out, ctx->stream));
+        return CUBIT_OK;
+    }
+    Emitter em;
+    bool empty = false;
+    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
+    if (empty) {
+        HIP_CHECK(hipMemsetAsync(d_out, 0, 2 * sizeof(int64_t), ctx->stream));
+        HIP_CHECK(hipMemsetAsync(count, 0, sizeof(uint64_t), ctx->stream));
+        return CUBIT_OK;
+    }
+    SumArgs sa{};
+    sa.a = static_cast<const int64_t*>(ait->second.data);
+    sa.a_valid = ait->second.validity;
+    sa.partials = ctx->partials;
+    std::vector<int64_t> vals;
+    std::vector<const uint64_t*> dl;
+    if (!(flags & CUBIT_SUM_GATHER_B) && decodable_values(t, nodes, n_nodes, col_b, vals, dl)) {
+        sa.b = nullptr;
+        sa.v0 = vals[0];
+        sa.n_decode = (uint32_t)dl.size();
+        for (size_t j = 0; j < dl.size(); ++j) {
+            sa.dleaf[j] = dl[j];
+            sa.delta[j] = vals[j + 1] - vals[j];
+        }
+        t->last_decoded = (uint32_t)dl.size() + 1;
+    } else {
+        sa.b = static_cast<const int64_t*>(bit->second.data);
+        sa.b_valid = bit->second.validity;
+        t->last_decoded = 0;
+    }
+    EvalArgs a{};
+    a.prog = em.prog;
+    a.n_rows = t->n_rows;
+    a.n_words = (t->n_rows + 63) / 64;
+    a.row_base = t->row_base;
+    a.count = count;
+    a.ticket = ctx->ticket;
+    a.num_tiles = (uint32_t)(padded_words(t->n_rows) / decode_tile_words());
+    const unsigned grid = std::min<unsigned>(a.num_tiles, sum_product_grid((unsigned)ctx->n_cus));
+    HIP_CHECK(launch_eval_sum_product(a, sa, std::max(grid, 1u), d_out, ctx->stream));
+    return CUBIT_OK;
 }
 
 extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_t* n_passes) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     if (n_leaves) *n_leaves = t->last_leaves;
     if (n_passes) *n_passes = t->last_passes;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_sum_decode(cubit_table* t, uint32_t* n_values) {
+    if (!t || !n_values) return fail(CUBIT_ERR_INVALID, "null argument");
+    *n_values = t->last_decoded;
     return CUBIT_OK;
 }
 

@@ -103,6 +103,28 @@ hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const i
                                      int64_t* out, hipStream_t stream);
 constexpr int kSumBlocks = 1024;  // partials buffer holds 2 * kSumBlocks int64
 
+// Fused filter + probe + reduce: sum(a[r] * b[r]) over the qualifying rows r (K1+K3).
+// b = nullptr: b is decoded from its range index, b = v0 + Σ_j delta[j]·[r ∉ dleaf[j]]
+// (dleaf[j] = L(v_j), the filter pins b to v0 < v1 < … ≤ kMaxDecode+1 values).
+constexpr int kMaxDecode = 3;
+struct SumArgs {
+    const int64_t* a;
+    const uint64_t* a_valid;  // optional
+    const int64_t* b;         // nullptr → decode
+    const uint64_t* b_valid;  // optional (gather mode)
+    const uint64_t* dleaf[kMaxDecode];
+    int64_t delta[kMaxDecode];
+    int64_t v0;
+    uint32_t n_decode;
+    int64_t* partials;  // 2 int64 (lo, hi) per workgroup
+};
+// grid = persistent workgroups; partials must hold 2·grid int64; out = {lo, hi}
+hipError_t launch_eval_sum_product(const EvalArgs& a, const SumArgs& s, unsigned grid, int64_t* out, hipStream_t stream);
+unsigned sum_product_grid(unsigned n_cus);
+// sum over i < *d_count of x[i]·y[i] (MVCC fallback of the fused path)
+hipError_t launch_sum_product_arrays(const int64_t* x, const int64_t* y, const uint64_t* d_count, uint64_t max_n,
+                                     int64_t* partials, int64_t* out, hipStream_t stream);
+
 // MVCC (K4)
 // visibility: words = valid-row mask, then clear rows whose delete is visible to txn
 hipError_t launch_visibility(const int64_t* del_rows, const uint64_t* del_ids, uint64_t n_del, uint64_t n_rows,

@@ -618,6 +618,208 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     if (t == 0) finish_ticket(a.ticket, a.count);
 }
 
+// ------------------------------------------------------------------ K1+K3: fused filter + probe-sum
+
+__device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, __int128 x) {
+    const uint64_t xl = (uint64_t)x;
+    const int64_t xh = (int64_t)(x >> 64);
+    const uint64_t nl = lo + xl;
+    hi += xh + (nl < lo ? 1 : 0);
+    lo = nl;
+}
+
+// SELECT sum(a * b) WHERE <program>: evaluate a tile, decode its set bits into LDS (row
+// offset, and b's value when b is decoded from its index), then gather a (and b) for the
+// staged rows with several loads in flight per thread, accumulating in 128 bits
+// (DECIMAL(38,4) storage, Q6's sum(l_extendedprice * l_discount)). No row ids are written.
+// Persistent like eval_decode_pairs; per-workgroup partials are summed by sum_partials_kernel;
+// the qualifying-row count goes through the claim ticket.
+template <int K, int M, int FORM>
+__global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s) {
+    constexpr int THREADS = 512, PAIRS = 2, NW = 4, STAGE = 4096;
+    constexpr int FB = 32;  // THREADS * 128 ≥ 65536
+    constexpr uint64_t FMASK = 0xffffffffull;
+    constexpr int FPW = 2, NPK = 1;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr int NWAVES = THREADS / 64;
+    __shared__ uint64_t s_wave_tot[NWAVES];
+    __shared__ uint32_t s_row[STAGE];
+    __shared__ int32_t s_w[M > 0 ? STAGE : 1];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint64_t acc_lo = 0;
+    int64_t acc_hi = 0;
+    uint64_t total = 0;
+
+    auto accumulate = [&](int64_t row, int64_t bval_decoded) {
+        const uint64_t r = (uint64_t)(row - a.row_base);
+        if (s.a_valid && !((s.a_valid[r >> 6] >> (r & 63)) & 1ull)) return;
+        int64_t bv = bval_decoded;
+        if (M == 0) {
+            if (s.b_valid && !((s.b_valid[r >> 6] >> (r & 63)) & 1ull)) return;
+            bv = s.b[r];
+        }
+        add128(acc_lo, acc_hi, (__int128)s.a[r] * (__int128)bv);
+    };
+
+    u64x2 v[K][PAIRS];
+    u64x2 dv[M > 0 ? M : 1][PAIRS];
+    uint32_t tile = blockIdx.x;
+    auto load_decode = [&](uint64_t tile_word0) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const u64x2* base = reinterpret_cast<const u64x2*>(s.dleaf[m] + tile_word0);
+#pragma unroll
+            for (int p = 0; p < PAIRS; ++p) dv[m][p] = __builtin_nontemporal_load(base + p * THREADS + t);
+        }
+    };
+    if (tile < a.num_tiles) {
+        load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+        load_decode((uint64_t)tile * TILE_WORDS);
+    }
+    while (tile < a.num_tiles) {
+        const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+        uint64_t r[NW];
+        eval_words<K, NW, FORM>(a.prog, v, r);
+        tail_mask<NW, THREADS>(a, tile_word0, t, r);
+        const uint32_t next = tile + gridDim.x;
+        if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        uint64_t packed = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p)
+            packed |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
+        const uint64_t incl = wave_incl_scan(packed, lane);
+        if (lane == 63) s_wave_tot[wave] = incl;
+        __syncthreads();
+        uint64_t wp = 0, bt = 0;
+#pragma unroll
+        for (int w = 0; w < NWAVES; ++w) {
+            const uint64_t x = s_wave_tot[w];
+            if (w < wave) wp += x;
+            bt += x;
+        }
+        uint64_t pair_off[PAIRS];
+        uint64_t tile_count = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            pair_off[p] = tile_count + (((wp + incl - packed) >> (FB * (p % FPW))) & FMASK);
+            tile_count += (bt >> (FB * (p % FPW))) & FMASK;
+        }
+        total += tile_count;
+        const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
+        const bool staged = tile_count <= (uint64_t)STAGE;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            uint32_t off = (uint32_t)pair_off[p];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                uint64_t w = r[2 * p + e];
+                const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                while (w) {
+                    const uint32_t b = (uint32_t)__builtin_ctzll(w);
+                    int64_t bval = 0;
+                    if (M > 0) {
+                        bval = s.v0;
+#pragma unroll
+                        for (int m = 0; m < M; ++m) {
+                            const u64x2 d = dv[m][p];
+                            const uint64_t dw = e ? d.y : d.x;
+                            if (!((dw >> b) & 1ull)) bval += s.delta[m];
+                        }
+                    }
+                    if (staged) {
+                        s_row[off] = wrow + b;
+                        if (M > 0) s_w[off] = (int32_t)bval;
+                    } else {
+                        accumulate(row0 + (int64_t)(wrow + b), bval);  // dense tile: direct
+                    }
+                    ++off;
+                    w &= w - 1;
+                }
+            }
+        }
+        if (M > 0 && next < a.num_tiles) load_decode((uint64_t)next * TILE_WORDS);
+        __syncthreads();  // stage complete
+        if (staged) {
+            // 4 gathers in flight per thread per round
+            for (uint32_t i = t; i < (uint32_t)tile_count; i += 4 * THREADS) {
+                int64_t av[4], bvv[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t k = i + u * THREADS;
+                    ok[u] = k < (uint32_t)tile_count;
+                    const uint64_t rr = (uint64_t)(row0 - a.row_base) + (ok[u] ? s_row[k] : 0u);
+                    av[u] = ok[u] ? s.a[rr] : 0;
+                    bvv[u] = M > 0 ? (ok[u] ? (int64_t)s_w[k] : 0) : (ok[u] ? s.b[rr] : 0);
+                    if (ok[u] && s.a_valid && !((s.a_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
+                    if (M == 0 && ok[u] && s.b_valid && !((s.b_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (ok[u]) add128(acc_lo, acc_hi, (__int128)av[u] * (__int128)bvv[u]);
+            }
+        }
+        __syncthreads();  // stage / wave totals free
+        tile = next;
+    }
+    // block reduce of the 128-bit partial sums
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t olo = __shfl_xor(acc_lo, d, 64);
+        const int64_t ohi = __shfl_xor(acc_hi, d, 64);
+        const uint64_t nlo = acc_lo + olo;
+        acc_hi = acc_hi + ohi + (nlo < acc_lo ? 1 : 0);
+        acc_lo = nlo;
+    }
+    __shared__ uint64_t s_lo[NWAVES];
+    __shared__ int64_t s_hi[NWAVES];
+    if (lane == 0) {
+        s_lo[wave] = acc_lo;
+        s_hi[wave] = acc_hi;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t lo = 0;
+        int64_t hi = 0;
+        for (int w = 0; w < NWAVES; ++w) add128(lo, hi, ((__int128)s_hi[w] << 64) | (unsigned __int128)s_lo[w]);
+        s.partials[2 * blockIdx.x] = (int64_t)lo;
+        s.partials[2 * blockIdx.x + 1] = hi;
+        // returning, consumed: performed before the arrival in finish_ticket
+        const unsigned long long before =
+            total ? atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)total) : 0ull;
+        if (before == ~0ull) __builtin_trap();
+        finish_ticket(a.ticket, a.count);
+    }
+}
+
+__global__ __launch_bounds__(256) void sum_product_arrays_kernel(const int64_t* __restrict__ x,
+                                                                 const int64_t* __restrict__ y,
+                                                                 const uint64_t* __restrict__ d_count, uint64_t max_n,
+                                                                 int64_t* __restrict__ partials) {
+    __shared__ __int128 s_part[4];
+    const uint64_t n = min(*d_count, max_n);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t lo = 0;
+    int64_t hi = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        add128(lo, hi, (__int128)x[i] * (__int128)y[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t olo = __shfl_xor(lo, d, 64);
+        const int64_t ohi = __shfl_xor(hi, d, 64);
+        const uint64_t nlo = lo + olo;
+        hi = hi + ohi + (nlo < lo ? 1 : 0);
+        lo = nlo;
+    }
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = ((__int128)hi << 64) | lo;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const __int128 tot = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+        partials[2 * blockIdx.x] = (int64_t)(uint64_t)tot;
+        partials[2 * blockIdx.x + 1] = (int64_t)(tot >> 64);
+    }
+}
+
 // ------------------------------------------------------------------ row-order pass
 
 // Exclusive scan of the per-tile run lengths (one workgroup, any tile count).
@@ -1045,6 +1247,55 @@ hipError_t launch_gather_sum_product(const int64_t* x, const int64_t* y, const i
                                      int64_t* out, hipStream_t stream) {
     hipLaunchKernelGGL(gather_sum_product_kernel, dim3(kSumBlocks), dim3(256), 0, stream, x, y, rowids, d_count, max_n,
                        row_base, partials);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, stream, partials, kSumBlocks, out);
+    return hipGetLastError();
+}
+
+unsigned sum_product_grid(unsigned n_cus) { return std::min<unsigned>(2 * n_cus, (unsigned)kSumBlocks); }
+
+template <int K, int M>
+void launch_sum_km(const EvalArgs& a, const SumArgs& s, unsigned grid, hipStream_t st) {
+    switch (eval_form(a.prog)) {
+    case FORM_CONJ: hipLaunchKernelGGL((eval_sum_product<K, M, FORM_CONJ>), dim3(grid), dim3(512), 0, st, a, s); break;
+    case FORM_DNF: hipLaunchKernelGGL((eval_sum_product<K, M, FORM_DNF>), dim3(grid), dim3(512), 0, st, a, s); break;
+    case FORM_CNF: hipLaunchKernelGGL((eval_sum_product<K, M, FORM_CNF>), dim3(grid), dim3(512), 0, st, a, s); break;
+    default: hipLaunchKernelGGL((eval_sum_product<K, M, FORM_POSTFIX>), dim3(grid), dim3(512), 0, st, a, s); break;
+    }
+}
+
+template <int K>
+void launch_sum_k(const EvalArgs& a, const SumArgs& s, unsigned grid, hipStream_t st) {
+    switch (s.b ? 0 : s.n_decode) {
+    case 0: launch_sum_km<K, 0>(a, s, grid, st); break;
+    case 1: launch_sum_km<K, 1>(a, s, grid, st); break;
+    case 2: launch_sum_km<K, 2>(a, s, grid, st); break;
+    default: launch_sum_km<K, 3>(a, s, grid, st); break;
+    }
+}
+
+hipError_t launch_eval_sum_product(const EvalArgs& a, const SumArgs& s, unsigned grid, int64_t* out, hipStream_t st) {
+    if (!s.b && s.n_decode > (uint32_t)kMaxDecode) return hipErrorInvalidValue;
+    switch (a.prog.n_leaves) {
+    case 1: launch_sum_k<1>(a, s, grid, st); break;
+    case 2: launch_sum_k<2>(a, s, grid, st); break;
+    case 3: launch_sum_k<3>(a, s, grid, st); break;
+    case 4: launch_sum_k<4>(a, s, grid, st); break;
+    case 5: launch_sum_k<5>(a, s, grid, st); break;
+    case 6: launch_sum_k<6>(a, s, grid, st); break;
+    case 7: launch_sum_k<7>(a, s, grid, st); break;
+    case 8: launch_sum_k<8>(a, s, grid, st); break;
+    default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, st, s.partials, (int)grid, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_product_arrays(const int64_t* x, const int64_t* y, const uint64_t* d_count, uint64_t max_n,
+                                     int64_t* partials, int64_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(sum_product_arrays_kernel, dim3(kSumBlocks), dim3(256), 0, stream, x, y, d_count, max_n,
+                       partials);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, stream, partials, kSumBlocks, out);
     return hipGetLastError();
 }

@@ -5,7 +5,7 @@ Everything here is a thin ctypes wrapper; the work happens in libcubitgpu.so.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Optional, Sequence
+from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -229,6 +229,31 @@ class CubitTable:
         L.check(self.lib.cubit_table_probe(self.handle, col, C.byref(txn) if txn is not None else None,
                                            C.c_void_p(rowids_dptr), C.c_void_p(count_dptr), max_n,
                                            C.c_void_p(out_dptr)))
+
+    def sum_product(self, col_a: int, col_b: int, filter_set: Optional[TableFilterSet] = None,
+                    residual: Optional[Residual] = None, txn: Optional[L.Txn] = None,
+                    gather_b: bool = False) -> Tuple[int, int]:
+        """SELECT sum(a*b), count(*) WHERE <filter> in one fused pass → (sum as a Python int
+        of the 128-bit DECIMAL storage, qualifying rows)."""
+        plan = serialize(filter_set, residual)
+        arr = to_ctypes(plan.nodes)
+        out = self.ctx.alloc(16)
+        cnt = self.ctx.alloc(16)
+        L.check(self.lib.cubit_table_sum_product(self.handle, arr, len(plan.nodes),
+                                                 C.byref(txn) if txn is not None else None, col_a, col_b,
+                                                 C.c_void_p(out.addr), C.c_void_p(cnt.addr),
+                                                 L.SUM_GATHER_B if gather_b else 0))
+        self.ctx.check()
+        lo, hi = (int(x) for x in out.download(np.int64, 2))
+        n = int(cnt.download(np.uint64, 1)[0])
+        out.free()
+        cnt.free()
+        return (hi << 64) + (lo & (2 ** 64 - 1)), n
+
+    def last_sum_decode(self) -> int:
+        v = C.c_uint32()
+        L.check(self.lib.cubit_table_last_sum_decode(self.handle, C.byref(v)))
+        return int(v.value)
 
     def last_plan(self):
         k = C.c_uint32()

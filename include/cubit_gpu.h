@@ -198,6 +198,21 @@ int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64
 /* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
 int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
 
+/* SELECT sum(a * b) WHERE <filter> as one fused pass (K1 + K3): evaluate the program,
+ * gather a (and b) for the qualifying rows only, accumulate in 128 bits — no row ids are
+ * materialised. Replaces the scan → FilterScan/Slice probe (column_data.cpp:305-309) → SUM
+ * chain of a query like TPC-H Q6 (sum(l_extendedprice * l_discount)). a and b are INT64
+ * columns (DECIMAL storage); rows where a or b is NULL do not contribute. When the filter
+ * pins b to at most 4 values of an exact range index, b is decoded from that index instead
+ * of gathered (CUBIT_SUM_GATHER_B forces the gather). d_out[0..1] = {lo, hi} of the 128-bit
+ * sum; d_count (optional) = qualifying rows. Visible MVCC updates on a or b fall back to
+ * scan + probe + sum (those columns must then be NOT NULL). */
+#define CUBIT_SUM_GATHER_B 1u
+int cubit_table_sum_product(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
+                            int col_a, int col_b, int64_t *d_out, uint64_t *d_count, uint32_t flags);
+/* How the last sum_product read b: number of values decoded from the index (0 = gathered). */
+int cubit_table_last_sum_decode(cubit_table *t, uint32_t *n_values);
+
 #ifdef __cplusplus
 }
 #endif

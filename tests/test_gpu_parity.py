@@ -415,3 +415,61 @@ def test_index_build_statistics_on_device(ctx):
     t2.build_index(0, L.INDEX_RANGE, [0])  # explicit keys are fine
     fs = F.TableFilterSet({0: F.ConstantFilter("<", 0)})
     assert np.array_equal(t2.scan(fs), np.arange(0, 20, 2))
+
+
+@pytest.mark.parametrize("sf", [0.1, 1.0])
+def test_fused_q6_revenue(ctx, golden, sf):
+    """SELECT sum(l_extendedprice*l_discount) WHERE <Q6> in one fused pass: the reference's
+    answer file exactly, with l_discount decoded from its range index (3 values) and gathered."""
+    li = lineitem(sf)
+    t = q6_table(ctx, li)
+    t.build_index(0, L.INDEX_BINS, [F.date(y, 1, 1) for y in range(1992, 2000)])
+    want = revenue_from_answer(golden["tpch"]["q6_revenue"]["1" if sf == 1.0 else str(sf)]["revenue"])
+    rev, n = t.sum_product(3, 1, F.q6_filter_set())
+    assert rev == want and n == len(oracle_q6(li))
+    assert t.last_sum_decode() == 3
+    rev2, n2 = t.sum_product(3, 1, F.q6_filter_set(), gather_b=True)
+    assert rev2 == want and n2 == n
+    assert t.last_sum_decode() == 0
+
+
+def test_fused_sum_product_nulls_mvcc_and_fallback(ctx):
+    n = 250_000
+    rng = np.random.default_rng(31)
+    a = rng.integers(-10_000, 10_000, n).astype(np.int64)
+    b = rng.integers(0, 12, n).astype(np.int64)
+    va = rng.random(n) > 0.1
+    t = CubitTable(ctx, n)
+    t.add_column(0, a, validity_from_mask(va))
+    t.add_column(1, b)
+    t.build_index(1, L.INDEX_RANGE)
+    fs = F.TableFilterSet({1: F.ConjunctionAndFilter([F.ConstantFilter(">=", 3), F.ConstantFilter("<=", 5)])})
+    rows = O.table_scan([O.Column(a, validity_from_mask(va)), O.Column(b)], F.serialize(fs), n)
+    keep = rows[va[rows]]
+    want = int((a[keep].astype(object) * b[keep].astype(object)).sum())
+    for gather in (False, True):
+        got, cnt = t.sum_product(0, 1, fs, gather_b=gather)
+        assert got == want and cnt == len(rows)
+        assert t.last_sum_decode() == (0 if gather else 3)
+    # deletes visible to the reader: fused path with the visibility leaf
+    dels = np.arange(0, n, 5, dtype=np.int64)
+    t.set_deletes(dels, np.full(len(dels), 3, dtype=np.uint64))
+    alive = np.ones(n, dtype=bool)
+    alive[dels] = False
+    keep2 = keep[alive[keep]]
+    want2 = int((a[keep2].astype(object) * b[keep2].astype(object)).sum())
+    got, _ = t.sum_product(0, 1, fs, txn=L.Txn(10, TXN_START + 1))
+    assert got == want2
+    # visible updates on b → scan + probe + sum fallback (b NOT NULL, a has NULLs → refused)
+    t2 = CubitTable(ctx, n)
+    t2.add_column(0, a)
+    t2.add_column(1, b)
+    t2.build_index(1, L.INDEX_RANGE)
+    up = np.arange(0, n, 9, dtype=np.int64)
+    t2.set_updates(1, up, np.full(len(up), 4), np.full(len(up), TXN_START + 1, dtype=np.uint64))
+    b2 = b.copy()
+    b2[up] = 4
+    rows2 = np.nonzero((b2 >= 3) & (b2 <= 5))[0]
+    want3 = int((a[rows2].astype(object) * b2[rows2].astype(object)).sum())
+    got, cnt = t2.sum_product(0, 1, fs, txn=L.Txn(2, TXN_START + 1))
+    assert got == want3 and cnt == len(rows2)
