@@ -934,6 +934,118 @@ extern "C" int cubit_table_index_info(cubit_table* t, int col, uint32_t* n_bitve
     return CUBIT_OK;
 }
 
+// ------------------------------------------------------------------ index persistence
+
+namespace {
+
+constexpr char kIndexMagic[8] = {'C', 'U', 'B', 'I', 'T', 'I', 'X', '1'};
+
+struct IndexFileHeader {
+    char magic[8];
+    uint32_t version;
+    uint32_t encoding;
+    uint64_t n_rows;
+    uint64_t nwp;
+    uint32_t exact_all;
+    uint32_t empty;
+    int64_t vmin;
+    int64_t vmax;
+    uint64_t n_keys;
+    uint64_t n_bv;
+};
+static_assert(sizeof(IndexFileHeader) == 72, "stable on-disk header");
+
+}  // namespace
+
+extern "C" int cubit_table_save_index(cubit_table* t, int col, int encoding, const char* path) {
+    if (!t || !path) return fail(CUBIT_ERR_INVALID, "null argument");
+    const Index* ix = nullptr;
+    if (encoding == CUBIT_INDEX_BINS) {
+        auto it = t->bins.find(col);
+        if (it != t->bins.end()) ix = &it->second;
+    } else {
+        auto it = t->idx.find(col);
+        if (it != t->idx.end() && it->second.encoding == encoding) ix = &it->second;
+    }
+    if (!ix) return fail(CUBIT_ERR_INVALID, "column %d has no index of encoding %d", col, encoding);
+    if (int rc = set_device(t->ctx)) return rc;
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(CUBIT_ERR_INVALID, "cannot open %s for writing", path);
+    IndexFileHeader h{};
+    std::memcpy(h.magic, kIndexMagic, 8);
+    h.version = 1;
+    h.encoding = (uint32_t)ix->encoding;
+    h.n_rows = t->n_rows;
+    h.nwp = t->nwp;
+    h.exact_all = ix->exact_all ? 1u : 0u;
+    h.empty = ix->empty ? 1u : 0u;
+    h.vmin = ix->vmin;
+    h.vmax = ix->vmax;
+    h.n_keys = ix->keys.size();
+    h.n_bv = ix->bvs.size();
+    bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1 &&
+              (h.n_keys == 0 || std::fwrite(ix->keys.data(), 8, h.n_keys, f) == h.n_keys);
+    std::vector<uint64_t> host(ok ? t->nwp : 0);
+    for (size_t k = 0; ok && k < ix->bvs.size(); ++k) {
+        if (hipMemcpy(host.data(), ix->bvs[k], t->nwp * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::fclose(f);
+            return fail(CUBIT_ERR_HIP, "index download failed");
+        }
+        ok = std::fwrite(host.data(), 8, t->nwp, f) == t->nwp;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? CUBIT_OK : fail(CUBIT_ERR_INVALID, "short write to %s", path);
+}
+
+extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path) {
+    if (!t || !path) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(CUBIT_ERR_INVALID, "cannot open %s", path);
+    auto bad = [&](const char* why) {
+        std::fclose(f);
+        return fail(CUBIT_ERR_INVALID, "%s: %s", path, why);
+    };
+    IndexFileHeader h{};
+    if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, kIndexMagic, 8) != 0 || h.version != 1)
+        return bad("not a cubit index file");
+    if (h.n_rows != t->n_rows || h.nwp != t->nwp) return bad("index was built for a partition of another size");
+    if (h.encoding > CUBIT_INDEX_BINS) return bad("unknown encoding");
+    const uint64_t want_bv = h.encoding == CUBIT_INDEX_BINS ? (h.n_keys ? h.n_keys - 1 : 0) : h.n_keys;
+    if (h.n_bv != want_bv || h.n_keys > (1ull << 32)) return bad("inconsistent header");
+    Index ix;
+    ix.encoding = (int)h.encoding;
+    ix.exact_all = h.exact_all != 0;
+    ix.empty = h.empty != 0;
+    ix.vmin = h.vmin;
+    ix.vmax = h.vmax;
+    ix.keys.resize(h.n_keys);
+    if (h.n_keys && std::fread(ix.keys.data(), 8, h.n_keys, f) != h.n_keys) return bad("truncated keys");
+    if (!std::is_sorted(ix.keys.begin(), ix.keys.end())) return bad("keys not sorted");
+    std::vector<uint64_t> host(t->nwp);
+    for (uint64_t k = 0; k < h.n_bv; ++k) {
+        if (std::fread(host.data(), 8, t->nwp, f) != t->nwp) return bad("truncated bitvectors");
+        auto b = std::make_unique<DevBuf>();
+        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) {
+            std::fclose(f);
+            return fail(CUBIT_ERR_OOM, "index bitvector allocation failed");
+        }
+        if (hipMemcpy(b->p, host.data(), t->nwp * 8, hipMemcpyHostToDevice) != hipSuccess) {
+            std::fclose(f);
+            return fail(CUBIT_ERR_HIP, "index upload failed");
+        }
+        ix.bvs.push_back(static_cast<uint64_t*>(b->p));
+        ix.owned.push_back(std::move(b));
+        ix.bytes += t->nwp * 8;
+    }
+    std::fclose(f);
+    if (ix.encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
+    else t->idx[col] = std::move(ix);
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, const uint64_t* ids, uint64_t n) {
     if (!t || (n && (!rows || !ids))) return fail(CUBIT_ERR_INVALID, "null argument");
     if (int rc = set_device(t->ctx)) return rc;

@@ -104,6 +104,8 @@ GPU_SIGNATURES = {
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
+    "cubit_table_save_index": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
+    "cubit_table_load_index": (C.c_int, [_P, C.c_int, C.c_char_p]),
 }
 
 GEN_SIGNATURES = {

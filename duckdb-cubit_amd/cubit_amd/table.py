@@ -172,6 +172,12 @@ class CubitTable:
         else:
             L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, None, 0))
 
+    def save_index(self, col: int, encoding: int, path) -> None:
+        L.check(self.lib.cubit_table_save_index(self.handle, col, encoding, str(path).encode()))
+
+    def load_index(self, col: int, path) -> None:
+        L.check(self.lib.cubit_table_load_index(self.handle, col, str(path).encode()))
+
     def index_info(self, col: int):
         n = C.c_uint32()
         b = C.c_uint64()

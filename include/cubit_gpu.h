@@ -178,6 +178,13 @@ int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, 
 int cubit_table_build_index(cubit_table *t, int col, int encoding, const int64_t *values, uint32_t n);
 /* Number of bitvectors and bytes held by the indexes on col, all encodings (0 if none). */
 int cubit_table_index_info(cubit_table *t, int col, uint32_t *n_bitvectors, uint64_t *bytes);
+/* Index persistence (the reference persists index state through IndexStorageInfo,
+ * bound_index.hpp:117-118): write a column's RANGE / EQUALITY / BINS index (keys,
+ * statistics, bitvectors) to one file, and load it back into a partition of the same size
+ * (it replaces that encoding's index on the column). The file does not carry the column
+ * data: load it only beside the column it was built from. */
+int cubit_table_save_index(cubit_table *t, int col, int encoding, const char *path);
+int cubit_table_load_index(cubit_table *t, int col, const char *path);
 
 /* MVCC delta. Deletes: rows with their delete ids (ChunkVectorInfo::deleted,
  * chunk_info.cpp:181-202). Updates on `col`: rows, new values and version ids

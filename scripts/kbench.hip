@@ -212,6 +212,7 @@ int main(int argc, char** argv) {
                                          dim3(512), 0, s, a, dir);
                   }, 0});
     DT("tiles P2 T512 x2/CU", 2, 4096, 512, 2);
+    DT("tiles P2 T512 grid=tiles", 2, 4096, 512, 1000000);
     DT("tiles P1 T512 x2/CU", 1, 2048, 512, 2);
     DT("tiles P1 T256 x4/CU", 1, 1024, 256, 4);
     DT("tiles P2 T256 x4/CU", 2, 2048, 256, 4);

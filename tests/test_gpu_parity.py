@@ -473,3 +473,32 @@ def test_fused_sum_product_nulls_mvcc_and_fallback(ctx):
     want3 = int((a[rows2].astype(object) * b2[rows2].astype(object)).sum())
     got, cnt = t2.sum_product(0, 1, fs, txn=L.Txn(2, TXN_START + 1))
     assert got == want3 and cnt == len(rows2)
+
+
+def test_index_save_and_load(ctx, tmp_path):
+    """Persisted indexes (range, equality, bins) load into a fresh partition and answer the
+    same scans; a file for another partition size or a foreign file is refused."""
+    li = lineitem(0.01)
+    t = q6_table(ctx, li)
+    years = [F.date(y, 1, 1) for y in range(1992, 2000)]
+    t.build_index(0, L.INDEX_BINS, years)
+    for col, enc in ((0, L.INDEX_RANGE), (0, L.INDEX_BINS), (1, L.INDEX_RANGE), (2, L.INDEX_RANGE)):
+        t.save_index(col, enc, tmp_path / f"c{col}_{enc}.cubitix")
+    t2 = CubitTable(ctx, li.n_rows, li.row_base)
+    for c, arr in enumerate((li.l_shipdate, li.l_discount, li.l_quantity, li.l_extendedprice)):
+        t2.add_column(c, arr)
+    for f in sorted(tmp_path.glob("*.cubitix")):
+        col = int(f.name[1])
+        t2.load_index(col, f)
+    assert t2.index_info(0) == t.index_info(0) and t2.index_info(2) == t.index_info(2)
+    got = t2.scan(F.q6_filter_set())
+    assert np.array_equal(got, oracle_q6(li))
+    assert t2.last_plan() == (4, 1)
+    t3 = CubitTable(ctx, li.n_rows - 1)
+    t3.add_column(0, li.l_shipdate[:-1])
+    with pytest.raises(Exception, match="another size"):
+        t3.load_index(0, tmp_path / "c0_0.cubitix")
+    junk = tmp_path / "junk.bin"
+    junk.write_bytes(b"x" * 200)
+    with pytest.raises(Exception, match="not a cubit index"):
+        t2.load_index(0, junk)
