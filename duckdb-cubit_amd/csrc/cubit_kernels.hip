@@ -419,7 +419,8 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     constexpr int NWAVES = THREADS / 64;
     typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
     __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
-    __shared__ uint64_t s_off;
+    __shared__ uint64_t s_off;        // claimed base of the pair being copied out
+    __shared__ uint64_t s_dense_off;  // claimed base of a dense tile
     __shared__ uint32_t s_stage[2][2 * STAGE];
     __shared__ uint32_t s_tile_a[2], s_tile_b[2], s_cnt_a[2], s_cnt_b[2], s_dense[2];
 
@@ -437,7 +438,25 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
     if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
 
     // evaluate the tile in v → r, block scan → per-pair offsets within the tile, tile count
-    auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS]) -> uint64_t {
+    // publish the previous pair's claim (thread 0, before a barrier): base + directory entries
+    auto publish = [&](int sp) {
+        s_off = pend_claim;
+        if (dir) {
+            // staged tiles (dense ones wrote their own entry); empty tiles get {0, 0}
+            const uint32_t ca = s_cnt_a[sp], cb = s_cnt_b[sp];
+            if (!(s_dense[sp] & 1)) {
+                dir[2 * s_tile_a[sp]] = ca ? pend_claim : 0;
+                dir[2 * s_tile_a[sp] + 1] = ca;
+            }
+            if (!(s_dense[sp] & 2) && s_tile_b[sp] < a.num_tiles) {
+                dir[2 * s_tile_b[sp]] = cb ? pend_claim + ca : 0;
+                dir[2 * s_tile_b[sp] + 1] = cb;
+            }
+        }
+    };
+
+    auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS],
+                         int publish_sp) -> uint64_t {
         const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
         eval_words<K, NW, FORM>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
@@ -453,6 +472,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
             incl[q] = wave_incl_scan(packed[q], lane);
             if (lane == 63) s_wave_tot[par][wave][q] = incl[q];
         }
+        if (publish_sp >= 0 && t == 0) publish(publish_sp);
         __syncthreads();
         uint64_t block_tot[NPK], wave_pre[NPK];
 #pragma unroll
@@ -505,14 +525,14 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         const int64_t row0 = a.row_base + (int64_t)((uint64_t)tl * TILE_ROWS);
         if (t == 0) {
             const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)tile_count);
-            s_off = c;
+            s_dense_off = c;
             if (dir) {
                 dir[2 * tl] = c;
                 dir[2 * tl + 1] = tile_count;
             }
         }
         __syncthreads();
-        const uint64_t base = s_off;
+        const uint64_t base = s_dense_off;
         if (write_ids) {
 #pragma unroll
             for (int p = 0; p < PAIRS; ++p) {
@@ -529,28 +549,15 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
                 }
             }
         }
-        __syncthreads();  // s_off free again
+        __syncthreads();  // s_dense_off free again
         return 0;
     };
 
-    // copy out stage sp (one contiguous run of cnt_a + cnt_b ids) at the claimed base
+    // copy out stage sp (one contiguous run of cnt_a + cnt_b ids) at the claimed base, which
+    // thread 0 published before the barrier that precedes this call. No barrier of its own:
+    // stage sp is next written two units later and s_off next published one pair later,
+    // both behind barriers every thread passes after this copy.
     auto copy_out = [&](int sp) {
-        if (t == 0) {
-            s_off = pend_claim;
-            if (dir) {
-                // staged tiles (dense ones wrote their own entry); empty tiles get {0, 0}
-                const uint32_t ca = s_cnt_a[sp], cb = s_cnt_b[sp];
-                if (!(s_dense[sp] & 1)) {
-                    dir[2 * s_tile_a[sp]] = ca ? pend_claim : 0;
-                    dir[2 * s_tile_a[sp] + 1] = ca;
-                }
-                if (!(s_dense[sp] & 2) && s_tile_b[sp] < a.num_tiles) {
-                    dir[2 * s_tile_b[sp]] = cb ? pend_claim + ca : 0;
-                    dir[2 * s_tile_b[sp] + 1] = cb;
-                }
-            }
-        }
-        __syncthreads();
         const uint64_t base = s_off;
         const uint32_t n = s_cnt_a[sp] + s_cnt_b[sp];
         if (write_ids && n) {
@@ -571,7 +578,6 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
                 }
             }
         }
-        __syncthreads();  // stage and s_off reusable
     };
 
     bool pending = false;  // a claimed pair waits for copy-out (uniform)
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         const int sp = (int)(pair & 1);
         // ---- unit A
         uint64_t r[NW], off[PAIRS];
-        const uint64_t cnt_a_all = eval_scan(tile, 0, r, off);
+        const uint64_t cnt_a_all = eval_scan(tile, 0, r, off, pending ? (sp ^ 1) : -1);
         if (pending) copy_out(sp ^ 1);
         const uint32_t tile_b = tile + G;
         if (tile_b < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile_b * TILE_WORDS, t, v);
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         uint32_t next = tile_b;
         bool dense_b = false;
         if (tile_b < a.num_tiles) {
-            const uint64_t cnt_b_all = eval_scan(tile_b, 1, r, off);
+            const uint64_t cnt_b_all = eval_scan(tile_b, 1, r, off, -1);
             dense_b = cnt_b_all > (uint64_t)STAGE;
             next = tile_b + G;
             const uint32_t staged_b = cnt_b_all <= (uint64_t)STAGE ? (uint32_t)cnt_b_all : 0;
@@ -614,7 +620,12 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(
         tile = next;
         ++pair;
     }
-    if (pending) copy_out((int)((pair - 1) & 1));
+    if (pending) {
+        const int sp = (int)((pair - 1) & 1);
+        if (t == 0) publish(sp);
+        __syncthreads();
+        copy_out(sp);
+    }
     if (t == 0) finish_ticket(a.ticket, a.count);
 }
 
