@@ -405,8 +405,9 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
 // Copy-out stores are issued before the prefetch they precede, so the wait for the prefetched
 // leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
 // STAGE hits claims on its own and writes straight to the output (dense path).
-template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX>
-__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_pairs(EvalArgs a, uint64_t* __restrict__ dir) {
+template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX, int WG_PER_CU = 2>
+__global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decode_pairs(EvalArgs a,
+                                                                                       uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
     // fake decode (same LDS traffic, no per-bit loop)
     constexpr int NW = 2 * PAIRS;

@@ -218,6 +218,18 @@ int main(int argc, char** argv) {
     DT("tiles P2 T256 x4/CU", 2, 2048, 256, 4);
     DP("pairs P1 T512 x2/CU", 1, 2048, 512, 2);
     DP("pairs P1 T256 x4/CU", 1, 1024, 256, 4);
+#define DPC(NAME, S, OCC)                                                                                      \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = dtiles;                                                                   \
+                      a.prog.negate = 0b01010;                                                                \
+                      a.prog.nops = 0;                                                                        \
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);                              \
+                      a.prog.ops = 0;                                                                         \
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, S, 512, 0, FORM_CONJ, OCC>),                \
+                                         dim3(std::min<unsigned>(dtiles, OCC * cus)), dim3(512), 0, s, a, dir); \
+                  }, 0})
+    // DPC("pairs conj S3072 x3/CU", 3072, 3);  // 80-VGPR cap spills 107 VGPRs: not viable
+    DPC("pairs conj S4096 x2/CU", 4096, 2);
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);
