@@ -1,0 +1,501 @@
+// DuckDB v1.1.2 loadable extension that routes table scans with pushed filters to the MI355X
+// bitmap-indexed scan (include/cubit_gpu.h, include/cubit_scan.h).
+//
+// This file is the DuckDB-side binding a maintainer adds. It compiles
+// against the DuckDB headers only: `make -C duckdb-cubit_amd shim-check DUCKDB_INCLUDE=…`
+// runs a full semantic check (g++ -fsyntax-only) against a DuckDB v1.1.2 source tree.
+// Linking it needs libduckdb, which this repository does not build.
+//
+//   PRAGMA cubit_attach('lineitem', 'l_shipdate,l_discount,l_quantity,l_extendedprice');
+//     copies those columns to the GPU (one partition per call) and builds an exact range
+//     index on each; from then on the optimizer swaps seq_scan for cubit_scan whenever every
+//     pushed filter of the scan is supported and every scanned column is attached.
+//
+// Reference interfaces used (src/include/duckdb/…):
+//   OptimizerExtension::optimize_function          optimizer/optimizer_extension.hpp:31-41
+//     run after the built-in optimizers, i.e. after filter pushdown (optimizer.cpp:222-227)
+//   LogicalGet::{function, bind_data, column_ids, projection_ids, table_filters}
+//                                                  planner/operator/logical_get.hpp:38-60
+//   TableFunction callbacks                        function/table_function.hpp:187-215
+//   TableFilterSet / ConstantFilter / Conjunction* / Is[Not]NullFilter
+//                                                  planner/table_filter.hpp:20-101, planner/filter/*.hpp
+//   DuckTransaction::{start_time, transaction_id}  transaction/duck_transaction.hpp:23-38
+#include "duckdb.hpp"
+#include "duckdb/catalog/catalog_entry/duck_table_entry.hpp"
+#include "duckdb/catalog/catalog_entry/table_catalog_entry.hpp"
+#include "duckdb/function/pragma_function.hpp"
+#include "duckdb/function/table_function.hpp"
+#include "duckdb/main/extension_util.hpp"
+#include "duckdb/optimizer/optimizer_extension.hpp"
+#include "duckdb/planner/filter/conjunction_filter.hpp"
+#include "duckdb/planner/filter/constant_filter.hpp"
+#include "duckdb/planner/filter/null_filter.hpp"
+#include "duckdb/planner/operator/logical_get.hpp"
+#include "duckdb/planner/table_filter.hpp"
+#include "duckdb/transaction/duck_transaction.hpp"
+
+#include "cubit_gpu.h"
+#include "cubit_scan.h"
+
+#include <mutex>
+
+namespace duckdb {
+
+// ------------------------------------------------------------------ registry
+
+// One GPU partition per attached table: the device context, the cubit_table and which
+// storage columns it holds (with their physical width).
+struct CubitAttached {
+    cubit_ctx *ctx = nullptr;
+    cubit_table *table = nullptr;
+    unordered_map<column_t, PhysicalType> columns;
+};
+
+class CubitRegistry {
+public:
+    static CubitAttached *Find(const TableCatalogEntry &t) {
+        lock_guard<mutex> g(lock);
+        auto it = map().find(&t);
+        return it == map().end() ? nullptr : &it->second;
+    }
+    static CubitAttached &Insert(const TableCatalogEntry &t) {
+        lock_guard<mutex> g(lock);
+        return map()[&t];
+    }
+
+private:
+    static unordered_map<const TableCatalogEntry *, CubitAttached> &map() {
+        static unordered_map<const TableCatalogEntry *, CubitAttached> m;
+        return m;
+    }
+    static mutex lock;
+};
+mutex CubitRegistry::lock;
+
+static void Check(int rc) {
+    if (rc != CUBIT_OK) {
+        throw InvalidInputException("cubit: %s", cubit_last_error());
+    }
+}
+
+// ------------------------------------------------------------------ filters
+
+static bool IntegerPhysical(PhysicalType t) {
+    return t == PhysicalType::INT32 || t == PhysicalType::INT64 || t == PhysicalType::INT16 ||
+           t == PhysicalType::INT8;
+}
+
+static bool Supported(const TableFilter &f) {
+    switch (f.filter_type) {
+    case TableFilterType::CONSTANT_COMPARISON: {
+        auto &c = f.Cast<ConstantFilter>();
+        if (!IntegerPhysical(c.constant.type().InternalType())) {
+            return false;
+        }
+        switch (c.comparison_type) {
+        case ExpressionType::COMPARE_EQUAL:
+        case ExpressionType::COMPARE_NOTEQUAL:
+        case ExpressionType::COMPARE_LESSTHAN:
+        case ExpressionType::COMPARE_LESSTHANOREQUALTO:
+        case ExpressionType::COMPARE_GREATERTHAN:
+        case ExpressionType::COMPARE_GREATERTHANOREQUALTO:
+            return true;
+        default:
+            return false;
+        }
+    }
+    case TableFilterType::IS_NULL:
+    case TableFilterType::IS_NOT_NULL:
+        return true;
+    case TableFilterType::CONJUNCTION_OR:
+        for (auto &ch : f.Cast<ConjunctionOrFilter>().child_filters) {
+            if (!Supported(*ch)) {
+                return false;
+            }
+        }
+        return true;
+    case TableFilterType::CONJUNCTION_AND:
+        for (auto &ch : f.Cast<ConjunctionAndFilter>().child_filters) {
+            if (!Supported(*ch)) {
+                return false;
+            }
+        }
+        return true;
+    default:
+        return false;  // STRUCT_EXTRACT and anything newer stay on seq_scan
+    }
+}
+
+static int64_t ConstantAsInt64(const Value &v) {
+    switch (v.type().InternalType()) {
+    case PhysicalType::INT8:
+        return v.GetValueUnsafe<int8_t>();
+    case PhysicalType::INT16:
+        return v.GetValueUnsafe<int16_t>();
+    case PhysicalType::INT32:
+        return v.GetValueUnsafe<int32_t>();  // DATE days, INTEGER, DECIMAL(≤9)
+    default:
+        return v.GetValueUnsafe<int64_t>();  // BIGINT, DECIMAL(10..18) scaled
+    }
+}
+
+// prefix-order cubit_filter_node tree of one column's TableFilter (kinds are numbered like
+// TableFilterType, comparisons like the CUBIT_CMP_* of ExpressionType::COMPARE_*)
+static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node> &out) {
+    cubit_filter_node n {};
+    n.column = column;
+    switch (f.filter_type) {
+    case TableFilterType::CONSTANT_COMPARISON: {
+        auto &c = f.Cast<ConstantFilter>();
+        n.kind = CUBIT_FILTER_CONSTANT;
+        switch (c.comparison_type) {
+        case ExpressionType::COMPARE_EQUAL:
+            n.cmp = CUBIT_CMP_EQ;
+            break;
+        case ExpressionType::COMPARE_NOTEQUAL:
+            n.cmp = CUBIT_CMP_NE;
+            break;
+        case ExpressionType::COMPARE_LESSTHAN:
+            n.cmp = CUBIT_CMP_LT;
+            break;
+        case ExpressionType::COMPARE_LESSTHANOREQUALTO:
+            n.cmp = CUBIT_CMP_LE;
+            break;
+        case ExpressionType::COMPARE_GREATERTHAN:
+            n.cmp = CUBIT_CMP_GT;
+            break;
+        default:
+            n.cmp = CUBIT_CMP_GE;
+            break;
+        }
+        n.constant = ConstantAsInt64(c.constant);
+        out.push_back(n);
+        return;
+    }
+    case TableFilterType::IS_NULL:
+        n.kind = CUBIT_FILTER_IS_NULL;
+        out.push_back(n);
+        return;
+    case TableFilterType::IS_NOT_NULL:
+        n.kind = CUBIT_FILTER_IS_NOT_NULL;
+        out.push_back(n);
+        return;
+    case TableFilterType::CONJUNCTION_OR:
+    case TableFilterType::CONJUNCTION_AND: {
+        const bool is_or = f.filter_type == TableFilterType::CONJUNCTION_OR;
+        auto &children = is_or ? f.Cast<ConjunctionOrFilter>().child_filters
+                               : f.Cast<ConjunctionAndFilter>().child_filters;
+        n.kind = is_or ? CUBIT_FILTER_OR : CUBIT_FILTER_AND;
+        n.n_children = (int32_t)children.size();
+        out.push_back(n);
+        for (auto &ch : children) {
+            Emit(*ch, column, out);
+        }
+        return;
+    }
+    default:
+        throw InternalException("cubit: unsupported table filter reached Emit");
+    }
+}
+
+// ------------------------------------------------------------------ table function
+
+struct CubitBindData : public TableFunctionData {
+    CubitBindData(DuckTableEntry &table_p, CubitAttached &attached_p) : table(table_p), attached(attached_p) {
+    }
+    DuckTableEntry &table;
+    CubitAttached &attached;
+};
+
+struct CubitGlobalState : public GlobalTableFunctionState {
+    ~CubitGlobalState() override {
+        if (scan) {
+            cubit_scan_destroy(scan);
+        }
+    }
+    idx_t MaxThreads() const override {
+        return max_threads;
+    }
+    cubit_scan *scan = nullptr;
+    idx_t max_threads = 1;
+    vector<LogicalType> out_types;  // output chunk column types, in output order
+};
+
+struct CubitLocalState : public LocalTableFunctionState {
+    ~CubitLocalState() override {
+        if (local) {
+            cubit_scan_local_destroy(local);
+        }
+    }
+    cubit_scan_local *local = nullptr;
+    vector<vector<int64_t>> staging;  // one STANDARD_VECTOR_SIZE int64 buffer per output column
+    vector<int64_t *> ptrs;
+};
+
+static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &context, TableFunctionInitInput &input) {
+    auto &bind = input.bind_data->Cast<CubitBindData>();
+    vector<cubit_filter_node> nodes;
+    if (input.filters && !input.filters->filters.empty()) {
+        // the TableFilterSet is an AND over columns; its keys index column_ids
+        nodes.push_back(cubit_filter_node {CUBIT_FILTER_AND, 0, 0, (int32_t)input.filters->filters.size(), 0});
+        for (auto &kv : input.filters->filters) {
+            Emit(*kv.second, (int32_t)input.column_ids[kv.first], nodes);
+        }
+    }
+    auto &tx = DuckTransaction::Get(context, bind.table.catalog);
+    cubit_txn txn {tx.start_time, tx.transaction_id};
+    vector<uint64_t> cols;
+    for (auto c : input.column_ids) {
+        cols.push_back(c == COLUMN_IDENTIFIER_ROW_ID ? CUBIT_COLUMN_ROW_ID : (uint64_t)c);
+    }
+    vector<uint64_t> proj(input.projection_ids.begin(), input.projection_ids.end());
+    auto g = make_uniq<CubitGlobalState>();
+    if (cubit_scan_init_global(bind.attached.table, cols.data(), (uint32_t)cols.size(), proj.data(),
+                               (uint32_t)proj.size(), nodes.data(), (uint32_t)nodes.size(), &txn,
+                               &g->scan) != CUBIT_OK) {
+        throw InvalidInputException("cubit_scan: %s", cubit_scan_last_error());
+    }
+    uint64_t mt = 1;
+    cubit_scan_max_threads(g->scan, &mt);
+    g->max_threads = mt;
+    const bool pruned = input.CanRemoveFilterColumns();
+    const idx_t n_out = pruned ? input.projection_ids.size() : input.column_ids.size();
+    for (idx_t i = 0; i < n_out; i++) {
+        const column_t c = input.column_ids[pruned ? input.projection_ids[i] : i];
+        g->out_types.push_back(c == COLUMN_IDENTIFIER_ROW_ID
+                                   ? LogicalType(LogicalType::ROW_TYPE)
+                                   : bind.table.GetColumn(LogicalIndex(c)).GetType());
+    }
+    return std::move(g);
+}
+
+static unique_ptr<LocalTableFunctionState> CubitInitLocal(ExecutionContext &context, TableFunctionInitInput &input,
+                                                          GlobalTableFunctionState *global_state) {
+    auto &g = global_state->Cast<CubitGlobalState>();
+    auto l = make_uniq<CubitLocalState>();
+    if (cubit_scan_init_local(g.scan, &l->local) != CUBIT_OK) {
+        throw InternalException("cubit_scan: %s", cubit_scan_last_error());
+    }
+    l->staging.resize(g.out_types.size(), vector<int64_t>(STANDARD_VECTOR_SIZE));
+    for (auto &s : l->staging) {
+        l->ptrs.push_back(s.data());
+    }
+    return std::move(l);
+}
+
+// int64 staging → the column's physical type (DATE/INTEGER narrow, BIGINT/DECIMAL copy)
+static void CopyOut(const int64_t *src, Vector &dst, idx_t n) {
+    switch (dst.GetType().InternalType()) {
+    case PhysicalType::INT8: {
+        auto d = FlatVector::GetData<int8_t>(dst);
+        for (idx_t i = 0; i < n; i++) {
+            d[i] = (int8_t)src[i];
+        }
+        break;
+    }
+    case PhysicalType::INT16: {
+        auto d = FlatVector::GetData<int16_t>(dst);
+        for (idx_t i = 0; i < n; i++) {
+            d[i] = (int16_t)src[i];
+        }
+        break;
+    }
+    case PhysicalType::INT32: {
+        auto d = FlatVector::GetData<int32_t>(dst);
+        for (idx_t i = 0; i < n; i++) {
+            d[i] = (int32_t)src[i];
+        }
+        break;
+    }
+    default:
+        memcpy(FlatVector::GetData<int64_t>(dst), src, n * sizeof(int64_t));
+        break;
+    }
+}
+
+static void CubitScanFunc(ClientContext &context, TableFunctionInput &data, DataChunk &output) {
+    auto &g = data.global_state->Cast<CubitGlobalState>();
+    auto &l = data.local_state->Cast<CubitLocalState>();
+    uint64_t n = 0;
+    if (cubit_scan_function(g.scan, l.local, l.ptrs.data(), &n) != CUBIT_OK) {
+        throw InternalException("cubit_scan: %s", cubit_scan_last_error());
+    }
+    for (idx_t c = 0; c < output.ColumnCount(); c++) {
+        CopyOut(l.ptrs[c], output.data[c], n);
+    }
+    output.SetCardinality(n);  // 0 rows = finished (PhysicalTableScan::GetData)
+}
+
+static idx_t CubitBatchIndex(ClientContext &context, const FunctionData *bind_data,
+                             LocalTableFunctionState *local_state, GlobalTableFunctionState *global_state) {
+    auto &g = global_state->Cast<CubitGlobalState>();
+    auto &l = local_state->Cast<CubitLocalState>();
+    uint64_t b = 0;
+    cubit_scan_batch_index(g.scan, l.local, &b);
+    return b;
+}
+
+static double CubitProgress(ClientContext &context, const FunctionData *bind_data,
+                            const GlobalTableFunctionState *global_state) {
+    auto &g = global_state->Cast<CubitGlobalState>();
+    double p = 0;
+    cubit_scan_progress(g.scan, &p);
+    return p;
+}
+
+TableFunction GetCubitScanFunction() {
+    TableFunction f("cubit_scan", {}, CubitScanFunc);
+    f.init_global = CubitInitGlobal;
+    f.init_local = CubitInitLocal;
+    f.get_batch_index = CubitBatchIndex;
+    f.table_scan_progress = CubitProgress;
+    f.projection_pushdown = true;  // as seq_scan (table_scan.cpp:436-438)
+    f.filter_pushdown = true;
+    f.filter_prune = true;
+    return f;
+}
+
+// ------------------------------------------------------------------ optimizer swap
+
+static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOperator> &plan) {
+    for (auto &child : plan->children) {
+        CubitOptimize(input, child);
+    }
+    if (plan->type != LogicalOperatorType::LOGICAL_GET) {
+        return;
+    }
+    auto &get = plan->Cast<LogicalGet>();
+    if (get.function.name != "seq_scan" || get.table_filters.filters.empty()) {
+        return;
+    }
+    auto table = get.GetTable();
+    if (!table || !table->IsDuckTable()) {
+        return;
+    }
+    auto attached = CubitRegistry::Find(*table);
+    if (!attached) {
+        return;
+    }
+    for (auto c : get.column_ids) {
+        if (c != COLUMN_IDENTIFIER_ROW_ID && !attached->columns.count(c)) {
+            return;  // a scanned column is not on the GPU
+        }
+    }
+    for (auto &kv : get.table_filters.filters) {
+        if (!Supported(*kv.second)) {
+            return;
+        }
+    }
+    get.function = GetCubitScanFunction();
+    get.bind_data = make_uniq<CubitBindData>(table->Cast<DuckTableEntry>(), *attached);
+}
+
+// ------------------------------------------------------------------ attach
+
+// PRAGMA cubit_attach(table, 'col,col,…'): read the columns in row-id order through a second
+// connection (its own transaction), upload them and build an exact range index per column.
+// Row ids missing from the scan (deleted rows) become committed deletes of the partition.
+static void CubitAttach(ClientContext &context, const FunctionParameters &parameters) {
+    const auto table_name = parameters.values[0].ToString();
+    const auto column_list = StringUtil::Split(parameters.values[1].ToString(), ',');
+    auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
+    Connection con(*context.db);
+    auto max_row = con.Query("SELECT max(rowid) FROM " + KeywordHelper::WriteOptionallyQuoted(table_name));
+    if (max_row->HasError()) {
+        max_row->ThrowError();
+    }
+    const auto top = max_row->GetValue(0, 0);
+    const uint64_t n_rows = top.IsNull() ? 0 : (uint64_t)top.GetValue<int64_t>() + 1;
+    if (n_rows == 0) {
+        throw InvalidInputException("cubit_attach: %s is empty", table_name);
+    }
+    auto &attached = CubitRegistry::Insert(entry);
+    if (!attached.ctx) {
+        Check(cubit_ctx_create(0, &attached.ctx));
+    }
+    if (attached.table) {
+        cubit_table_destroy(attached.table);
+        attached.columns.clear();
+    }
+    Check(cubit_table_create(attached.ctx, n_rows, 0, &attached.table));
+    vector<bool> present(n_rows, false);
+    for (auto name : column_list) {
+        StringUtil::Trim(name);
+        const auto &def = entry.GetColumn(name);
+        const auto phys = def.GetType().InternalType();
+        if (!IntegerPhysical(phys)) {
+            throw InvalidInputException("cubit_attach: column %s is not integer-backed", name);
+        }
+        const bool wide = phys == PhysicalType::INT64;
+        vector<int32_t> v32(wide ? 0 : n_rows, 0);
+        vector<int64_t> v64(wide ? n_rows : 0, 0);
+        vector<uint64_t> valid((n_rows + 63) / 64, 0);
+        auto res = con.Query("SELECT rowid, " + KeywordHelper::WriteOptionallyQuoted(name) + " FROM " +
+                             KeywordHelper::WriteOptionallyQuoted(table_name) + " ORDER BY rowid");
+        if (res->HasError()) {
+            res->ThrowError();
+        }
+        while (auto chunk = res->Fetch()) {
+            chunk->Flatten();
+            auto rows = FlatVector::GetData<int64_t>(chunk->data[0]);
+            auto &vals = chunk->data[1];
+            auto &mask = FlatVector::Validity(vals);
+            for (idx_t i = 0; i < chunk->size(); i++) {
+                const uint64_t r = (uint64_t)rows[i];
+                present[r] = true;
+                if (!mask.RowIsValid(i)) {
+                    continue;
+                }
+                valid[r >> 6] |= 1ull << (r & 63);
+                switch (phys) {
+                case PhysicalType::INT8:
+                    v32[r] = FlatVector::GetData<int8_t>(vals)[i];
+                    break;
+                case PhysicalType::INT16:
+                    v32[r] = FlatVector::GetData<int16_t>(vals)[i];
+                    break;
+                case PhysicalType::INT32:
+                    v32[r] = FlatVector::GetData<int32_t>(vals)[i];
+                    break;
+                default:
+                    v64[r] = FlatVector::GetData<int64_t>(vals)[i];
+                    break;
+                }
+            }
+        }
+        const column_t storage = def.StorageOid();
+        Check(cubit_table_add_column(attached.table, (int)storage, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
+                                     wide ? (const void *)v64.data() : (const void *)v32.data(), valid.data(), 0));
+        Check(cubit_table_build_index(attached.table, (int)storage, CUBIT_INDEX_RANGE, nullptr, 0));
+        attached.columns[storage] = phys;
+    }
+    vector<int64_t> gone;
+    for (uint64_t r = 0; r < n_rows; r++) {
+        if (!present[r]) {
+            gone.push_back((int64_t)r);
+        }
+    }
+    if (!gone.empty()) {
+        vector<uint64_t> ids(gone.size(), 0);  // committed before every later transaction
+        Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
+    }
+}
+
+} // namespace duckdb
+
+extern "C" {
+
+DUCKDB_EXTENSION_API void cubit_init(duckdb::DatabaseInstance &db) {
+    auto &config = duckdb::DBConfig::GetConfig(db);
+    duckdb::OptimizerExtension ext;
+    ext.optimize_function = duckdb::CubitOptimize;
+    config.optimizer_extensions.push_back(std::move(ext));
+    duckdb::ExtensionUtil::RegisterFunction(
+        db, duckdb::PragmaFunction::PragmaCall("cubit_attach", duckdb::CubitAttach,
+                                               {duckdb::LogicalType::VARCHAR, duckdb::LogicalType::VARCHAR}));
+}
+
+DUCKDB_EXTENSION_API const char *cubit_version() {
+    return duckdb::DuckDB::LibraryVersion();
+}
+}
