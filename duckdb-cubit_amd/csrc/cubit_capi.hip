@@ -131,7 +131,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     hipEvent_t start = stop ? ctx->evs[ctx->n_timed].first : nullptr;
     if (stop) ctx->n_timed++;
     if (mode == RunMode::kCount) {
-        a.num_tiles = (uint32_t)(pw / count_tile_words());
+        a.num_tiles = (uint32_t)(pw / count_tile_words(prog.n_leaves));
         HIP_CHECK(launch_eval_count(a, ctx->stream, start, stop));
         return CUBIT_OK;
     }

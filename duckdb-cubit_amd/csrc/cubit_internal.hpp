@@ -73,7 +73,7 @@ constexpr uint32_t kTicketWords = kTicketStride * (kTicketGroups + 2);
 
 // launchers (cubit_kernels.hip); all asynchronous on `stream`
 uint64_t decode_tile_words();  // words per eval_decode_tiles tile
-uint64_t count_tile_words();   // words per eval_count_kernel tile
+uint64_t count_tile_words(uint32_t n_leaves);  // words per eval_count_kernel tile
 int decode_block_threads();
 // evaluate + decode into per-tile runs; dir (optional) gets {start, length} per tile
 // ev0 / ev1 (optional): events stamped by the kernel dispatch itself (hipExtLaunchKernel), so

@@ -200,24 +200,37 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
 // ------------------------------------------------------------------ K1: count / materialise
 
 // count(*) of the program and/or its result bitvector. Persistent: workgroup g takes tiles
-// g, g+G, …, keeps its count in registers, and claims once at the end (one returning atomic
-// per workgroup instead of one per tile).
+// g, g+G, …, two tiles in flight (register double buffer: the loads of tile i+2 are issued
+// as soon as tile i is evaluated), keeps its count in registers and claims once at the end
+// (one returning atomic per workgroup).
 template <int K, int PAIRS, int FORM = FORM_POSTFIX>
-__global__ __launch_bounds__(256) void eval_count_kernel(EvalArgs a) {
-    constexpr int THREADS = 256, NW = 2 * PAIRS;
+__global__ __launch_bounds__(512, 4) void eval_count_kernel(EvalArgs a) {
+    constexpr int THREADS = 512, NW = 2 * PAIRS;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     const int t = threadIdx.x;
+    const uint32_t G = gridDim.x;
     uint64_t c = 0;
-    for (uint32_t tile = blockIdx.x; tile < a.num_tiles; tile += gridDim.x) {
-        const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
-        u64x2 v[K][PAIRS];
-        load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+    u64x2 v0[K][PAIRS], v1[K][PAIRS];
+    uint32_t tile = blockIdx.x;
+    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v0);
+    if (tile + G < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)(tile + G) * TILE_WORDS, t, v1);
+    auto step = [&](u64x2 (&v)[K][PAIRS], uint32_t tl) {
+        const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
         uint64_t r[NW];
         eval_words<K, NW, FORM>(a.prog, v, r);
+        const uint32_t ahead = tl + 2 * G;
+        if (ahead < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)ahead * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
 #pragma unroll
         for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
+    };
+    while (tile < a.num_tiles) {
+        step(v0, tile);
+        tile += G;
+        if (tile >= a.num_tiles) break;
+        step(v1, tile);
+        tile += G;
     }
     __shared__ uint64_t s_part[THREADS / 64];
     c = wave_sum(c);
@@ -1109,11 +1122,13 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 // STAGE 4,096 staged ids (16 KiB LDS); count tiles of 256 threads × 8 pairs = 4,096 words.
 // Chosen from the interleaved variant sweep in scripts/kbench.hip.
 constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
-constexpr int kCountPairs = 8;
-constexpr int kCountGrid = 1024;  // persistent count grid: 4 workgroups per CU
+// count tiles: 512 threads × 2 pairs = 2,048 words for K ≤ 4, × 1 pair above (two tiles in
+// flight must fit the 128-VGPR budget of 4 waves per SIMD)
+constexpr int count_pairs(uint32_t k) { return k <= 4 ? 2 : 1; }
+constexpr int kCountGrid = 512;   // persistent count grid: 2 workgroups per CU
 
 uint64_t decode_tile_words() { return (uint64_t)kDecodeThreads * 2 * kDecodePairs; }
-uint64_t count_tile_words() { return 256ull * 2 * kCountPairs; }
+uint64_t count_tile_words(uint32_t n_leaves) { return 512ull * 2 * (uint64_t)count_pairs(n_leaves); }
 int decode_block_threads() { return kDecodeThreads; }
 
 // A left-deep chain of ANDs (nops = 0,1,1,…; every op AND) evaluates as a plain conjunction.
@@ -1152,7 +1167,7 @@ hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipS
 template <int K, int FORM>
 void launch_count_kf(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const unsigned grid = std::min<unsigned>(a.num_tiles, (unsigned)kCountGrid);
-    hipExtLaunchKernelGGL((eval_count_kernel<K, kCountPairs, FORM>), dim3(grid), dim3(256), 0, s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL((eval_count_kernel<K, count_pairs(K), FORM>), dim3(grid), dim3(512), 0, s, e0, e1, 0, a);
 }
 
 template <int K>

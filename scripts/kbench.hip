@@ -117,9 +117,9 @@ int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 600037902ull;
     const int rounds = argc > 2 ? atoi(argv[2]) : 15;
     const uint64_t W = (n + 63) / 64, pw = padded_words(n);
-    const double dens[5] = {0.25, 0.40, 0.50, 0.45, 0.46};
-    uint64_t* leaf[5];
-    for (int k = 0; k < 5; ++k) {
+    const double dens[6] = {0.25, 0.40, 0.50, 0.45, 0.46, 0.01};
+    uint64_t* leaf[6];
+    for (int k = 0; k < 6; ++k) {
         CK(hipMalloc(&leaf[k], pw * 8));
         hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, leaf[k], pw, n, (uint32_t)(dens[k] * 4294967296.0),
                            (uint64_t)k + 1);
@@ -218,18 +218,19 @@ int main(int argc, char** argv) {
     DT("tiles P2 T256 x4/CU", 2, 2048, 256, 4);
     DP("pairs P1 T512 x2/CU", 1, 2048, 512, 2);
     DP("pairs P1 T256 x4/CU", 1, 1024, 256, 4);
-#define DPC(NAME, S, OCC)                                                                                      \
+#define DPC(NAME, S, OCC, T)                                                                                   \
     vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
-                      a.num_tiles = dtiles;                                                                   \
+                      a.num_tiles = (uint32_t)(pw / ((uint64_t)T * 4));                                       \
                       a.prog.negate = 0b01010;                                                                \
                       a.prog.nops = 0;                                                                        \
                       for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);                              \
                       a.prog.ops = 0;                                                                         \
-                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, S, 512, 0, FORM_CONJ, OCC>),                \
-                                         dim3(std::min<unsigned>(dtiles, OCC * cus)), dim3(512), 0, s, a, dir); \
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 2, S, T, 0, FORM_CONJ, OCC>),                  \
+                                         dim3(std::min<unsigned>(a.num_tiles, OCC * cus)), dim3(T), 0, s, a, dir); \
                   }, 0})
-    // DPC("pairs conj S3072 x3/CU", 3072, 3);  // 80-VGPR cap spills 107 VGPRs: not viable
-    DPC("pairs conj S4096 x2/CU", 4096, 2);
+    // DPC("pairs conj S3072 x3/CU", 3072, 3, 512);  // 80-VGPR cap spills 107 VGPRs: not viable
+    DPC("pairs conj S4096 x2/CU", 4096, 2, 512);
+    DPC("pairs conj T256 S2048 x4/CU", 2048, 4, 256);
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);
@@ -261,6 +262,32 @@ int main(int argc, char** argv) {
     DX("diag no-decode", true, false);
     DX("diag no-claim no-decode", false, false);
 
+    // K = 1 at 1 % density (config 2's shape): production path vs a non-persistent grid
+    auto k1 = [&](EvalArgs& a) {
+        a.prog = EvalProgram{};
+        a.prog.leaf[0] = leaf[5];
+        a.prog.n_leaves = 1;
+    };
+    vs.push_back({"K1 1% prod (pairs)", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 3});
+    vs.push_back({"K1 1% tiles grid=tiles", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((eval_decode_tiles<1, 2, 4096, 512>), dim3(dtiles), dim3(512), 0, s, a, dir);
+                  }, 3});
+    vs.push_back({"K1 1% tiles P1 grid=tiles", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = (uint32_t)(pw / 1024);
+                      hipLaunchKernelGGL((eval_decode_tiles<1, 1, 2048, 512>), dim3(a.num_tiles), dim3(512), 0, s, a, dir);
+                  }, 3});
+    vs.push_back({"K1 1% count only", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = (uint32_t)(pw / count_tile_words(a.prog.n_leaves));
+                      CK(launch_eval_count(a, s));
+                  }, 3});
     vs.push_back({"decode + ordered pass", [&](EvalArgs& a, hipStream_t s) {
                       a.num_tiles = dtiles;
                       a.rowids = ids2;
@@ -268,7 +295,7 @@ int main(int argc, char** argv) {
                       CK(launch_order_runs(dir, dtiles, dst_off, ids2, cap, ids, s));
                   }, 1});
     vs.push_back({"count only", [&](EvalArgs& a, hipStream_t s) {
-                      a.num_tiles = (uint32_t)(pw / count_tile_words());
+                      a.num_tiles = (uint32_t)(pw / count_tile_words(a.prog.n_leaves));
                       CK(launch_eval_count(a, s));
                   }, 2});
 
