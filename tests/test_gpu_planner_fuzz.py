@@ -47,7 +47,7 @@ def rand_residual(rng, n_cols, depth=0):
 
 def test_random_filter_sets_match_oracle(ctx):
     rng = np.random.default_rng(2024)
-    n = 70_001
+    n = 400_003  # four tiles: pairs, a lone tile and a tail
     cols, ocols = [], []
     t = CubitTable(ctx, n, row_base=11)
     for c in range(4):
