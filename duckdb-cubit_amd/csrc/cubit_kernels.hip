@@ -432,6 +432,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
     constexpr int NWAVES = THREADS / 64;
     constexpr bool EARLY = K <= 4;
+    static_assert(TILE_WORDS * 64 < (1ull << 32), "tile-local offsets are 32-bit");
     typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
     __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
     __shared__ uint64_t s_off;        // claimed base of the pair being copied out
@@ -475,7 +476,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     // K ≤ 4 only — at K ≥ 5 the leaves in flight beside the scan state spill, measured
     // 92 vs 88 µs, so the loads wait until after the copy-out / claim);
     // block scan → per-pair offsets within the tile, tile count
-    auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint64_t (&pair_off)[PAIRS],
+    auto eval_scan = [&](uint32_t tl, int par, uint64_t (&r)[NW], uint32_t (&pair_off)[PAIRS],
                          int publish_sp, uint32_t prefetch) -> uint64_t {
         const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
         eval_words<K, NW, FORM>(a.prog, v, r);
@@ -508,12 +509,13 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
             block_tot[q] = bt;
             wave_pre[q] = wp;
         }
-        uint64_t tile_count = 0;
+        // in-tile offsets and counts fit 32 bits (≤ TILE_WORDS·64 < 2^32, static_assert below)
+        uint32_t tile_count = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
             pair_off[p] = tile_count +
-                          (((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
-            tile_count += (block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK;
+                          (uint32_t)(((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
+            tile_count += (uint32_t)((block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK);
         }
         return tile_count;
     };
@@ -521,7 +523,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     // decode r into stage sp at stage_base with row offsets + delta; dense tiles go direct.
     // Returns the staged count (0 for a dense tile).
     auto decode = [&](uint32_t tl, int sp, uint32_t stage_base, uint32_t delta, const uint64_t (&r)[NW],
-                      const uint64_t (&pair_off)[PAIRS], uint64_t tile_count) -> uint32_t {
+                      const uint32_t (&pair_off)[PAIRS], uint64_t tile_count) -> uint32_t {
         if (tile_count <= (uint64_t)STAGE) {
             if (DIAG & 2) {
                 for (uint32_t i = t; i < (uint32_t)tile_count; i += THREADS) s_stage[sp][stage_base + i] = delta + i * 53;
@@ -606,7 +608,8 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     while (tile < a.num_tiles) {
         const int sp = (int)(pair & 1);
         // ---- unit A
-        uint64_t r[NW], off[PAIRS];
+        uint64_t r[NW];
+        uint32_t off[PAIRS];
         const uint32_t tile_b = tile + G;
         const uint64_t cnt_a_all = eval_scan(tile, 0, r, off, pending ? (sp ^ 1) : -1, tile_b);
         if (pending) copy_out(sp ^ 1);
