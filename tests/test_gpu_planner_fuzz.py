@@ -82,3 +82,49 @@ def test_random_filter_sets_match_oracle(ctx):
             ref_t = O.table_scan(ocols, plan, n, row_base=11, tx=tx)
             got_t = t.scan(fs, residual, txn=L.Txn(10, TXN_START + 1))
             assert np.array_equal(got_t, ref_t), ("txn", i, fs, residual)
+
+
+def test_random_filter_sets_with_updates_and_deletes(ctx):
+    """The same fuzz with an MVCC delta: deletes from two transactions and updates on indexed
+    columns (range, equality, bins) from a writer; the writer, a reader that predates it and
+    a reader that sees the committed half must each get the oracle's rows."""
+    rng = np.random.default_rng(77)
+    n = 300_007
+    writer = TXN_START + 5
+    cols, data = [], []
+    t = CubitTable(ctx, n)
+    for c in range(3):
+        d = rng.integers(0, 50, n).astype(np.int64)
+        valid = rng.random(n) > 0.1
+        vw = validity_from_mask(valid)
+        t.add_column(c, d, vw)
+        data.append((d, vw))
+    t.build_index(0, L.INDEX_RANGE)
+    t.build_index(1, L.INDEX_EQUALITY)
+    t.build_index(2, L.INDEX_RANGE, [10, 20, 30, 40])
+    t.build_index(2, L.INDEX_BINS, [0, 10, 20, 30, 40, 50])
+    upd = {}
+    for c in range(3):
+        rows = np.sort(rng.choice(n, size=3000, replace=False)).astype(np.int64)
+        vals = rng.integers(0, 50, len(rows)).astype(np.int64)
+        vers = np.where(rng.random(len(rows)) < 0.5, np.uint64(3), np.uint64(writer)).astype(np.uint64)
+        t.set_updates(c, rows, vals, vers)
+        upd[c] = (rows, vals, vers)
+    ocols = [O.Column(d, vw, updates=upd[c]) for c, (d, vw) in enumerate(data)]
+    del_rows = np.sort(rng.choice(n, size=20_000, replace=False)).astype(np.int64)
+    del_ids = np.where(rng.random(len(del_rows)) < 0.5, np.uint64(4), np.uint64(writer)).astype(np.uint64)
+    t.set_deletes(del_rows, del_ids)
+    deleted = np.full(n, np.uint64(2 ** 64 - 2), dtype=np.uint64)
+    deleted[del_rows] = del_ids
+    views = [(2, writer), (2, TXN_START + 6), (10, TXN_START + 7)]
+    for i in range(60):
+        filters = {}
+        for c in rng.choice(3, size=rng.integers(1, 4), replace=False):
+            filters[int(c)] = rand_const_filter(rng)
+        fs = F.TableFilterSet(filters)
+        residual = rand_residual(rng, 3) if rng.random() < 0.4 else None
+        plan = F.serialize(fs, residual)
+        start, tid = views[i % 3]
+        ref = O.table_scan(ocols, plan, n, tx=O.Mvcc(start, tid, deleted=deleted))
+        got = t.scan(fs, residual, txn=L.Txn(start, tid))
+        assert np.array_equal(got, ref), (i, start, tid, fs, residual)
