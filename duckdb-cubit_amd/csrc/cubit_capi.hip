@@ -747,6 +747,27 @@ int ones_bv(cubit_table* t, const uint64_t** out) {
     return CUBIT_OK;
 }
 
+// padded device copy of a validity mask (the NN bitvector: kernels read whole tiles), bits
+// past n_rows cleared
+int copy_validity(cubit_table* t, Column& c, const uint64_t* validity, int on_device) {
+    hipStream_t s = t->ctx->stream;
+    auto b = std::make_unique<DevBuf>();
+    if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "validity allocation failed");
+    HIP_CHECK(hipMemsetAsync(b->p, 0, t->nwp * 8, s));
+    const uint64_t nw = (t->n_rows + 63) / 64;
+    HIP_CHECK(hipMemcpyAsync(b->p, validity, nw * 8, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    if (t->n_rows & 63) {
+        uint64_t last = 0;
+        HIP_CHECK(hipMemcpyAsync(&last, static_cast<uint64_t*>(b->p) + nw - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        last &= (1ull << (t->n_rows & 63)) - 1;
+        HIP_CHECK(hipMemcpyAsync(static_cast<uint64_t*>(b->p) + nw - 1, &last, 8, hipMemcpyHostToDevice, s));
+    }
+    c.validity = static_cast<const uint64_t*>(b->p);
+    c.owned.push_back(std::move(b));
+    return CUBIT_OK;
+}
+
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
     const uint64_t esz = type == CUBIT_TYPE_INT32 ? 4 : 8;
     hipStream_t s = t->ctx->stream;
@@ -761,31 +782,13 @@ int copy_column(cubit_table* t, Column& c, int type, const void* data, const uin
         c.owned.push_back(std::move(b));
     }
     if (validity) {
-        // padded copy (the NN bitvector): kernels read whole tiles
-        auto b = std::make_unique<DevBuf>();
-        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "validity allocation failed");
-        HIP_CHECK(hipMemsetAsync(b->p, 0, t->nwp * 8, s));
-        const uint64_t nw = (t->n_rows + 63) / 64;
-        HIP_CHECK(hipMemcpyAsync(b->p, validity, nw * 8, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                 s));
-        // clear bits past n_rows
-        if (t->n_rows & 63) {
-            uint64_t last = 0;
-            HIP_CHECK(hipMemcpyAsync(&last, static_cast<uint64_t*>(b->p) + nw - 1, 8, hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
-            last &= (1ull << (t->n_rows & 63)) - 1;
-            HIP_CHECK(hipMemcpyAsync(static_cast<uint64_t*>(b->p) + nw - 1, &last, 8, hipMemcpyHostToDevice, s));
-        }
-        c.validity = static_cast<const uint64_t*>(b->p);
-        c.owned.push_back(std::move(b));
+        if (int rc = copy_validity(t, c, validity, on_device)) return rc;
     }
     HIP_CHECK(hipStreamSynchronize(s));
     c.type = type;
     return CUBIT_OK;
 }
 
-// distinct non-null values and min/max of a column (host pass over a D2H copy; index build
-// is setup work, not the scan path)
 // Index-build statistics on the device: min / max / any valid, and (want_distinct) the
 // distinct valid values through a presence bitmap of vmax - vmin + 1 bits (≤ 2^32 values;
 // an index with more distinct keys than that is not a bitmap index anyone should build).
@@ -860,6 +863,85 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     if (int rc = set_device(t->ctx)) return rc;
     Column c;
     if (int rc = copy_column(t, c, type, data, validity, on_device)) return rc;
+    t->cols[col] = std::move(c);
+    t->idx.erase(col);
+    t->bins.erase(col);
+    return CUBIT_OK;
+}
+
+// DuckDB BITPACKING segments → device column (K5). The host walks each segment's metadata
+// (header = end of the metadata words, one word per 2,048-row group, highest address first:
+// BitpackingScanState / LoadNextGroup, bitpacking.cpp:620-690), checks every group's bounds,
+// and the GPU unpacks all groups in parallel.
+extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int type, const uint8_t* bytes,
+                                                uint64_t n_bytes, const uint64_t* seg_offsets,
+                                                const uint64_t* seg_rows, uint32_t n_segments,
+                                                const uint64_t* validity) {
+    if (!t || !bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    const uint64_t tsz = type == CUBIT_TYPE_INT32 ? 4 : 8;
+    std::vector<BpGroup> groups;
+    uint64_t row = 0;
+    for (uint32_t sg = 0; sg < n_segments; ++sg) {
+        const uint64_t base = seg_offsets[sg];
+        if (base % 8 || base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
+        uint64_t meta_end;
+        std::memcpy(&meta_end, bytes + base, 8);
+        const uint64_t n_groups = (seg_rows[sg] + 2047) / 2048;
+        if (meta_end > n_bytes - base || meta_end < 8 + 4 * n_groups)
+            return fail(CUBIT_ERR_INVALID, "segment %u: bad metadata offset", sg);
+        for (uint64_t g = 0; g < n_groups; ++g) {
+            uint32_t enc;
+            std::memcpy(&enc, bytes + base + meta_end - 4 * (g + 1), 4);
+            BpGroup bg{};
+            bg.mode = enc >> 24;
+            bg.data_off = base + (enc & 0x00ffffffu);
+            bg.row_start = row + g * 2048;
+            bg.count = (uint32_t)std::min<uint64_t>(2048, seg_rows[sg] - g * 2048);
+            uint64_t need = 0;
+            if (bg.mode == 2) {
+                need = tsz;
+            } else if (bg.mode == 3) {
+                need = 2 * tsz;
+            } else if (bg.mode == 4 || bg.mode == 5) {
+                if (bg.data_off + 2 * tsz > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: truncated", sg, (unsigned long long)g);
+                const uint8_t w = bytes[bg.data_off + tsz];
+                if (w > 8 * tsz) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: width %u", sg, (unsigned long long)g, w);
+                need = (bg.mode == 4 ? 3 : 2) * tsz + ((uint64_t)bg.count + 31) / 32 * 32 * w / 8;
+            } else {
+                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: mode %u", sg, (unsigned long long)g, bg.mode);
+            }
+            if (bg.data_off + need > n_bytes || bg.data_off < base + 8)
+                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
+            groups.push_back(bg);
+        }
+        row += seg_rows[sg];
+    }
+    if (row != t->n_rows)
+        return fail(CUBIT_ERR_INVALID, "segments hold %llu rows, partition has %llu", (unsigned long long)row,
+                    (unsigned long long)t->n_rows);
+    hipStream_t s = t->ctx->stream;
+    DevBuf d_bytes, d_groups;
+    auto out = std::make_unique<DevBuf>();
+    if (hipMalloc(&d_bytes.p, n_bytes) != hipSuccess ||
+        hipMalloc(&d_groups.p, groups.size() * sizeof(BpGroup)) != hipSuccess ||
+        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * tsz, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "bitpacked column allocation failed");
+    HIP_CHECK(hipMemcpyAsync(d_bytes.p, bytes, n_bytes, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_groups.p, groups.data(), groups.size() * sizeof(BpGroup), hipMemcpyHostToDevice, s));
+    HIP_CHECK(launch_bitunpack(static_cast<const uint8_t*>(d_bytes.p), static_cast<const BpGroup*>(d_groups.p),
+                               groups.size(), type, out->p, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    Column c;
+    c.type = type;
+    c.data = out->p;
+    c.owned.push_back(std::move(out));
+    if (validity) {
+        if (int rc = copy_validity(t, c, validity, 0)) return rc;
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
     t->cols[col] = std::move(c);
     t->idx.erase(col);
     t->bins.erase(col);

@@ -96,6 +96,16 @@ hipError_t launch_column_minmax(const void* col, int type, const uint64_t* valid
                                 hipStream_t stream);
 hipError_t launch_presence(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t vmin,
                            uint64_t range, uint64_t* bits, hipStream_t stream);
+// K5: DuckDB BITPACKING groups → plain values. One record per 2,048-value metadata group
+// (mode: 2 CONSTANT, 3 CONSTANT_DELTA, 4 DELTA_FOR, 5 FOR — BitpackingMode).
+struct BpGroup {
+    uint64_t data_off;   // byte offset of the group's data in the segment bytes
+    uint64_t row_start;  // first row of the group
+    uint32_t count;      // rows in the group (≤ 2,048)
+    uint32_t mode;
+};
+hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
+                            hipStream_t stream);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,

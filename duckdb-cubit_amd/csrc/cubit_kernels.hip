@@ -674,7 +674,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
     constexpr int THREADS = 512, PAIRS = 2, NW = 4, STAGE = 4096;
     constexpr int FB = 32;  // THREADS * 128 ≥ 65536
     constexpr uint64_t FMASK = 0xffffffffull;
-    constexpr int FPW = 2, NPK = 1;
+    constexpr int FPW = 2;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     constexpr int NWAVES = THREADS / 64;
     __shared__ uint64_t s_wave_tot[NWAVES];
@@ -1022,6 +1022,89 @@ __global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col
     }
 }
 
+// ------------------------------------------------------------------ K5: bit-unpack
+
+// One workgroup per DuckDB bitpacking metadata group (BitpackingScanPartial,
+// bitpacking.cpp:785-868): CONSTANT, CONSTANT_DELTA (first + i·delta), FOR (unpacked + min)
+// and DELTA_FOR (running sum of unpacked + min_delta from delta_offset, a block scan here).
+// Packed values are horizontal (fastpforlib fastpack): value i at bits [i·w, (i+1)·w) of
+// little-endian 32-bit words; each thread unpacks 8 consecutive values. U = unsigned T, the
+// reference's wrap-around arithmetic.
+template <typename T, typename U>
+__global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restrict__ bytes,
+                                                        const BpGroup* __restrict__ groups, T* __restrict__ out) {
+    constexpr int PER = 8;
+    __shared__ U s_tot[4];
+    const BpGroup g = groups[blockIdx.x];
+    const int t = threadIdx.x;
+    const uint8_t* p = bytes + g.data_off;
+    auto load_t = [](const uint8_t* q) -> U { return *reinterpret_cast<const U*>(q); };
+    T* dst = out + g.row_start;
+    const uint32_t i0 = (uint32_t)t * PER;
+    if (g.mode == 2) {  // CONSTANT
+        const U c = load_t(p);
+        for (uint32_t k = 0; k < PER; ++k)
+            if (i0 + k < g.count) dst[i0 + k] = (T)c;
+        return;
+    }
+    if (g.mode == 3) {  // CONSTANT_DELTA
+        const U base = load_t(p), d = load_t(p + sizeof(T));
+        for (uint32_t k = 0; k < PER; ++k)
+            if (i0 + k < g.count) dst[i0 + k] = (T)(U)(d * (U)(i0 + k) + base);
+        return;
+    }
+    const U fr = load_t(p);
+    const uint32_t w = (uint32_t)(uint8_t)load_t(p + sizeof(T));
+    const bool delta = g.mode == 4;
+    const U doff = delta ? load_t(p + 2 * sizeof(T)) : (U)0;
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(p + (delta ? 3 : 2) * sizeof(T));
+    U v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t i = i0 + k;
+        uint64_t x = 0;
+        if (w && i < g.count) {
+            const uint64_t bit = (uint64_t)i * w;
+            const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
+            const uint32_t nwords = (off + w + 31) / 32;
+            uint64_t lo = words[wi];
+            if (nwords > 1) lo |= (uint64_t)words[wi + 1] << 32;
+            x = lo >> off;
+            if (nwords > 2) x |= (uint64_t)words[wi + 2] << (64 - off);
+            if (w < 64) x &= (1ull << w) - 1;
+        }
+        v[k] = (U)x + fr;
+    }
+    if (!delta) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k)
+            if (i0 + k < g.count) dst[i0 + k] = (T)v[k];
+        return;
+    }
+    // DELTA_FOR: inclusive prefix over the group (rows past count add nothing)
+    U run = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (i0 + k >= g.count) v[k] = 0;
+        run += v[k];
+        v[k] = run;
+    }
+    const int lane = t & 63, wave = t >> 6;
+    U incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const U y = (U)__shfl_up((uint64_t)incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_tot[wave] = incl;
+    __syncthreads();
+    U pre = doff + incl - run;
+    for (int w2 = 0; w2 < wave; ++w2) pre += s_tot[w2];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (i0 + k < g.count) dst[i0 + k] = (T)(U)(v[k] + pre);
+}
+
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -1334,6 +1417,19 @@ hipError_t launch_sum_product_arrays(const int64_t* x, const int64_t* y, const u
     hipLaunchKernelGGL(sum_product_arrays_kernel, dim3(kSumBlocks), dim3(256), 0, stream, x, y, d_count, max_n,
                        partials);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, stream, partials, kSumBlocks, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
+                            hipStream_t stream) {
+    if (n_groups == 0) return hipSuccess;
+    if (n_groups > 0x7fffffffull) return hipErrorInvalidValue;
+    if (type == 0)
+        hipLaunchKernelGGL((bitunpack_kernel<int32_t, uint32_t>), dim3((unsigned)n_groups), dim3(256), 0, stream, bytes,
+                           groups, static_cast<int32_t*>(out));
+    else
+        hipLaunchKernelGGL((bitunpack_kernel<int64_t, uint64_t>), dim3((unsigned)n_groups), dim3(256), 0, stream, bytes,
+                           groups, static_cast<int64_t*>(out));
     return hipGetLastError();
 }
 

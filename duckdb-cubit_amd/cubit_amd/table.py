@@ -160,6 +160,19 @@ class CubitTable:
         L.check(self.lib.cubit_table_add_column(self.handle, col, t, data.ctypes.data, vptr, 0))
         self.types[col] = t
 
+    def add_bitpacked_column(self, col: int, data: np.ndarray, seg_offsets: np.ndarray, seg_rows: np.ndarray,
+                             dtype, validity: Optional[np.ndarray] = None) -> None:
+        """A column given as DuckDB BITPACKING segment images (uint8 bytes, per-segment byte
+        offsets and row counts); unpacked on the GPU (K5)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        so = np.ascontiguousarray(seg_offsets, dtype=np.uint64)
+        sr = np.ascontiguousarray(seg_rows, dtype=np.uint64)
+        vw = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
+        typ = L.TYPE_INT32 if np.dtype(dtype) == np.int32 else L.TYPE_INT64
+        L.check(self.lib.cubit_table_add_bitpacked_column(self.handle, col, typ, data.ctypes.data, data.nbytes,
+                                                          so.ctypes.data, sr.ctypes.data, len(so),
+                                                          vw.ctypes.data if vw is not None else None))
+
     def add_device_column(self, col: int, dptr: int, type_: int, validity_dptr: Optional[int] = None) -> None:
         L.check(self.lib.cubit_table_add_column(self.handle, col, type_, C.c_void_p(dptr),
                                                 C.c_void_p(validity_dptr) if validity_dptr else None, 1))

@@ -172,6 +172,17 @@ int cubit_table_info(cubit_table *t, uint64_t *n_rows, int64_t *row_base, cubit_
  * table only references them). validity may be NULL (no NULLs). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
+/* Register a column given as DuckDB BITPACKING segments (K5; the reference's persistent
+ * integer storage, src/storage/compression/bitpacking.cpp): `bytes` holds the segment images
+ * (each: 8-byte header = end of its metadata words, group data, metadata words of the
+ * 2,048-row groups growing down), segment i at seg_offsets[i] (8-aligned) with seg_rows[i]
+ * rows; the segments cover the partition in row order. The GPU unpacks every group
+ * (CONSTANT, CONSTANT_DELTA, FOR, DELTA_FOR) into the column; NULLs come from `validity`
+ * (host words; DuckDB keeps them in a separate validity segment). Malformed segments are
+ * refused before anything is launched. */
+int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
+                                     const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
+                                     const uint64_t *validity);
 /* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
  * distinct values of the column" (exact for every constant). RANGE / EQUALITY replace the
  * column's primary index; BINS (n >= 2 edges) adds a secondary binned index. */

@@ -79,6 +79,14 @@ def lib():
         l.oracle_build_bitvector.argtypes = [C.POINTER(OCol), C.c_uint64, C.c_int, C.c_int64, C.c_void_p]
         l.oracle_xor_hash.restype = C.c_uint64
         l.oracle_xor_hash.argtypes = [C.c_void_p, C.c_uint64]
+        l.oracle_bp_compress.restype = C.c_int
+        l.oracle_bp_compress.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64, C.c_int, C.c_uint64, C.c_void_p,
+                                         C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.POINTER(C.c_uint32)]
+        l.oracle_bp_decode.restype = C.c_int
+        l.oracle_bp_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.c_void_p]
+        l.oracle_bp_group_modes.restype = C.c_int
+        l.oracle_bp_group_modes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]
         _lib = l
     return _lib
 
@@ -200,3 +208,64 @@ def build_bitvector(column: Column, n_rows: int, cmp: int, constant: int) -> np.
 def xor_hash(rowids: np.ndarray) -> int:
     rowids = np.ascontiguousarray(rowids, dtype=np.int64)
     return int(lib().oracle_xor_hash(rowids.ctypes.data, len(rowids)))
+
+
+# ---------------------------------------------------------------- DuckDB BITPACKING (bitpacking_ref.c)
+
+BP_MODES = {"auto": 1, "constant": 2, "constant_delta": 3, "delta_for": 4, "for": 5}
+BP_MODE_NAMES = {v: k for k, v in BP_MODES.items()}
+DUCKDB_BLOCK_SIZE = 262144 - 8  # Storage::BLOCK_SIZE (storage_info.hpp:40-45)
+
+
+class BitpackedColumn:
+    """Segments of one column in DuckDB's BITPACKING format: all segment images concatenated
+    in `data`, with per-segment byte offsets / sizes / row counts."""
+
+    def __init__(self, data, seg_off, seg_size, seg_count, dtype):
+        self.data, self.seg_off, self.seg_size, self.seg_count, self.dtype = data, seg_off, seg_size, seg_count, dtype
+
+    @property
+    def n_rows(self) -> int:
+        return int(self.seg_count.sum())
+
+
+def bp_compress(values: np.ndarray, valid: Optional[np.ndarray] = None, mode: str = "auto",
+                block_size: int = DUCKDB_BLOCK_SIZE) -> Optional[BitpackedColumn]:
+    """Compress like DuckDB's checkpoint would with force_bitpacking_mode=`mode` (None when
+    the column is not bitpackable, e.g. a group whose max - min overflows)."""
+    values = np.ascontiguousarray(values)
+    assert values.dtype in (np.int32, np.int64)
+    n = len(values)
+    vb = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
+    cap = n * values.itemsize * 2 + (n // 2048 + 8) * 64 + 4 * block_size
+    out = np.zeros(cap, dtype=np.uint8)
+    max_segs = cap // 64 + 16
+    so = np.zeros(max_segs, dtype=np.uint64)
+    ss = np.zeros(max_segs, dtype=np.uint64)
+    sc = np.zeros(max_segs, dtype=np.uint64)
+    ns = C.c_uint32()
+    rc = lib().oracle_bp_compress(values.ctypes.data, values.itemsize, vb.ctypes.data if vb is not None else None, n,
+                                  BP_MODES[mode], block_size, out.ctypes.data, cap, so.ctypes.data, ss.ctypes.data,
+                                  sc.ctypes.data, max_segs, C.byref(ns))
+    if rc == 1:
+        return None
+    assert rc == 0, rc
+    k = ns.value
+    used = int(so[k - 1] + ss[k - 1]) if k else 0
+    return BitpackedColumn(out[:used].copy(), so[:k].copy(), ss[:k].copy(), sc[:k].copy(), values.dtype)
+
+
+def bp_decode(col: BitpackedColumn) -> np.ndarray:
+    out = np.zeros(max(col.n_rows, 1), dtype=col.dtype)
+    rc = lib().oracle_bp_decode(col.data.ctypes.data, col.seg_off.ctypes.data, col.seg_count.ctypes.data,
+                                len(col.seg_off), np.dtype(col.dtype).itemsize, out.ctypes.data)
+    assert rc == 0
+    return out[:col.n_rows]
+
+
+def bp_group_modes(col: BitpackedColumn):
+    cap = col.n_rows // 2048 + len(col.seg_off) + 1
+    m = np.zeros(cap, dtype=np.uint8)
+    k = lib().oracle_bp_group_modes(col.data.ctypes.data, col.seg_off.ctypes.data, col.seg_count.ctypes.data,
+                                    len(col.seg_off), m.ctypes.data, cap)
+    return [BP_MODE_NAMES.get(int(x), "invalid") for x in m[:k]]
