@@ -5,6 +5,7 @@ Everything here is a thin ctypes wrapper; the work happens in libcubitgpu.so.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import Dict, Optional, Sequence, Tuple
 
 import numpy as np
@@ -22,6 +23,7 @@ class Context:
         L.check(self.lib.cubit_ctx_create(device, C.byref(h)))
         self.handle = h
         self.device = device
+        self._tables = weakref.WeakSet()  # partitions to destroy before the context
         if stream is not None:
             L.check(self.lib.cubit_ctx_set_stream(h, C.c_void_p(stream)))
 
@@ -75,6 +77,8 @@ class Context:
 
     def close(self) -> None:
         if self.handle:
+            for t in list(self._tables):
+                t.close()
             self.lib.cubit_ctx_destroy(self.handle)
             self.handle = None
 
@@ -141,6 +145,7 @@ class CubitTable:
         h = C.c_void_p()
         L.check(self.lib.cubit_table_create(ctx.handle, self.n_rows, self.row_base, C.byref(h)))
         self.handle = h
+        ctx._tables.add(self)
         self.types: Dict[int, int] = {}
         self._keep = []
 
@@ -281,9 +286,10 @@ class CubitTable:
         return int(k.value), int(p.value)
 
     def close(self) -> None:
-        if self.handle:
+        # a partition never outlives its context (Context.close destroys it first)
+        if self.handle and self.ctx.handle:
             self.lib.cubit_table_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):
         try:

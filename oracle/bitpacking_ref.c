@@ -156,6 +156,9 @@ static void seg_flush(bp_writer *w) {
     memmove(w->blk + meta_at, w->blk + w->meta_off, meta_size);
     const uint64_t header = meta_at + meta_size;
     memcpy(w->blk, &header, 8);
+    /* segments start 8-aligned in the concatenated image (each is a block of its own in the
+     * reference, so every field stays aligned to its width) */
+    w->out_used = (w->out_used + 7) / 8 * 8;
     if (w->n_segs >= w->max_segs || w->out_used + total > w->out_cap) {
         w->failed = 1;
         return;
