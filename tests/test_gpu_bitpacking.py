@@ -84,5 +84,5 @@ def test_malformed_segments_are_refused(ctx):
     bad[:8] = np.frombuffer(np.uint64(len(bad) * 4).tobytes(), np.uint8)  # metadata past the end
     with pytest.raises(Exception, match="metadata"):
         t.add_bitpacked_column(0, bad, c.seg_off, c.seg_count, np.int64)
-    with pytest.raises(Exception, match="truncated|out of bounds"):
+    with pytest.raises(Exception, match="metadata|truncated|out of bounds"):
         t.add_bitpacked_column(0, c.data[: len(c.data) // 2], c.seg_off, c.seg_count, np.int64)
