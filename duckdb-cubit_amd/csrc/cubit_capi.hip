@@ -101,6 +101,23 @@ int set_device(cubit_ctx* ctx) {
     return CUBIT_OK;
 }
 
+// Start/stop events for the next timed kernel (stamped by its dispatch through
+// hipExtLaunchKernelGGL); both stay null when timing is off.
+int timing_events(cubit_ctx* ctx, hipEvent_t& start, hipEvent_t& stop) {
+    start = stop = nullptr;
+    if (!ctx->timing) return CUBIT_OK;
+    if (ctx->n_timed == ctx->evs.size()) {
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        ctx->evs.emplace_back(e0, e1);
+    }
+    start = ctx->evs[ctx->n_timed].first;
+    stop = ctx->evs[ctx->n_timed].second;
+    ctx->n_timed++;
+    return CUBIT_OK;
+}
+
 enum class RunMode { kDecode, kCount };
 
 // Launch the evaluator over a compiled program (asynchronous on the context stream).
@@ -118,18 +135,9 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.result_words = result_words;
     a.ticket = ctx->ticket;
     const uint64_t pw = padded_words(n_rows);
-    hipEvent_t stop = nullptr;
-    if (timed && ctx->timing) {
-        if (ctx->n_timed == ctx->evs.size()) {
-            hipEvent_t e0, e1;
-            HIP_CHECK(hipEventCreate(&e0));
-            HIP_CHECK(hipEventCreate(&e1));
-            ctx->evs.emplace_back(e0, e1);
-        }
-        stop = ctx->evs[ctx->n_timed].second;
-    }
-    hipEvent_t start = stop ? ctx->evs[ctx->n_timed].first : nullptr;
-    if (stop) ctx->n_timed++;
+    hipEvent_t start = nullptr, stop = nullptr;
+    if (timed)
+        if (int rc = timing_events(ctx, start, stop)) return rc;
     if (mode == RunMode::kCount) {
         a.num_tiles = (uint32_t)(pw / count_tile_words(prog.n_leaves));
         HIP_CHECK(launch_eval_count(a, ctx->stream, start, stop));
@@ -896,24 +904,35 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
             uint32_t enc;
             std::memcpy(&enc, bytes + base + meta_end - 4 * (g + 1), 4);
             BpGroup bg{};
-            bg.mode = enc >> 24;
-            bg.data_off = base + (enc & 0x00ffffffu);
+            const uint32_t mode = enc >> 24;
+            const uint64_t data_off = base + (enc & 0x00ffffffu);
+            bg.mode = (uint16_t)mode;
             bg.row_start = row + g * 2048;
             bg.count = (uint32_t)std::min<uint64_t>(2048, seg_rows[sg] - g * 2048);
-            uint64_t need = 0;
-            if (bg.mode == 2) {
-                need = tsz;
-            } else if (bg.mode == 3) {
-                need = 2 * tsz;
-            } else if (bg.mode == 4 || bg.mode == 5) {
-                if (bg.data_off + 2 * tsz > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: truncated", sg, (unsigned long long)g);
-                const uint8_t w = bytes[bg.data_off + tsz];
-                if (w > 8 * tsz) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: width %u", sg, (unsigned long long)g, w);
-                need = (bg.mode == 4 ? 3 : 2) * tsz + ((uint64_t)bg.count + 31) / 32 * 32 * w / 8;
-            } else {
-                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: mode %u", sg, (unsigned long long)g, bg.mode);
+            // header fields (BitpackingScanState::LoadNextGroup, bitpacking.cpp:620-690)
+            const uint64_t n_fields = mode == 2 ? 1 : (mode == 3 || mode == 5) ? 2 : mode == 4 ? 3 : 0;
+            if (n_fields == 0)
+                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: mode %u", sg, (unsigned long long)g, mode);
+            if (data_off < base + 8 || data_off + n_fields * tsz > n_bytes)
+                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
+            auto field = [&](uint64_t i) {
+                uint64_t v = 0;  // the T's bits, zero-extended (the kernel truncates to T)
+                std::memcpy(&v, bytes + data_off + i * tsz, tsz);
+                return v;
+            };
+            bg.base = field(0);
+            uint64_t packed = 0;
+            if (mode == 3) {
+                bg.aux = field(1);
+            } else if (mode == 4 || mode == 5) {
+                const uint64_t w = field(1) & 0xff;  // the reference reads the width as a T, uses its low byte
+                if (w > 8 * tsz) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: width %u", sg, (unsigned long long)g, (unsigned)w);
+                bg.width = (uint16_t)w;
+                if (mode == 4) bg.aux = field(2);
+                packed = ((uint64_t)bg.count + 31) / 32 * 32 * w / 8;
             }
-            if (bg.data_off + need > n_bytes || bg.data_off < base + 8)
+            bg.words_off = data_off + n_fields * tsz;
+            if (bg.words_off + packed > n_bytes)
                 return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
             groups.push_back(bg);
         }
@@ -925,14 +944,17 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     hipStream_t s = t->ctx->stream;
     DevBuf d_bytes, d_groups;
     auto out = std::make_unique<DevBuf>();
-    if (hipMalloc(&d_bytes.p, n_bytes) != hipSuccess ||
+    // +16: the kernel stages packed words with 16-byte-aligned loads that may run past the end
+    if (hipMalloc(&d_bytes.p, (n_bytes + 15) / 16 * 16 + 16) != hipSuccess ||
         hipMalloc(&d_groups.p, groups.size() * sizeof(BpGroup)) != hipSuccess ||
         hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * tsz, 16)) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "bitpacked column allocation failed");
     HIP_CHECK(hipMemcpyAsync(d_bytes.p, bytes, n_bytes, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_groups.p, groups.data(), groups.size() * sizeof(BpGroup), hipMemcpyHostToDevice, s));
+    hipEvent_t e0, e1;
+    if (int rc = timing_events(t->ctx, e0, e1)) return rc;
     HIP_CHECK(launch_bitunpack(static_cast<const uint8_t*>(d_bytes.p), static_cast<const BpGroup*>(d_groups.p),
-                               groups.size(), type, out->p, s));
+                               groups.size(), type, out->p, s, e0, e1));
     HIP_CHECK(hipStreamSynchronize(s));
     Column c;
     c.type = type;
@@ -1869,5 +1891,14 @@ extern "C" int cubit_table_info(cubit_table* t, uint64_t* n_rows, int64_t* row_b
     if (n_rows) *n_rows = t->n_rows;
     if (row_base) *row_base = t->row_base;
     if (ctx) *ctx = t->ctx;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_column_data(cubit_table* t, int col, const void** data, int* type) {
+    if (!t || !data) return fail(CUBIT_ERR_INVALID, "null argument");
+    auto it = t->cols.find(col);
+    if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    *data = it->second.data;
+    if (type) *type = it->second.type;
     return CUBIT_OK;
 }

@@ -98,14 +98,19 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
                            uint64_t range, uint64_t* bits, hipStream_t stream);
 // K5: DuckDB BITPACKING groups → plain values. One record per 2,048-value metadata group
 // (mode: 2 CONSTANT, 3 CONSTANT_DELTA, 4 DELTA_FOR, 5 FOR — BitpackingMode).
+// The host reads each group's header (the T-sized fields before the packed words) into the
+// record, so a workgroup's only dependent load chain is record → packed words.
 struct BpGroup {
-    uint64_t data_off;   // byte offset of the group's data in the segment bytes
+    uint64_t words_off;  // byte offset of the packed words (FOR / DELTA_FOR)
     uint64_t row_start;  // first row of the group
+    uint64_t base;       // CONSTANT value | CONSTANT_DELTA first | FOR minimum | DELTA_FOR min_delta (T bits)
+    uint64_t aux;        // CONSTANT_DELTA delta | DELTA_FOR delta_offset (T bits)
     uint32_t count;      // rows in the group (≤ 2,048)
-    uint32_t mode;
+    uint16_t mode;
+    uint16_t width;      // bit width of the packed values (FOR / DELTA_FOR)
 };
 hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
-                            hipStream_t stream);
+                            hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,

@@ -1028,81 +1028,125 @@ __global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col
 // bitpacking.cpp:785-868): CONSTANT, CONSTANT_DELTA (first + i·delta), FOR (unpacked + min)
 // and DELTA_FOR (running sum of unpacked + min_delta from delta_offset, a block scan here).
 // Packed values are horizontal (fastpforlib fastpack): value i at bits [i·w, (i+1)·w) of
-// little-endian 32-bit words; each thread unpacks 8 consecutive values. U = unsigned T, the
+// little-endian 32-bit words. The group's packed words (≤ 2,048·64 bits = 16 KiB) are staged
+// in LDS with coalesced loads; thread t then owns the 4-value quads t and t + 256 (values
+// 4t..4t+3 and 1024+4t..1024+4t+3), so every wave store is a contiguous 16 B per lane
+// (HBM-write-bound: the output is 4–8 B per value, the input w/8). U = unsigned T, the
 // reference's wrap-around arithmetic.
 template <typename T, typename U>
 __global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restrict__ bytes,
                                                         const BpGroup* __restrict__ groups, T* __restrict__ out) {
-    constexpr int PER = 8;
-    __shared__ U s_tot[4];
+    constexpr int THREADS = 256, QUADS = 2;
+    constexpr uint32_t MAXW = 2048 * 64 / 32;  // packed words of a 64-bit-wide group
+    __shared__ __attribute__((aligned(16))) uint32_t s_words[MAXW + 8];  // + alignment shift + 3-word window
+    __shared__ U s_tot[THREADS / 64];
     const BpGroup g = groups[blockIdx.x];
     const int t = threadIdx.x;
-    const uint8_t* p = bytes + g.data_off;
-    auto load_t = [](const uint8_t* q) -> U { return *reinterpret_cast<const U*>(q); };
     T* dst = out + g.row_start;
-    const uint32_t i0 = (uint32_t)t * PER;
-    if (g.mode == 2) {  // CONSTANT
-        const U c = load_t(p);
-        for (uint32_t k = 0; k < PER; ++k)
-            if (i0 + k < g.count) dst[i0 + k] = (T)c;
-        return;
-    }
-    if (g.mode == 3) {  // CONSTANT_DELTA
-        const U base = load_t(p), d = load_t(p + sizeof(T));
-        for (uint32_t k = 0; k < PER; ++k)
-            if (i0 + k < g.count) dst[i0 + k] = (T)(U)(d * (U)(i0 + k) + base);
-        return;
-    }
-    const U fr = load_t(p);
-    const uint32_t w = (uint32_t)(uint8_t)load_t(p + sizeof(T));
-    const bool delta = g.mode == 4;
-    const U doff = delta ? load_t(p + 2 * sizeof(T)) : (U)0;
-    const uint32_t* words = reinterpret_cast<const uint32_t*>(p + (delta ? 3 : 2) * sizeof(T));
-    U v[PER];
+    // store quad c of this thread: values 4·(t + 256c) + 0..3
+    auto store_quad = [&](int c, const U (&v)[4]) {
+        const uint32_t i0 = 4u * (uint32_t)(t + THREADS * c);
+        if (i0 + 4 <= g.count) {
+            if (sizeof(T) == 4) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 o;
+                o.x = (uint32_t)v[0], o.y = (uint32_t)v[1], o.z = (uint32_t)v[2], o.w = (uint32_t)v[3];
+                *reinterpret_cast<u32x4*>(dst + i0) = o;
+            } else {
+                u64x2 o0, o1;
+                o0.x = (uint64_t)v[0], o0.y = (uint64_t)v[1], o1.x = (uint64_t)v[2], o1.y = (uint64_t)v[3];
+                reinterpret_cast<u64x2*>(dst + i0)[0] = o0;
+                reinterpret_cast<u64x2*>(dst + i0)[1] = o1;
+            }
+        } else {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const uint32_t i = i0 + k;
-        uint64_t x = 0;
-        if (w && i < g.count) {
-            const uint64_t bit = (uint64_t)i * w;
-            const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
-            const uint32_t nwords = (off + w + 31) / 32;
-            uint64_t lo = words[wi];
-            if (nwords > 1) lo |= (uint64_t)words[wi + 1] << 32;
-            x = lo >> off;
-            if (nwords > 2) x |= (uint64_t)words[wi + 2] << (64 - off);
-            if (w < 64) x &= (1ull << w) - 1;
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j < g.count) dst[i0 + j] = (T)v[j];
         }
-        v[k] = (U)x + fr;
+    };
+    if (g.mode == 2 || g.mode == 3) {  // CONSTANT, CONSTANT_DELTA
+        const U base = (U)g.base, d = g.mode == 3 ? (U)g.aux : (U)0;
+#pragma unroll
+        for (int c = 0; c < QUADS; ++c) {
+            U v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (U)(d * (U)(4u * (uint32_t)(t + THREADS * c) + j) + base);
+            store_quad(c, v);
+        }
+        return;
     }
+    const U fr = (U)g.base;
+    const uint32_t w = g.width;
+    const bool delta = g.mode == 4;
+    const U doff = delta ? (U)g.aux : (U)0;
+    // packed words start 4-aligned: stage the 16-byte-aligned span that covers them with
+    // dwordx4 loads (the upload pads the bytes by 16), word 0 lands at s_words[sh]
+    const uint32_t nwords = (g.count + 31) / 32 * w;  // validated on the host against the bytes
+    const uint64_t a0 = g.words_off & ~15ull;
+    const uint32_t sh = (uint32_t)(g.words_off - a0) / 4;
+    const uint32_t nvec = (sh + nwords + 3) / 4;
+    {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* src = reinterpret_cast<const u32x4*>(bytes + a0);
+        u32x4* sw = reinterpret_cast<u32x4*>(s_words);
+        for (uint32_t i = t; i < nvec; i += THREADS) sw[i] = src[i];
+    }
+    // (a value's window may read one word past its last bit: those bits are masked off)
+    __syncthreads();
+    U v[QUADS][4];
+#pragma unroll
+    for (int c = 0; c < QUADS; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = 4u * (uint32_t)(t + THREADS * c) + j;
+            uint64_t x = 0;
+            if (w && i < g.count) {
+                const uint64_t bit = (uint64_t)i * w;
+                const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
+                x = ((uint64_t)s_words[sh + wi] | (uint64_t)s_words[sh + wi + 1] << 32) >> off;
+                if (off + w > 64) x |= (uint64_t)s_words[sh + wi + 2] << (64 - off);
+                if (w < 64) x &= (1ull << w) - 1;
+            }
+            v[c][j] = (U)x + fr;
+        }
     if (!delta) {
 #pragma unroll
-        for (int k = 0; k < PER; ++k)
-            if (i0 + k < g.count) dst[i0 + k] = (T)v[k];
+        for (int c = 0; c < QUADS; ++c) store_quad(c, v[c]);
         return;
     }
-    // DELTA_FOR: inclusive prefix over the group (rows past count add nothing)
-    U run = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        if (i0 + k >= g.count) v[k] = 0;
-        run += v[k];
-        v[k] = run;
-    }
+    // DELTA_FOR: inclusive prefix over the group in value order: quad c = 0 covers values
+    // 0..1023, c = 1 covers 1024..2047 (carry = the first half's total). Values past count add 0.
     const int lane = t & 63, wave = t >> 6;
-    U incl = run;
+    U carry = doff;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const U y = (U)__shfl_up((uint64_t)incl, d, 64);
-        if (lane >= d) incl += y;
+    for (int c = 0; c < QUADS; ++c) {
+        U run = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (4u * (uint32_t)(t + THREADS * c) + j >= g.count) v[c][j] = 0;
+            run += v[c][j];
+            v[c][j] = run;
+        }
+        U incl = run;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const U y = (U)__shfl_up((uint64_t)incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_tot[wave] = incl;
+        __syncthreads();
+        U pre = carry + incl - run, tot = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < THREADS / 64; ++w2) {
+            if (w2 < wave) pre += s_tot[w2];
+            tot += s_tot[w2];
+        }
+        __syncthreads();  // s_tot is rewritten by the next half
+        carry += tot;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[c][j] += pre;
+        store_quad(c, v[c]);
     }
-    if (lane == 63) s_tot[wave] = incl;
-    __syncthreads();
-    U pre = doff + incl - run;
-    for (int w2 = 0; w2 < wave; ++w2) pre += s_tot[w2];
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-        if (i0 + k < g.count) dst[i0 + k] = (T)(U)(v[k] + pre);
 }
 
 // ------------------------------------------------------------------ K3: probe
@@ -1421,15 +1465,15 @@ hipError_t launch_sum_product_arrays(const int64_t* x, const int64_t* y, const u
 }
 
 hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
-                            hipStream_t stream) {
+                            hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
     if (n_groups == 0) return hipSuccess;
     if (n_groups > 0x7fffffffull) return hipErrorInvalidValue;
     if (type == 0)
-        hipLaunchKernelGGL((bitunpack_kernel<int32_t, uint32_t>), dim3((unsigned)n_groups), dim3(256), 0, stream, bytes,
-                           groups, static_cast<int32_t*>(out));
+        hipExtLaunchKernelGGL((bitunpack_kernel<int32_t, uint32_t>), dim3((unsigned)n_groups), dim3(256), 0, stream,
+                              start, stop, 0, bytes, groups, static_cast<int32_t*>(out));
     else
-        hipLaunchKernelGGL((bitunpack_kernel<int64_t, uint64_t>), dim3((unsigned)n_groups), dim3(256), 0, stream, bytes,
-                           groups, static_cast<int64_t*>(out));
+        hipExtLaunchKernelGGL((bitunpack_kernel<int64_t, uint64_t>), dim3((unsigned)n_groups), dim3(256), 0, stream,
+                              start, stop, 0, bytes, groups, static_cast<int64_t*>(out));
     return hipGetLastError();
 }
 

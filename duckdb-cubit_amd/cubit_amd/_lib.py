@@ -105,6 +105,7 @@ GPU_SIGNATURES = {
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
+    "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),
     "cubit_table_save_index": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
     "cubit_table_load_index": (C.c_int, [_P, C.c_int, C.c_char_p]),
 }
@@ -115,6 +116,7 @@ GEN_SIGNATURES = {
     "cubit_tpch_lineitem_gen": (_I64, [C.c_double, _I64, _I64, _P, _P, _P, _P, C.c_int]),
     "cubit_splitmix64": (_U64, [_U64, _U64]),
     "cubit_synth_uniform_i32": (C.c_int, [_U64, _U64, _U64, _U32, _P, C.c_int]),
+    "cubit_bitpack_for": (_U32, [_P, C.c_int, _U64, _U64, _P, _U64, _P, _P, _U32, C.POINTER(_U64), C.c_int]),
 }
 
 SCAN_SIGNATURES = {

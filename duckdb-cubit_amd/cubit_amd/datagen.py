@@ -6,6 +6,7 @@
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -66,6 +67,36 @@ def uniform_i32(seed: int, n: int, modulus: int, row_begin: int = 0, threads: in
     rc = L.gen_lib().cubit_synth_uniform_i32(seed, row_begin, n, modulus, out.ctypes.data, threads)
     assert rc == 0
     return out
+
+
+@dataclass
+class Bitpacked:
+    """DuckDB BITPACKING segment images of one column (cubit_table_add_bitpacked_column input)."""
+    data: np.ndarray       # uint8 segment images, segment i at seg_off[i]
+    seg_off: np.ndarray    # uint64
+    seg_count: np.ndarray  # uint64 rows per segment
+
+
+def bitpack_for(values: np.ndarray, block_size: int = 262144, threads: int = 0) -> Bitpacked:
+    """Bench input: CONSTANT / FOR groups in 256 KiB segments, one row group per segment run
+    (csrc/bitpack_gen.cpp). Test parity uses the oracle's restatement of the reference
+    compressor instead."""
+    v = np.ascontiguousarray(values)
+    if v.dtype not in (np.int32, np.int64):
+        raise TypeError(v.dtype)
+    n = int(v.shape[0])
+    ngroups = (n + 2047) // 2048
+    cap = n * v.itemsize + ngroups * 64 + 4096
+    max_segs = ngroups + (n + 122879) // 122880 + 1
+    out = np.empty(cap, dtype=np.uint8)
+    off = np.empty(max_segs, dtype=np.uint64)
+    rows = np.empty(max_segs, dtype=np.uint64)
+    used = ctypes.c_uint64(0)
+    ns = L.gen_lib().cubit_bitpack_for(v.ctypes.data, v.itemsize, n, block_size, out.ctypes.data, cap,
+                                       off.ctypes.data, rows.ctypes.data, max_segs, ctypes.byref(used), threads)
+    if ns == 0:
+        raise RuntimeError("cubit_bitpack_for failed")
+    return Bitpacked(out[: used.value], off[:ns].copy(), rows[:ns].copy())
 
 
 def validity_from_mask(valid: np.ndarray) -> np.ndarray:

@@ -178,6 +178,19 @@ class CubitTable:
                                                           so.ctypes.data, sr.ctypes.data, len(so),
                                                           vw.ctypes.data if vw is not None else None))
 
+    def column_data(self, col: int):
+        """(device pointer, CUBIT type) of a registered column's values."""
+        ptr, typ = C.c_void_p(), C.c_int()
+        L.check(self.lib.cubit_table_column_data(self.handle, col, C.byref(ptr), C.byref(typ)))
+        return int(ptr.value or 0), int(typ.value)
+
+    def download_column(self, col: int) -> np.ndarray:
+        ptr, typ = self.column_data(col)
+        out = np.empty(self.n_rows, dtype=np.int32 if typ == L.TYPE_INT32 else np.int64)
+        if self.n_rows:
+            L.check(self.lib.cubit_memcpy_d2h(self.ctx.handle, out.ctypes.data, C.c_void_p(ptr), out.nbytes))
+        return out
+
     def add_device_column(self, col: int, dptr: int, type_: int, validity_dptr: Optional[int] = None) -> None:
         L.check(self.lib.cubit_table_add_column(self.handle, col, type_, C.c_void_p(dptr),
                                                 C.c_void_p(validity_dptr) if validity_dptr else None, 1))

@@ -168,6 +168,10 @@ int cubit_table_create(cubit_ctx *ctx, uint64_t n_rows, int64_t row_base, cubit_
 int cubit_table_destroy(cubit_table *t);
 /* rows, row base and owning context of a partition */
 int cubit_table_info(cubit_table *t, uint64_t *n_rows, int64_t *row_base, cubit_ctx **ctx);
+/* Device pointer (read-only, owned by the table or the caller that registered it) and type
+ * of column `col`'s values — e.g. a column unpacked by K5 (ColumnData's decoded vectors,
+ * src/storage/table/column_data.cpp:135-188). */
+int cubit_table_column_data(cubit_table *t, int col, const void **data, int *type);
 /* Register column `col`. data/validity are host pointers unless on_device = 1 (then the
  * table only references them). validity may be NULL (no NULLs). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
@@ -179,7 +183,8 @@ int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, 
  * rows; the segments cover the partition in row order. The GPU unpacks every group
  * (CONSTANT, CONSTANT_DELTA, FOR, DELTA_FOR) into the column; NULLs come from `validity`
  * (host words; DuckDB keeps them in a separate validity segment). Malformed segments are
- * refused before anything is launched. */
+ * refused before anything is launched. With timing on, the unpack kernel is a timed launch
+ * (cubit_last_kernel_ms). */
 int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
                                      const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
                                      const uint64_t *validity);

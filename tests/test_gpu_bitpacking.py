@@ -52,6 +52,7 @@ def test_unpack_matches_values(ctx, name, mode):
     t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, v.dtype)
     got = probe_all(ctx, t, 0, n, row_base=5)
     assert np.array_equal(got, v.astype(np.int64)), (name, mode, sorted(set(O.bp_group_modes(c))))
+    assert np.array_equal(t.download_column(0), v)
 
 
 def test_nulls_index_and_scan(ctx):
@@ -86,3 +87,21 @@ def test_malformed_segments_are_refused(ctx):
         t.add_bitpacked_column(0, bad, c.seg_off, c.seg_count, np.int64)
     with pytest.raises(Exception, match="metadata|truncated|out of bounds"):
         t.add_bitpacked_column(0, c.data[: len(c.data) // 2], c.seg_off, c.seg_count, np.int64)
+
+
+@pytest.mark.parametrize("name", ["l_shipdate", "l_discount", "l_quantity", "l_extendedprice"])
+def test_bench_packer_lineitem(ctx, name):
+    """bench.py's K5 leg input (CONSTANT/FOR segments from libcubit_datagen) at SF1: the GPU
+    unpack equals the column and the oracle's decode of the same bytes."""
+    from cubit_amd import datagen
+
+    li = datagen.tpch_lineitem(1.0, columns=(name,))
+    v = getattr(li, name)
+    b = datagen.bitpack_for(v)
+    t = CubitTable(ctx, len(v))
+    t.add_bitpacked_column(0, b.data, b.seg_off, b.seg_count, v.dtype)
+    got = t.download_column(0)
+    assert np.array_equal(got, v)
+    col = O.BitpackedColumn(b.data, b.seg_off, None, b.seg_count, v.dtype)
+    assert np.array_equal(O.bp_decode(col), got)
+    t.close()

@@ -65,3 +65,21 @@ def test_nulls_and_all_null_groups():
     d = O.bp_decode(c)
     assert np.array_equal(d[valid], v[valid])
     assert O.bp_group_modes(c)[1] == "constant"
+
+
+@pytest.mark.parametrize("kind", ["dates", "wide64", "constant", "price"])
+def test_bench_packer_decodes_with_oracle(kind, li01):
+    """bench.py's K5 input generator (libcubit_datagen cubit_bitpack_for) writes segments the
+    oracle's restatement of the reference decoder reads back exactly."""
+    from cubit_amd import datagen
+
+    rng = np.random.default_rng(3)
+    n = 400_009
+    v = {"dates": li01.l_shipdate[:n],
+         "wide64": rng.integers(-2 ** 62, 2 ** 62, n).astype(np.int64),
+         "constant": np.full(n, 42, np.int32),
+         "price": li01.l_extendedprice[:n]}[kind]
+    b = datagen.bitpack_for(v)
+    col = O.BitpackedColumn(b.data, b.seg_off, None, b.seg_count, v.dtype)
+    assert np.array_equal(O.bp_decode(col), v)
+    assert set(O.bp_group_modes(col)) <= {"constant", "for"}
