@@ -999,22 +999,23 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
         if (encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) return fail(CUBIT_ERR_INVALID, "bins need >= 2 edges");
     }
     const size_t n_bv = encoding == CUBIT_INDEX_BINS ? ix.keys.size() - 1 : ix.keys.size();
-    for (size_t k = 0; k < n_bv; ++k) {
-        auto b = std::make_unique<DevBuf>();
-        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
-            return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(), n_bv);
-        hipError_t e;
-        if (encoding == CUBIT_INDEX_BINS)
-            e = launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows, kCmpBetween, ix.keys[k],
-                                         static_cast<uint64_t*>(b->p), t->ctx->stream, ix.keys[k + 1]);
-        else
-            e = launch_compare_bitvector(c.data, c.type, c.validity, t->n_rows,
-                                         encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ, ix.keys[k],
-                                         static_cast<uint64_t*>(b->p), t->ctx->stream);
-        HIP_CHECK(e);
-        ix.bvs.push_back(static_cast<uint64_t*>(b->p));
-        ix.owned.push_back(std::move(b));
-        ix.bytes += t->nwp * 8;
+    // one pass of the column per kMultiKeys bitvectors
+    const int cmp = encoding == CUBIT_INDEX_BINS ? kCmpBetween : encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ;
+    for (size_t k0 = 0; k0 < n_bv; k0 += kMultiKeys) {
+        MultiKeyArgs mk{};
+        for (size_t k = k0; k < std::min(n_bv, k0 + kMultiKeys); ++k) {
+            auto b = std::make_unique<DevBuf>();
+            if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
+                return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(), n_bv);
+            mk.c[mk.m] = ix.keys[k];
+            mk.c2[mk.m] = encoding == CUBIT_INDEX_BINS ? ix.keys[k + 1] : 0;
+            mk.out[mk.m] = static_cast<uint64_t*>(b->p);
+            ++mk.m;
+            ix.bvs.push_back(static_cast<uint64_t*>(b->p));
+            ix.owned.push_back(std::move(b));
+            ix.bytes += t->nwp * 8;
+        }
+        HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
     }
     HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
     if (encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);

@@ -90,6 +90,17 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
 constexpr int kCmpBetween = 6;
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                                     int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2 = 0);
+// K0 over several keys in one pass of the column (index build): out[k] = cmp(v, c[k], c2[k]),
+// cmp ∈ {EQ, LT, between}
+constexpr int kMultiKeys = 16;
+struct MultiKeyArgs {
+    int64_t c[kMultiKeys];
+    int64_t c2[kMultiKeys];
+    uint64_t* out[kMultiKeys];
+    uint32_t m;
+};
+hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
+                                     const MultiKeyArgs& a, hipStream_t stream);
 // index-build statistics (out3 = {min, max, valid count}, pre-set by the caller) and the
 // presence bitmap of the valid values (bit v - vmin, `range` bits, zeroed by the caller)
 hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,

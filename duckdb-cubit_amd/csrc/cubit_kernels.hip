@@ -934,6 +934,83 @@ __global__ __launch_bounds__(256) void compare_bitvector_kernel(const T* __restr
     }
 }
 
+// Index build (K0, several keys per pass): one read of the column produces up to
+// kMultiKeys bitvectors (range L(k), equality E(k) or bins [k, k2)). A wave handles 64
+// consecutive words; 16 rows per lane are loaded ahead, then every key's predicate is one
+// ballot per word, kept by lane j for word j, and each key's 64 words leave as one 512-byte
+// store. Bytes per pass: n·w_c read + m·n/8 written, instead of m·(n·w_c + n/8).
+template <typename T, typename CT, int CMP>
+__global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __restrict__ col,
+                                                                 const uint64_t* __restrict__ validity,
+                                                                 uint64_t n_rows, uint64_t n_words_padded,
+                                                                 MultiKeyArgs a) {
+    // CT: compare type (int32 when the column and every key fit 32 bits: one VALU compare)
+    constexpr int JB = 16;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w0 = wave_id * 64; w0 < n_words_padded; w0 += n_waves * 64) {
+        uint32_t lo[kMultiKeys], hi[kMultiKeys];  // lane j keeps word j of every key
+#pragma unroll
+        for (int k = 0; k < kMultiKeys; ++k) lo[k] = hi[k] = 0;
+        for (int jb = 0; jb < 64; jb += JB) {
+            CT v[JB];
+            bool ok[JB];
+#pragma unroll
+            for (int j = 0; j < JB; ++j) {
+                const uint64_t row = (w0 + jb + j) * 64 + lane;
+                ok[j] = row < n_rows;
+                v[j] = ok[j] ? (CT)col[row] : (CT)0;
+                if (validity) ok[j] = ok[j] && ((validity[w0 + jb + j] >> lane) & 1ull);
+            }
+#pragma unroll
+            for (int j = 0; j < JB; ++j) {
+                // every key's ballot for word jb + j (uniform, SGPRs), then lane jb + j alone
+                // moves them into its registers under the exec mask: per (word, key) one
+                // compare and two moves
+                // (keys past a.m repeat the last key: the host pads them, their words are not stored)
+                const uint64_t okm = __ballot(ok[j]);
+                uint64_t b[kMultiKeys];
+#pragma unroll
+                for (int k = 0; k < kMultiKeys; ++k) {
+                    const CT c = (CT)a.c[k], c2 = (CT)a.c2[k];
+                    bool p;
+                    if (CMP == 0) p = v[j] == c;
+                    else if (CMP == 2) p = v[j] < c;
+                    else p = v[j] >= c && v[j] < c2;
+                    b[k] = __ballot(p) & okm;
+                }
+                if (lane == jb + j) {
+#pragma unroll
+                    for (int k = 0; k < kMultiKeys; ++k) {
+                        lo[k] = (uint32_t)b[k];
+                        hi[k] = (uint32_t)(b[k] >> 32);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kMultiKeys; ++k)
+            if (k < (int)a.m) a.out[k][w0 + lane] = ((uint64_t)hi[k] << 32) | lo[k];
+    }
+}
+
+template <typename T, typename CT>
+hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp,
+                                  const MultiKeyArgs& a, hipStream_t stream) {
+    const uint64_t nw = padded_words(n_rows);
+    const uint64_t waves = nw / 64;
+    const uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
+    const dim3 grid((unsigned)std::max<uint64_t>(blocks, 1)), block(256);
+    switch (cmp) {
+    case 0: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 0>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
+    case 2: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 2>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
+    case 6: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 6>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_compare_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp, int64_t c, int64_t c2,
                             uint64_t* out, hipStream_t stream) {
@@ -1362,6 +1439,27 @@ hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* v
                                          out_words, stream);
     return launch_compare_t<int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, constant, constant2,
                                      out_words, stream);
+}
+
+hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
+                                     const MultiKeyArgs& args, hipStream_t stream) {
+    if (args.m == 0) return hipSuccess;
+    if (args.m > (uint32_t)kMultiKeys) return hipErrorInvalidValue;
+    MultiKeyArgs a = args;
+    for (uint32_t k = a.m; k < (uint32_t)kMultiKeys; ++k) {  // the kernel evaluates every slot
+        a.c[k] = a.c[a.m - 1];
+        a.c2[k] = a.c2[a.m - 1];
+        a.out[k] = nullptr;
+    }
+    bool keys32 = true;  // every key (and bin end) an int32: compare an int32 column in 32 bits
+    for (uint32_t k = 0; k < a.m; ++k)
+        keys32 = keys32 && a.c[k] >= INT32_MIN && a.c[k] <= INT32_MAX &&
+                 (cmp != kCmpBetween || (a.c2[k] >= INT32_MIN && a.c2[k] <= INT32_MAX));
+    if (type == 0 && keys32)
+        return launch_compare_multi_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a, stream);
+    if (type == 0)
+        return launch_compare_multi_t<int32_t, int64_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a, stream);
+    return launch_compare_multi_t<int64_t, int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a, stream);
 }
 
 hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,
