@@ -231,6 +231,22 @@ int main(int argc, char** argv) {
     // DPC("pairs conj S3072 x3/CU", 3072, 3, 512);  // 80-VGPR cap spills 107 VGPRs: not viable
     DPC("pairs conj S4096 x2/CU", 4096, 2, 512);
     DPC("pairs conj T256 S2048 x4/CU", 2048, 4, 256);
+    // K = 4 (Q6 with the year bin): L0 ∧ ¬L1 ∧ L2 ∧ L4 as CONJ, at 2 and 3 workgroups per CU
+#define DK4(NAME, S, OCC)                                                                                      \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = dtiles;                                                                   \
+                      a.prog.leaf[3] = leaf[4];                                                               \
+                      a.prog.n_leaves = 4;                                                                    \
+                      a.prog.negate = 0b0010;                                                                 \
+                      a.prog.nops = 0;                                                                        \
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);                              \
+                      a.prog.ops = 0;                                                                         \
+                      hipLaunchKernelGGL((eval_decode_pairs<4, 2, S, 512, 0, FORM_CONJ, OCC>),                \
+                                         dim3(std::min<unsigned>(dtiles, OCC * cus)), dim3(512), 0, s, a, dir); \
+                  }, 3})
+    DK4("K4 conj x2/CU (prod)", 4096, 2);
+    // (S3072 x3/CU: the 80-VGPR cap spills 192 B per thread, 199 µs — not viable)
+    DK4("K4 conj S3072 x2/CU", 3072, 2);
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);

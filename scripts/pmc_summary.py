@@ -70,6 +70,25 @@ def main():
                       "(rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE; separate passes)",
         }
         print(workload, json.dumps(summary[workload], indent=1))
+        k5 = line.get("k5_bitunpack")
+        if k5:
+            # K5 leg (bench.py --bitpacked): every bitunpack launch of the run, all columns
+            kf = [r for r in rows(f"{wdir}/fetch/**/*counter_collection.csv") if "bitunpack_kernel" in r["Kernel_Name"]]
+            kw = [r for r in rows(f"{wdir}/write/**/*counter_collection.csv") if "bitunpack_kernel" in r["Kernel_Name"]]
+            if kf and kw:
+                alg = k5["launches_per_column"] * k5["all_columns"]["bytes"]
+                rd = 2 * sum(float(r["Counter_Value"]) for r in kf) * 1024
+                wr = sum(float(r["Counter_Value"]) for r in kw) * 1024
+                summary["k5_bitunpack"] = {
+                    "kernel": "bitunpack_kernel<int|long>",
+                    "launches": len(kf),
+                    "hbm_read_bytes": rd, "hbm_write_bytes": wr,
+                    "algorithmic_bytes": alg,
+                    "hbm_over_algorithmic": (rd + wr) / alg,
+                    "correction": "FETCH_SIZE x2 (16 B/lane loads of the packed words), WRITE_SIZE exact (16 B/lane stores)",
+                    "source": f"gpurun_out/prof/{w} with BENCH_EXTRA=--bitpacked (rocprofv3 --pmc passes as above)",
+                }
+                print("k5_bitunpack", json.dumps(summary["k5_bitunpack"], indent=1))
     summary_p.write_text(json.dumps(summary, indent=1) + "\n")
 
 
