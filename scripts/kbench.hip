@@ -230,6 +230,16 @@ int main(int argc, char** argv) {
                   }, 0})
     // DPC("pairs conj S3072 x3/CU", 3072, 3, 512);  // 80-VGPR cap spills 107 VGPRs: not viable
     DPC("pairs conj S4096 x2/CU", 4096, 2, 512);
+    // one pair of words per thread: 1,024-word tiles (finer balance for mid-size partitions)
+    vs.push_back({"pairs conj P1 S2048", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = (uint32_t)(pw / 1024);
+                      a.prog.negate = 0b01010;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_pairs<5, 1, 2048, 512, 0, FORM_CONJ, 2>),
+                                         dim3(std::min<unsigned>(a.num_tiles, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 0});
     DPC("pairs conj T256 S2048 x4/CU", 2048, 4, 256);
     // K = 4 (Q6 with the year bin): L0 ∧ ¬L1 ∧ L2 ∧ L4 as CONJ, at 2 and 3 workgroups per CU
 #define DK4(NAME, S, OCC)                                                                                      \
@@ -288,6 +298,12 @@ int main(int argc, char** argv) {
                       k1(a);
                       a.num_tiles = dtiles;
                       CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 3});
+    vs.push_back({"K1 1% pairs P1", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = (uint32_t)(pw / 1024);
+                      hipLaunchKernelGGL((eval_decode_pairs<1, 1, 2048, 512, 0, FORM_CONJ, 2>),
+                                         dim3(std::min<unsigned>(a.num_tiles, 2 * cus)), dim3(512), 0, s, a, dir);
                   }, 3});
     vs.push_back({"K1 1% tiles grid=tiles", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
