@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -69,9 +70,15 @@ struct cubit_ctx {
     uint64_t tmp_cap = 0;
     int64_t* partials = nullptr;
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
+    std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
 namespace {
+
+// Every entry point that reads or changes a context's state (its stream, claim ticket, tile
+// directory, timing events, tables) holds the context's mutex, so DuckDB pipeline threads
+// may share one context; results named "last" belong to its most recent call.
+#define CUBIT_LOCK(c) std::lock_guard<std::recursive_mutex> cubit_lock_((c)->mu)
 
 int ensure_dir(cubit_ctx* ctx, uint64_t tiles) {
     if (tiles <= ctx->dir_tiles && ctx->dir) return CUBIT_OK;
@@ -212,18 +219,21 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
 
 int cubit_ctx_set_stream(cubit_ctx* ctx, void* stream) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    CUBIT_LOCK(ctx);
     ctx->stream = static_cast<hipStream_t>(stream);
     return CUBIT_OK;
 }
 
 int cubit_ctx_enable_timing(cubit_ctx* ctx, int on) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    CUBIT_LOCK(ctx);
     ctx->timing = on != 0;
     return CUBIT_OK;
 }
 
 int cubit_last_kernel_ms(cubit_ctx* ctx, float* ms) {
     if (!ctx || !ms) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     if (ctx->n_timed == 0) return fail(CUBIT_ERR_INVALID, "no timed kernel recorded (enable timing first)");
     const auto& e = ctx->evs[ctx->n_timed - 1];
     HIP_CHECK(hipEventSynchronize(e.second));
@@ -233,12 +243,14 @@ int cubit_last_kernel_ms(cubit_ctx* ctx, float* ms) {
 
 int cubit_ctx_timing_reset(cubit_ctx* ctx) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    CUBIT_LOCK(ctx);
     ctx->n_timed = 0;
     return CUBIT_OK;
 }
 
 int cubit_ctx_kernel_times(cubit_ctx* ctx, float* ms, uint32_t cap, uint32_t* n) {
     if (!ctx || !n) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     const uint32_t m = (uint32_t)std::min<size_t>(cap, ctx->n_timed);
     for (uint32_t i = 0; i < m; ++i) {
         HIP_CHECK(hipEventSynchronize(ctx->evs[i].second));
@@ -291,6 +303,7 @@ int cubit_ctx_check(cubit_ctx* ctx) {
 
 int cubit_ctx_last_tiles(cubit_ctx* ctx, const uint64_t** d_dir, uint32_t* n_tiles, uint64_t* rows_per_tile) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    CUBIT_LOCK(ctx);
     if (d_dir) *d_dir = ctx->dir;
     if (n_tiles) *n_tiles = ctx->last_tiles;
     if (rows_per_tile) *rows_per_tile = ctx->last_tile_rows;
@@ -306,6 +319,7 @@ int cubit_sync(cubit_ctx* ctx) {
 int cubit_build_bitvector(cubit_ctx* ctx, const void* d_col, int type, const uint64_t* d_validity, uint64_t n_rows,
                           int cmp, int64_t constant, uint64_t* d_words) {
     if (!ctx || !d_col || !d_words) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (cmp < 0 || cmp > 5) return fail(CUBIT_ERR_INVALID, "cmp %d", cmp);
     HIP_CHECK(launch_compare_bitvector(d_col, type, d_validity, n_rows, cmp, constant, d_words, ctx->stream));
@@ -591,6 +605,7 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
                                     int64_t row_base, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
                                     uint64_t* d_result_words, uint32_t flags) {
     if (!ctx || !d_leaves || !prog || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "n_rows is 0");
     const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
     if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
@@ -633,6 +648,7 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
 extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const int64_t* d_rowids,
                             const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* d_out) {
     if (!ctx || !d_col || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     HIP_CHECK(launch_gather(d_col, type, d_rowids, d_count, max_n, row_base, d_out, ctx->stream));
     return CUBIT_OK;
@@ -642,6 +658,7 @@ extern "C" int cubit_gather_sum_product(cubit_ctx* ctx, const int64_t* d_a, cons
                                         const int64_t* d_rowids, const uint64_t* d_count, uint64_t max_n,
                                         int64_t row_base, int64_t* d_out) {
     if (!ctx || !d_a || !d_b || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     HIP_CHECK(launch_gather_sum_product(d_a, d_b, d_rowids, d_count, max_n, row_base, ctx->partials, d_out,
                                         ctx->stream));
     return CUBIT_OK;
@@ -838,6 +855,7 @@ int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct
 
 extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_base, cubit_table** out) {
     if (!ctx || !out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
     if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "empty partition");
     if (int rc = set_device(ctx)) return rc;
     auto* t = new cubit_table();
@@ -857,6 +875,7 @@ extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_b
 
 extern "C" int cubit_table_destroy(cubit_table* t) {
     if (!t) return CUBIT_OK;
+    CUBIT_LOCK(t->ctx);
     (void)hipSetDevice(t->ctx->device);
     (void)hipStreamSynchronize(t->ctx->stream);
     delete t;
@@ -866,6 +885,7 @@ extern "C" int cubit_table_destroy(cubit_table* t) {
 extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const void* data, const uint64_t* validity,
                                       int on_device) {
     if (!t || !data) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (int rc = set_device(t->ctx)) return rc;
@@ -886,6 +906,7 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
                                                 const uint64_t* seg_rows, uint32_t n_segments,
                                                 const uint64_t* validity) {
     if (!t || !bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (int rc = set_device(t->ctx)) return rc;
@@ -972,6 +993,7 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
 
 extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, const int64_t* values, uint32_t n) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
     auto it = t->cols.find(col);
     if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
     if (encoding != CUBIT_INDEX_RANGE && encoding != CUBIT_INDEX_EQUALITY && encoding != CUBIT_INDEX_BINS)
@@ -1025,6 +1047,7 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
 
 extern "C" int cubit_table_index_info(cubit_table* t, int col, uint32_t* n_bitvectors, uint64_t* bytes) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
     uint32_t nb = 0;
     uint64_t by = 0;
     for (auto* m : {&t->idx, &t->bins}) {
@@ -1064,6 +1087,7 @@ static_assert(sizeof(IndexFileHeader) == 72, "stable on-disk header");
 
 extern "C" int cubit_table_save_index(cubit_table* t, int col, int encoding, const char* path) {
     if (!t || !path) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     const Index* ix = nullptr;
     if (encoding == CUBIT_INDEX_BINS) {
         auto it = t->bins.find(col);
@@ -1105,6 +1129,7 @@ extern "C" int cubit_table_save_index(cubit_table* t, int col, int encoding, con
 
 extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path) {
     if (!t || !path) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
     if (int rc = set_device(t->ctx)) return rc;
     FILE* f = std::fopen(path, "rb");
@@ -1153,6 +1178,7 @@ extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path)
 
 extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, const uint64_t* ids, uint64_t n) {
     if (!t || (n && (!rows || !ids))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (int rc = set_device(t->ctx)) return rc;
     for (uint64_t i = 0; i < n; ++i)
         if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "delete row out of range");
@@ -1175,6 +1201,7 @@ extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, cons
 extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
                                        const uint64_t* versions, uint64_t n) {
     if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
     if (int rc = set_device(t->ctx)) return rc;
     for (uint64_t i = 0; i < n; ++i)
@@ -1736,6 +1763,7 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
                                 const cubit_txn* txn, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
                                 uint32_t flags) {
     if (!t || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
     if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
     if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
@@ -1756,6 +1784,7 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
                                        const cubit_txn* txn, int col_a, int col_b, int64_t* d_out,
                                        uint64_t* d_count, uint32_t flags) {
     if (!t || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
     auto ait = t->cols.find(col_a), bit = t->cols.find(col_b);
     if (ait == t->cols.end() || bit == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column not registered");
@@ -1828,6 +1857,7 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
 
 extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_t* n_passes) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
     if (n_leaves) *n_leaves = t->last_leaves;
     if (n_passes) *n_passes = t->last_passes;
     return CUBIT_OK;
@@ -1835,6 +1865,7 @@ extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_
 
 extern "C" int cubit_table_last_sum_decode(cubit_table* t, uint32_t* n_values) {
     if (!t || !n_values) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     *n_values = t->last_decoded;
     return CUBIT_OK;
 }
@@ -1869,6 +1900,7 @@ __global__ void patch_probe_kernel(const int64_t* __restrict__ rowids, const uin
 extern "C" int cubit_table_probe(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_rowids,
                                  const uint64_t* d_count, uint64_t max_n, int64_t* d_out) {
     if (!t || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     auto it = t->cols.find(col);
     if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
     if (int rc = set_device(t->ctx)) return rc;
@@ -1897,6 +1929,7 @@ extern "C" int cubit_table_info(cubit_table* t, uint64_t* n_rows, int64_t* row_b
 
 extern "C" int cubit_table_column_data(cubit_table* t, int col, const void** data, int* type) {
     if (!t || !data) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
     auto it = t->cols.find(col);
     if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
     *data = it->second.data;

@@ -11,8 +11,11 @@
  *
  * Conventions: every call returns an int status (CUBIT_OK = 0), never
  * throws across the ABI, and records a message readable with cubit_last_error() (thread
- * local). Output buffers are caller-owned device buffers. One context per device; each
- * calling thread may give the context its own HIP stream (cubit_ctx_set_stream).
+ * local). Output buffers are caller-owned device buffers. A context owns one HIP stream
+ * (cubit_ctx_set_stream), a claim ticket and a tile directory; every call on a context or on
+ * its tables holds the context's mutex, so DuckDB's pipeline threads may share it (calls
+ * serialise; GPU work stays asynchronous on the stream). Results named "last" belong to the
+ * context's most recent call: threads that need their own give themselves a context each.
  * Row ids are int64 (DuckDB ROW_TYPE). Bitvectors are LSB-first 64-bit words, the layout
  * of DuckDB's ValidityMask (src/include/duckdb/common/types/validity_mask.hpp:22,164-168).
  */

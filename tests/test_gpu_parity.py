@@ -502,3 +502,41 @@ def test_index_save_and_load(ctx, tmp_path):
     junk.write_bytes(b"x" * 200)
     with pytest.raises(Exception, match="not a cubit index"):
         t2.load_index(0, junk)
+
+
+def test_concurrent_scans_share_a_context(ctx):
+    """DuckDB's pipeline threads call the scan concurrently (pipeline.cpp:113-125): scans from
+    four threads on one context and table, each with its own output buffers and predicate,
+    are each bit-exact (calls serialise on the context's mutex, the GPU work on its stream)."""
+    import threading
+
+    li = lineitem(0.01)
+    t = q6_table(ctx, li)
+    cols = [O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity)]
+    qty = [1200, 2400, 3600, 4800]
+    want = {}
+    for q in qty:
+        fs = F.TableFilterSet()
+        fs.push_filter(0, F.ConstantFilter(">=", F.date(1994, 1, 1)))
+        fs.push_filter(0, F.ConstantFilter("<", F.date(1995, 1, 1)))
+        fs.push_filter(2, F.ConstantFilter("<", q))
+        want[q] = (fs, O.table_scan(cols, F.serialize(fs), li.n_rows, row_base=li.row_base))
+    errors = []
+
+    def worker(q):
+        try:
+            fs, ref = want[q]
+            for _ in range(6):
+                got = t.scan(fs, ordered=bool(q % 2400 == 0))
+                if not np.array_equal(np.sort(got), ref):
+                    errors.append((q, len(got), len(ref)))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((q, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(q,)) for q in qty]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    t.close()
+    assert not errors, errors
