@@ -187,13 +187,24 @@ __device__ __forceinline__ void store_words(uint64_t* out, uint64_t tile_word0, 
     }
 }
 
+// tile_word0 is uniform: each leaf's tile base goes into a buffer descriptor built from
+// SGPRs (readfirstlane), and every load is `buffer_load_dwordx4 v, v_off32, s[rsrc] offen nt`
+// with one 32-bit per-thread offset shared by all leaves — no 64-bit VGPR address per leaf
+// and pair (MI355X guide T8). The descriptor covers exactly the tile's bytes.
 template <int K, int PAIRS, int THREADS>
 __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0, int t, u64x2 (&v)[K][PAIRS]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t tw = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tile_word0 >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tile_word0);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const u64x2* base = reinterpret_cast<const u64x2*>(a.prog.leaf[k] + tile_word0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.prog.leaf[k] + tw), (short)0, PAIRS * THREADS * 16, 0x00020000);
 #pragma unroll
-        for (int p = 0; p < PAIRS; ++p) v[k][p] = __builtin_nontemporal_load(base + p * THREADS + t);
+        for (int p = 0; p < PAIRS; ++p) {
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(p * THREADS + t) * 16u, 0, 2);
+            v[k][p] = __builtin_bit_cast(u64x2, x);
+        }
     }
 }
 
