@@ -734,6 +734,19 @@ struct cubit_table {
     std::vector<uint64_t> del_ids_sorted;
     std::unique_ptr<DevBuf> vis_cache;
     int64_t vis_prefix = -1;
+    // Insert versions: row ranges [begin, end) appended by one transaction with its insert
+    // id (ChunkConstantInfo::insert_id / ChunkVectorInfo::inserted, chunk_info.cpp); rows
+    // outside every range were inserted before any snapshot. Sorted by id: for a reader
+    // without inserts of its own the visible ranges are an id prefix, which also keys the
+    // cached visibility bitvector (vis_ins_prefix).
+    struct InsRange {
+        int64_t begin, end;
+        uint64_t id;
+    };
+    std::vector<InsRange> ins;
+    std::unique_ptr<DevBuf> hidden_dev;  // invisible ranges of the last visibility build
+    std::vector<int64_t> hidden_host;
+    int64_t vis_ins_prefix = -1;
     std::map<int, Updates> upd;
     // scratch bitvectors (reused across scans)
     std::vector<std::unique_ptr<DevBuf>> scratch;
@@ -1198,6 +1211,26 @@ extern "C" int cubit_table_set_deletes(cubit_table* t, const int64_t* rows, cons
     return CUBIT_OK;
 }
 
+extern "C" int cubit_table_set_inserts(cubit_table* t, const int64_t* row_begin, const int64_t* row_end,
+                                       const uint64_t* ids, uint64_t n) {
+    if (!t || (n && (!row_begin || !row_end || !ids))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    std::vector<cubit_table::InsRange> r(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (row_begin[i] < 0 || row_begin[i] >= row_end[i] || (uint64_t)row_end[i] > t->n_rows)
+            return fail(CUBIT_ERR_INVALID, "insert range %llu out of range", (unsigned long long)i);
+        r[i] = {row_begin[i], row_end[i], ids[i]};
+    }
+    std::sort(r.begin(), r.end(), [](const auto& a, const auto& b) { return a.begin < b.begin; });
+    for (uint64_t i = 1; i < n; ++i)
+        if (r[i].begin < r[i - 1].end) return fail(CUBIT_ERR_INVALID, "insert ranges overlap");
+    std::stable_sort(r.begin(), r.end(), [](const auto& a, const auto& b) { return a.id < b.id; });
+    t->ins = std::move(r);
+    t->vis_prefix = -1;
+    t->vis_ins_prefix = -1;
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
                                        const uint64_t* versions, uint64_t n) {
     if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
@@ -1658,11 +1691,23 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
         if (!t->upd.empty()) {
             if (int rc = patch_updates(t, e, txn, patched)) return rc;
         }
-        if (t->n_del) {
-            const auto& ids = t->del_ids_sorted;
-            const int64_t prefix = std::lower_bound(ids.begin(), ids.end(), txn->start_time) - ids.begin();
-            const bool own = std::binary_search(ids.begin(), ids.end(), txn->transaction_id) &&
+        // visibility leaf: insert ranges the reader may not see, then deletes in effect
+        // (ChunkVectorInfo::TemplatedGetSelVector, chunk_info.cpp:123-161)
+        const auto& ids = t->del_ids_sorted;
+        const int64_t prefix = std::lower_bound(ids.begin(), ids.end(), txn->start_time) - ids.begin();
+        const bool own_del = t->n_del && std::binary_search(ids.begin(), ids.end(), txn->transaction_id) &&
                              txn->transaction_id >= txn->start_time;
+        const int64_t ins_prefix =
+            std::lower_bound(t->ins.begin(), t->ins.end(), txn->start_time,
+                             [](const cubit_table::InsRange& a, uint64_t v) { return a.id < v; }) -
+            t->ins.begin();
+        bool own_ins = false, any_hidden = false;
+        for (int64_t i = ins_prefix; i < (int64_t)t->ins.size(); ++i) {
+            own_ins |= t->ins[i].id == txn->transaction_id;
+            any_hidden |= t->ins[i].id != txn->transaction_id;
+        }
+        if (prefix > 0 || own_del || any_hidden) {
+            const bool own = own_del || own_ins;
             uint64_t* vis = nullptr;
             if (!own) {
                 if (!t->vis_cache) {
@@ -1675,11 +1720,33 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
             } else if (int rc = scratch_bv(t, &vis)) {
                 return rc;
             }
-            if (own || prefix != t->vis_prefix) {
-                HIP_CHECK(launch_visibility(static_cast<const int64_t*>(t->del_rows->p),
-                                            static_cast<const uint64_t*>(t->del_ids->p), t->n_del, t->n_rows,
-                                            txn->start_time, txn->transaction_id, vis, ctx->stream));
-                if (!own) t->vis_prefix = prefix;
+            if (own || prefix != t->vis_prefix || ins_prefix != t->vis_ins_prefix) {
+                // hidden insert ranges: ids at or past start_time, except the reader's own
+                t->hidden_host.clear();
+                for (int64_t i = ins_prefix; i < (int64_t)t->ins.size(); ++i)
+                    if (t->ins[i].id != txn->transaction_id) {
+                        t->hidden_host.push_back(t->ins[i].begin);
+                        t->hidden_host.push_back(t->ins[i].end);
+                    }
+                const uint32_t n_hidden = (uint32_t)(t->hidden_host.size() / 2);
+                if (n_hidden) {
+                    t->hidden_dev = std::make_unique<DevBuf>();
+                    if (hipMalloc(&t->hidden_dev->p, t->hidden_host.size() * 8) != hipSuccess)
+                        return fail(CUBIT_ERR_OOM, "insert range allocation failed");
+                    HIP_CHECK(hipMemcpyAsync(t->hidden_dev->p, t->hidden_host.data(), t->hidden_host.size() * 8,
+                                             hipMemcpyHostToDevice, ctx->stream));
+                }
+                HIP_CHECK(launch_visibility(t->n_del ? static_cast<const int64_t*>(t->del_rows->p) : nullptr,
+                                            t->n_del ? static_cast<const uint64_t*>(t->del_ids->p) : nullptr,
+                                            t->n_del, t->n_rows, txn->start_time, txn->transaction_id, vis,
+                                            ctx->stream,
+                                            n_hidden ? static_cast<const int64_t*>(t->hidden_dev->p) : nullptr,
+                                            n_hidden));
+                if (n_hidden) HIP_CHECK(hipStreamSynchronize(ctx->stream));  // hidden_host / hidden_dev reuse
+                if (!own) {  // a reader with its own versions builds into scratch: the cache stays
+                    t->vis_prefix = prefix;
+                    t->vis_ins_prefix = ins_prefix;
+                }
             }
             Leaf l;
             l.bv = vis;

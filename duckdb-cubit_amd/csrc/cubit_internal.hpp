@@ -154,7 +154,8 @@ hipError_t launch_sum_product_arrays(const int64_t* x, const int64_t* y, const u
 // MVCC (K4)
 // visibility: words = valid-row mask, then clear rows whose delete is visible to txn
 hipError_t launch_visibility(const int64_t* del_rows, const uint64_t* del_ids, uint64_t n_del, uint64_t n_rows,
-                             uint64_t start_time, uint64_t transaction_id, uint64_t* words, hipStream_t stream);
+                             uint64_t start_time, uint64_t transaction_id, uint64_t* words, hipStream_t stream,
+                             const int64_t* hidden_ranges = nullptr, uint32_t n_hidden = 0);
 // mark rows with an update visible to txn into `mask` (atomicOr)
 hipError_t launch_update_mask(const int64_t* upd_rows, const uint64_t* upd_versions, uint64_t n_upd,
                               uint64_t start_time, uint64_t transaction_id, uint64_t* mask, hipStream_t stream);

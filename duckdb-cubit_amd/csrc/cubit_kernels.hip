@@ -1337,6 +1337,24 @@ __global__ __launch_bounds__(256) void visibility_kernel(const int64_t* __restri
     }
 }
 
+// Rows of insert ranges the reader may not see (UseInsertedVersion false for the range's
+// insert id, chunk_info.cpp:11-19, ChunkConstantInfo / ChunkVectorInfo::inserted): clear
+// [begin, end) of range blockIdx.y. Ranges are disjoint, so only a range's first and last
+// word can be shared with another range (atomicAnd); inner words are stored as 0.
+__global__ __launch_bounds__(256) void clear_ranges_kernel(const int64_t* __restrict__ ranges, uint64_t* __restrict__ words) {
+    const uint64_t b = (uint64_t)ranges[2 * blockIdx.y], e = (uint64_t)ranges[2 * blockIdx.y + 1];
+    if (b >= e) return;
+    const uint64_t w0 = b >> 6, w1 = (e - 1) >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w <= w1; w += stride) {
+        uint64_t clear = ~0ull;
+        if (w == w0) clear &= ~0ull << (b & 63);
+        if (w == w1 && (e & 63)) clear &= (1ull << (e & 63)) - 1;
+        if (w == w0 || w == w1) atomicAnd(reinterpret_cast<unsigned long long*>(&words[w]), ~clear);
+        else words[w] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void update_mask_kernel(const int64_t* __restrict__ rows,
                                                           const uint64_t* __restrict__ versions, uint64_t n,
                                                           uint64_t start_time, uint64_t tid,
@@ -1608,9 +1626,17 @@ hipError_t launch_fill_valid(uint64_t* words, uint64_t n_rows, hipStream_t strea
 }
 
 hipError_t launch_visibility(const int64_t* del_rows, const uint64_t* del_ids, uint64_t n_del, uint64_t n_rows,
-                             uint64_t start_time, uint64_t transaction_id, uint64_t* words, hipStream_t stream) {
+                             uint64_t start_time, uint64_t transaction_id, uint64_t* words, hipStream_t stream,
+                             const int64_t* hidden_ranges, uint32_t n_hidden) {
     hipError_t e = launch_fill_valid(words, n_rows, stream);
-    if (e != hipSuccess || n_del == 0) return e;
+    if (e != hipSuccess) return e;
+    for (uint32_t r0 = 0; r0 < n_hidden; r0 += 65535) {
+        const unsigned ny = (unsigned)std::min<uint32_t>(65535, n_hidden - r0);
+        hipLaunchKernelGGL(clear_ranges_kernel, dim3(64, ny), dim3(256), 0, stream, hidden_ranges + 2 * (uint64_t)r0,
+                           words);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (n_del == 0) return hipSuccess;
     hipLaunchKernelGGL(visibility_kernel, dim3(grid_for(n_del)), dim3(256), 0, stream, del_rows, del_ids, n_del,
                        start_time, transaction_id, words);
     return hipGetLastError();

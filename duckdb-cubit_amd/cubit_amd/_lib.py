@@ -106,6 +106,7 @@ GPU_SIGNATURES = {
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
     "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),
+    "cubit_table_set_inserts": (C.c_int, [_P, _P, _P, _P, _U64]),
     "cubit_table_save_index": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
     "cubit_table_load_index": (C.c_int, [_P, C.c_int, C.c_char_p]),
 }

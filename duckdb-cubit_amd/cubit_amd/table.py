@@ -220,6 +220,13 @@ class CubitTable:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         L.check(self.lib.cubit_table_set_deletes(self.handle, rows.ctypes.data, ids.ctypes.data, len(rows)))
 
+    def set_inserts(self, row_begin: np.ndarray, row_end: np.ndarray, ids: np.ndarray) -> None:
+        """Insert versions: disjoint row ranges [begin, end) with the inserting transaction's id."""
+        b = np.ascontiguousarray(row_begin, dtype=np.int64)
+        e = np.ascontiguousarray(row_end, dtype=np.int64)
+        i = np.ascontiguousarray(ids, dtype=np.uint64)
+        L.check(self.lib.cubit_table_set_inserts(self.handle, b.ctypes.data, e.ctypes.data, i.ctypes.data, len(b)))
+
     def set_updates(self, col: int, rows: np.ndarray, values: np.ndarray, versions: np.ndarray) -> None:
         rows = np.ascontiguousarray(rows, dtype=np.int64)
         values = np.ascontiguousarray(values, dtype=np.int64)

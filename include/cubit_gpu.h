@@ -211,6 +211,13 @@ int cubit_table_load_index(cubit_table *t, int col, const char *path);
 int cubit_table_set_deletes(cubit_table *t, const int64_t *rows, const uint64_t *ids, uint64_t n);
 int cubit_table_set_updates(cubit_table *t, int col, const int64_t *rows, const int64_t *values,
                             const uint64_t *versions, uint64_t n);
+/* Inserts: n disjoint row ranges [row_begin[i], row_end[i]) appended by one transaction each,
+ * with its insert id (ChunkConstantInfo::insert_id / ChunkVectorInfo::inserted,
+ * src/storage/table/chunk_info.cpp:36-53, 123-161); a reader sees a range when
+ * UseInsertedVersion(start_time, transaction_id, id) holds (chunk_info.cpp:11-19). Rows
+ * outside every range were inserted before any snapshot. Replaces the previous set. */
+int cubit_table_set_inserts(cubit_table *t, const int64_t *row_begin, const int64_t *row_end, const uint64_t *ids,
+                            uint64_t n);
 
 /* The scan: evaluate a predicate tree (prefix nodes) for transaction `txn` (NULL = see
  * every committed row, no MVCC delta applied) and write the qualifying row ids into
