@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/cubit_gpu.h"
@@ -711,6 +712,22 @@ struct Updates {
         if (distinct_versions.front() < txn->start_time) return true;
         return std::binary_search(distinct_versions.begin(), distinct_versions.end(), txn->transaction_id);
     }
+    // Patched leaves kept across scans. A leaf's content is fixed by its predicate on this
+    // column (index leaf or K0 bitvector alike), and for a reader without updates of its own
+    // the visible records are a version prefix, so (predicate, prefix) names the patched
+    // copy. Dropped whenever the column, its indexes or the update list change.
+    struct PatchKey {
+        int pred, cmp;
+        int64_t c, c2;
+        bool operator<(const PatchKey& o) const {
+            return std::tie(pred, cmp, c, c2) < std::tie(o.pred, o.cmp, o.c, o.c2);
+        }
+    };
+    struct Patched {
+        int64_t prefix = -1;
+        std::unique_ptr<DevBuf> bv;
+    };
+    std::map<PatchKey, Patched> cache;
 };
 
 }  // namespace
@@ -759,6 +776,12 @@ struct cubit_table {
 };
 
 namespace {
+
+// The column's values or indexes changed: its patched leaves are stale.
+void drop_patches(cubit_table* t, int col) {
+    auto it = t->upd.find(col);
+    if (it != t->upd.end()) it->second.cache.clear();
+}
 
 int scratch_bv(cubit_table* t, uint64_t** out) {
     if (t->scratch_used < t->scratch.size()) {
@@ -905,6 +928,7 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     Column c;
     if (int rc = copy_column(t, c, type, data, validity, on_device)) return rc;
     t->cols[col] = std::move(c);
+    drop_patches(t, col);
     t->idx.erase(col);
     t->bins.erase(col);
     return CUBIT_OK;
@@ -999,6 +1023,7 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
         HIP_CHECK(hipStreamSynchronize(s));
     }
     t->cols[col] = std::move(c);
+    drop_patches(t, col);
     t->idx.erase(col);
     t->bins.erase(col);
     return CUBIT_OK;
@@ -1053,6 +1078,7 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
         HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
     }
     HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    drop_patches(t, col);
     if (encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
     else t->idx[col] = std::move(ix);
     return CUBIT_OK;
@@ -1184,6 +1210,7 @@ extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path)
         ix.bytes += t->nwp * 8;
     }
     std::fclose(f);
+    drop_patches(t, col);
     if (ix.encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
     else t->idx[col] = std::move(ix);
     return CUBIT_OK;
@@ -1640,12 +1667,32 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
         if (uit == t->upd.end() || !uit->second.any_visible(txn)) return CUBIT_OK;
         auto pit = patched.find(e->leaf.bv);
         uint64_t* copy = nullptr;
+        Updates& u = uit->second;
+        const auto& dv = u.distinct_versions;
+        const bool own = txn->transaction_id >= txn->start_time &&
+                         std::binary_search(dv.begin(), dv.end(), txn->transaction_id);
+        const int64_t prefix = std::lower_bound(dv.begin(), dv.end(), txn->start_time) - dv.begin();
+        const Updates::PatchKey key{e->leaf.pred, e->leaf.cmp, e->leaf.constant, e->leaf.constant2};
+        Updates::Patched* slot = own ? nullptr : &u.cache[key];
         if (pit != patched.end()) {
             copy = pit->second;
+        } else if (slot && slot->bv && slot->prefix == prefix) {
+            copy = static_cast<uint64_t*>(slot->bv->p);  // patched by an earlier scan of this snapshot set
+            patched[e->leaf.bv] = copy;
         } else {
-            if (int rc = scratch_bv(t, &copy)) return rc;
+            if (slot) {
+                if (!slot->bv) {
+                    auto b = std::make_unique<DevBuf>();
+                    if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
+                        return fail(CUBIT_ERR_OOM, "patched leaf allocation failed");
+                    slot->bv = std::move(b);
+                }
+                copy = static_cast<uint64_t*>(slot->bv->p);
+                slot->prefix = prefix;
+            } else if (int rc = scratch_bv(t, &copy)) {
+                return rc;
+            }
             HIP_CHECK(hipMemcpyAsync(copy, e->leaf.bv, t->nwp * 8, hipMemcpyDeviceToDevice, t->ctx->stream));
-            const Updates& u = uit->second;
             const unsigned grid = (unsigned)std::min<uint64_t>((u.n + 255) / 256, 4096);
             hipLaunchKernelGGL(patch_leaf_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, t->ctx->stream,
                                static_cast<const int64_t*>(u.rows->p), static_cast<const int64_t*>(u.values->p),
@@ -1688,6 +1735,10 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     }
     if (txn) {
         std::map<const uint64_t*, uint64_t*> patched;
+        // bound the patched-leaf caches between scans (never during one: a slot freed
+        // mid-plan could be reallocated to another leaf of the same plan)
+        for (auto& kv : t->upd)
+            if (kv.second.cache.size() >= 16) kv.second.cache.clear();
         if (!t->upd.empty()) {
             if (int rc = patch_updates(t, e, txn, patched)) return rc;
         }

@@ -388,6 +388,46 @@ def test_insert_versions_and_deletes_across_snapshots(ctx):
     t.close()
 
 
+def test_patched_leaf_cache_across_snapshots(ctx):
+    """Committed updates at versions 5 / 20 / 40 plus an uncommitted writer's: patched leaves
+    are cached per (predicate, visible version prefix); snapshots that reuse, rebuild and
+    bypass the cache, an index rebuild and a new update list all match the oracle."""
+    n = 300_000
+    a = uniform_i32(21, n, 1000).astype(np.int64)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE)
+    rng = np.random.default_rng(8)
+    rows = rng.choice(n, size=20_000, replace=False).astype(np.int64)
+    writer = TXN_START + 3
+    vers = np.array([5, 20, 40, writer], dtype=np.uint64)[rng.integers(0, 4, len(rows))]
+    vals = rng.integers(0, 1000, len(rows)).astype(np.int64)
+    fss = [F.TableFilterSet({0: F.ConstantFilter("<", 300)}),
+           F.TableFilterSet({0: F.ConstantFilter("=", 17)}),
+           F.TableFilterSet({0: F.ConstantFilter(">=", 950)})]
+
+    def check(start, tid):
+        col = O.Column(a, updates=(rows, vals, vers))
+        for fs in fss:
+            got = t.scan(fs, txn=L.Txn(start, tid))
+            ref = O.table_scan([col], F.serialize(fs), n, tx=O.Mvcc(start, tid))
+            assert np.array_equal(got, ref), (start, tid)
+
+    t.set_updates(0, rows, vals, vers)
+    snaps = ((10, TXN_START + 1), (10, TXN_START + 2), (30, writer), (30, TXN_START + 4), (50, TXN_START + 5),
+             (10, TXN_START + 6), (3, TXN_START + 7))
+    for st, tid in snaps:
+        check(st, tid)
+    t.build_index(0, L.INDEX_RANGE, [17, 18, 300, 950])  # new leaves: cached patches dropped
+    for st, tid in snaps[:3]:
+        check(st, tid)
+    vals = (vals + 500) % 1000
+    t.set_updates(0, rows, vals, vers)  # new update list
+    for st, tid in snaps[:3]:
+        check(st, tid)
+    t.close()
+
+
 def test_q6_with_year_bins_reads_four_bitvectors(ctx, golden):
     """A binned index (year edges) beside the month range index: Q6's one-year shipdate range
     reads one bin instead of two range bitvectors (K 5 → 4); rows identical."""
