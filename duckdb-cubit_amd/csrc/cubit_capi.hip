@@ -607,7 +607,12 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
                                     uint64_t* d_result_words, uint32_t flags) {
     if (!ctx || !d_leaves || !prog || !d_count) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "n_rows is 0");
+    if (n_rows == 0) {  // no rows: nothing qualifies, nothing to launch
+        if (int rc = set_device(ctx)) return rc;
+        ctx->last_tiles = 0;
+        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+        return CUBIT_OK;
+    }
     const bool count_only = (flags & CUBIT_SCAN_COUNT_ONLY) != 0;
     if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
     // postfix → expression (validates arity), then the emitter re-linearises it
@@ -831,6 +836,11 @@ int copy_validity(cubit_table* t, Column& c, const uint64_t* validity, int on_de
 
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
     const uint64_t esz = type == CUBIT_TYPE_INT32 ? 4 : 8;
+    if (t->n_rows == 0) {  // empty partition: nothing to copy
+        c.type = type;
+        c.data = on_device ? data : nullptr;
+        return CUBIT_OK;
+    }
     hipStream_t s = t->ctx->stream;
     if (on_device) {
         c.data = data;
@@ -892,7 +902,8 @@ int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct
 extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_base, cubit_table** out) {
     if (!ctx || !out) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (n_rows == 0) return fail(CUBIT_ERR_INVALID, "empty partition");
+    // n_rows = 0 is an empty partition (an empty table, or a rank with no rows): every scan
+    // of it returns no rows without a launch
     if (int rc = set_device(ctx)) return rc;
     auto* t = new cubit_table();
     t->ctx = ctx;
@@ -942,10 +953,20 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
                                                 uint64_t n_bytes, const uint64_t* seg_offsets,
                                                 const uint64_t* seg_rows, uint32_t n_segments,
                                                 const uint64_t* validity) {
-    if (!t || !bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (!t) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(t->ctx);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (t->n_rows == 0 && n_segments == 0) {  // empty partition, no segments
+        Column c;
+        c.type = type;
+        t->cols[col] = std::move(c);
+        drop_patches(t, col);
+        t->idx.erase(col);
+        t->bins.erase(col);
+        return CUBIT_OK;
+    }
+    if (!bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
     if (int rc = set_device(t->ctx)) return rc;
     const uint64_t tsz = type == CUBIT_TYPE_INT32 ? 4 : 8;
     std::vector<BpGroup> groups;
@@ -1042,6 +1063,14 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     const Column& c = it->second;
     Index ix;
     ix.encoding = encoding;
+    if (t->n_rows == 0) {  // empty partition: an empty index (scans of it launch nothing)
+        ix.empty = true;
+        if (n) ix.keys.assign(values, values + n);
+        drop_patches(t, col);
+        if (encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
+        else t->idx[col] = std::move(ix);
+        return CUBIT_OK;
+    }
     std::vector<int64_t> distinct;
     bool any = false;
     if (int rc = column_stats(t, c, distinct, n == 0, ix.vmin, ix.vmax, any)) return rc;
@@ -1886,6 +1915,12 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
     if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
     if (int rc = set_device(t->ctx)) return rc;
+    if (t->n_rows == 0) {  // empty partition
+        t->ctx->last_tiles = 0;
+        t->last_leaves = t->last_passes = 0;
+        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
+        return CUBIT_OK;
+    }
     Emitter em;
     bool empty = false;
     if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
@@ -1911,6 +1946,11 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
     if (int rc = set_device(t->ctx)) return rc;
     cubit_ctx* ctx = t->ctx;
     uint64_t* count = d_count ? d_count : t->dummy_count;
+    if (t->n_rows == 0) {  // empty partition: sum 0 over 0 rows
+        HIP_CHECK(hipMemsetAsync(d_out, 0, 2 * sizeof(int64_t), ctx->stream));
+        HIP_CHECK(hipMemsetAsync(count, 0, sizeof(uint64_t), ctx->stream));
+        return CUBIT_OK;
+    }
     auto visible_updates = [&](int col) {
         auto u = t->upd.find(col);
         return txn && u != t->upd.end() && u->second.any_visible(txn);

@@ -428,6 +428,34 @@ def test_patched_leaf_cache_across_snapshots(ctx):
     t.close()
 
 
+def test_empty_partition(ctx):
+    """An empty table (or a rank whose row range is empty): columns, indexes, MVCC lists and
+    every scan form are accepted and return no rows / a zero sum without a launch."""
+    from cubit_amd.scan_function import CubitScanFunction
+
+    t = CubitTable(ctx, 0, row_base=100)
+    t.add_column(0, np.zeros(0, dtype=np.int32))
+    t.add_column(1, np.zeros(0, dtype=np.int64))
+    t.add_column(2, np.zeros(0, dtype=np.int64))
+    t.add_column(3, np.zeros(0, dtype=np.int64))
+    t.build_index(0, L.INDEX_RANGE, [F.date(1994, 1, 1), F.date(1995, 1, 1)])
+    t.build_index(1, L.INDEX_RANGE)
+    t.build_index(2, L.INDEX_EQUALITY)
+    t.set_deletes(np.zeros(0, np.int64), np.zeros(0, np.uint64))
+    for txn in (None, L.Txn(10, TXN_START + 1)):
+        assert len(t.scan(F.q6_filter_set(), txn=txn)) == 0
+        assert len(t.scan(F.q6_filter_set(), txn=txn, ordered=False)) == 0
+        assert t.count(F.q6_filter_set(), txn=txn) == 0
+        assert t.count(None, txn=txn) == 0
+        assert t.sum_product(3, 1, F.q6_filter_set(), txn=txn)[0] == 0
+    sf = CubitScanFunction(t, [0, 1, 3], filter_set=F.q6_filter_set())
+    loc = sf.init_local()
+    assert all(len(c) == 0 for c in sf.function(loc))  # the first chunk is empty: FINISHED
+    assert sf.progress() >= 0.0
+    sf.close()
+    t.close()
+
+
 def test_q6_with_year_bins_reads_four_bitvectors(ctx, golden):
     """A binned index (year edges) beside the month range index: Q6's one-year shipdate range
     reads one bin instead of two range bitvectors (K 5 → 4); rows identical."""
