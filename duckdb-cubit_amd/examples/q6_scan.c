@@ -1,0 +1,166 @@
+/*
+ * q6_scan — TPC-H Q6 through the C ABI alone (no Python, no PyTorch): what a C/C++ host such
+ * as a DuckDB extension does with libcubitgpu.so and libcubit_scan.so.
+ *
+ *   q6_scan <sf>      e.g. q6_scan 1
+ *
+ * 1. generates lineitem's Q6 columns with libcubit_datagen (the repo's dbgen restatement);
+ * 2. registers them on the GPU and builds the bitmap indexes (cubit_table_add_column /
+ *    cubit_table_build_index);
+ * 3. runs Q6's TableFilterSet three ways: cubit_table_scan (row ids in HBM), the fused
+ *    cubit_table_sum_product (revenue), and the seq_scan-shaped callbacks of cubit_scan.h
+ *    (init_global / init_local / function until an empty chunk);
+ * 4. prints one line: rows, rows from the table function, Σ row ids, revenue.
+ * tests/test_gpu_c_example.py checks that line against the reference's answer files.
+ */
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "cubit_gpu.h"
+#include "cubit_scan.h"
+
+/* libcubit_datagen.so */
+int64_t cubit_tpch_orders(double sf);
+int64_t cubit_tpch_lineitem_rows(double sf, int64_t order_begin, int64_t order_end, int nthreads);
+int64_t cubit_tpch_lineitem_gen(double sf, int64_t order_begin, int64_t order_end, int32_t *shipdate,
+                                int64_t *discount, int64_t *quantity, int64_t *extprice, int nthreads);
+
+#define CHECK(call)                                                                  \
+    do {                                                                             \
+        int rc_ = (call);                                                            \
+        if (rc_ != CUBIT_OK) {                                                       \
+            fprintf(stderr, "%s failed (%d): %s\n", #call, rc_, cubit_last_error()); \
+            exit(1);                                                                 \
+        }                                                                            \
+    } while (0)
+#define CHECK_SCAN(call)                                                                  \
+    do {                                                                                  \
+        int rc_ = (call);                                                                 \
+        if (rc_ != CUBIT_OK) {                                                            \
+            fprintf(stderr, "%s failed (%d): %s\n", #call, rc_, cubit_scan_last_error()); \
+            exit(1);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+/* days since 1970-01-01 of y-m-1 (DuckDB DATE) */
+static int32_t date_of(int y, int m) {
+    static const int cum[12] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334};
+    int32_t days = 0;
+    for (int yy = 1970; yy < y; ++yy) days += (yy % 4 == 0 && (yy % 100 != 0 || yy % 400 == 0)) ? 366 : 365;
+    days += cum[m - 1];
+    if (m > 2 && (y % 4 == 0 && (y % 100 != 0 || y % 400 == 0))) days += 1;
+    return days;
+}
+
+int main(int argc, char **argv) {
+    const double sf = argc > 1 ? atof(argv[1]) : 1.0;
+    const int64_t orders = cubit_tpch_orders(sf);
+    const int64_t n = cubit_tpch_lineitem_rows(sf, 0, orders, 0);
+    int32_t *shipdate = malloc(n * sizeof(int32_t));
+    int64_t *discount = malloc(n * sizeof(int64_t)), *quantity = malloc(n * sizeof(int64_t));
+    int64_t *extprice = malloc(n * sizeof(int64_t));
+    if (!shipdate || !discount || !quantity || !extprice) return 1;
+    if (cubit_tpch_lineitem_gen(sf, 0, orders, shipdate, discount, quantity, extprice, 0) != n) return 1;
+
+    cubit_ctx *ctx;
+    cubit_table *t;
+    CHECK(cubit_ctx_create(0, &ctx));
+    CHECK(cubit_table_create(ctx, (uint64_t)n, 0, &t));
+    CHECK(cubit_table_add_column(t, 0, CUBIT_TYPE_INT32, shipdate, NULL, 0));
+    CHECK(cubit_table_add_column(t, 1, CUBIT_TYPE_INT64, discount, NULL, 0));
+    CHECK(cubit_table_add_column(t, 2, CUBIT_TYPE_INT64, quantity, NULL, 0));
+    CHECK(cubit_table_add_column(t, 3, CUBIT_TYPE_INT64, extprice, NULL, 0));
+    int64_t edges[85];
+    int ne = 0;
+    for (int y = 1992; y <= 1998; ++y)
+        for (int m = 1; m <= 12; ++m) edges[ne++] = date_of(y, m);
+    edges[ne++] = date_of(1999, 1);
+    CHECK(cubit_table_build_index(t, 0, CUBIT_INDEX_RANGE, edges, (uint32_t)ne));
+    CHECK(cubit_table_build_index(t, 1, CUBIT_INDEX_RANGE, NULL, 0));
+    CHECK(cubit_table_build_index(t, 2, CUBIT_INDEX_RANGE, NULL, 0));
+
+    /* the TableFilterSet DuckDB pushes for Q6 (AND root over the per-column filters) */
+    const cubit_filter_node q6[] = {
+        {CUBIT_FILTER_AND, 0, 0, 3, 0},
+        {CUBIT_FILTER_AND, 0, 0, 3, 0},
+        {CUBIT_FILTER_CONSTANT, CUBIT_CMP_GE, 0, 0, date_of(1994, 1)},
+        {CUBIT_FILTER_CONSTANT, CUBIT_CMP_LT, 0, 0, date_of(1995, 1)},
+        {CUBIT_FILTER_IS_NOT_NULL, 0, 0, 0, 0},
+        {CUBIT_FILTER_AND, 0, 1, 3, 0},
+        {CUBIT_FILTER_CONSTANT, CUBIT_CMP_GE, 1, 0, 5},
+        {CUBIT_FILTER_CONSTANT, CUBIT_CMP_LE, 1, 0, 7},
+        {CUBIT_FILTER_IS_NOT_NULL, 0, 1, 0, 0},
+        {CUBIT_FILTER_AND, 0, 2, 2, 0},
+        {CUBIT_FILTER_CONSTANT, CUBIT_CMP_LT, 2, 0, 2400},
+        {CUBIT_FILTER_IS_NOT_NULL, 0, 2, 0, 0},
+    };
+    const uint32_t nn = sizeof(q6) / sizeof(q6[0]);
+
+    /* 1. row ids in HBM (ascending with CUBIT_SCAN_ORDERED) */
+    void *d_ids, *d_cnt, *d_sum;
+    CHECK(cubit_dev_alloc(ctx, (uint64_t)n * 8, &d_ids));
+    CHECK(cubit_dev_alloc(ctx, 16, &d_cnt));
+    CHECK(cubit_dev_alloc(ctx, 16, &d_sum));
+    CHECK(cubit_table_scan(t, q6, nn, NULL, d_ids, (uint64_t)n, d_cnt, CUBIT_SCAN_ORDERED));
+    CHECK(cubit_sync(ctx));
+    uint64_t q = 0;
+    CHECK(cubit_memcpy_d2h(ctx, &q, d_cnt, 8));
+    int64_t *ids = malloc((q ? q : 1) * sizeof(int64_t));
+    CHECK(cubit_memcpy_d2h(ctx, ids, d_ids, q * 8));
+    uint64_t sum_ids = 0;
+    for (uint64_t i = 0; i < q; ++i) {
+        if (i && ids[i] <= ids[i - 1]) {
+            fprintf(stderr, "row ids not ascending at %" PRIu64 "\n", i);
+            return 1;
+        }
+        sum_ids += (uint64_t)ids[i];
+    }
+
+    /* 2. fused sum(l_extendedprice * l_discount) */
+    CHECK(cubit_table_sum_product(t, q6, nn, NULL, 3, 1, d_sum, NULL, 0));
+    CHECK(cubit_sync(ctx));
+    int64_t s[2];
+    CHECK(cubit_memcpy_d2h(ctx, s, d_sum, 16));
+    const __int128 rev = ((__int128)s[1] << 64) | (unsigned __int128)(uint64_t)s[0];
+    const int64_t whole = (int64_t)(rev / 10000), frac = (int64_t)(rev % 10000);
+
+    /* 3. the seq_scan callbacks: project l_extendedprice and the row id, drain every chunk */
+    const uint64_t column_ids[] = {3, CUBIT_COLUMN_ROW_ID};
+    cubit_scan *scan;
+    cubit_scan_local *local;
+    CHECK_SCAN(cubit_scan_init_global(t, column_ids, 2, NULL, 0, q6, nn, NULL, &scan));
+    CHECK_SCAN(cubit_scan_init_local(scan, &local));
+    int64_t *cols[2] = {malloc(2048 * 8), malloc(2048 * 8)};
+    uint64_t rows_tf = 0, sum_tf = 0, got = 0;
+    do {
+        CHECK_SCAN(cubit_scan_function(scan, local, cols, &got));
+        for (uint64_t i = 0; i < got; ++i) {
+            if (cols[0][i] != extprice[cols[1][i]]) {
+                fprintf(stderr, "probe mismatch at row %" PRId64 "\n", cols[1][i]);
+                return 1;
+            }
+            sum_tf += (uint64_t)cols[1][i];
+        }
+        rows_tf += got;
+    } while (got);
+    CHECK_SCAN(cubit_scan_local_destroy(local));
+    CHECK_SCAN(cubit_scan_destroy(scan));
+
+    printf("rows %" PRIu64 " table_function_rows %" PRIu64 " sum_rowid %" PRIu64 " table_function_sum_rowid %" PRIu64
+           " revenue %" PRId64 ".%04" PRId64 "\n",
+           q, rows_tf, sum_ids, sum_tf, whole, frac);
+    CHECK(cubit_dev_free(ctx, d_ids));
+    CHECK(cubit_dev_free(ctx, d_cnt));
+    CHECK(cubit_dev_free(ctx, d_sum));
+    CHECK(cubit_table_destroy(t));
+    CHECK(cubit_ctx_destroy(ctx));
+    free(cols[0]);
+    free(cols[1]);
+    free(ids);
+    free(shipdate);
+    free(discount);
+    free(quantity);
+    free(extprice);
+    return 0;
+}

@@ -1,0 +1,36 @@
+"""The C ABI from a plain-C host (duckdb-cubit_amd/examples/q6_scan.c, built by
+__graft_entry__.build()): TPC-H SF1 Q6 through cubit_table_scan, the fused
+cubit_table_sum_product and the seq_scan-shaped callbacks of cubit_scan.h, with no Python or
+PyTorch in the process. Its output must equal the reference's SF1 fingerprint and answer."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+EXE = ROOT / "duckdb-cubit_amd" / "lib" / "q6_scan"
+
+
+@pytest.mark.gpu
+def test_q6_from_c(golden):
+    if not EXE.exists():
+        pytest.fail(f"{EXE} is missing: run __graft_entry__.build()")
+    out = subprocess.run([str(EXE), "1"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    f = out.stdout.split()
+    got = dict(zip(f[0::2], f[1::2]))
+    fp = golden["tpch"]["fingerprints"]["sf1_q6"]
+    assert int(got["rows"]) == fp["count"]
+    assert int(got["table_function_rows"]) == fp["count"]
+    assert int(got["sum_rowid"]) == fp["sum_rowid"]
+    assert int(got["table_function_sum_rowid"]) == fp["sum_rowid"]
+    assert got["revenue"] == golden["tpch"]["q6_revenue"]["1"]["revenue"]
+
+
+def test_c_example_links_against_the_abi():
+    """CPU: the example is built and its dynamic dependencies are the repo's own libraries."""
+    if not EXE.exists():
+        pytest.fail(f"{EXE} is missing: run __graft_entry__.build()")
+    out = subprocess.run(["ldd", str(EXE)], capture_output=True, text=True)
+    for lib in ("libcubitgpu.so", "libcubit_scan.so", "libcubit_datagen.so"):
+        assert lib in out.stdout, out.stdout
