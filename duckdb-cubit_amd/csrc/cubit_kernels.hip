@@ -907,9 +907,16 @@ __global__ __launch_bounds__(256) void order_copy_kernel(const uint64_t* __restr
 
 // ------------------------------------------------------------------ K0: compare → bitvector
 
+// K0: predicate → bitvector over a raw column, for M keys in one read of the column (M = 1:
+// a constant with no index key at query time; M = kMultiKeys: index build — range L(k),
+// equality E(k) or bins [k, k2)). A wave handles 64 consecutive words; 16 rows per lane are
+// loaded ahead, then every key's predicate is one ballot per word, kept by lane j for word j,
+// and each key's 64 words leave as one 512-byte store. Bytes per pass: n·w_c read + M·n/8
+// written, instead of M·(n·w_c + n/8). Comparison semantics are TemplatedFilterSelection's
+// (column_segment.cpp:261-349): NULL rows never qualify.
 // CMP 0..5 = EQ NE LT LE GT GE (CUBIT_CMP_*); 6 = c <= v < c2 (bin of a CUBIT_INDEX_BINS index)
-template <int CMP>
-__device__ __forceinline__ bool cmp_op(int64_t v, int64_t c, int64_t c2) {
+template <int CMP, typename CT>
+__device__ __forceinline__ bool cmp_v(CT v, CT c, CT c2) {
     if (CMP == 0) return v == c;
     if (CMP == 1) return v != c;
     if (CMP == 2) return v < c;
@@ -919,51 +926,21 @@ __device__ __forceinline__ bool cmp_op(int64_t v, int64_t c, int64_t c2) {
     return v >= c && v < c2;
 }
 
-// Each wave produces 64 consecutive words: for word j every lane tests one row and the
-// ballot is the word; lane j keeps it, then the wave stores 512 contiguous bytes.
-template <typename T, int CMP>
-__global__ __launch_bounds__(256) void compare_bitvector_kernel(const T* __restrict__ col,
-                                                                const uint64_t* __restrict__ validity,
-                                                                uint64_t n_rows, uint64_t n_words_padded,
-                                                                int64_t c, int64_t c2, uint64_t* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t w0 = wave_id * 64; w0 < n_words_padded; w0 += n_waves * 64) {
-        uint64_t mine = 0;
-        for (int j = 0; j < 64; ++j) {
-            const uint64_t row = (w0 + j) * 64 + lane;
-            bool p = false;
-            if (row < n_rows) {
-                const bool valid = validity ? ((validity[w0 + j] >> lane) & 1ull) : true;
-                p = valid && cmp_op<CMP>((int64_t)col[row], c, c2);
-            }
-            const uint64_t b = __ballot(p);
-            if (lane == j) mine = b;
-        }
-        out[w0 + lane] = mine;
-    }
-}
-
-// Index build (K0, several keys per pass): one read of the column produces up to
-// kMultiKeys bitvectors (range L(k), equality E(k) or bins [k, k2)). A wave handles 64
-// consecutive words; 16 rows per lane are loaded ahead, then every key's predicate is one
-// ballot per word, kept by lane j for word j, and each key's 64 words leave as one 512-byte
-// store. Bytes per pass: n·w_c read + m·n/8 written, instead of m·(n·w_c + n/8).
-template <typename T, typename CT, int CMP>
+template <typename T, typename CT, int CMP, int M>
 __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __restrict__ col,
                                                                  const uint64_t* __restrict__ validity,
                                                                  uint64_t n_rows, uint64_t n_words_padded,
                                                                  MultiKeyArgs a) {
     // CT: compare type (int32 when the column and every key fit 32 bits: one VALU compare)
+    static_assert(M >= 1 && M <= kMultiKeys, "keys per pass");
     constexpr int JB = 16;
     const int lane = threadIdx.x & 63;
     const uint64_t wave_id = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t w0 = wave_id * 64; w0 < n_words_padded; w0 += n_waves * 64) {
-        uint32_t lo[kMultiKeys], hi[kMultiKeys];  // lane j keeps word j of every key
+        uint32_t lo[M], hi[M];  // lane j keeps word j of every key
 #pragma unroll
-        for (int k = 0; k < kMultiKeys; ++k) lo[k] = hi[k] = 0;
+        for (int k = 0; k < M; ++k) lo[k] = hi[k] = 0;
         for (int jb = 0; jb < 64; jb += JB) {
             CT v[JB];
             bool ok[JB];
@@ -981,19 +958,15 @@ __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __rest
                 // compare and two moves
                 // (keys past a.m repeat the last key: the host pads them, their words are not stored)
                 const uint64_t okm = __ballot(ok[j]);
-                uint64_t b[kMultiKeys];
+                uint64_t b[M];
 #pragma unroll
-                for (int k = 0; k < kMultiKeys; ++k) {
+                for (int k = 0; k < M; ++k) {
                     const CT c = (CT)a.c[k], c2 = (CT)a.c2[k];
-                    bool p;
-                    if (CMP == 0) p = v[j] == c;
-                    else if (CMP == 2) p = v[j] < c;
-                    else p = v[j] >= c && v[j] < c2;
-                    b[k] = __ballot(p) & okm;
+                    b[k] = __ballot(cmp_v<CMP, CT>(v[j], c, c2)) & okm;
                 }
                 if (lane == jb + j) {
 #pragma unroll
-                    for (int k = 0; k < kMultiKeys; ++k) {
+                    for (int k = 0; k < M; ++k) {
                         lo[k] = (uint32_t)b[k];
                         hi[k] = (uint32_t)(b[k] >> 32);
                     }
@@ -1001,50 +974,65 @@ __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __rest
             }
         }
 #pragma unroll
-        for (int k = 0; k < kMultiKeys; ++k)
+        for (int k = 0; k < M; ++k)
             if (k < (int)a.m) a.out[k][w0 + lane] = ((uint64_t)hi[k] << 32) | lo[k];
     }
 }
 
-template <typename T, typename CT>
+template <typename T, typename CT, int M>
 hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp,
                                   const MultiKeyArgs& a, hipStream_t stream) {
     const uint64_t nw = padded_words(n_rows);
     const uint64_t waves = nw / 64;
     const uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
     const dim3 grid((unsigned)std::max<uint64_t>(blocks, 1)), block(256);
-    switch (cmp) {
-    case 0: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 0>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
-    case 2: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 2>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
-    case 6: hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, 6>), grid, block, 0, stream, col, validity, n_rows, nw, a); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template <typename T>
-hipError_t launch_compare_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp, int64_t c, int64_t c2,
-                            uint64_t* out, hipStream_t stream) {
-    const uint64_t nw = padded_words(n_rows);
-    const uint64_t waves = nw / 64;
-    const uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 8192);
-    const dim3 grid((unsigned)std::max<uint64_t>(blocks, 1)), block(256);
 #define CUBIT_CMP_CASE(C)                                                                                       \
     case C:                                                                                                     \
-        hipLaunchKernelGGL((compare_bitvector_kernel<T, C>), grid, block, 0, stream, col, validity, n_rows, nw, c, c2, out); \
+        hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, C, M>), grid, block, 0, stream, col, validity, n_rows, nw, a); \
         break;
-    switch (cmp) {
-        CUBIT_CMP_CASE(0)
-        CUBIT_CMP_CASE(1)
-        CUBIT_CMP_CASE(2)
-        CUBIT_CMP_CASE(3)
-        CUBIT_CMP_CASE(4)
-        CUBIT_CMP_CASE(5)
-        CUBIT_CMP_CASE(6)
-    default: return hipErrorInvalidValue;
+    if constexpr (M == 1) {  // a query-time constant: every comparison
+        switch (cmp) {
+            CUBIT_CMP_CASE(0)
+            CUBIT_CMP_CASE(1)
+            CUBIT_CMP_CASE(2)
+            CUBIT_CMP_CASE(3)
+            CUBIT_CMP_CASE(4)
+            CUBIT_CMP_CASE(5)
+            CUBIT_CMP_CASE(6)
+        default: return hipErrorInvalidValue;
+        }
+    } else {  // index build: L(k) = v < k, E(k) = v == k, bins k <= v < k2
+        switch (cmp) {
+            CUBIT_CMP_CASE(0)
+            CUBIT_CMP_CASE(2)
+            CUBIT_CMP_CASE(6)
+        default: return hipErrorInvalidValue;
+        }
     }
 #undef CUBIT_CMP_CASE
     return hipGetLastError();
+}
+
+// every key (and bin end) an int32: an int32 column compares in 32 bits
+bool keys_fit32(const MultiKeyArgs& a, int cmp) {
+    for (uint32_t k = 0; k < a.m; ++k)
+        if (a.c[k] < INT32_MIN || a.c[k] > INT32_MAX ||
+            (cmp == kCmpBetween && (a.c2[k] < INT32_MIN || a.c2[k] > INT32_MAX)))
+            return false;
+    return true;
+}
+
+template <int M>
+hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
+                            const MultiKeyArgs& a, hipStream_t stream) {
+    if (type == 0 && keys_fit32(a, cmp))
+        return launch_compare_multi_t<int32_t, int32_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
+                                                           stream);
+    if (type == 0)
+        return launch_compare_multi_t<int32_t, int64_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
+                                                           stream);
+    return launch_compare_multi_t<int64_t, int64_t, M>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
+                                                       stream);
 }
 
 // ------------------------------------------------------------------ index build: column stats
@@ -1478,11 +1466,12 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
 
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                                     int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2) {
-    if (type == 0)
-        return launch_compare_t<int32_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, constant, constant2,
-                                         out_words, stream);
-    return launch_compare_t<int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, constant, constant2,
-                                     out_words, stream);
+    MultiKeyArgs a{};
+    a.m = 1;
+    a.c[0] = constant;
+    a.c2[0] = constant2;
+    a.out[0] = out_words;
+    return launch_compare_m<1>(col, type, validity, n_rows, cmp, a, stream);
 }
 
 hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
@@ -1495,15 +1484,11 @@ hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* 
         a.c2[k] = a.c2[a.m - 1];
         a.out[k] = nullptr;
     }
-    bool keys32 = true;  // every key (and bin end) an int32: compare an int32 column in 32 bits
-    for (uint32_t k = 0; k < a.m; ++k)
-        keys32 = keys32 && a.c[k] >= INT32_MIN && a.c[k] <= INT32_MAX &&
-                 (cmp != kCmpBetween || (a.c2[k] >= INT32_MIN && a.c2[k] <= INT32_MAX));
-    if (type == 0 && keys32)
-        return launch_compare_multi_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a, stream);
-    if (type == 0)
-        return launch_compare_multi_t<int32_t, int64_t>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a, stream);
-    return launch_compare_multi_t<int64_t, int64_t>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a, stream);
+    // the smallest key count that covers m: the ballots per word grow with it
+    if (a.m == 1) return launch_compare_m<1>(col, type, validity, n_rows, cmp, a, stream);
+    if (a.m <= 4) return launch_compare_m<4>(col, type, validity, n_rows, cmp, a, stream);
+    if (a.m <= 8) return launch_compare_m<8>(col, type, validity, n_rows, cmp, a, stream);
+    return launch_compare_m<kMultiKeys>(col, type, validity, n_rows, cmp, a, stream);
 }
 
 hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,
