@@ -134,6 +134,8 @@ enum class RunMode { kDecode, kCount };
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
              uint64_t capacity, uint64_t* d_count, uint64_t* result_words, RunMode mode, bool timed = false,
              bool ordered = false) {
+    // the claim ticket carries row sums in 48 bits (finish_ticket)
+    if (n_rows >= (1ull << 47)) return fail(CUBIT_ERR_INVALID, "%llu rows exceed 2^47", (unsigned long long)n_rows);
     EvalArgs a{};
     a.prog = prog;
     a.n_rows = n_rows;
@@ -158,8 +160,12 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.num_tiles = (uint32_t)tiles;
     a.rowids = ordered && rowids ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
-    // persistent grid: two 512-thread workgroups per CU (VGPR-limited to 4 waves per SIMD)
-    const unsigned grid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)ctx->n_cus * 2);
+    // persistent grid: two 512-thread workgroups per CU (VGPR-limited to 4 waves per SIMD).
+    // Between one and two tiles per workgroup, every workgroup takes a whole pair instead
+    // (grid = tiles / 2): the same critical path (one pair), a third fewer claims queued on
+    // the ticket word at once (768 tiles: 384 instead of 512, ≈11 ns each).
+    const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
+    const unsigned grid = (unsigned)(tiles <= max_grid ? tiles : tiles <= 2 * max_grid ? (tiles + 1) / 2 : max_grid);
     HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop));
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
@@ -904,6 +910,7 @@ extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_b
     CUBIT_LOCK(ctx);
     // n_rows = 0 is an empty partition (an empty table, or a rank with no rows): every scan
     // of it returns no rows without a launch
+    if (n_rows >= (1ull << 47)) return fail(CUBIT_ERR_INVALID, "%llu rows exceed 2^47", (unsigned long long)n_rows);
     if (int rc = set_device(ctx)) return rc;
     auto* t = new cubit_table();
     t->ctx = ctx;
