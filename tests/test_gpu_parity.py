@@ -654,3 +654,32 @@ def test_concurrent_scans_share_a_context(ctx):
         x.join()
     t.close()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("n", [80_000_017, 140_000_003])
+def test_mid_size_grids_scan_count_sum(ctx, n):
+    """Partitions of 611 and 1,069 tiles: the decode grid takes one pair per workgroup
+    (tiles / 2) below 2 tiles per workgroup and the full persistent grid above; the claim
+    ticket's arrivals carry every workgroup's rows across all eight arrival groups. Scan
+    (tile runs and ordered), count(*) and the fused sum against numpy on the same rows."""
+    v = uniform_i32(7, n, 1_000_000)
+    rng = np.random.default_rng(n)
+    a = rng.integers(-1_000_000, 1_000_000, n).astype(np.int64)
+    b = rng.integers(0, 100, n).astype(np.int64)
+    t = CubitTable(ctx, n, row_base=5)
+    t.add_column(0, v)
+    t.add_column(1, a)
+    t.add_column(2, b)
+    t.build_index(0, L.INDEX_RANGE, [20_000])
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 20_000)})
+    want = np.nonzero(v < 20_000)[0]
+    got = t.scan(fs, ordered=False)
+    directory, _ = ctx.last_tiles()
+    assert int(directory[:, 1].sum()) == len(want)
+    assert np.array_equal(runs_in_row_order(got, directory), want + 5)
+    assert np.array_equal(t.scan(fs), want + 5)
+    assert t.count(fs) == len(want)
+    rev, cnt = t.sum_product(1, 2, fs, gather_b=True)
+    assert cnt == len(want)
+    assert rev == int((a[want].astype(object) * b[want].astype(object)).sum())
+    t.close()
