@@ -1398,6 +1398,39 @@ struct Planner {
         return nullptr;
     }
 
+    // {v < c} (cmp LT) or {v == c} (cmp EQ) for a constant that is not a key of the range
+    // index: the constant lies in one bin [k_lo, k_hi) between neighbouring keys, and only that
+    // bin's rows are checked on the raw column (launch_candidate_check). This is the binned
+    // bitmap index's candidate check: reads L(k_lo), L(k_hi) and the column at the bin's rows
+    // instead of K0's whole column. nullptr when the bin is estimated (uniform values over
+    // [vmin, vmax]) to hold more than a quarter of the rows, where K0's sequential read of the
+    // column is cheaper; rc is set on a launch or allocation failure.
+    ExprP candidate(int col, const Index& ix, int cmp, int64_t c) {
+        auto hi_it = std::upper_bound(ix.keys.begin(), ix.keys.end(), c);  // first key > c
+        const bool has_lo = hi_it != ix.keys.begin(), has_hi = hi_it != ix.keys.end();
+        const double lo_v = has_lo ? (double)*(hi_it - 1) : (double)ix.vmin;
+        const double hi_v = has_hi ? (double)*hi_it : (double)ix.vmax + 1.0;
+        const double span = (double)ix.vmax - (double)ix.vmin + 1.0;
+        if ((std::min(hi_v, (double)ix.vmax + 1.0) - std::max(lo_v, (double)ix.vmin)) > 0.25 * span) return nullptr;
+        const Column& cl = t->cols.at(col);
+        uint64_t* bv = nullptr;
+        if ((rc = scratch_bv(t, &bv))) return nullptr;
+        const uint64_t* lo_bv = has_lo ? ix.bvs[hi_it - 1 - ix.keys.begin()] : nullptr;
+        const uint64_t* hi_bv = has_hi ? ix.bvs[hi_it - ix.keys.begin()] : nullptr;
+        hipError_t e = launch_candidate_check(cl.data, cl.type, cl.validity, lo_bv, hi_bv, t->n_rows, cmp, c, bv,
+                                              t->ctx->stream);
+        if (e != hipSuccess) {
+            rc = fail(CUBIT_ERR_HIP, "candidate check kernel: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+        Leaf l;
+        l.bv = bv;
+        l.column = col;
+        l.cmp = cmp;
+        l.constant = c;
+        return mk_leaf(l);
+    }
+
     ExprP eq_leaf(int col, const Index& ix, int64_t c, bool& exact) {
         exact = true;
         auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
@@ -1420,20 +1453,40 @@ struct Planner {
             const Index& ix = ixit->second;
             const bool top = c == INT64_MAX;
             if (ix.encoding == CUBIT_INDEX_RANGE) {
-                ExprP lt_c = range_lt(col, ix, c);
-                ExprP lt_c1 = top ? nn(col) : range_lt(col, ix, c + 1);
+                // {v < k}: an index leaf when k is a key, else the candidate check of k's bin
+                auto lt = [&](int64_t k) -> ExprP {
+                    ExprP e = range_lt(col, ix, k);
+                    return e ? e : candidate(col, ix, CUBIT_CMP_LT, k);
+                };
                 ExprP r;
                 switch (cmp) {
-                case CUBIT_CMP_LT: r = lt_c; break;
-                case CUBIT_CMP_LE: r = lt_c1; break;
-                case CUBIT_CMP_GT: r = lt_c1 ? mk_bin(Expr::ANDNOT, nn(col), lt_c1) : nullptr; break;
-                case CUBIT_CMP_GE: r = lt_c ? mk_bin(Expr::ANDNOT, nn(col), lt_c) : nullptr; break;
-                case CUBIT_CMP_EQ: r = (lt_c && lt_c1) ? mk_bin(Expr::ANDNOT, lt_c1, lt_c) : nullptr; break;
-                case CUBIT_CMP_NE:
-                    r = (lt_c && lt_c1) ? mk_bin(Expr::OR, mk_bin(Expr::ANDNOT, nn(col), lt_c1), lt_c) : nullptr;
+                case CUBIT_CMP_LT: r = lt(c); break;
+                case CUBIT_CMP_LE: r = top ? nn(col) : lt(c + 1); break;
+                case CUBIT_CMP_GT: {
+                    ExprP e = top ? nn(col) : lt(c + 1);
+                    r = e ? mk_bin(Expr::ANDNOT, nn(col), e) : nullptr;
                     break;
+                }
+                case CUBIT_CMP_GE: {
+                    ExprP e = lt(c);
+                    r = e ? mk_bin(Expr::ANDNOT, nn(col), e) : nullptr;
+                    break;
+                }
+                case CUBIT_CMP_EQ:
+                case CUBIT_CMP_NE: {
+                    ExprP lt_c = range_lt(col, ix, c);
+                    ExprP lt_c1 = top ? nn(col) : range_lt(col, ix, c + 1);
+                    if (lt_c && lt_c1) {
+                        r = cmp == CUBIT_CMP_EQ ? mk_bin(Expr::ANDNOT, lt_c1, lt_c)
+                                                : mk_bin(Expr::OR, mk_bin(Expr::ANDNOT, nn(col), lt_c1), lt_c);
+                    } else if (ExprP eq = candidate(col, ix, CUBIT_CMP_EQ, c)) {
+                        r = cmp == CUBIT_CMP_EQ ? eq : mk_bin(Expr::ANDNOT, nn(col), eq);
+                    }
+                    break;
+                }
                 default: break;
                 }
+                if (rc) return nullptr;
                 if (r) return r;
             } else {
                 bool exact = true;

@@ -90,6 +90,12 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
 constexpr int kCmpBetween = 6;
 hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                                     int64_t constant, uint64_t* out_words, hipStream_t stream, int64_t constant2 = 0);
+// candidate check of a constant inside one bin [k_lo, k_hi) of a range index: cand =
+// hi_bv \ lo_bv (lo_bv null = ∅, hi_bv null = every valid row); out = (cmp LT: lo_bv ∪)
+// {r ∈ cand : v[r] cmp constant}; cmp ∈ {CUBIT_CMP_EQ, CUBIT_CMP_LT}
+hipError_t launch_candidate_check(const void* col, int type, const uint64_t* validity, const uint64_t* lo_bv,
+                                  const uint64_t* hi_bv, uint64_t n_rows, int cmp, int64_t constant,
+                                  uint64_t* out_words, hipStream_t stream);
 // K0 over several keys in one pass of the column (index build): out[k] = cmp(v, c[k], c2[k]),
 // cmp ∈ {EQ, LT, between}
 constexpr int kMultiKeys = 16;

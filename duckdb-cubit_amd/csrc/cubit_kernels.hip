@@ -1024,6 +1024,82 @@ hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64
     return hipGetLastError();
 }
 
+// Candidate check (binned range index): a query-time constant c that is not an index key
+// falls in one bin [k_lo, k_hi) of the range index. Its rows are cand = L(k_hi) \ L(k_lo)
+// (L(k) = valid rows with v < k; no k_lo → ∅, no k_hi → every valid row), and only they
+// need the raw value:
+//   v <  c  =  L(k_lo) ∪ {r ∈ cand : v[r] < c}
+//   v == c  =           {r ∈ cand : v[r] == c}
+// Per word: two bitvector words read, the column read at the candidate rows only, one word
+// written — instead of K0's read of the whole column. Each thread owns two consecutive
+// words (16-byte loads and stores), so a wave's bitvector traffic is 1 KiB per instruction;
+// the candidate values are gathered per set bit (line-granular reads of the column where a
+// line holds a candidate). Comparison semantics are TemplatedFilterSelection's
+// (column_segment.cpp:261-349); NULL rows are never candidates.
+template <typename T, typename CT, int CMP>
+__global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restrict__ col,
+                                                              const uint64_t* __restrict__ validity,
+                                                              const uint64_t* __restrict__ lo_bv,
+                                                              const uint64_t* __restrict__ hi_bv, uint64_t n_rows,
+                                                              uint64_t n_words_padded, CT c,
+                                                              uint64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n_words = (n_rows + 63) / 64;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * p < n_words_padded; p += stride) {
+        const uint64_t w0 = 2 * p;
+        u64x2 lo = {0ull, 0ull}, hi;
+        if (lo_bv) lo = reinterpret_cast<const u64x2*>(lo_bv)[p];
+        if (hi_bv) {
+            hi = reinterpret_cast<const u64x2*>(hi_bv)[p];
+        } else {
+            // every valid row of the partition: full words, the tail word's rows, nothing past it
+            hi.x = w0 < n_words ? ~0ull : 0ull;
+            hi.y = w0 + 1 < n_words ? ~0ull : 0ull;
+            if (w0 + 1 == n_words && (n_rows & 63)) hi.x = (1ull << (n_rows & 63)) - 1;
+            if (w0 + 2 == n_words && (n_rows & 63)) hi.y = (1ull << (n_rows & 63)) - 1;
+            if (validity) {
+                const u64x2 vw = reinterpret_cast<const u64x2*>(validity)[p];
+                hi.x &= vw.x;
+                hi.y &= vw.y;
+            }
+        }
+        u64x2 res;
+        res.x = CMP == 2 ? lo.x : 0ull;
+        res.y = CMP == 2 ? lo.y : 0ull;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            uint64_t cand = e ? (hi.y & ~lo.y) : (hi.x & ~lo.x);
+            uint64_t hit = 0;
+            const T* base = col + (w0 + e) * 64;
+            while (cand) {
+                const int b = __builtin_ctzll(cand);
+                const CT v = (CT)base[b];
+                if (CMP == 2 ? v < c : v == c) hit |= 1ull << b;
+                cand &= cand - 1;
+            }
+            if (e) res.y |= hit;
+            else res.x |= hit;
+        }
+        reinterpret_cast<u64x2*>(out)[p] = res;
+    }
+}
+
+template <typename T, typename CT>
+hipError_t launch_candidate_t(const T* col, const uint64_t* validity, const uint64_t* lo_bv, const uint64_t* hi_bv,
+                              uint64_t n_rows, int cmp, CT c, uint64_t* out, hipStream_t stream) {
+    const uint64_t nw = padded_words(n_rows);
+    const dim3 grid((unsigned)std::min<uint64_t>((nw / 2 + 255) / 256, 8192)), block(256);
+    if (cmp == 2)
+        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 2>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
+                           n_rows, nw, c, out);
+    else if (cmp == 0)
+        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 0>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
+                           n_rows, nw, c, out);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // every key (and bin end) an int32: an int32 column compares in 32 bits
 bool keys_fit32(const MultiKeyArgs& a, int cmp) {
     for (uint32_t k = 0; k < a.m; ++k)
@@ -1483,6 +1559,19 @@ hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* v
     a.c2[0] = constant2;
     a.out[0] = out_words;
     return launch_compare_m<1>(col, type, validity, n_rows, cmp, a, stream);
+}
+
+hipError_t launch_candidate_check(const void* col, int type, const uint64_t* validity, const uint64_t* lo_bv,
+                                  const uint64_t* hi_bv, uint64_t n_rows, int cmp, int64_t constant,
+                                  uint64_t* out_words, hipStream_t stream) {
+    if (type == 0 && constant >= INT32_MIN && constant <= INT32_MAX)
+        return launch_candidate_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
+                                                    cmp, (int32_t)constant, out_words, stream);
+    if (type == 0)
+        return launch_candidate_t<int32_t, int64_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
+                                                    cmp, constant, out_words, stream);
+    return launch_candidate_t<int64_t, int64_t>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows, cmp,
+                                                constant, out_words, stream);
 }
 
 hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,

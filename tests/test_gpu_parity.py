@@ -683,3 +683,46 @@ def test_mid_size_grids_scan_count_sum(ctx, n):
     assert cnt == len(want)
     assert rev == int((a[want].astype(object) * b[want].astype(object)).sum())
     t.close()
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64])
+def test_candidate_check_off_key_constants(ctx, dtype):
+    """Constants that are not keys of an edge-keyed range index: each comparison reads the
+    constant's bin [k_lo, k_hi) on the raw column (candidate check), including the open bins
+    below the first and above the last key, NULL rows, EQ / NE off the keys, and a bin too
+    wide for the check (K0 instead). Every result equals the oracle's, also with updates
+    visible to the reader (the candidate leaf is patched like any value leaf)."""
+    n = 300_001
+    rng = np.random.default_rng(77)
+    a = rng.integers(-50, 1000, n).astype(dtype)
+    valid = rng.random(n) > 0.1
+    t = CubitTable(ctx, n, row_base=3)
+    t.add_column(0, a, validity_from_mask(valid))
+    t.build_index(0, L.INDEX_RANGE, list(range(100, 1000, 100)))
+    t2 = CubitTable(ctx, n, row_base=3)  # one key: the bin above it spans ~90 % of the values → K0
+    t2.add_column(0, a, validity_from_mask(valid))
+    t2.build_index(0, L.INDEX_RANGE, [50])
+    col = O.Column(a, validity_from_mask(valid))
+    consts = [-51, -50, -7, 0, 99, 100, 101, 150, 199, 555, 900, 901, 999, 1000, 1200]
+    for c in consts:
+        for cmp in ("<", "<=", ">", ">=", "=", "!="):
+            fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
+            ref = O.table_scan([col], F.serialize(fs), n, row_base=3)
+            assert np.array_equal(t.scan(fs), ref), (c, cmp)
+            assert np.array_equal(t2.scan(fs), ref), (c, cmp, "wide bin")
+    # Q6-shaped interval off the keys, and updates visible to the reader
+    fs = F.TableFilterSet()
+    fs.push_filter(0, F.ConstantFilter(">=", 123))
+    fs.push_filter(0, F.ConstantFilter("<", 456))
+    assert np.array_equal(t.scan(fs), O.table_scan([col], F.serialize(fs), n, row_base=3))
+    rows = rng.choice(n, size=5_000, replace=False).astype(np.int64)
+    vals = rng.integers(-50, 1000, len(rows)).astype(np.int64)
+    vers = np.full(len(rows), 5, dtype=np.uint64)
+    t.set_updates(0, rows, vals, vers)
+    ucol = O.Column(a, validity_from_mask(valid), updates=(rows, vals, vers))
+    for c, cmp in ((150, "<"), (555, ">="), (901, "=")):
+        fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
+        ref = O.table_scan([ucol], F.serialize(fs), n, row_base=3, tx=O.Mvcc(10, TXN_START + 1))
+        assert np.array_equal(t.scan(fs, txn=L.Txn(10, TXN_START + 1)), ref), (c, cmp)
+    t.close()
+    t2.close()
