@@ -2,11 +2,13 @@
 // DuckDB-style predicate tree (TableFilter mirror) into bitvector programs for the
 // fused eval/decode kernel.
 //
-// Planner semantics (all exact; a leaf the index cannot answer exactly is built by K0 from
-// the raw column, never approximated):
+// Planner semantics (all exact; a leaf the index cannot answer exactly is built from the raw
+// column — by the candidate check of its bin, or by K0 — never approximated):
 //   range index, L(k) = {valid & v < k}:  v<c = L(c'), v<=c = L(c+1), v>c = NN∖L(c+1),
 //     v>=c = NN∖L(c), v==c = L(c+1)∖L(c), v!=c = (NN∖L(c+1)) ∪ L(c); where L(c') is the
-//     bitvector of the smallest key ≥ c when the index holds every distinct value.
+//     bitvector of the smallest key ≥ c when the index holds every distinct value. A
+//     constant between keys k_lo < c < k_hi: v<c = L(k_lo) ∪ {r ∈ L(k_hi)∖L(k_lo) : v[r] < c}
+//     (candidate check), v==c = {r ∈ L(k_hi)∖L(k_lo) : v[r] == c}.
 //   equality index, E(k) = {v == k}: v==c = E(c), v!=c = NN∖E(c), ranges = ∪ E(k).
 //   NULLs never satisfy a comparison (TemplatedFilterSelection HAS_NULL path,
 //   column_segment.cpp:261-276) — NN is the column's validity bitvector.
