@@ -117,9 +117,14 @@ int timing_events(cubit_ctx* ctx, hipEvent_t& start, hipEvent_t& stop) {
     start = stop = nullptr;
     if (!ctx->timing) return CUBIT_OK;
     if (ctx->n_timed == ctx->evs.size()) {
+        // timing-only events: no system-scope release when they are recorded, so a stamp does
+        // not wait for an L2 writeback of the kernel's dirty lines (HIP documents this for
+        // timing accuracy on AMD devices). Measured: the stamped mean stays 2-4 % above
+        // rocprofv3's kernel trace (73.7 vs 71.1 µs at SF100 Q6), as with default events.
+        // Results stay ordered by the stream; readers synchronise on it.
         hipEvent_t e0, e1;
-        HIP_CHECK(hipEventCreate(&e0));
-        HIP_CHECK(hipEventCreate(&e1));
+        HIP_CHECK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));
+        HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
         ctx->evs.emplace_back(e0, e1);
     }
     start = ctx->evs[ctx->n_timed].first;

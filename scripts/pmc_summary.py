@@ -38,9 +38,12 @@ def main():
         stats = glob.glob(f"{wdir}/kt/**/*kernel_stats.csv", recursive=True)
         if stats:
             (ROOT / "profiles" / f"{ROUND}_{w}_kernel_stats.csv").write_text(Path(stats[0]).read_text())
-        kt = [r for r in rows(f"{wdir}/kt/**/*kernel_trace.csv") if KERNEL in r["Kernel_Name"]]
-        fetch = [r for r in rows(f"{wdir}/fetch/**/*counter_collection.csv") if KERNEL in r["Kernel_Name"]]
-        write = [r for r in rows(f"{wdir}/write/**/*counter_collection.csv") if KERNEL in r["Kernel_Name"]]
+        # the dominant kernel's own instantiation (K leaves): the bench's side legs launch
+        # other instantiations of the same template (e.g. K = 1 for the equality query)
+        kname = f"{KERNEL}<{line['config']['bitvectors_read_K']}, "
+        kt = [r for r in rows(f"{wdir}/kt/**/*kernel_trace.csv") if kname in r["Kernel_Name"]]
+        fetch = [r for r in rows(f"{wdir}/fetch/**/*counter_collection.csv") if kname in r["Kernel_Name"]]
+        write = [r for r in rows(f"{wdir}/write/**/*counter_collection.csv") if kname in r["Kernel_Name"]]
         if not (fetch and write):
             continue
         for name, rs in (("pmc_fetch", fetch), ("pmc_write", write)):
