@@ -426,6 +426,8 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_tiles(
     if (t == 0) finish_ticket(a.ticket, a.count, mine);
 }
 
+__device__ uint64_t* g_diag_times;  // DIAG & 4 builds only (scripts/kbench.hip)
+
 // Pair-claimed evaluate + decode: one returning atomic per PAIR of tiles, issued one unit
 // before its result is needed, so the claim latency is covered by the next tile's work.
 // Per pair (tiles A = u, B = u + G of this workgroup's walk):
@@ -443,7 +445,8 @@ template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FOR
 __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decode_pairs(EvalArgs a,
                                                                                        uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
-    // fake decode (same LDS traffic, no per-bit loop)
+    // fake decode (same LDS traffic, no per-bit loop), bit 2 = record each workgroup's start
+    // and end (s_memrealtime, 100 MHz) into g_diag_times[2·blockIdx + {0, 1}]
     constexpr int NW = 2 * PAIRS;
     constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
     constexpr int FPW = 64 / FB;
@@ -468,6 +471,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     // B's rows as offsets from A's first row must fit 32 bits
     if ((uint64_t)G * TILE_ROWS + TILE_ROWS >= (1ull << 32)) __builtin_trap();
     const bool write_ids = a.rowids != nullptr;
+    if ((DIAG & 4) && t == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     uint64_t pend_claim = 0;  // thread 0: the previous pair's claimed base
     uint64_t mine = 0;        // thread 0: rows claimed by this workgroup (carried by its arrival)
 
@@ -677,6 +681,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
         copy_out(sp);
     }
     if (t == 0) finish_ticket(a.ticket, a.count, mine);
+    if ((DIAG & 4) && t == 0) g_diag_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------ K1+K3: fused filter + probe-sum

@@ -393,6 +393,77 @@ int main(int argc, char** argv) {
             }
         }
     }
+    // per-workgroup start / end stamps of the production K = 4 CONJ decode (Q6-like 2.3 %
+    // density): how much of the launch is dispatch ramp and how much is the tail after the
+    // first workgroup finishes (what dynamic tile scheduling could recover)
+    {
+        const unsigned grid = std::min<unsigned>(dtiles, 2 * cus);
+        uint64_t* d_times;
+        CK(hipMalloc(&d_times, 2 * grid * 8));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_times), &d_times, sizeof(d_times)));
+        std::vector<uint64_t> h(2 * grid);
+        std::vector<double> ramp, tail, span;
+        for (int r = 0; r < rounds + 1; ++r) {
+            EvalArgs a = base;
+            a.num_tiles = dtiles;
+            a.prog.leaf[3] = leaf[4];
+            a.prog.n_leaves = 4;
+            a.prog.negate = 0;
+            a.prog.nops = 0;
+            for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
+            a.prog.ops = 0;
+            hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 4, FORM_CONJ>), dim3(grid), dim3(512), 0, 0, a, dir);
+            CK(hipDeviceSynchronize());
+            if (r == 0) continue;
+            CK(hipMemcpy(h.data(), d_times, h.size() * 8, hipMemcpyDeviceToHost));
+            uint64_t s0 = ~0ull, s1 = 0, e0 = ~0ull, e1 = 0;
+            for (unsigned g = 0; g < grid; ++g) {
+                s0 = std::min(s0, h[2 * g]);
+                s1 = std::max(s1, h[2 * g]);
+                e0 = std::min(e0, h[2 * g + 1]);
+                e1 = std::max(e1, h[2 * g + 1]);
+            }
+            ramp.push_back((s1 - s0) / 100.0);  // 100 MHz ticks → µs
+            tail.push_back((e1 - e0) / 100.0);
+            span.push_back((e1 - s0) / 100.0);
+            if (r == rounds) {
+                // the last round's end-time distribution, overall and per XCD (blockIdx % 8)
+                std::vector<double> ends;
+                double xsum[8] = {0}, xmax[8] = {0};
+                int xn[8] = {0};
+                for (unsigned g = 0; g < grid; ++g) {
+                    const double e = (h[2 * g + 1] - s0) / 100.0;
+                    ends.push_back(e);
+                    xsum[g % 8] += e;
+                    xmax[g % 8] = std::max(xmax[g % 8], e);
+                    xn[g % 8]++;
+                }
+                std::sort(ends.begin(), ends.end());
+                printf("  end times (us from first start): p0 %.1f p10 %.1f p25 %.1f p50 %.1f p75 %.1f p90 %.1f p100 %.1f\n",
+                       ends[0], ends[grid / 10], ends[grid / 4], ends[grid / 2], ends[3 * grid / 4], ends[9 * grid / 10],
+                       ends[grid - 1]);
+                printf("  per XCD mean/max end:");
+                for (int x = 0; x < 8; ++x) printf(" %.1f/%.1f", xsum[x] / std::max(xn[x], 1), xmax[x]);
+                printf("\n  by tiles: ");
+                double t9 = 0, t8 = 0;
+                int n9 = 0, n8 = 0;
+                for (unsigned g = 0; g < grid; ++g) {
+                    const uint32_t tiles_g = (dtiles - g + grid - 1) / grid;
+                    const double e = (h[2 * g + 1] - s0) / 100.0;
+                    if (tiles_g == (dtiles + grid - 1) / grid) { t9 += e; ++n9; } else { t8 += e; ++n8; }
+                }
+                printf("%d WGs with more tiles end at %.1f mean, %d with fewer at %.1f mean\n", n9, t9 / std::max(n9, 1),
+                       n8, t8 / std::max(n8, 1));
+            }
+        }
+        auto med = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            return v[v.size() / 2];
+        };
+        printf("K4 conj 2.3%% per-WG stamps: start spread %.1f us, end spread %.1f us, first start -> last end %.1f us\n",
+               med(ramp), med(tail), med(span));
+        CK(hipFree(d_times));
+    }
     const double alg = 8.0 * W * 5 + 8.0 * ref_count;
     printf("%-26s %10s %10s %10s\n", "variant", "median_us", "min_us", "alg_GB/s");
     for (size_t i = 0; i < vs.size(); ++i) {
