@@ -255,6 +255,20 @@ int main(int argc, char** argv) {
                                          dim3(std::min<unsigned>(dtiles, OCC * cus)), dim3(512), 0, s, a, dir); \
                   }, 3})
     DK4("K4 conj x2/CU (prod)", 4096, 2);
+    // K = 4 at Q6's density (L0 ∧ L1 ∧ L2 ∧ L4 ≈ 2.3 %). Measured: issuing B's loads after
+    // the copy-out stores instead of right after A's evaluation changed nothing (72.9 vs
+    // 73.1 µs), so the wait for B does not pay for the stores
+    vs.push_back({"K4 q6-density conj (prod)", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.leaf[3] = leaf[4];
+                      a.prog.n_leaves = 4;
+                      a.prog.negate = 0;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 0, FORM_CONJ>),
+                                         dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
     // (S3072 x3/CU: the 80-VGPR cap spills 192 B per thread, 199 µs — not viable)
     DK4("K4 conj S3072 x2/CU", 3072, 2);
     DPD("pairs diag no-claim", 1);
