@@ -2,7 +2,9 @@
 // interleaved in one process on SF100-sized bitvectors (600,037,902 rows, K = 5 leaves,
 // Q6-like densities, ~1.9 % selected) and checks every variant against the production
 // decode (row ids rebuilt in row order through the tile directory).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I duckdb-cubit_amd/csrc scripts/kbench.hip -o scripts/kbench
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-atomic-optimizer-strategy=None \
+//         -I duckdb-cubit_amd/csrc scripts/kbench.hip -o scripts/kbench
+// (the library's flags: the claims stay single-lane atomics, as in libcubitgpu.so)
 // The variant sweep that chose the production geometry is summarised in DESIGN.md §3.
 #include "cubit_kernels.hip"
 
