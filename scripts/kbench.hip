@@ -321,6 +321,21 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<1, 1, 2048, 512, 0, FORM_CONJ, 2>),
                                          dim3(std::min<unsigned>(a.num_tiles, 2 * cus)), dim3(512), 0, s, a, dir);
                   }, 3});
+    // fewer claims for small inputs: one pair per workgroup (the library's grid for ≤ 2 tiles
+    // per workgroup), and 4,096-word tiles with half the workgroups and half the claims
+    vs.push_back({"K1 1% P2 grid=tiles/2", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((eval_decode_pairs<1, 2, 4096, 512, 0, FORM_CONJ, 2>),
+                                         dim3(std::min<unsigned>((dtiles + 1) / 2, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
+    vs.push_back({"K1 1% P4 grid=tiles/2", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = (uint32_t)(pw / 4096);
+                      hipLaunchKernelGGL((eval_decode_pairs<1, 4, 4096, 512, 0, FORM_CONJ, 2>),
+                                         dim3(std::min<unsigned>((a.num_tiles + 1) / 2, 2 * cus)), dim3(512), 0, s, a,
+                                         dir);
+                  }, 3});
     vs.push_back({"K1 1% tiles grid=tiles", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
                       a.num_tiles = dtiles;
