@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Planner soak (development tool): the GPU planner fuzz of tests/test_gpu_planner_fuzz.py at
+a larger size and for a fixed wall-clock budget, with fresh seeds — random pushed
+TableFilterSets and residual AND/OR trees over range / equality / edge-keyed range + bins /
+unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
+updates from a writer. Every result is compared with the oracle; prints one summary line.
+
+  python scripts/fuzz_soak.py [seconds] [rows]
+"""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "duckdb-cubit_amd"), str(ROOT), str(ROOT / "tests")]
+
+from cubit_amd import _lib as L  # noqa: E402
+from cubit_amd import filters as F  # noqa: E402
+from cubit_amd.datagen import validity_from_mask  # noqa: E402
+from cubit_amd.table import Context, CubitTable  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from test_gpu_planner_fuzz import TXN_START, rand_const_filter, rand_residual  # noqa: E402
+
+
+def round_(ctx, seed, n, with_updates):
+    rng = np.random.default_rng(seed)
+    row_base = int(rng.integers(0, 1 << 40))
+    t = CubitTable(ctx, n, row_base=row_base)
+    data = []
+    for c in range(4):
+        d = rng.integers(0, 50, n).astype(np.int32 if c % 2 == 0 else np.int64)
+        valid = rng.random(n) > (0.12 if c != 1 else 0.0)
+        vw = validity_from_mask(valid) if c != 1 else None
+        t.add_column(c, d, vw)
+        data.append((d, vw))
+    t.build_index(0, L.INDEX_RANGE)
+    t.build_index(1, L.INDEX_EQUALITY)
+    t.build_index(2, L.INDEX_RANGE, [10, 20, 30, 40])
+    t.build_index(2, L.INDEX_BINS, [0, 10, 20, 30, 40, 50])
+    writer = TXN_START + 5
+    upd = {}
+    if with_updates:
+        for c in (0, 2, 3):
+            rows = np.sort(rng.choice(n, size=n // 100, replace=False)).astype(np.int64)
+            vals = rng.integers(0, 50, len(rows)).astype(np.int64)
+            vers = np.where(rng.random(len(rows)) < 0.5, np.uint64(3), np.uint64(writer)).astype(np.uint64)
+            t.set_updates(c, rows, vals, vers)
+            upd[c] = (rows, vals, vers)
+    ocols = [O.Column(d, vw, updates=upd.get(c)) for c, (d, vw) in enumerate(data)]
+    del_rows = np.sort(rng.choice(n, size=n // 20, replace=False)).astype(np.int64)
+    del_ids = np.where(rng.random(len(del_rows)) < 0.5, np.uint64(4), np.uint64(writer)).astype(np.uint64)
+    t.set_deletes(del_rows, del_ids)
+    deleted = np.full(n, np.uint64(2 ** 64 - 2), dtype=np.uint64)
+    deleted[del_rows] = del_ids
+    views = [(2, writer), (2, TXN_START + 6), (10, TXN_START + 7)]
+    checks = 0
+    for i in range(30):
+        filters = {int(c): rand_const_filter(rng) for c in rng.choice(4, size=rng.integers(0, 4), replace=False)}
+        fs = F.TableFilterSet(filters)
+        residual = rand_residual(rng, 4) if rng.random() < 0.5 else None
+        plan = F.serialize(fs, residual)
+        start, tid = views[i % 3]
+        ref = O.table_scan(ocols, plan, n, row_base=row_base, tx=O.Mvcc(start, tid, deleted=deleted))
+        got = t.scan(fs, residual, txn=L.Txn(start, tid), ordered=bool(i % 2))
+        if i % 2 == 0:
+            got = np.sort(got)
+        if not np.array_equal(got, ref):
+            raise AssertionError(f"seed {seed} case {i}: {len(got)} vs {len(ref)} rows; {fs} {residual}")
+        if residual is None:
+            c = t.count(fs, txn=L.Txn(start, tid))
+            if c != len(ref):
+                raise AssertionError(f"seed {seed} case {i}: count {c} vs {len(ref)}")
+        checks += 1
+    t.close()
+    return checks
+
+
+def main():
+    budget = float(sys.argv[1]) if len(sys.argv) > 1 else 90.0
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_003
+    ctx = Context(0)
+    t_end = time.perf_counter() + budget
+    rounds = checks = 0
+    seed = 10_000
+    while time.perf_counter() < t_end:
+        checks += round_(ctx, seed, n, with_updates=bool(rounds % 2))
+        rounds += 1
+        seed += 1
+        print(f"round {rounds}: {checks} scans match the oracle", flush=True)
+    ctx.close()
+    print(f"fuzz soak: {rounds} tables of {n} rows (seeds 10000..{seed - 1}), {checks} random scans, "
+          f"every one equal to the oracle")
+
+
+if __name__ == "__main__":
+    main()
