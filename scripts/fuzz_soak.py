@@ -5,7 +5,7 @@ TableFilterSets and residual AND/OR trees over range / equality / edge-keyed ran
 unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
 updates from a writer. Every result is compared with the oracle; prints one summary line.
 
-  python scripts/fuzz_soak.py [seconds] [rows]
+  python scripts/fuzz_soak.py [seconds] [rows] [first seed]
 """
 import sys
 import time
@@ -80,17 +80,18 @@ def round_(ctx, seed, n, with_updates):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 90.0
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_003
+    seed0 = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
     ctx = Context(0)
     t_end = time.perf_counter() + budget
     rounds = checks = 0
-    seed = 10_000
+    seed = seed0
     while time.perf_counter() < t_end:
         checks += round_(ctx, seed, n, with_updates=bool(rounds % 2))
         rounds += 1
         seed += 1
         print(f"round {rounds}: {checks} scans match the oracle", flush=True)
     ctx.close()
-    print(f"fuzz soak: {rounds} tables of {n} rows (seeds 10000..{seed - 1}), {checks} random scans, "
+    print(f"fuzz soak: {rounds} tables of {n} rows (seeds {seed0}..{seed - 1}), {checks} random scans, "
           f"every one equal to the oracle")
 
 
