@@ -140,7 +140,10 @@ enum class RunMode { kDecode, kCount };
 //            row order with one extra pass); kCount: count(*) and/or result words.
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
              uint64_t capacity, uint64_t* d_count, uint64_t* result_words, RunMode mode, bool timed = false,
-             bool ordered = false) {
+             bool ordered = false, bool check_capacity = false) {
+    // the directory describes only the decode launched here: a count, a failed launch or a
+    // folded-away filter leaves no tiles behind for cubit_ctx_last_tiles to hand out
+    ctx->last_tiles = 0;
     // the claim ticket carries row sums in 48 bits (finish_ticket)
     if (n_rows >= (1ull << 47)) return fail(CUBIT_ERR_INVALID, "%llu rows exceed 2^47", (unsigned long long)n_rows);
     EvalArgs a{};
@@ -179,6 +182,14 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     if (ordered && rowids)
         HIP_CHECK(launch_order_runs(ctx->dir, (uint32_t)tiles, ctx->dst_off, ctx->tmp_ids, capacity, rowids,
                                     ctx->stream));
+    if (check_capacity && rowids) {
+        uint64_t n = 0;
+        HIP_CHECK(hipMemcpyAsync(&n, d_count, sizeof(n), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (n > capacity)
+            return fail(CUBIT_ERR_CAPACITY, "%llu qualifying rows exceed the capacity of %llu row ids",
+                        (unsigned long long)n, (unsigned long long)capacity);
+    }
     return CUBIT_OK;
 }
 
@@ -234,7 +245,15 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
 int cubit_ctx_set_stream(cubit_ctx* ctx, void* stream) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
     CUBIT_LOCK(ctx);
-    ctx->stream = static_cast<hipStream_t>(stream);
+    hipStream_t next = static_cast<hipStream_t>(stream);
+    if (next != ctx->stream) {
+        // the claim ticket, tile directory, scratch ids and partials are re-armed / reused in
+        // stream order: a launch still in flight on the old stream must finish before the
+        // first launch on the new one
+        if (int rc = set_device(ctx)) return rc;
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->stream = next;
     return CUBIT_OK;
 }
 
@@ -661,7 +680,8 @@ extern "C" int cubit_bitvector_eval(cubit_ctx* ctx, const uint64_t* const* d_lea
         return fail(CUBIT_ERR_UNSUPPORTED, "program needs %d leaves / depth %d (max %d / 4)", count_leaves(st[0]),
                     em.max_depth, kMaxLeaves);
     return run_eval(ctx, em.prog, n_rows, row_base, count_only ? nullptr : d_rowids, capacity, d_count, d_result_words,
-                    count_only ? RunMode::kCount : RunMode::kDecode, true, (flags & CUBIT_SCAN_ORDERED) != 0);
+                    count_only ? RunMode::kCount : RunMode::kDecode, true, (flags & CUBIT_SCAN_ORDERED) != 0,
+                    (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0);
 }
 
 extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const int64_t* d_rowids,
@@ -1982,8 +2002,8 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     if (!count_only && !d_rowids) return fail(CUBIT_ERR_INVALID, "d_rowids is null without COUNT_ONLY");
     if (n_nodes && !nodes) return fail(CUBIT_ERR_INVALID, "nodes is null");
     if (int rc = set_device(t->ctx)) return rc;
+    t->ctx->last_tiles = 0;  // until this scan's decode is launched (a planning error leaves none)
     if (t->n_rows == 0) {  // empty partition
-        t->ctx->last_tiles = 0;
         t->last_leaves = t->last_passes = 0;
         HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
         return CUBIT_OK;
@@ -1991,13 +2011,14 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     Emitter em;
     bool empty = false;
     if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
-    if (empty) {
+    if (empty) {  // the filter folded to FALSE: no launch, no tiles
+        t->ctx->last_tiles = 0;
         HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
         return CUBIT_OK;
     }
     return run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
                     nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
-                    (flags & CUBIT_SCAN_ORDERED) != 0);
+                    (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0);
 }
 
 extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
@@ -2012,6 +2033,7 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
         return fail(CUBIT_ERR_UNSUPPORTED, "sum_product needs INT64 (DECIMAL storage) columns");
     if (int rc = set_device(t->ctx)) return rc;
     cubit_ctx* ctx = t->ctx;
+    ctx->last_tiles = 0;  // writes no row ids, so no tile directory (the fallback's scan resets it below)
     uint64_t* count = d_count ? d_count : t->dummy_count;
     if (t->n_rows == 0) {  // empty partition: sum 0 over 0 rows
         HIP_CHECK(hipMemsetAsync(d_out, 0, 2 * sizeof(int64_t), ctx->stream));
@@ -2037,6 +2059,7 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
         if (int rc = cubit_table_probe(t, col_a, txn, ids, count, cap, xa)) return rc;
         if (int rc = cubit_table_probe(t, col_b, txn, ids, count, cap, xb)) return rc;
         HIP_CHECK(launch_sum_product_arrays(xa, xb, count, cap, ctx->partials, d_out, ctx->stream));
+        ctx->last_tiles = 0;  // the directory described ids in scratch, not a caller's buffer
         return CUBIT_OK;
     }
     Emitter em;
@@ -2059,7 +2082,7 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
         sa.n_decode = (uint32_t)dl.size();
         for (size_t j = 0; j < dl.size(); ++j) {
             sa.dleaf[j] = dl[j];
-            sa.delta[j] = vals[j + 1] - vals[j];
+            sa.delta[j] = (int64_t)((uint64_t)vals[j + 1] - (uint64_t)vals[j]);  // modular: no signed overflow
         }
         t->last_decoded = (uint32_t)dl.size() + 1;
     } else {

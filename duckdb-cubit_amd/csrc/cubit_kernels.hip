@@ -695,7 +695,9 @@ __device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, __int128 x) {
 }
 
 // SELECT sum(a * b) WHERE <program>: evaluate a tile, decode its set bits into LDS (row
-// offset, and b's value when b is decoded from its index), then gather a (and b) for the
+// offset, and — when b is decoded from its index — which of the M decode leaves miss the row,
+// as M bits above the 17-bit tile-local offset, so b = v0 + Σ delta[m] over those bits is
+// rebuilt in full int64 at the gather), then gather a (and b) for the
 // staged rows with several loads in flight per thread, accumulating in 128 bits
 // (DECIMAL(38,4) storage, Q6's sum(l_extendedprice * l_discount)). No row ids are written.
 // Persistent like eval_decode_pairs; per-workgroup partials are summed by sum_partials_kernel;
@@ -709,13 +711,24 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     constexpr int NWAVES = THREADS / 64;
     __shared__ uint64_t s_wave_tot[NWAVES];
+    // s_row: tile-local row offset (bits 0..16) | decode-leaf miss bits (bits kMissShift..)
+    constexpr int kMissShift = 24;
+    static_assert(TILE_WORDS * 64 <= (1u << kMissShift) && M <= 32 - kMissShift, "s_row packing");
     __shared__ uint32_t s_row[STAGE];
-    __shared__ int32_t s_w[M > 0 ? STAGE : 1];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint64_t acc_lo = 0;
     int64_t acc_hi = 0;
     uint64_t total = 0;
 
+    // b decoded from its range index: v0 plus the deltas of the leaves that miss the row (full
+    // int64 — b may be any BIGINT / DECIMAL(18,x) storage value)
+    auto decoded_b = [&](uint32_t miss) -> int64_t {
+        uint64_t v = (uint64_t)s.v0;  // modular: v0 + Σ deltas lands on a stored value
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if ((miss >> m) & 1u) v += (uint64_t)s.delta[m];
+        return (int64_t)v;
+    };
     auto accumulate = [&](int64_t row, int64_t bval_decoded) {
         const uint64_t r = (uint64_t)(row - a.row_base);
         if (s.a_valid && !((s.a_valid[r >> 6] >> (r & 63)) & 1ull)) return;
@@ -782,21 +795,17 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                 const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
                 while (w) {
                     const uint32_t b = (uint32_t)__builtin_ctzll(w);
-                    int64_t bval = 0;
-                    if (M > 0) {
-                        bval = s.v0;
+                    uint32_t miss = 0;  // bit m: the row is not in decode leaf m (b >= v_{m+1})
 #pragma unroll
-                        for (int m = 0; m < M; ++m) {
-                            const u64x2 d = dv[m][p];
-                            const uint64_t dw = e ? d.y : d.x;
-                            if (!((dw >> b) & 1ull)) bval += s.delta[m];
-                        }
+                    for (int m = 0; m < M; ++m) {
+                        const u64x2 d = dv[m][p];
+                        const uint64_t dw = e ? d.y : d.x;
+                        miss |= (uint32_t)(((dw >> b) & 1ull) ^ 1ull) << m;
                     }
                     if (staged) {
-                        s_row[off] = wrow + b;
-                        if (M > 0) s_w[off] = (int32_t)bval;
+                        s_row[off] = (wrow + b) | (miss << kMissShift);
                     } else {
-                        accumulate(row0 + (int64_t)(wrow + b), bval);  // dense tile: direct
+                        accumulate(row0 + (int64_t)(wrow + b), decoded_b(miss));  // dense tile: direct
                     }
                     ++off;
                     w &= w - 1;
@@ -814,9 +823,10 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                 for (int u = 0; u < 4; ++u) {
                     const uint32_t k = i + u * THREADS;
                     ok[u] = k < (uint32_t)tile_count;
-                    const uint64_t rr = (uint64_t)(row0 - a.row_base) + (ok[u] ? s_row[k] : 0u);
+                    const uint32_t sr = ok[u] ? s_row[k] : 0u;
+                    const uint64_t rr = (uint64_t)(row0 - a.row_base) + (sr & ((1u << kMissShift) - 1));
                     av[u] = ok[u] ? s.a[rr] : 0;
-                    bvv[u] = M > 0 ? (ok[u] ? (int64_t)s_w[k] : 0) : (ok[u] ? s.b[rr] : 0);
+                    bvv[u] = M > 0 ? (ok[u] ? decoded_b(sr >> kMissShift) : 0) : (ok[u] ? s.b[rr] : 0);
                     if (ok[u] && s.a_valid && !((s.a_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
                     if (M == 0 && ok[u] && s.b_valid && !((s.b_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
                 }

@@ -27,6 +27,7 @@ SUM_GATHER_B = 1
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2
+SCAN_CHECK_CAPACITY = 4  # synchronise; ERR_CAPACITY when the count exceeds the buffer
 
 
 class FilterNode(C.Structure):

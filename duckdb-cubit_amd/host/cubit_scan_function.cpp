@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <thread>
 
 #include "../../include/cubit_scan.h"
@@ -78,12 +79,25 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     const uint64_t* d_dir = nullptr;
     uint32_t n_tiles = 0;
     check(cubit_ctx_last_tiles(ctx, &d_dir, &n_tiles, &g->rows_per_tile), "tiles");
+    if (g->count > cap) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count exceeds the table's rows");
+    if (g->count == 0) n_tiles = 0;  // nothing qualified: no run to hand out, whatever the directory holds
     g->dir.resize(2 * (size_t)n_tiles);
     if (n_tiles) check(cubit_memcpy_d2h(ctx, g->dir.data(), d_dir, g->dir.size() * 8), "directory");
     g->rowids.resize(g->count);
     if (g->count) check(cubit_memcpy_d2h(ctx, g->rowids.data(), d_ids.p, g->count * 8), "row ids");
-    for (uint32_t t = 0; t < n_tiles; ++t)
-        if (g->dir[2 * t + 1]) g->tiles.push_back(t);
+    uint64_t covered = 0;
+    for (uint32_t t = 0; t < n_tiles; ++t) {
+        const uint64_t start = g->dir[2 * t], len = g->dir[2 * t + 1];
+        if (!len) continue;
+        // every run lies inside this scan's output (a directory of another launch would not)
+        if (start > g->count || len > g->count - start)
+            throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile directory does not describe this scan's output");
+        covered += len;
+        g->tiles.push_back(t);
+    }
+    if (covered != g->count)
+        throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(covered) + " of " +
+                                               std::to_string(g->count) + " row ids");
     // probe every emitted storage column at the row ids (ColumnData::FilterScan semantics)
     g->columns.resize(g->emit.size());
     for (size_t e = 0; e < g->emit.size(); ++e) {

@@ -76,9 +76,15 @@ extern "C" {
  * parallel table scan, whose morsels reach the sink in nondeterministic order with a batch
  * index (src/function/table/table_scan.cpp:179-189). cubit_ctx_last_tiles() returns the
  * tile directory ({start, length} per tile) that restores row order for free.
- * CUBIT_SCAN_ORDERED lays the runs out ascending with one extra device pass. */
-#define CUBIT_SCAN_COUNT_ONLY 1u /* do not materialise row ids */
-#define CUBIT_SCAN_ORDERED 2u    /* one globally ascending array */
+ * CUBIT_SCAN_ORDERED lays the runs out ascending with one extra device pass.
+ * Capacity: *d_count is always the full number of qualifying rows. When it exceeds
+ * `capacity` the calls still return CUBIT_OK (they do not wait for the kernel) and the
+ * buffer holds an unspecified subset of the ids (runs are claimed in nondeterministic order;
+ * with CUBIT_SCAN_ORDERED the ordered array has holes) — compare *d_count with capacity, or
+ * pass CUBIT_SCAN_CHECK_CAPACITY, which waits for the scan and returns CUBIT_ERR_CAPACITY. */
+#define CUBIT_SCAN_COUNT_ONLY 1u     /* do not materialise row ids */
+#define CUBIT_SCAN_ORDERED 2u        /* one globally ascending array */
+#define CUBIT_SCAN_CHECK_CAPACITY 4u /* synchronise; CUBIT_ERR_CAPACITY when *d_count > capacity */
 
 typedef struct cubit_ctx cubit_ctx;
 typedef struct cubit_table cubit_table;
