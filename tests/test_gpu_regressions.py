@@ -81,8 +81,10 @@ def test_fused_sum_decoded_b_beyond_int32(ctx, base):
     (staged) and dense (direct) tiles."""
     n = 700_000
     rng = np.random.default_rng(base & 0xFFFF)
-    steps = np.array([0, 7, 2 ** 20, 2 ** 31 + 5, 2 ** 32 + 9, 2 ** 33], dtype=np.int64)
-    vals = (np.int64(base) + steps) if base < 2 ** 62 else (np.int64(base) + steps * 3)
+    # a narrow spread far from zero: the all-distinct-values range index builds (presence
+    # bitmap over [vmin, vmax]), and every value is outside int32
+    steps = np.array([0, 7, 19, 20, 1000, 40_000], dtype=np.int64)
+    vals = np.int64(base) + steps
     b = vals[rng.integers(0, len(vals), n)]
     a = rng.integers(-(10 ** 9), 10 ** 9, n).astype(np.int64)
     # c: sparse tiles (2 % pass) in the first half, every row passes in the second (dense tiles)
