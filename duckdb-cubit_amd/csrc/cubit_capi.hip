@@ -720,7 +720,8 @@ struct DevBuf {
 struct Column {
     int type = 0;
     const void* data = nullptr;        // device
-    const uint64_t* validity = nullptr;  // device, padded (null = no NULLs)
+    const uint64_t* validity = nullptr;  // device, padded to the table's cap_words (null = no NULLs)
+    uint64_t cap_rows = 0;  // rows the owned data buffer holds (0 = caller-owned device data)
     std::vector<std::unique_ptr<DevBuf>> owned;
     // value statistics (zonemap-like), computed at index build
 };
@@ -742,6 +743,10 @@ struct Updates {
     std::vector<uint64_t> h_versions;
     std::vector<uint64_t> distinct_versions;  // sorted
     uint64_t n = 0;
+    // distinct updated values, sorted: the update statistics the planner widens the index
+    // statistics with (DuckDB's zonemaps consult update statistics the same way,
+    // standard_column_data.cpp:50-57)
+    std::vector<int64_t> stat_values;
     // does any record pass TransactionVersionOperator::UseInsertedVersion for this
     // transaction (id < start_time || id == transaction_id)? If not, the transaction sees
     // the base values and no patch is needed.
@@ -775,6 +780,9 @@ struct cubit_table {
     uint64_t n_rows = 0;
     int64_t row_base = 0;
     uint64_t nwp = 0;  // padded words
+    // words allocated per table-owned bitvector (index leaves, validity): ≥ nwp, zero past the
+    // rows; appends grow the table in place until nwp would exceed it (cubit_table_append)
+    uint64_t cap_words = 0;
     std::map<int, Column> cols;
     std::map<int, Index> idx;
     std::map<int, Index> bins;  // CUBIT_INDEX_BINS (secondary)
@@ -821,6 +829,26 @@ void drop_patches(cubit_table* t, int col) {
     if (it != t->upd.end()) it->second.cache.clear();
 }
 
+// a table-owned bitvector of cap_words words, all zero (the kernels that fill it write nwp
+// words; the rest must stay zero for appends that grow into it)
+int alloc_table_bv(cubit_table* t, DevBuf& b) {
+    if (hipMalloc(&b.p, std::max<uint64_t>(t->cap_words, 1) * 8) != hipSuccess) return CUBIT_ERR_OOM;
+    if (hipMemsetAsync(b.p, 0, std::max<uint64_t>(t->cap_words, 1) * 8, t->ctx->stream) != hipSuccess) return CUBIT_ERR_HIP;
+    return CUBIT_OK;
+}
+
+// Everything derived from the row count (scratch / ones / visibility / patched leaves, all
+// nwp words): dropped when the table grows or its base changes.
+void drop_derived(cubit_table* t) {
+    t->scratch.clear();
+    t->scratch_used = 0;
+    t->ones.reset();
+    t->vis_cache.reset();
+    t->vis_prefix = -1;
+    t->vis_ins_prefix = -1;
+    for (auto& kv : t->upd) kv.second.cache.clear();
+}
+
 int scratch_bv(cubit_table* t, uint64_t** out) {
     if (t->scratch_used < t->scratch.size()) {
         *out = static_cast<uint64_t*>(t->scratch[t->scratch_used++]->p);
@@ -851,8 +879,8 @@ int ones_bv(cubit_table* t, const uint64_t** out) {
 int copy_validity(cubit_table* t, Column& c, const uint64_t* validity, int on_device) {
     hipStream_t s = t->ctx->stream;
     auto b = std::make_unique<DevBuf>();
-    if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "validity allocation failed");
-    HIP_CHECK(hipMemsetAsync(b->p, 0, t->nwp * 8, s));
+    if (hipMalloc(&b->p, t->cap_words * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "validity allocation failed");
+    HIP_CHECK(hipMemsetAsync(b->p, 0, t->cap_words * 8, s));
     const uint64_t nw = (t->n_rows + 63) / 64;
     HIP_CHECK(hipMemcpyAsync(b->p, validity, nw * 8, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     if (t->n_rows & 63) {
@@ -883,6 +911,7 @@ int copy_column(cubit_table* t, Column& c, int type, const void* data, const uin
             return fail(CUBIT_ERR_OOM, "column allocation failed");
         HIP_CHECK(hipMemcpyAsync(b->p, data, t->n_rows * esz, hipMemcpyHostToDevice, s));
         c.data = b->p;
+        c.cap_rows = t->n_rows;
         c.owned.push_back(std::move(b));
     }
     if (validity) {
@@ -896,9 +925,9 @@ int copy_column(cubit_table* t, Column& c, int type, const void* data, const uin
 // Index-build statistics on the device: min / max / any valid, and (want_distinct) the
 // distinct valid values through a presence bitmap of vmax - vmin + 1 bits (≤ 2^32 values;
 // an index with more distinct keys than that is not a bitmap index anyone should build).
-int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct, bool want_distinct,
-                 int64_t& vmin, int64_t& vmax, bool& any) {
-    const uint64_t n = t->n_rows;
+int value_stats(cubit_table* t, const void* data, int type, const uint64_t* validity, uint64_t n,
+                std::vector<int64_t>& distinct, bool want_distinct, int64_t& vmin, int64_t& vmax, bool& any) {
+    const Column c{type, data, validity};
     DevBuf stats;
     if (hipMalloc(&stats.p, 3 * sizeof(int64_t)) != hipSuccess) return fail(CUBIT_ERR_OOM, "stats allocation failed");
     int64_t h[3] = {INT64_MAX, INT64_MIN, 0};
@@ -930,6 +959,11 @@ int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct
     return CUBIT_OK;
 }
 
+int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct, bool want_distinct,
+                 int64_t& vmin, int64_t& vmax, bool& any) {
+    return value_stats(t, c.data, c.type, c.validity, t->n_rows, distinct, want_distinct, vmin, vmax, any);
+}
+
 }  // namespace
 
 extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_base, cubit_table** out) {
@@ -944,6 +978,7 @@ extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_b
     t->n_rows = n_rows;
     t->row_base = row_base;
     t->nwp = padded_words(n_rows);
+    t->cap_words = t->nwp;
     t->dummy = std::make_unique<DevBuf>();
     if (hipMalloc(&t->dummy->p, 64) != hipSuccess) {
         delete t;
@@ -1072,6 +1107,7 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     Column c;
     c.type = type;
     c.data = out->p;
+    c.cap_rows = t->n_rows;
     c.owned.push_back(std::move(out));
     if (validity) {
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
@@ -1099,7 +1135,12 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     ix.encoding = encoding;
     if (t->n_rows == 0) {  // empty partition: an empty index (scans of it launch nothing)
         ix.empty = true;
+        ix.exact_all = n == 0;  // every distinct value of no rows; appends keep it exact
         if (n) ix.keys.assign(values, values + n);
+        if (n && !std::is_sorted(ix.keys.begin(), ix.keys.end()))
+            return fail(CUBIT_ERR_INVALID, "index keys must be sorted ascending");
+        ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end()), ix.keys.end());
+        if (encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) return fail(CUBIT_ERR_INVALID, "bins need >= 2 edges");
         drop_patches(t, col);
         if (encoding == CUBIT_INDEX_BINS) t->bins[col] = std::move(ix);
         else t->idx[col] = std::move(ix);
@@ -1128,15 +1169,15 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
         MultiKeyArgs mk{};
         for (size_t k = k0; k < std::min(n_bv, k0 + kMultiKeys); ++k) {
             auto b = std::make_unique<DevBuf>();
-            if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess)
-                return fail(CUBIT_ERR_OOM, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(), n_bv);
+            if (int rc = alloc_table_bv(t, *b))
+                return fail(rc, "index bitvector allocation failed after %zu of %zu", ix.bvs.size(), n_bv);
             mk.c[mk.m] = ix.keys[k];
             mk.c2[mk.m] = encoding == CUBIT_INDEX_BINS ? ix.keys[k + 1] : 0;
             mk.out[mk.m] = static_cast<uint64_t*>(b->p);
             ++mk.m;
             ix.bvs.push_back(static_cast<uint64_t*>(b->p));
             ix.owned.push_back(std::move(b));
-            ix.bytes += t->nwp * 8;
+            ix.bytes += t->cap_words * 8;
         }
         HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
     }
@@ -1260,7 +1301,7 @@ extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path)
     for (uint64_t k = 0; k < h.n_bv; ++k) {
         if (std::fread(host.data(), 8, t->nwp, f) != t->nwp) return bad("truncated bitvectors");
         auto b = std::make_unique<DevBuf>();
-        if (hipMalloc(&b->p, t->nwp * 8) != hipSuccess) {
+        if (alloc_table_bv(t, *b)) {
             std::fclose(f);
             return fail(CUBIT_ERR_OOM, "index bitvector allocation failed");
         }
@@ -1270,7 +1311,7 @@ extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path)
         }
         ix.bvs.push_back(static_cast<uint64_t*>(b->p));
         ix.owned.push_back(std::move(b));
-        ix.bytes += t->nwp * 8;
+        ix.bytes += t->cap_words * 8;
     }
     std::fclose(f);
     drop_patches(t, col);
@@ -1321,15 +1362,12 @@ extern "C" int cubit_table_set_inserts(cubit_table* t, const int64_t* row_begin,
     return CUBIT_OK;
 }
 
-extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
-                                       const uint64_t* versions, uint64_t n) {
-    if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
-    CUBIT_LOCK(t->ctx);
-    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
-    if (int rc = set_device(t->ctx)) return rc;
-    for (uint64_t i = 0; i < n; ++i)
-        if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
-    // group records by row, keeping each row's records in chronological order
+namespace {
+
+// store an update list (rows, values, versions) for col: records grouped by row, each row's
+// records kept in chronological order (UpdateInfo chains, update_info.hpp)
+int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values, const uint64_t* versions,
+                  uint64_t n) {
     std::vector<uint64_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
@@ -1344,6 +1382,9 @@ extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* r
     std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
     u.distinct_versions.erase(std::unique(u.distinct_versions.begin(), u.distinct_versions.end()),
                               u.distinct_versions.end());
+    u.stat_values = u.h_values;
+    std::sort(u.stat_values.begin(), u.stat_values.end());
+    u.stat_values.erase(std::unique(u.stat_values.begin(), u.stat_values.end()), u.stat_values.end());
     u.rows = std::make_unique<DevBuf>();
     u.values = std::make_unique<DevBuf>();
     u.versions = std::make_unique<DevBuf>();
@@ -1360,9 +1401,441 @@ extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* r
     return CUBIT_OK;
 }
 
+}  // namespace
+
+extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
+                                       const uint64_t* versions, uint64_t n) {
+    if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
+    return store_updates(t, col, rows, values, versions, n);
+}
+
+// ------------------------------------------------------------------ index maintenance
+
+namespace {
+
+// Every table-owned bitvector (index leaves, bins, validity) grown to `words` words: copy the
+// nwp words in use, zero the rest. Index leaf pointers change, so everything derived from them
+// (patched leaves, scratch) is dropped by the caller.
+int grow_bitvectors(cubit_table* t, uint64_t words) {
+    hipStream_t s = t->ctx->stream;
+    auto regrow = [&](void*& p) -> int {
+        void* np = nullptr;
+        if (hipMalloc(&np, words * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "bitvector growth failed");
+        HIP_CHECK(hipMemsetAsync(np, 0, words * 8, s));
+        if (p && t->nwp) HIP_CHECK(hipMemcpyAsync(np, p, t->nwp * 8, hipMemcpyDeviceToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        if (p) (void)hipFree(p);
+        p = np;
+        return CUBIT_OK;
+    };
+    for (auto* m : {&t->idx, &t->bins}) {
+        for (auto& kv : *m) {
+            Index& ix = kv.second;
+            for (size_t k = 0; k < ix.owned.size(); ++k) {
+                if (int rc = regrow(ix.owned[k]->p)) return rc;
+                ix.bvs[k] = static_cast<uint64_t*>(ix.owned[k]->p);
+            }
+            ix.bytes = ix.owned.size() * words * 8;
+        }
+    }
+    for (auto& kv : t->cols) {
+        Column& c = kv.second;
+        if (!c.validity) continue;
+        for (auto& b : c.owned) {
+            if (b->p != (const void*)c.validity) continue;
+            if (int rc = regrow(b->p)) return rc;
+            c.validity = static_cast<const uint64_t*>(b->p);
+            break;
+        }
+    }
+    t->cap_words = words;
+    return CUBIT_OK;
+}
+
+// an owned data buffer of at least `rows` rows holding the column's first n_rows values
+int own_column(cubit_table* t, Column& c, uint64_t rows) {
+    if (c.cap_rows >= rows && c.cap_rows) return CUBIT_OK;
+    const uint64_t esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
+    auto b = std::make_unique<DevBuf>();
+    if (hipMalloc(&b->p, std::max<uint64_t>(rows * esz, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "column allocation failed");
+    if (c.data && t->n_rows)
+        HIP_CHECK(hipMemcpyAsync(b->p, c.data, t->n_rows * esz, hipMemcpyDeviceToDevice, t->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    // release the old owned data buffer (not the validity buffer)
+    for (auto it = c.owned.begin(); it != c.owned.end(); ++it)
+        if ((*it)->p == c.data) {
+            c.owned.erase(it);
+            break;
+        }
+    c.data = b->p;
+    c.cap_rows = rows;
+    c.owned.push_back(std::move(b));
+    return CUBIT_OK;
+}
+
+// The keys an exact_all index must hold after the column gained the values `added` (sorted,
+// distinct, all valid): RANGE keeps every distinct value but the minimum, EQUALITY every
+// distinct value. Missing keys get full-column bitvectors (the column already holds its new
+// values); more than kMaxNewKeys missing keys turn the index into an edges index instead
+// (exact for its keys, the candidate check for other constants).
+constexpr size_t kMaxNewKeys = 64;
+int maintain_exact_keys(cubit_table* t, int col, Index& ix, const std::vector<int64_t>& added, int64_t old_min,
+                        bool was_empty) {
+    if (!ix.exact_all || ix.encoding == CUBIT_INDEX_BINS || added.empty()) return CUBIT_OK;
+    std::vector<int64_t> want;  // keys the index must hold
+    if (ix.encoding == CUBIT_INDEX_RANGE) {
+        // old distinct values ⊆ keys ∪ {old_min}; the new minimum needs no key
+        if (!was_empty && old_min > ix.vmin) want.push_back(old_min);
+        for (int64_t v : added)
+            if (v > ix.vmin) want.push_back(v);
+    } else {
+        want = added;
+    }
+    std::vector<int64_t> missing;
+    for (int64_t v : want)
+        if (!std::binary_search(ix.keys.begin(), ix.keys.end(), v)) missing.push_back(v);
+    std::sort(missing.begin(), missing.end());
+    missing.erase(std::unique(missing.begin(), missing.end()), missing.end());
+    if (missing.empty()) return CUBIT_OK;
+    if (missing.size() > kMaxNewKeys) {
+        ix.exact_all = false;
+        return CUBIT_OK;
+    }
+    const Column& c = t->cols.at(col);
+    const int cmp = ix.encoding == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ;
+    std::vector<std::pair<int64_t, std::unique_ptr<DevBuf>>> fresh;
+    for (size_t k0 = 0; k0 < missing.size(); k0 += kMultiKeys) {
+        MultiKeyArgs mk{};
+        for (size_t k = k0; k < std::min(missing.size(), k0 + kMultiKeys); ++k) {
+            auto b = std::make_unique<DevBuf>();
+            if (int rc = alloc_table_bv(t, *b)) return fail(rc, "index bitvector allocation failed");
+            mk.c[mk.m] = missing[k];
+            mk.out[mk.m] = static_cast<uint64_t*>(b->p);
+            ++mk.m;
+            fresh.emplace_back(missing[k], std::move(b));
+        }
+        HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
+    }
+    HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+    // merge into the sorted key list (keys, bvs and owned stay parallel)
+    std::vector<int64_t> keys;
+    std::vector<uint64_t*> bvs;
+    std::vector<std::unique_ptr<DevBuf>> owned;
+    size_t i = 0, j = 0;
+    std::vector<std::unique_ptr<DevBuf>> old_owned = std::move(ix.owned);
+    while (i < ix.keys.size() || j < fresh.size()) {
+        if (j == fresh.size() || (i < ix.keys.size() && ix.keys[i] < fresh[j].first)) {
+            keys.push_back(ix.keys[i]);
+            bvs.push_back(ix.bvs[i]);
+            owned.push_back(std::move(old_owned[i]));
+            ++i;
+        } else {
+            keys.push_back(fresh[j].first);
+            bvs.push_back(static_cast<uint64_t*>(fresh[j].second->p));
+            owned.push_back(std::move(fresh[j].second));
+            ++j;
+        }
+    }
+    ix.keys = std::move(keys);
+    ix.bvs = std::move(bvs);
+    ix.owned = std::move(owned);
+    ix.bytes = ix.owned.size() * t->cap_words * 8;
+    return CUBIT_OK;
+}
+
+// bitvectors an index of this encoding holds for its keys
+size_t index_bv_count(const Index& ix) {
+    return ix.encoding == CUBIT_INDEX_BINS ? (ix.keys.size() >= 2 ? ix.keys.size() - 1 : 0) : ix.keys.size();
+}
+
+}  // namespace
+
+// Append rows to the partition (RowGroupCollection::Append + every BoundIndex::Append,
+// bound_index.hpp:67-70): the new rows get local ids n_rows … n_rows + n_new - 1. Values are
+// host arrays, one per registered column (cols[i] names the column of data[i]); validity[i]
+// (LSB-first words for the appended rows, bit 0 = first appended row) may be null = all valid.
+// Every index of every column is maintained incrementally: the index-build compare kernel runs
+// over the appended slice only and its words are spliced into each bitvector at bit n_rows;
+// statistics widen, and an index over every distinct value gains keys for new values.
+// insert_id ≠ 0 records the rows as an insert range of that transaction (ChunkVectorInfo
+// inserted ids): readers with start_time ≤ insert_id (other than the inserting transaction)
+// do not see them. Storage grows in place, geometrically, when the padding is exhausted.
+extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* cols, const void* const* data,
+                                  const uint64_t* const* validity, uint32_t n_cols, uint64_t insert_id) {
+    if (!t || (n_cols && (!cols || !data))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    if (n_new == 0) return CUBIT_OK;
+    const uint64_t n_old = t->n_rows, n_total = n_old + n_new;
+    if (n_total >= (1ull << 47) || n_total < n_old)
+        return fail(CUBIT_ERR_INVALID, "%llu rows exceed 2^47", (unsigned long long)n_total);
+    if (n_cols != t->cols.size())
+        return fail(CUBIT_ERR_INVALID, "append gives %u columns, the table has %zu", n_cols, t->cols.size());
+    std::map<int, uint32_t> at;
+    for (uint32_t i = 0; i < n_cols; ++i) {
+        if (!t->cols.count(cols[i])) return fail(CUBIT_ERR_INVALID, "column %d not registered", cols[i]);
+        if (!data[i]) return fail(CUBIT_ERR_INVALID, "column %d: null data", cols[i]);
+        if (!at.emplace(cols[i], i).second) return fail(CUBIT_ERR_INVALID, "column %d given twice", cols[i]);
+    }
+    if (int rc = set_device(t->ctx)) return rc;
+    hipStream_t s = t->ctx->stream;
+    HIP_CHECK(hipStreamSynchronize(s));
+    // 1. capacity: bitvectors and columns grow together (×1.25 at least)
+    const uint64_t need_words = padded_words(n_total);
+    if (need_words > t->cap_words) {
+        const uint64_t words = std::max(need_words, padded_words(n_old + n_old / 4));
+        if (int rc = grow_bitvectors(t, words)) return rc;
+    }
+    for (auto& kv : t->cols)
+        if (int rc = own_column(t, kv.second, std::max(n_total, kv.second.cap_rows >= n_total ? kv.second.cap_rows
+                                                                                          : t->cap_words * 64)))
+            return rc;
+    // 2. per column: values, validity, then every index on it
+    const uint64_t slice_words = padded_words(n_new);
+    DevBuf tmp_col, tmp_valid, tmp_bits;
+    const uint32_t n_tmp_bv = (uint32_t)kMultiKeys;
+    if (hipMalloc(&tmp_col.p, n_new * 8 + 16) != hipSuccess || hipMalloc(&tmp_valid.p, slice_words * 8) != hipSuccess ||
+        hipMalloc(&tmp_bits.p, slice_words * 8 * n_tmp_bv) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "append staging allocation failed");
+    for (auto& kv : t->cols) {
+        const int col = kv.first;
+        Column& c = kv.second;
+        const uint32_t i = at[col];
+        const uint64_t esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
+        HIP_CHECK(hipMemcpyAsync(tmp_col.p, data[i], n_new * esz, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(static_cast<char*>(const_cast<void*>(c.data)) + n_old * esz, tmp_col.p, n_new * esz,
+                                 hipMemcpyDeviceToDevice, s));
+        const uint64_t* slice_valid = nullptr;
+        if (validity && validity[i]) {
+            HIP_CHECK(hipMemsetAsync(tmp_valid.p, 0, slice_words * 8, s));
+            HIP_CHECK(hipMemcpyAsync(tmp_valid.p, validity[i], (n_new + 63) / 64 * 8, hipMemcpyHostToDevice, s));
+            if (n_new & 63) {  // bits past the appended rows are not rows
+                uint64_t last = validity[i][(n_new - 1) / 64] & ((1ull << (n_new & 63)) - 1);
+                HIP_CHECK(hipMemcpyAsync(static_cast<uint64_t*>(tmp_valid.p) + (n_new - 1) / 64, &last, 8,
+                                         hipMemcpyHostToDevice, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+            }
+            slice_valid = static_cast<const uint64_t*>(tmp_valid.p);
+            if (!c.validity) {  // first NULLs of the column: the old rows are all valid
+                auto b = std::make_unique<DevBuf>();
+                if (int rc = alloc_table_bv(t, *b)) return fail(rc, "validity allocation failed");
+                if (n_old) HIP_CHECK(launch_fill_valid(static_cast<uint64_t*>(b->p), n_old, s));
+                c.validity = static_cast<const uint64_t*>(b->p);
+                c.owned.push_back(std::move(b));
+            }
+            HIP_CHECK(launch_splice_bits(const_cast<uint64_t*>(c.validity), slice_valid, n_old, n_new, s));
+        } else if (c.validity) {  // a column with NULLs gets all-valid rows
+            HIP_CHECK(launch_fill_valid(static_cast<uint64_t*>(tmp_valid.p), n_new, s));
+            HIP_CHECK(launch_splice_bits(const_cast<uint64_t*>(c.validity), static_cast<const uint64_t*>(tmp_valid.p),
+                                         n_old, n_new, s));
+        }
+        Index* ixs[2] = {t->idx.count(col) ? &t->idx[col] : nullptr, t->bins.count(col) ? &t->bins[col] : nullptr};
+        if (!ixs[0] && !ixs[1]) continue;
+        // statistics of the appended slice (+ its distinct values for an every-distinct-value index)
+        bool want_distinct = ixs[0] && ixs[0]->exact_all;
+        std::vector<int64_t> added;
+        int64_t smin = 0, smax = 0;
+        bool sany = false;
+        int rc = value_stats(t, tmp_col.p, c.type, slice_valid, n_new, added, want_distinct, smin, smax, sany);
+        if (rc == CUBIT_ERR_UNSUPPORTED && want_distinct) {  // too wide a span for a presence bitmap
+            ixs[0]->exact_all = false;
+            want_distinct = false;
+            rc = value_stats(t, tmp_col.p, c.type, slice_valid, n_new, added, false, smin, smax, sany);
+        }
+        if (rc) return rc;
+        for (Index* ix : ixs) {
+            if (!ix) continue;
+            const int enc = ix->encoding;
+            const size_t n_bv = index_bv_count(*ix);
+            while (ix->owned.size() < n_bv) {  // an index built on an empty partition has no bitvectors yet
+                auto b = std::make_unique<DevBuf>();
+                if (int rc2 = alloc_table_bv(t, *b)) return fail(rc2, "index bitvector allocation failed");
+                ix->owned.push_back(std::move(b));
+            }
+            ix->bvs.resize(n_bv);
+            for (size_t k = 0; k < n_bv; ++k) ix->bvs[k] = static_cast<uint64_t*>(ix->owned[k]->p);
+            ix->bytes = ix->owned.size() * t->cap_words * 8;
+            const int cmp = enc == CUBIT_INDEX_BINS ? kCmpBetween : enc == CUBIT_INDEX_RANGE ? CUBIT_CMP_LT : CUBIT_CMP_EQ;
+            for (size_t k0 = 0; k0 < n_bv; k0 += kMultiKeys) {
+                MultiKeyArgs mk{};
+                for (size_t k = k0; k < std::min(n_bv, k0 + kMultiKeys); ++k) {
+                    mk.c[mk.m] = ix->keys[k];
+                    mk.c2[mk.m] = enc == CUBIT_INDEX_BINS ? ix->keys[k + 1] : 0;
+                    mk.out[mk.m] = static_cast<uint64_t*>(tmp_bits.p) + (uint64_t)mk.m * slice_words;
+                    ++mk.m;
+                }
+                HIP_CHECK(launch_compare_bitvectors(tmp_col.p, c.type, slice_valid, n_new, cmp, mk, s));
+                for (uint32_t m = 0; m < mk.m; ++m)
+                    HIP_CHECK(launch_splice_bits(ix->bvs[k0 + m], mk.out[m], n_old, n_new, s));
+            }
+            if (sany) {
+                const bool was_empty = ix->empty;
+                const int64_t old_min = ix->vmin;
+                ix->vmin = was_empty ? smin : std::min(ix->vmin, smin);
+                ix->vmax = was_empty ? smax : std::max(ix->vmax, smax);
+                ix->empty = false;
+                // the new keys' bitvectors span the whole column: counted with the new rows
+                t->n_rows = n_total;
+                t->nwp = need_words;
+                rc = maintain_exact_keys(t, col, *ix, added, old_min, was_empty);
+                t->n_rows = n_old;
+                t->nwp = padded_words(n_old);
+                if (rc) return rc;
+            }
+        }
+        HIP_CHECK(hipStreamSynchronize(s));  // tmp_col / tmp_valid reused by the next column
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    t->n_rows = n_total;
+    t->nwp = need_words;
+    if (insert_id) {
+        t->ins.push_back({(int64_t)n_old, (int64_t)n_total, insert_id});
+        std::stable_sort(t->ins.begin(), t->ins.end(), [](const auto& a, const auto& b) { return a.id < b.id; });
+    }
+    drop_derived(t);
+    return CUBIT_OK;
+}
+
+// Merge committed updates of one column into its base values and indexes (the checkpoint of
+// update chains; CUBIT folds its update bitvectors into the index the same way). Every record
+// with version < horizon — visible to every snapshot the caller still serves (start_time ≥
+// horizon, as DuckDB's lowest active start bounds what a checkpoint may fold) — leaves the
+// update list: each row takes its newest such value (records of a row are chronological; the
+// merged records are the row's prefix below horizon) and becomes valid, and every index
+// bitvector of the column flips the rows whose predicate changed (merge_rows_kernel). Records
+// at or past horizon stay in the list. *n_merged (optional) = rows whose base changed.
+extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horizon, uint64_t* n_merged) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    if (n_merged) *n_merged = 0;
+    auto cit = t->cols.find(col);
+    if (cit == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    auto uit = t->upd.find(col);
+    if (uit == t->upd.end() || uit->second.n == 0) return CUBIT_OK;
+    if (int rc = set_device(t->ctx)) return rc;
+    hipStream_t s = t->ctx->stream;
+    Column& c = cit->second;
+    const Updates& u = uit->second;
+    std::vector<int64_t> m_rows, m_vals, k_rows, k_vals;
+    std::vector<uint64_t> k_vers;
+    for (uint64_t i = 0; i < u.n;) {
+        uint64_t j = i;
+        while (j < u.n && u.h_rows[j] == u.h_rows[i]) ++j;
+        uint64_t p = i;  // merged prefix [i, p)
+        while (p < j && u.h_versions[p] < horizon) ++p;
+        if (p > i) {
+            const int64_t v = u.h_values[p - 1];
+            if (c.type == CUBIT_TYPE_INT32 && (v < INT32_MIN || v > INT32_MAX))
+                return fail(CUBIT_ERR_INVALID, "row %lld: value %lld does not fit an INT32 column",
+                            (long long)u.h_rows[i], (long long)v);
+            m_rows.push_back(u.h_rows[i]);
+            m_vals.push_back(v);
+        }
+        for (uint64_t q = p; q < j; ++q) {
+            k_rows.push_back(u.h_rows[q]);
+            k_vals.push_back(u.h_values[q]);
+            k_vers.push_back(u.h_versions[q]);
+        }
+        i = j;
+    }
+    if (m_rows.empty()) return CUBIT_OK;
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (int rc = own_column(t, c, std::max<uint64_t>(t->n_rows, c.cap_rows))) return rc;
+    const uint64_t m = m_rows.size();
+    DevBuf d_rows, d_vals;
+    if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "merge list allocation failed");
+    HIP_CHECK(hipMemcpyAsync(d_rows.p, m_rows.data(), m * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_vals.p, m_vals.data(), m * 8, hipMemcpyHostToDevice, s));
+    Index* ixs[2] = {t->idx.count(col) ? &t->idx[col] : nullptr, t->bins.count(col) ? &t->bins[col] : nullptr};
+    MergeIndex mi[2] = {};
+    DevBuf d_keys[2], d_bvs[2];
+    for (int x = 0; x < 2; ++x) {
+        Index* ix = ixs[x];
+        if (!ix || index_bv_count(*ix) == 0 || ix->bvs.size() != index_bv_count(*ix)) continue;
+        if (hipMalloc(&d_keys[x].p, ix->keys.size() * 8) != hipSuccess ||
+            hipMalloc(&d_bvs[x].p, ix->bvs.size() * sizeof(uint64_t*)) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "merge index descriptor allocation failed");
+        HIP_CHECK(hipMemcpyAsync(d_keys[x].p, ix->keys.data(), ix->keys.size() * 8, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_bvs[x].p, ix->bvs.data(), ix->bvs.size() * sizeof(uint64_t*), hipMemcpyHostToDevice, s));
+        mi[x].keys = static_cast<const int64_t*>(d_keys[x].p);
+        mi[x].bvs = static_cast<uint64_t* const*>(d_bvs[x].p);
+        mi[x].n_keys = (uint32_t)ix->keys.size();
+        mi[x].encoding = ix->encoding == CUBIT_INDEX_RANGE ? 0 : ix->encoding == CUBIT_INDEX_EQUALITY ? 1 : 2;
+    }
+    HIP_CHECK(launch_merge_rows(static_cast<const int64_t*>(d_rows.p), static_cast<const int64_t*>(d_vals.p), m,
+                                const_cast<void*>(c.data), c.type, const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    // statistics and exact keys for the merged values
+    std::vector<int64_t> added = m_vals;
+    std::sort(added.begin(), added.end());
+    added.erase(std::unique(added.begin(), added.end()), added.end());
+    for (Index* ix : ixs) {
+        if (!ix) continue;
+        const bool was_empty = ix->empty;
+        const int64_t old_min = ix->vmin;
+        ix->vmin = was_empty ? added.front() : std::min(ix->vmin, added.front());
+        ix->vmax = was_empty ? added.back() : std::max(ix->vmax, added.back());
+        ix->empty = false;
+        if (int rc = maintain_exact_keys(t, col, *ix, added, old_min, was_empty)) return rc;
+    }
+    // the records left (each row's suffix at or past horizon), still grouped and chronological
+    if (int rc = store_updates(t, col, k_rows.data(), k_vals.data(), k_vers.data(), k_rows.size())) return rc;
+    if (k_rows.empty()) t->upd.erase(col);
+    drop_derived(t);
+    if (n_merged) *n_merged = m;
+    return CUBIT_OK;
+}
+
 // ------------------------------------------------------------------ planner
 
 namespace {
+
+// An index as the planner may use it: its keys and bitvectors with statistics widened by the
+// column's update records (any version: wider bounds are always safe). Folding a constant
+// against the base statistics alone would drop rows whose visible updated value lies outside
+// them, and "every distinct value" exactness holds only while every updated value is a key.
+struct IndexView {
+    int encoding;
+    bool exact_all, empty;
+    int64_t vmin, vmax;
+    const std::vector<int64_t>& keys;
+    const std::vector<uint64_t*>& bvs;
+};
+
+IndexView view_of(const cubit_table* t, int col, const Index& ix) {
+    IndexView v{ix.encoding, ix.exact_all, ix.empty, ix.vmin, ix.vmax, ix.keys, ix.bvs};
+    auto uit = t->upd.find(col);
+    if (uit == t->upd.end() || uit->second.stat_values.empty()) return v;
+    const std::vector<int64_t>& uv = uit->second.stat_values;
+    v.vmin = ix.empty ? uv.front() : std::min(ix.vmin, uv.front());
+    v.vmax = ix.empty ? uv.back() : std::max(ix.vmax, uv.back());
+    v.empty = false;
+    if (v.exact_all) {
+        auto is_key = [&](int64_t x) { return std::binary_search(ix.keys.begin(), ix.keys.end(), x); };
+        if (ix.encoding == CUBIT_INDEX_RANGE) {
+            // values ⊆ keys ∪ {vmin}: the base minimum and every updated value
+            if (!ix.empty && ix.vmin != v.vmin && !is_key(ix.vmin)) v.exact_all = false;
+            for (int64_t x : uv)
+                if (x != v.vmin && !is_key(x)) {
+                    v.exact_all = false;
+                    break;
+                }
+        } else {
+            for (int64_t x : uv)
+                if (!is_key(x)) {
+                    v.exact_all = false;
+                    break;
+                }
+        }
+    }
+    return v;
+}
 
 struct Planner {
     cubit_table* t;
@@ -1410,7 +1883,7 @@ struct Planner {
     }
 
     // {v < c} from a range index; nullptr when the index cannot answer exactly
-    ExprP range_lt(int col, const Index& ix, int64_t c) {
+    ExprP range_lt(int col, const IndexView& ix, int64_t c) {
         if (ix.empty || c <= ix.vmin) return mk_false();
         if (c > ix.vmax) return nn(col);
         auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
@@ -1432,7 +1905,7 @@ struct Planner {
     // instead of K0's whole column. nullptr when the bin is estimated (uniform values over
     // [vmin, vmax]) to hold more than a quarter of the rows, where K0's sequential read of the
     // column is cheaper; rc is set on a launch or allocation failure.
-    ExprP candidate(int col, const Index& ix, int cmp, int64_t c) {
+    ExprP candidate(int col, const IndexView& ix, int cmp, int64_t c) {
         auto hi_it = std::upper_bound(ix.keys.begin(), ix.keys.end(), c);  // first key > c
         const bool has_lo = hi_it != ix.keys.begin(), has_hi = hi_it != ix.keys.end();
         const double lo_v = has_lo ? (double)*(hi_it - 1) : (double)ix.vmin;
@@ -1458,7 +1931,7 @@ struct Planner {
         return mk_leaf(l);
     }
 
-    ExprP eq_leaf(int col, const Index& ix, int64_t c, bool& exact) {
+    ExprP eq_leaf(int col, const IndexView& ix, int64_t c, bool& exact) {
         exact = true;
         auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
         if (it != ix.keys.end() && *it == c) {
@@ -1477,7 +1950,7 @@ struct Planner {
     ExprP constant(int col, int cmp, int64_t c) {
         auto ixit = t->idx.find(col);
         if (ixit != t->idx.end()) {
-            const Index& ix = ixit->second;
+            const IndexView ix = view_of(t, col, ixit->second);
             const bool top = c == INT64_MAX;
             if (ix.encoding == CUBIT_INDEX_RANGE) {
                 // {v < k}: an index leaf when k is a key, else the candidate check of k's bin
@@ -1556,7 +2029,7 @@ struct Planner {
     ExprP interval_from_bins(int col, int64_t lo, int64_t hi, bool has_lo, bool has_hi) {
         auto bit = t->bins.find(col);
         if (bit == t->bins.end()) return nullptr;
-        const Index& b = bit->second;
+        const IndexView b = view_of(t, col, bit->second);
         if (b.empty) return mk_false();
         const std::vector<int64_t>& e = b.keys;
         const size_t nb = e.size() - 1;
@@ -1946,10 +2419,9 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
 bool decodable_values(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes, int col,
                       std::vector<int64_t>& vals, std::vector<const uint64_t*>& leaves) {
     auto ixit = t->idx.find(col);
-    if (ixit == t->idx.end() || ixit->second.encoding != CUBIT_INDEX_RANGE || !ixit->second.exact_all ||
-        ixit->second.empty || n_nodes == 0)
-        return false;
-    const Index& ix = ixit->second;
+    if (ixit == t->idx.end() || n_nodes == 0) return false;
+    const IndexView ix = view_of(t, col, ixit->second);
+    if (ix.encoding != CUBIT_INDEX_RANGE || !ix.exact_all || ix.empty) return false;
     int64_t lo = ix.vmin, hi = ix.vmax;  // inclusive bounds
     bool bounded = false;
     // constants on col reachable through AND nodes only

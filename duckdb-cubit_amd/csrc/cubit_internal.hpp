@@ -167,4 +167,20 @@ hipError_t launch_update_mask(const int64_t* upd_rows, const uint64_t* upd_versi
                               uint64_t start_time, uint64_t transaction_id, uint64_t* mask, hipStream_t stream);
 hipError_t launch_fill_valid(uint64_t* words, uint64_t n_rows, hipStream_t stream);
 
+// Index maintenance. Append: splice n_bits bits of src (bit 0 = first appended row) into dst
+// at bit offset bit_off (dst words outside the splice untouched). Merge: base values of the
+// merged rows replaced (rows become valid) and the bits of every index bitvector whose
+// predicate changes for a row flipped. encoding: 0 range L(k) = {v < k}, 1 equality, 2 bins
+// (keys = edges, n_keys - 1 bitvectors); bvs = nullptr: no index.
+struct MergeIndex {
+    const int64_t* keys;  // device, sorted
+    uint64_t* const* bvs; // device array of bitvector pointers
+    uint32_t n_keys;
+    int32_t encoding;
+};
+hipError_t launch_splice_bits(uint64_t* dst, const uint64_t* src, uint64_t bit_off, uint64_t n_bits,
+                              hipStream_t stream);
+hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, uint64_t m, void* col, int type,
+                             uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1, hipStream_t stream);
+
 }  // namespace cubit

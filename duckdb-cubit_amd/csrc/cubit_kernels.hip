@@ -1417,6 +1417,109 @@ __global__ __launch_bounds__(256) void fill_valid_kernel(uint64_t* __restrict__ 
     }
 }
 
+// ------------------------------------------------------------------ index maintenance
+
+// Append (BoundIndex::Append, bound_index.hpp:67-70): splice the n_bits bits of src (bit 0 =
+// the first appended row) into dst at bit offset bit_off. One thread per destination word, so
+// no word is written twice; the first word keeps its bits below bit_off (the rows already
+// there) and the last keeps its bits past the splice (padding, zero). The appended rows'
+// bitvector words come from the index-build compare kernel run over the appended slice alone.
+__global__ __launch_bounds__(256) void splice_bits_kernel(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src,
+                                                          uint64_t bit_off, uint64_t n_bits) {
+    const uint64_t w0 = bit_off >> 6, w1 = (bit_off + n_bits + 63) >> 6;
+    const uint32_t sh = (uint32_t)(bit_off & 63);
+    const uint64_t src_words = (n_bits + 63) >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t d = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < w1; d += stride) {
+        const uint64_t j = d - w0;  // src word whose low bits land in d (shifted up by sh)
+        uint64_t v = j < src_words ? src[j] << sh : 0ull;
+        if (sh && j >= 1 && j - 1 < src_words) v |= src[j - 1] >> (64 - sh);
+        // bits of d that belong to the splice: rows [max(64d, bit_off), min(64d + 64, bit_off + n_bits))
+        const uint64_t lo = d == w0 ? sh : 0;
+        const uint64_t end = bit_off + n_bits - 64 * d;  // > 0
+        const uint64_t hi = end >= 64 ? 64 : end;
+        const uint64_t m = (hi == 64 ? ~0ull : ((1ull << hi) - 1)) & ~((1ull << lo) - 1);
+        dst[d] = (dst[d] & ~m) | (v & m);
+    }
+}
+
+// Merge of committed updates into the base (the checkpoint of update chains, cf.
+// UpdateSegment / ColumnData checkpointing; CUBIT merges its update bitvectors the same way):
+// row r gets its newest merged value, becomes valid (an UPDATE of a NULL sets it), and every
+// index bitvector whose predicate changes for r flips r's bit. Rows are distinct, so each
+// thread owns its row's value; bits of one word may belong to several threads, so bits flip
+// with atomicXor (commutative: the order of the flips does not matter). Only the keys whose
+// predicate changes are touched: for a range index L(k) = {v < k}, the keys in
+// (min(old, new), max(old, new)] (binary search over the sorted keys); for an equality index
+// E(old) and E(new); for bins the old and the new bin.
+__device__ __forceinline__ uint32_t upper_key(const int64_t* keys, uint32_t n, int64_t v) {  // first key > v
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (keys[mid] <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void flip_bit(uint64_t* bv, int64_t r) {
+    atomicXor(reinterpret_cast<unsigned long long*>(&bv[r >> 6]), 1ull << (r & 63));
+}
+
+__global__ __launch_bounds__(256) void merge_rows_kernel(const int64_t* __restrict__ rows,
+                                                         const int64_t* __restrict__ values, uint64_t m, void* col,
+                                                         int type, uint64_t* validity, MergeIndex ix0, MergeIndex ix1) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const int64_t r = rows[i];
+        const int64_t nv = values[i];
+        const bool old_valid = !validity || ((validity[r >> 6] >> (r & 63)) & 1ull);
+        int64_t ov;
+        if (type == 0) {
+            ov = static_cast<int32_t*>(col)[r];
+            static_cast<int32_t*>(col)[r] = (int32_t)nv;
+        } else {
+            ov = static_cast<int64_t*>(col)[r];
+            static_cast<int64_t*>(col)[r] = nv;
+        }
+        if (!old_valid) atomicOr(reinterpret_cast<unsigned long long*>(&validity[r >> 6]), 1ull << (r & 63));
+        for (int x = 0; x < 2; ++x) {
+            const MergeIndex& ix = x ? ix1 : ix0;
+            if (!ix.bvs) continue;
+            const uint32_t n = ix.n_keys;
+            if (ix.encoding == 0) {  // range: L(k) = {valid, v < k}
+                uint32_t a, b;     // flip keys [a, b)
+                if (!old_valid) {
+                    a = upper_key(ix.keys, n, nv);  // new membership: every key > nv
+                    b = n;
+                } else {
+                    const int64_t lo = ov < nv ? ov : nv, hi = ov < nv ? nv : ov;
+                    a = upper_key(ix.keys, n, lo);
+                    b = upper_key(ix.keys, n, hi);  // keys in (lo, hi]
+                }
+                for (uint32_t k = a; k < b; ++k) flip_bit(ix.bvs[k], r);
+            } else if (ix.encoding == 1) {  // equality: E(k) = {valid, v == k}
+                if (old_valid && ov == nv) continue;
+                if (old_valid) {
+                    const uint32_t k = upper_key(ix.keys, n, ov);
+                    if (k > 0 && ix.keys[k - 1] == ov) flip_bit(ix.bvs[k - 1], r);
+                }
+                const uint32_t k = upper_key(ix.keys, n, nv);
+                if (k > 0 && ix.keys[k - 1] == nv) flip_bit(ix.bvs[k - 1], r);
+            } else {  // bins: B_i = {valid, e_i <= v < e_{i+1}}, n = edges
+                auto bin = [&](int64_t v) -> int64_t {
+                    const uint32_t k = upper_key(ix.keys, n, v);  // e_{k-1} <= v < e_k
+                    return (k == 0 || k == n) ? -1 : (int64_t)k - 1;
+                };
+                const int64_t ob = old_valid ? bin(ov) : -1, nb = bin(nv);
+                if (ob == nb) continue;
+                if (ob >= 0) flip_bit(ix.bvs[ob], r);
+                if (nb >= 0) flip_bit(ix.bvs[nb], r);
+            }
+        }
+    }
+}
+
 // A delete is in effect for the reader when UseInsertedVersion(start, tid, delete_id)
 // (chunk_info.cpp:11-19): clear that row.
 __global__ __launch_bounds__(256) void visibility_kernel(const int64_t* __restrict__ rows,
@@ -1747,6 +1850,22 @@ hipError_t launch_visibility(const int64_t* del_rows, const uint64_t* del_ids, u
     if (n_del == 0) return hipSuccess;
     hipLaunchKernelGGL(visibility_kernel, dim3(grid_for(n_del)), dim3(256), 0, stream, del_rows, del_ids, n_del,
                        start_time, transaction_id, words);
+    return hipGetLastError();
+}
+
+hipError_t launch_splice_bits(uint64_t* dst, const uint64_t* src, uint64_t bit_off, uint64_t n_bits,
+                              hipStream_t stream) {
+    if (n_bits == 0) return hipSuccess;
+    const uint64_t words = ((bit_off + n_bits + 63) >> 6) - (bit_off >> 6);
+    hipLaunchKernelGGL(splice_bits_kernel, dim3(grid_for(words)), dim3(256), 0, stream, dst, src, bit_off, n_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, uint64_t m, void* col, int type,
+                             uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1, hipStream_t stream) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(merge_rows_kernel, dim3(grid_for(m)), dim3(256), 0, stream, rows, values, m, col, type, validity,
+                       ix0, ix1);
     return hipGetLastError();
 }
 

@@ -177,6 +177,7 @@ class CubitTable:
         L.check(self.lib.cubit_table_add_bitpacked_column(self.handle, col, typ, data.ctypes.data, data.nbytes,
                                                           so.ctypes.data, sr.ctypes.data, len(so),
                                                           vw.ctypes.data if vw is not None else None))
+        self.types[col] = typ
 
     def column_data(self, col: int):
         """(device pointer, CUBIT type) of a registered column's values."""
@@ -233,6 +234,38 @@ class CubitTable:
         versions = np.ascontiguousarray(versions, dtype=np.uint64)
         L.check(self.lib.cubit_table_set_updates(self.handle, col, rows.ctypes.data, values.ctypes.data,
                                                  versions.ctypes.data, len(rows)))
+
+    # ------------------------------------------------------------------ index maintenance
+    def append(self, columns: Dict[int, np.ndarray], validity: Optional[Dict[int, np.ndarray]] = None,
+               insert_id: int = 0) -> None:
+        """Append rows (RowGroupCollection::Append + BoundIndex::Append): one array per
+        registered column, of the column's dtype; validity = LSB-first words per column (bit 0
+        = the first appended row), absent = all valid. insert_id != 0 hides the rows from
+        snapshots that predate it (an insert range)."""
+        cols = sorted(columns)
+        n_new = len(columns[cols[0]]) if cols else 0
+        keep = []
+        for c in cols:
+            a = np.ascontiguousarray(columns[c])
+            want = np.int32 if self.types.get(c) == L.TYPE_INT32 else np.int64
+            if a.dtype != want or len(a) != n_new:
+                raise ValueError(f"column {c}: {len(a)} values of {a.dtype}, want {n_new} of {np.dtype(want)}")
+            keep.append(a)
+        vkeep = []
+        for c in cols:
+            v = None if validity is None else validity.get(c)
+            vkeep.append(None if v is None else np.ascontiguousarray(v, dtype=np.uint64))
+        cid = (C.c_int * max(len(cols), 1))(*cols)
+        dptr = (C.c_void_p * max(len(cols), 1))(*[a.ctypes.data for a in keep])
+        vptr = (C.c_void_p * max(len(cols), 1))(*[(v.ctypes.data if v is not None else None) for v in vkeep])
+        L.check(self.lib.cubit_table_append(self.handle, n_new, cid, dptr, vptr, len(cols), int(insert_id)))
+        self.n_rows += n_new
+
+    def merge_updates(self, col: int, horizon: int) -> int:
+        """Fold the update records of `col` below `horizon` into the base and its indexes."""
+        n = C.c_uint64()
+        L.check(self.lib.cubit_table_merge_updates(self.handle, col, int(horizon), C.byref(n)))
+        return int(n.value)
 
     # ------------------------------------------------------------------ scan
     def scan_into(self, plan_nodes, rowids_dptr: int, capacity: int, count_dptr: int,

@@ -225,6 +225,26 @@ int cubit_table_set_updates(cubit_table *t, int col, const int64_t *rows, const 
 int cubit_table_set_inserts(cubit_table *t, const int64_t *row_begin, const int64_t *row_end, const uint64_t *ids,
                             uint64_t n);
 
+/* Index maintenance. Append n_new rows to the partition
+ * (RowGroupCollection::Append, src/storage/table/row_group_collection.cpp, with every index's
+ * BoundIndex::Append, src/include/duckdb/execution/index/bound_index.hpp:67-70): data[i] /
+ * validity[i] are host arrays for column cols[i], one entry per registered column; validity[i]
+ * = NULL (or validity = NULL) means all valid, else LSB-first words with bit 0 = the first
+ * appended row. The new rows get local ids n_rows … n_rows+n_new-1; every index on every column
+ * is maintained in place (bitvectors of the appended slice spliced in at bit n_rows; statistics
+ * widened; an every-distinct-value index gains keys for values it has not seen). insert_id != 0
+ * records [n_rows, n_rows+n_new) as an insert range of that transaction (see set_inserts);
+ * 0 = visible to every snapshot. Storage grows geometrically when the padding runs out. */
+int cubit_table_append(cubit_table *t, uint64_t n_new, const int *cols, const void *const *data,
+                       const uint64_t *const *validity, uint32_t n_cols, uint64_t insert_id);
+/* Merge the update records of `col` with version < horizon into the base values and the
+ * column's indexes (the checkpoint of update chains, UpdateSegment, update_segment.cpp;
+ * CUBIT's merge of its update bitvectors): each row takes its newest merged value and becomes
+ * valid, and the index bitvectors flip the rows whose predicate changed. Only snapshots with
+ * start_time >= horizon may be served afterwards (as the reference folds versions only below
+ * the lowest active start). Records at or past horizon stay. *n_merged = rows merged. */
+int cubit_table_merge_updates(cubit_table *t, int col, uint64_t horizon, uint64_t *n_merged);
+
 /* The scan: evaluate a predicate tree (prefix nodes) for transaction `txn` (NULL = see
  * every committed row, no MVCC delta applied) and write the qualifying row ids into
  * d_rowids (tile runs, or ascending with CUBIT_SCAN_ORDERED), the count into *d_count. Replaces TableScanFunc → DataTable::Scan →

@@ -315,6 +315,28 @@ int main(int argc, char** argv) {
                       a.num_tiles = dtiles;
                       CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
                   }, 3});
+    // K = 1 breakdown: no claim (fixed offsets), uniform fake decode, both; the streaming floor
+    // of the same bytes (1 leaf read + 1,310 ids per tile written as 16 B runs)
+#define K1D(NAME, D)                                                                                           \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      k1(a);                                                                                  \
+                      a.num_tiles = dtiles;                                                                   \
+                      hipLaunchKernelGGL((eval_decode_pairs<1, 2, 4096, 512, D, FORM_CONJ>),                  \
+                                         dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir); \
+                  }, 3})
+    K1D("K1 1% diag no-claim", 1);
+    K1D("K1 1% diag fake-decode", 2);
+    K1D("K1 1% diag no-claim fake", 3);
+    vs.push_back({"K1 1% floor: 16B ids", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<1, 1310, 2>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
+    vs.push_back({"K1 1% floor: LDS stage", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((stream_floor<1, 1310, 4>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
+                  }, 3});
     vs.push_back({"K1 1% pairs P1", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
                       a.num_tiles = (uint32_t)(pw / 1024);

@@ -106,7 +106,7 @@ def test_random_filter_sets_with_updates_and_deletes(ctx):
     upd = {}
     for c in range(3):
         rows = np.sort(rng.choice(n, size=3000, replace=False)).astype(np.int64)
-        vals = rng.integers(0, 50, len(rows)).astype(np.int64)
+        vals = rng.integers(-5, 56, len(rows)).astype(np.int64)  # also outside the base statistics
         vers = np.where(rng.random(len(rows)) < 0.5, np.uint64(3), np.uint64(writer)).astype(np.uint64)
         t.set_updates(c, rows, vals, vers)
         upd[c] = (rows, vals, vers)

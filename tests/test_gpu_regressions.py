@@ -162,3 +162,42 @@ def test_stream_switch_between_scans(ctx):
     c2.set_stream(None)
     t.close()
     c2.close()
+
+
+def test_updates_outside_index_statistics(ctx):
+    """Round 2: the planner folded constants against the index's base statistics (vmin / vmax,
+    every-distinct-value exactness) alone, so a visible update to a value outside them was
+    dropped (e.g. `v < -3` folded to FALSE while an update set a row to -7). The statistics are
+    now widened with the update values, as DuckDB's zonemaps consult update statistics
+    (standard_column_data.cpp:50-57)."""
+    rng = np.random.default_rng(12)
+    n = 70_001
+    t = CubitTable(ctx, n)
+    cols = []
+    for c, enc in enumerate((L.INDEX_RANGE, L.INDEX_EQUALITY, L.INDEX_RANGE)):
+        d = rng.integers(0, 50, n).astype(np.int64)
+        t.add_column(c, d)
+        t.build_index(c, enc, [10, 20, 30, 40] if c == 2 else None)
+        if c == 2:
+            t.build_index(c, L.INDEX_BINS, [0, 10, 20, 30, 40, 50])
+        rows = np.array([5, 77, 1000, 5000, 60_000], dtype=np.int64)
+        vals = np.array([-7, 80, 23, 55, -1], dtype=np.int64)  # 23: inside, the rest outside [0, 50)
+        vers = np.array([1, 1, 1, 1, 9], dtype=np.uint64)
+        t.set_updates(c, rows, vals, vers)
+        cols.append(O.Column(d, updates=(rows, vals, vers)))
+    for start in (2, 10):
+        tx = L.Txn(start, TXN_START_REG + start)
+        for c in range(3):
+            for cmp, k in (("<", -3), ("<", 0), ("<=", -7), ("=", -7), ("=", 80), (">", 60), (">=", 50),
+                           ("!=", 23), ("=", -1), ("<", 51), (">", -8)):
+                fs = F.TableFilterSet({c: F.ConstantFilter(cmp, k)})
+                ref = O.table_scan(cols, F.serialize(fs), n, tx=O.Mvcc(start, TXN_START_REG + start))
+                got = t.scan(fs, txn=tx)
+                assert np.array_equal(got, ref), (start, c, cmp, k)
+            fs = F.TableFilterSet({c: F.ConjunctionAndFilter([F.ConstantFilter(">=", 50), F.ConstantFilter("<", 90)])})
+            ref = O.table_scan(cols, F.serialize(fs), n, tx=O.Mvcc(start, TXN_START_REG + start))
+            assert np.array_equal(t.scan(fs, txn=tx), ref), (start, c, "interval")
+    t.close()
+
+
+TXN_START_REG = 4611686018427388000
