@@ -73,6 +73,7 @@ struct cubit_ctx {
     uint64_t tmp_cap = 0;
     int64_t* partials = nullptr;
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
+    int decode_kernel = CUBIT_DECODE_AUTO;  // cubit_ctx_set_decode_kernel
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -176,7 +177,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     // the ticket word at once (768 tiles: 384 instead of 512, ≈11 ns each).
     const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
     const unsigned grid = (unsigned)(tiles <= max_grid ? tiles : tiles <= 2 * max_grid ? (tiles + 1) / 2 : max_grid);
-    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop));
+    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel));
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (ordered && rowids)
@@ -254,6 +255,14 @@ int cubit_ctx_set_stream(cubit_ctx* ctx, void* stream) {
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
     }
     ctx->stream = next;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_set_decode_kernel(cubit_ctx* ctx, int kernel) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "null context");
+    if (kernel < CUBIT_DECODE_AUTO || kernel > CUBIT_DECODE_RUNS) return fail(CUBIT_ERR_INVALID, "decode kernel %d", kernel);
+    CUBIT_LOCK(ctx);
+    ctx->decode_kernel = kernel;
     return CUBIT_OK;
 }
 

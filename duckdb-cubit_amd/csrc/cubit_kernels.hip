@@ -684,6 +684,253 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     if ((DIAG & 4) && t == 0) g_diag_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Run-claimed evaluate + decode: the workgroup keeps decoding tiles into one LDS stage (a
+// *run*) until the next tile would not fit (or the run holds MAXT tiles), then claims the whole
+// run with ONE returning atomic and switches to the other stage; the claim returns while the
+// next tile is evaluated, and the closed run is copied out (16-byte stores) after that tile's
+// scan barrier. The claim count follows the output volume (≈ q / RUN_CAP + workgroups) instead
+// of the tile count (pairs: one per two tiles), and a tile costs one block barrier instead of
+// one and a half. A stage entry is the row's offset from the run's first tile row (a unit is
+// G·TILE_ROWS further; a run spans at most MAXU units so that fits 32 bits), so the copy-out adds
+// one base per run. Tiles with more than RUN_CAP hits claim on
+// their own and write straight to the output (dense path). The directory gets {start, len} per
+// tile ({0, 0} for empty tiles) as with pairs.
+// Workgroup g takes tiles g, g+G, … (static striding). A dynamic hand-out of the last third of
+// the tiles from per-XCD heads (scripts/kbench.hip) evened the workgroups' end
+// times (spread 25 → 14 µs) but slowed every workgroup more than that gained: its dequeue is a
+// returning atomic that the next wait on the leaf loads (vmcnt counts in order) also waits for.
+template <int K, int PAIRS, int RUN_CAP, int THREADS, int FORM = FORM_POSTFIX, int MAXT = 16, bool STAMP = false>
+__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(EvalArgs a, uint64_t* __restrict__ dir) {
+    // STAMP (scripts/kbench.hip only): each workgroup's start / end (s_memrealtime) into g_diag_times
+    if (STAMP && threadIdx.x == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    constexpr int NW = 2 * PAIRS;
+    constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
+    constexpr int FPW = 64 / FB;
+    constexpr uint64_t FMASK = (FB == 16) ? 0xffffull : 0xffffffffull;
+    constexpr int NPK = (PAIRS + FPW - 1) / FPW;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
+    static_assert(MAXT <= 64, "directory entries per run");
+    constexpr int NWAVES = THREADS / 64;
+    constexpr bool EARLY = K <= 4;
+    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+    __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
+    __shared__ uint64_t s_off;        // claimed base of the run being copied out
+    __shared__ uint64_t s_dense_off;  // claimed base of a dense tile
+    __shared__ uint32_t s_stage[2][RUN_CAP];
+    __shared__ uint32_t s_rt[2][MAXT], s_ro[2][MAXT], s_rc[2][MAXT];  // run tiles: tile, offset, count
+    __shared__ uint32_t s_rn[2], s_rfill[2], s_rfirst[2];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const uint32_t G = gridDim.x;
+    // offsets (u - u_first)·G·TILE_ROWS + row must fit 32 bits
+    const uint32_t MAXU = (uint32_t)((1ull << 32) / ((uint64_t)G * TILE_ROWS)) < 64
+                              ? (uint32_t)((1ull << 32) / ((uint64_t)G * TILE_ROWS)) : 64u;
+    if (MAXU < 1) __builtin_trap();
+    const bool write_ids = a.rowids != nullptr;
+    uint64_t pend_claim = 0;  // thread 0: the closed run's claimed base
+    uint64_t mine = 0;        // thread 0: rows claimed by this workgroup
+
+    u64x2 v[K][PAIRS];
+    uint32_t tile = blockIdx.x;
+    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+
+    // copy out closed run rs at s_off (published before the preceding barrier) and write its
+    // directory entries
+    auto copy_out = [&](int rs) {
+        const uint64_t base = s_off;
+        const uint32_t n = s_rfill[rs];
+        const uint32_t nt = s_rn[rs];
+        if (dir && t < (int)nt) {
+            dir[2 * s_rt[rs][t]] = s_rc[rs][t] ? base + s_ro[rs][t] : 0;
+            dir[2 * s_rt[rs][t] + 1] = s_rc[rs][t];
+        }
+        if (write_ids && n) {
+            const int64_t row0 = a.row_base + (int64_t)((uint64_t)s_rfirst[rs] * TILE_ROWS);
+            int64_t* out = a.rowids + base;
+            const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
+            auto id = [&](uint32_t i) -> int64_t { return row0 + (int64_t)s_stage[rs][i]; };
+            if (t == 0 && head && base < a.capacity) out[0] = id(0);
+            const uint64_t room = a.capacity > base ? a.capacity - base : 0;
+            for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
+                if (i + 1 < n && i + 1 < room) {
+                    i64x2 val;
+                    val.x = id(i);
+                    val.y = id(i + 1);
+                    *reinterpret_cast<i64x2*>(out + i) = val;
+                } else if (i < room) {
+                    out[i] = id(i);
+                }
+            }
+        }
+    };
+
+    int rs = 0;              // the open run's stage
+    uint32_t fill = 0, rn = 0, u_first = 0;  // open run: entries, tiles, first unit (uniform)
+    bool pending = false;    // a closed run (stage rs ^ 1) waits for its claim and copy-out
+    uint32_t u = 0;
+    while (tile < a.num_tiles) {
+        const int par = (int)(u & 1);
+        const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+        const uint32_t next = tile + G;
+        uint64_t r[NW];
+        eval_words<K, NW, FORM>(a.prog, v, r);
+        if (EARLY && next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        tail_mask<NW, THREADS>(a, tile_word0, t, r);
+        if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+        uint64_t packed[NPK], incl[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) packed[q] = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p)
+            packed[p / FPW] |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            incl[q] = wave_incl_scan(packed[q], lane);
+            if (lane == 63) s_wave_tot[par][wave][q] = incl[q];
+        }
+        if (pending && t == 0) s_off = pend_claim;  // the closed run's claim returned meanwhile
+        __syncthreads();
+        uint64_t block_tot[NPK], wave_pre[NPK];
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) {
+            uint64_t wp = 0, bt = 0;
+#pragma unroll
+            for (int w = 0; w < NWAVES; ++w) {
+                const uint64_t x = s_wave_tot[par][w][q];
+                if (w < wave) wp += x;
+                bt += x;
+            }
+            block_tot[q] = bt;
+            wave_pre[q] = wp;
+        }
+        uint32_t pair_off[PAIRS];
+        uint32_t tile_count = 0;
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            pair_off[p] = tile_count +
+                          (uint32_t)(((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
+            tile_count += (uint32_t)((block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK);
+        }
+        const bool dense = tile_count > (uint32_t)RUN_CAP;
+        // close the open run when this tile does not fit (claimed after the previous run's
+        // copy-out: issuing the claim before it measured 3 µs slower at K = 5)
+        const bool close = !dense && rn > 0 &&
+                           (fill + tile_count > (uint32_t)RUN_CAP || rn == (uint32_t)MAXT || u - u_first >= MAXU);
+        const bool copied = pending;
+        if (pending) {
+            copy_out(rs ^ 1);
+            pending = false;
+        }
+        if (!EARLY && next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        const int64_t row0 = a.row_base + (int64_t)tile_word0 * 64;
+        if (dense) {
+            // dense tile: its own claim, direct writes
+            if (t == 0) {
+                const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)tile_count);
+                mine += tile_count;
+                s_dense_off = c;
+                if (dir) {
+                    dir[2 * tile] = c;
+                    dir[2 * tile + 1] = tile_count;
+                }
+            }
+            __syncthreads();
+            const uint64_t base = s_dense_off;
+            if (write_ids) {
+#pragma unroll
+                for (int p = 0; p < PAIRS; ++p) {
+                    uint64_t off = base + pair_off[p];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        uint64_t w = r[2 * p + e];
+                        const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                        while (w) {
+                            if (off < a.capacity) a.rowids[off] = row0 + (int64_t)(wrow + (uint32_t)__builtin_ctzll(w));
+                            ++off;
+                            w &= w - 1;
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // s_dense_off free again
+        } else {
+            if (close) {
+                // one claim for the whole run (returns during the next tile)
+                if (t == 0) {
+                    s_rn[rs] = rn;
+                    s_rfill[rs] = fill;
+                    s_rfirst[rs] = blockIdx.x + u_first * G;
+                    pend_claim = 0;
+                    if (fill) {
+                        pend_claim = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)fill);
+                        mine += fill;
+                    }
+                }
+                pending = true;
+                rs ^= 1;
+                fill = 0;
+                rn = 0;
+                // the stage we switch to was copied out in this unit: every thread must be done
+                if (copied) __syncthreads();
+            }
+            if (rn == 0) u_first = u;
+            if (tile_count && write_ids) {
+                const uint32_t delta = (u - u_first) * G * (uint32_t)TILE_ROWS;
+#pragma unroll
+                for (int p = 0; p < PAIRS; ++p) {
+                    uint32_t off = fill + pair_off[p];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        uint64_t w = r[2 * p + e];
+                        const uint32_t wrow = delta + (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                        while (w) {
+                            s_stage[rs][off++] = wrow + (uint32_t)__builtin_ctzll(w);
+                            w &= w - 1;
+                        }
+                    }
+                }
+            }
+            if (t == 0) {
+                s_rt[rs][rn] = tile;
+                s_ro[rs][rn] = fill;
+                s_rc[rs][rn] = tile_count;
+            }
+            fill += tile_count;
+            ++rn;
+        }
+        tile = next;
+        ++u;
+    }
+    // drain: the closed run (if any), then the open one
+    if (pending) {
+        if (t == 0) s_off = pend_claim;
+        __syncthreads();
+        copy_out(rs ^ 1);
+    }
+    if (rn > 0) {
+        if (t == 0) {
+            s_rn[rs] = rn;
+            s_rfill[rs] = fill;
+            s_rfirst[rs] = blockIdx.x + u_first * G;
+            uint64_t c = 0;
+            if (fill) {
+                c = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)fill);
+                mine += fill;
+            }
+            pend_claim = c;
+        }
+        __syncthreads();  // s_off may still be read by the copy-out above
+        if (t == 0) s_off = pend_claim;
+        __syncthreads();
+        copy_out(rs);
+    }
+    if (t == 0) finish_ticket(a.ticket, a.count, mine);
+    if (STAMP && t == 0) g_diag_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
 // ------------------------------------------------------------------ K1+K3: fused filter + probe-sum
 
 __device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, __int128 x) {
@@ -1579,6 +1826,7 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 // STAGE 4,096 staged ids (16 KiB LDS); count tiles of 256 threads × 8 pairs = 4,096 words.
 // Chosen from the interleaved variant sweep in scripts/kbench.hip.
 constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
+constexpr int kRunCap = 2 * kDecodeStage;  // eval_decode_runs: the same 64 KiB of LDS stages
 // count tiles: 512 threads × 2 pairs = 2,048 words for K ≤ 4, × 1 pair above (two tiles in
 // flight must fit the 128-VGPR budget of 4 waves per SIMD)
 constexpr int count_pairs(uint32_t k) { return k <= 4 ? 2 : 1; }
@@ -1601,22 +1849,31 @@ uint32_t eval_form(const EvalProgram& p) {
     return is_conjunction(p) ? FORM_CONJ : FORM_POSTFIX;
 }
 
-// production decode: the pair-claimed kernel (scripts/kbench.hip: 83 µs vs 94 µs for the
-// per-tile claim kernel on SF100 Q6-shaped leaves)
+// production decode (scripts/kbench.hip): the run-claimed kernel wherever a
+// workgroup walks three or more tiles — one claim per filled LDS stage instead of one per pair
+// (SF100-sized, 1 % / 0.75 % / 0.4 % selected at K = 1 / 2 / 3: 41 / 39 / 44 µs vs 46 / 50 / 57
+// µs; K = 5 at 1.9 %: 82 vs 84 µs) — except K = 4, where at Q6's density a run holds two tiles
+// and the pair kernel measured as fast or 1 % faster (73.2 vs 74.2 µs); the pair kernel for one
+// or two tiles per workgroup (small inputs: one claim per workgroup either way).
 template <int K, int FORM>
-void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, FORM>), dim3(grid),
-                          dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
+void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                      int kernel) {
+    if (kernel == 2 || (kernel == 0 && K != 4 && a.num_tiles > 2ull * grid))
+        hipExtLaunchKernelGGL((eval_decode_runs<K, kDecodePairs, kRunCap, kDecodeThreads, FORM>), dim3(grid),
+                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
+    else
+        hipExtLaunchKernelGGL((eval_decode_pairs<K, kDecodePairs, kDecodeStage, kDecodeThreads, 0, FORM>), dim3(grid),
+                              dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
 }
 
 template <int K>
 hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
-                           hipEvent_t e1) {
+                           hipEvent_t e1, int kernel) {
     switch (eval_form(a.prog)) {
-    case FORM_CONJ: launch_decode_kf<K, FORM_CONJ>(a, dir, grid, s, e0, e1); break;
-    case FORM_DNF: launch_decode_kf<K, FORM_DNF>(a, dir, grid, s, e0, e1); break;
-    case FORM_CNF: launch_decode_kf<K, FORM_CNF>(a, dir, grid, s, e0, e1); break;
-    default: launch_decode_kf<K, FORM_POSTFIX>(a, dir, grid, s, e0, e1); break;
+    case FORM_CONJ: launch_decode_kf<K, FORM_CONJ>(a, dir, grid, s, e0, e1, kernel); break;
+    case FORM_DNF: launch_decode_kf<K, FORM_DNF>(a, dir, grid, s, e0, e1, kernel); break;
+    case FORM_CNF: launch_decode_kf<K, FORM_CNF>(a, dir, grid, s, e0, e1, kernel); break;
+    default: launch_decode_kf<K, FORM_POSTFIX>(a, dir, grid, s, e0, e1, kernel); break;
     }
     return hipGetLastError();
 }
@@ -1639,16 +1896,16 @@ hipError_t launch_count_k(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEv
 }
 
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1) {
+                              hipEvent_t e1, int kernel) {
     switch (a.prog.n_leaves) {
-    case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1);
-    case 2: return launch_decode_k<2>(a, dir, grid, s, e0, e1);
-    case 3: return launch_decode_k<3>(a, dir, grid, s, e0, e1);
-    case 4: return launch_decode_k<4>(a, dir, grid, s, e0, e1);
-    case 5: return launch_decode_k<5>(a, dir, grid, s, e0, e1);
-    case 6: return launch_decode_k<6>(a, dir, grid, s, e0, e1);
-    case 7: return launch_decode_k<7>(a, dir, grid, s, e0, e1);
-    case 8: return launch_decode_k<8>(a, dir, grid, s, e0, e1);
+    case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1, kernel);
+    case 2: return launch_decode_k<2>(a, dir, grid, s, e0, e1, kernel);
+    case 3: return launch_decode_k<3>(a, dir, grid, s, e0, e1, kernel);
+    case 4: return launch_decode_k<4>(a, dir, grid, s, e0, e1, kernel);
+    case 5: return launch_decode_k<5>(a, dir, grid, s, e0, e1, kernel);
+    case 6: return launch_decode_k<6>(a, dir, grid, s, e0, e1, kernel);
+    case 7: return launch_decode_k<7>(a, dir, grid, s, e0, e1, kernel);
+    case 8: return launch_decode_k<8>(a, dir, grid, s, e0, e1, kernel);
     default: return hipErrorInvalidValue;
     }
 }

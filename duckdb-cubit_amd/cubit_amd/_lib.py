@@ -28,6 +28,7 @@ OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2
 SCAN_CHECK_CAPACITY = 4  # synchronise; ERR_CAPACITY when the count exceeds the buffer
+DECODE_AUTO, DECODE_PAIRS, DECODE_RUNS = 0, 1, 2
 
 
 class FilterNode(C.Structure):
@@ -109,6 +110,7 @@ GPU_SIGNATURES = {
     "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),
     "cubit_table_set_inserts": (C.c_int, [_P, _P, _P, _P, _U64]),
     "cubit_table_append": (C.c_int, [_P, _U64, _P, _P, _P, C.c_uint32, _U64]),
+    "cubit_ctx_set_decode_kernel": (C.c_int, [_P, C.c_int]),
     "cubit_table_merge_updates": (C.c_int, [_P, C.c_int, _U64, _P]),
     "cubit_table_save_index": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
     "cubit_table_load_index": (C.c_int, [_P, C.c_int, C.c_char_p]),

@@ -30,6 +30,10 @@ class Context:
     def set_stream(self, stream: Optional[int]) -> None:
         L.check(self.lib.cubit_ctx_set_stream(self.handle, C.c_void_p(stream or 0)))
 
+    def set_decode_kernel(self, kernel: int) -> None:
+        """L.DECODE_AUTO (measured policy), L.DECODE_PAIRS or L.DECODE_RUNS."""
+        L.check(self.lib.cubit_ctx_set_decode_kernel(self.handle, kernel))
+
     def enable_timing(self, on: bool = True) -> None:
         L.check(self.lib.cubit_ctx_enable_timing(self.handle, 1 if on else 0))
 

@@ -113,6 +113,13 @@ int cubit_ctx_destroy(cubit_ctx *ctx);
 /* stream is a hipStream_t (NULL = the null stream). */
 int cubit_ctx_set_stream(cubit_ctx *ctx, void *stream);
 const char *cubit_last_error(void);
+/* Which evaluate + decode kernel the context's scans launch: AUTO (the measured policy: the
+ * run-claimed kernel when a workgroup walks three or more tiles and K != 4, else the
+ * pair-claimed one), or one of them always (tests and benchmarks). Results are identical. */
+#define CUBIT_DECODE_AUTO 0
+#define CUBIT_DECODE_PAIRS 1
+#define CUBIT_DECODE_RUNS 2
+int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
 /* Filter-kernel durations measured with HIP events recorded around each launch on the
  * context stream (ms); requires cubit_ctx_enable_timing(ctx, 1). */
 int cubit_ctx_enable_timing(cubit_ctx *ctx, int on);

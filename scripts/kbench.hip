@@ -213,6 +213,25 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<5, 2, 4096, 512, 0, FORM_CONJ>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
                                          dim3(512), 0, s, a, dir);
                   }, 0});
+    // run-claimed decode (one claim per LDS-stage-full run, one barrier per tile)
+    vs.push_back({"runs conj", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.negate = 0b01010;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_runs<5, 2, 8192, 512, FORM_CONJ>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
+                                         dim3(512), 0, s, a, dir);
+                  }, 0});
+    vs.push_back({"runs conj MAXT8", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.negate = 0b01010;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 5; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_runs<5, 2, 8192, 512, FORM_CONJ, 8>), dim3(std::min<unsigned>(dtiles, 2 * cus)),
+                                         dim3(512), 0, s, a, dir);
+                  }, 0});
     DT("tiles P2 T512 x2/CU", 2, 4096, 512, 2);
     DT("tiles P2 T512 grid=tiles", 2, 4096, 512, 1000000);
     DT("tiles P1 T512 x2/CU", 1, 2048, 512, 2);
@@ -273,6 +292,28 @@ int main(int argc, char** argv) {
                   }, 3});
     // (S3072 x3/CU: the 80-VGPR cap spills 192 B per thread, 199 µs — not viable)
     DK4("K4 conj S3072 x2/CU", 3072, 2);
+    vs.push_back({"K4 q6-density runs cap9984", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.leaf[3] = leaf[4];
+                      a.prog.n_leaves = 4;
+                      a.prog.negate = 0;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ>),
+                                         dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
+    vs.push_back({"K4 q6-density runs", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.leaf[3] = leaf[4];
+                      a.prog.n_leaves = 4;
+                      a.prog.negate = 0;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 8192, 512, FORM_CONJ>),
+                                         dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
     DPD("pairs diag no-claim", 1);
     DPD("pairs diag fake-decode", 2);
     DPD("pairs diag no-claim fake-decode", 3);
@@ -337,6 +378,39 @@ int main(int argc, char** argv) {
                       a.num_tiles = dtiles;
                       hipLaunchKernelGGL((stream_floor<1, 1310, 4>), dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, ids2);
                   }, 3});
+    vs.push_back({"K1 1% runs", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((eval_decode_runs<1, 2, 8192, 512, FORM_CONJ>),
+                                         dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
+    vs.push_back({"K1 1% runs grid=tiles/2", [&](EvalArgs& a, hipStream_t s) {
+                      k1(a);
+                      a.num_tiles = dtiles;
+                      hipLaunchKernelGGL((eval_decode_runs<1, 2, 8192, 512, FORM_CONJ>),
+                                         dim3(std::min<unsigned>((dtiles + 1) / 2, 2 * cus)), dim3(512), 0, s, a, dir);
+                  }, 3});
+    // K = 2 (1 % ∧ ¬25 %) and K = 3 (1 % ∧ ¬25 % ∧ ¬50 %), CONJ: pairs vs runs
+#define KPR(NAME, KK, NEG, RUNS)                                                                               \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.prog = EvalProgram{};                                                                 \
+                      a.prog.leaf[0] = leaf[5];                                                               \
+                      a.prog.leaf[1] = leaf[0];                                                               \
+                      a.prog.leaf[2] = leaf[2];                                                               \
+                      a.prog.n_leaves = KK;                                                                   \
+                      a.prog.negate = NEG;                                                                    \
+                      a.num_tiles = dtiles;                                                                   \
+                      if (RUNS)                                                                               \
+                          hipLaunchKernelGGL((eval_decode_runs<KK, 2, 8192, 512, FORM_CONJ>),                 \
+                                             dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir); \
+                      else                                                                                    \
+                          hipLaunchKernelGGL((eval_decode_pairs<KK, 2, 4096, 512, 0, FORM_CONJ>),             \
+                                             dim3(std::min<unsigned>(dtiles, 2 * cus)), dim3(512), 0, s, a, dir); \
+                  }, 3})
+    KPR("K2 0.75% pairs", 2, 0b10, false);
+    KPR("K2 0.75% runs", 2, 0b10, true);
+    KPR("K3 0.4% pairs", 3, 0b110, false);
+    KPR("K3 0.4% runs", 3, 0b110, true);
     vs.push_back({"K1 1% pairs P1", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
                       a.num_tiles = (uint32_t)(pw / 1024);
@@ -446,10 +520,9 @@ int main(int argc, char** argv) {
             }
         }
     }
-    // per-workgroup start / end stamps of the production K = 4 CONJ decode (Q6-like 2.3 %
-    // density): how much of the launch is dispatch ramp and how much is the tail after the
-    // first workgroup finishes (what dynamic tile scheduling could recover)
-    {
+    // per-workgroup start / end stamps of K = 4 CONJ decodes (Q6-like 2.3 % density): how much
+    // of the launch is dispatch ramp and how much is the tail after the first workgroup finishes
+    auto stamps = [&](const char* label, std::function<void(EvalArgs&, uint64_t*)> launch) {
         const unsigned grid = std::min<unsigned>(dtiles, 2 * cus);
         uint64_t* d_times;
         CK(hipMalloc(&d_times, 2 * grid * 8));
@@ -465,7 +538,7 @@ int main(int argc, char** argv) {
             a.prog.nops = 0;
             for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
             a.prog.ops = 0;
-            hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 4, FORM_CONJ>), dim3(grid), dim3(512), 0, 0, a, dir);
+            launch(a, d_times);
             CK(hipDeviceSynchronize());
             if (r == 0) continue;
             CK(hipMemcpy(h.data(), d_times, h.size() * 8, hipMemcpyDeviceToHost));
@@ -480,7 +553,6 @@ int main(int argc, char** argv) {
             tail.push_back((e1 - e0) / 100.0);
             span.push_back((e1 - s0) / 100.0);
             if (r == rounds) {
-                // the last round's end-time distribution, overall and per XCD (blockIdx % 8)
                 std::vector<double> ends;
                 double xsum[8] = {0}, xmax[8] = {0};
                 int xn[8] = {0};
@@ -492,30 +564,31 @@ int main(int argc, char** argv) {
                     xn[g % 8]++;
                 }
                 std::sort(ends.begin(), ends.end());
-                printf("  end times (us from first start): p0 %.1f p10 %.1f p25 %.1f p50 %.1f p75 %.1f p90 %.1f p100 %.1f\n",
-                       ends[0], ends[grid / 10], ends[grid / 4], ends[grid / 2], ends[3 * grid / 4], ends[9 * grid / 10],
-                       ends[grid - 1]);
-                printf("  per XCD mean/max end:");
+                printf("  [%s] end times (us from first start): p0 %.1f p10 %.1f p25 %.1f p50 %.1f p75 %.1f p90 %.1f p100 %.1f\n",
+                       label, ends[0], ends[grid / 10], ends[grid / 4], ends[grid / 2], ends[3 * grid / 4],
+                       ends[9 * grid / 10], ends[grid - 1]);
+                printf("  [%s] per XCD mean/max end:", label);
                 for (int x = 0; x < 8; ++x) printf(" %.1f/%.1f", xsum[x] / std::max(xn[x], 1), xmax[x]);
-                printf("\n  by tiles: ");
-                double t9 = 0, t8 = 0;
-                int n9 = 0, n8 = 0;
-                for (unsigned g = 0; g < grid; ++g) {
-                    const uint32_t tiles_g = (dtiles - g + grid - 1) / grid;
-                    const double e = (h[2 * g + 1] - s0) / 100.0;
-                    if (tiles_g == (dtiles + grid - 1) / grid) { t9 += e; ++n9; } else { t8 += e; ++n8; }
-                }
-                printf("%d WGs with more tiles end at %.1f mean, %d with fewer at %.1f mean\n", n9, t9 / std::max(n9, 1),
-                       n8, t8 / std::max(n8, 1));
+                printf("\n");
             }
         }
         auto med = [](std::vector<double> v) {
             std::sort(v.begin(), v.end());
             return v[v.size() / 2];
         };
-        printf("K4 conj 2.3%% per-WG stamps: start spread %.1f us, end spread %.1f us, first start -> last end %.1f us\n",
+        printf("%s per-WG stamps: start spread %.1f us, end spread %.1f us, first start -> last end %.1f us\n", label,
                med(ramp), med(tail), med(span));
         CK(hipFree(d_times));
+    };
+    {
+        const unsigned grid = std::min<unsigned>(dtiles, 2 * cus);
+        stamps("K4 pairs", [&](EvalArgs& a, uint64_t*) {
+            hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 4, FORM_CONJ>), dim3(grid), dim3(512), 0, 0, a, dir);
+        });
+        stamps("K4 runs", [&](EvalArgs& a, uint64_t*) {
+            hipLaunchKernelGGL((eval_decode_runs<4, 2, 8192, 512, FORM_CONJ, 16, true>), dim3(grid), dim3(512), 0, 0, a,
+                               dir);
+        });
     }
     const double alg = 8.0 * W * 5 + 8.0 * ref_count;
     printf("%-26s %10s %10s %10s\n", "variant", "median_us", "min_us", "alg_GB/s");

@@ -1,0 +1,147 @@
+"""The two evaluate + decode kernels — pair-claimed (eval_decode_pairs) and run-claimed
+(eval_decode_runs) — against the oracle's CPU bitmap evaluator, forced one at a time through
+cubit_ctx_set_decode_kernel and under the automatic policy.
+
+The run-claimed kernel keeps decoding a workgroup's tiles into one LDS stage until the next
+tile does not fit, so its interesting cases need workgroups that walk many tiles: tables of
+more than 2 × 512 tiles of 131,072 rows (the production grid is two workgroups per CU), with
+tiles of every kind — empty, sparse (many tiles per run, up to the 16-tile cap), around the
+8,192-entry stage (runs of one or two tiles, switches on consecutive tiles) and dense (more
+hits than a stage: the direct path). Row ids are compared bit-exactly, in tile-run order
+through the directory and in the ordered layout, with a row base offset.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from cubit_amd import _lib as L
+from cubit_amd import filters as F
+from cubit_amd.table import Context, CubitTable, padded_words, runs_in_row_order
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TILE_WORDS = 2048  # 131,072 rows
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.set_decode_kernel(L.DECODE_AUTO)
+    c.close()
+
+
+def rand_words(rng, n, k):
+    """AND of k random words: each bit set with probability 2^-k."""
+    w = rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+    for _ in range(k - 1):
+        w &= rng.integers(0, 2 ** 64, n, dtype=np.uint64)
+    return w
+
+
+def shaped_leaf(rng, n_rows):
+    """A leaf whose tiles differ: empty, 1/128, 1/16 (≈ one stage), all ones (dense)."""
+    nw = (n_rows + 63) // 64
+    tiles = (nw + TILE_WORDS - 1) // TILE_WORDS
+    kinds = rng.choice(4, size=tiles, p=[0.15, 0.55, 0.2, 0.1])
+    w = np.zeros(nw, dtype=np.uint64)
+    sparse = rand_words(rng, nw, 7)
+    mid = rand_words(rng, nw, 4)
+    for t, k in enumerate(kinds):
+        sl = slice(t * TILE_WORDS, min(nw, (t + 1) * TILE_WORDS))
+        if k == 1:
+            w[sl] = sparse[sl]
+        elif k == 2:
+            w[sl] = mid[sl]
+        elif k == 3:
+            w[sl] = ~np.uint64(0)
+    if n_rows & 63:
+        w[-1] &= np.uint64((1 << (n_rows & 63)) - 1)
+    return w
+
+
+def run_program(ctx, dleaves, k, neg, prog, n, base, out, cnt, ordered):
+    ptrs = (C.c_void_p * k)(*[d.ptr.value for d in dleaves[:k]])
+    p = (C.c_int32 * len(prog))(*prog)
+    L.check(ctx.lib.cubit_bitvector_eval(ctx.handle, ptrs, k, neg, p, len(prog), n, base, out.ptr, out.nbytes // 8,
+                                         cnt.ptr, None, L.SCAN_ORDERED if ordered else 0))
+    ctx.check()
+    c = int(cnt.download(np.uint64, 1)[0])
+    got = out.download(np.int64, c)
+    if not ordered:
+        d, _ = ctx.last_tiles()
+        assert int(d[:, 1].sum()) == c
+        got = runs_in_row_order(got, d)
+    return got
+
+
+@pytest.mark.parametrize("n", [1_000_003, 140_000_001])
+def test_pairs_and_runs_match_oracle(ctx, n):
+    rng = np.random.default_rng(n % 1000)
+    pw = padded_words(n)
+    nw = (n + 63) // 64
+    # leaf 0 shapes the tiles, the others are 1/2-density noise (so a CONJ of k leaves keeps
+    # ≈ 2^-(k-1) of leaf 0's rows), leaf 5 is sparse everywhere (for ORs)
+    host = [shaped_leaf(rng, n)] + [rand_words(rng, nw, 1) for _ in range(4)] + [rand_words(rng, nw, 8)]
+    for w in host[1:]:
+        if n & 63:
+            w[-1] &= np.uint64((1 << (n & 63)) - 1)
+    dleaves = [ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])) for w in host]
+    out = ctx.alloc(max(n // 2, 1024) * 8)
+    cnt = ctx.alloc(16)
+    programs = [  # (k, negate mask, postfix program)
+        (1, 0, [0]),
+        (2, 0, [0, 1, L.OP_AND]),
+        (2, 0b10, [0, 1, L.OP_AND]),
+        (3, 0b100, [0, 1, L.OP_AND, 2, L.OP_AND]),
+        (4, 0, [0, 1, L.OP_AND, 2, L.OP_AND, 3, L.OP_AND]),
+        (5, 0b01010, [0, 1, L.OP_AND, 2, L.OP_AND, 3, L.OP_AND, 4, L.OP_AND]),
+        (6, 0, [0, 1, L.OP_AND, 2, 3, L.OP_AND, L.OP_AND, 4, 5, L.OP_AND, L.OP_OR]),  # DNF-ish with a sparse OR arm
+    ]
+    for i, (k, neg, prog) in enumerate(programs):
+        ol = [(~host[j] if (neg >> j) & 1 else host[j]) for j in range(k)]
+        if neg and n & 63:
+            for j in range(k):
+                if (neg >> j) & 1:
+                    ol[j] = ol[j].copy()
+                    ol[j][-1] &= np.uint64((1 << (n & 63)) - 1)
+        ref, _ = O.bitmap_eval(ol, prog, n, 1_000_000_007)
+        assert len(ref) <= out.nbytes // 8
+        for kernel in (L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_AUTO):
+            ctx.set_decode_kernel(kernel)
+            for ordered in (False, True):
+                got = run_program(ctx, dleaves, k, neg, prog, n, 1_000_000_007, out, cnt, ordered)
+                assert np.array_equal(got, ref), (kernel, ordered, k, neg, prog)
+    ctx.set_decode_kernel(L.DECODE_AUTO)
+
+
+def test_auto_policy_large_table_scan(ctx):
+    """A 140 M-row table, K = 1..3 filters (the run-claimed kernel under the automatic policy):
+    every row id equals numpy's evaluation of the same predicate."""
+    rng = np.random.default_rng(4)
+    n = 140_000_001
+    a = rng.integers(0, 10_000, n, dtype=np.int32)
+    b = rng.integers(0, 100, n, dtype=np.int32)
+    t = CubitTable(ctx, n, row_base=77)
+    t.add_column(0, a)
+    t.add_column(1, b)
+    t.build_index(0, L.INDEX_RANGE, [50, 100, 5_000])
+    t.build_index(1, L.INDEX_RANGE)
+    cases = [
+        (F.TableFilterSet({0: F.ConstantFilter("<", 100)}), a < 100),
+        (F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 50), F.ConstantFilter("<", 100)])}),
+         (a >= 50) & (a < 100)),
+        (F.TableFilterSet({0: F.ConstantFilter("<", 5_000), 1: F.ConstantFilter("=", 42)}), (a < 5_000) & (b == 42)),
+    ]
+    for fs, mask in cases:
+        ref = np.flatnonzero(mask).astype(np.int64) + 77
+        for ordered in (False, True):
+            got = t.scan(fs, ordered=ordered)
+            if not ordered:
+                d, _ = ctx.last_tiles()
+                got = runs_in_row_order(got, d)
+            assert np.array_equal(got, ref)
+        assert t.count(fs) == len(ref)
+    t.close()
