@@ -74,6 +74,7 @@ struct cubit_ctx {
     int64_t* partials = nullptr;
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
     int decode_kernel = CUBIT_DECODE_AUTO;  // cubit_ctx_set_decode_kernel
+    int last_decode = 0;                    // kernel of the last decode (CUBIT_DECODE_PAIRS / _RUNS)
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -178,6 +179,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
     const unsigned grid = (unsigned)(tiles <= max_grid ? tiles : tiles <= 2 * max_grid ? (tiles + 1) / 2 : max_grid);
     HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel));
+    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (ordered && rowids)
@@ -263,6 +265,13 @@ int cubit_ctx_set_decode_kernel(cubit_ctx* ctx, int kernel) {
     if (kernel < CUBIT_DECODE_AUTO || kernel > CUBIT_DECODE_RUNS) return fail(CUBIT_ERR_INVALID, "decode kernel %d", kernel);
     CUBIT_LOCK(ctx);
     ctx->decode_kernel = kernel;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_last_decode_kernel(cubit_ctx* ctx, int* kernel) {
+    if (!ctx || !kernel) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    *kernel = ctx->last_decode;
     return CUBIT_OK;
 }
 

@@ -78,7 +78,9 @@ int decode_block_threads();
 // evaluate + decode into per-tile runs; dir (optional) gets {start, length} per tile
 // ev0 / ev1 (optional): events stamped by the kernel dispatch itself (hipExtLaunchKernel), so
 // their elapsed time is the kernel's execution, as rocprofv3's kernel trace reports it
-// kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed
+// kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed;
+// decode_kernel_for resolves it (1 or 2) for a launch
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel);
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream,
                               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int kernel = 0);
 // evaluate + count (and/or write the result bitvector)

@@ -1855,10 +1855,15 @@ uint32_t eval_form(const EvalProgram& p) {
 // µs; K = 5 at 1.9 %: 82 vs 84 µs) — except K = 4, where at Q6's density a run holds two tiles
 // and the pair kernel measured as fast or 1 % faster (73.2 vs 74.2 µs); the pair kernel for one
 // or two tiles per workgroup (small inputs: one claim per workgroup either way).
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel) {
+    if (kernel == 1 || kernel == 2) return kernel;
+    return n_leaves != 4 && num_tiles > 2ull * grid ? 2 : 1;
+}
+
 template <int K, int FORM>
 void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                       int kernel) {
-    if (kernel == 2 || (kernel == 0 && K != 4 && a.num_tiles > 2ull * grid))
+    if (decode_kernel_for(K, a.num_tiles, grid, kernel) == 2)
         hipExtLaunchKernelGGL((eval_decode_runs<K, kDecodePairs, kRunCap, kDecodeThreads, FORM>), dim3(grid),
                               dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
     else

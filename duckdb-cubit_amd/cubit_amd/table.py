@@ -34,6 +34,11 @@ class Context:
         """L.DECODE_AUTO (measured policy), L.DECODE_PAIRS or L.DECODE_RUNS."""
         L.check(self.lib.cubit_ctx_set_decode_kernel(self.handle, kernel))
 
+    def last_decode_kernel(self) -> int:
+        k = C.c_int()
+        L.check(self.lib.cubit_ctx_last_decode_kernel(self.handle, C.byref(k)))
+        return int(k.value)
+
     def enable_timing(self, on: bool = True) -> None:
         L.check(self.lib.cubit_ctx_enable_timing(self.handle, 1 if on else 0))
 

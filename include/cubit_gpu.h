@@ -120,6 +120,8 @@ const char *cubit_last_error(void);
 #define CUBIT_DECODE_PAIRS 1
 #define CUBIT_DECODE_RUNS 2
 int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
+/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS or CUBIT_DECODE_RUNS). */
+int cubit_ctx_last_decode_kernel(cubit_ctx *ctx, int *kernel);
 /* Filter-kernel durations measured with HIP events recorded around each launch on the
  * context stream (ms); requires cubit_ctx_enable_timing(ctx, 1). */
 int cubit_ctx_enable_timing(cubit_ctx *ctx, int on);
