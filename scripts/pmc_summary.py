@@ -13,7 +13,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 ROUND = sys.argv[1] if len(sys.argv) > 1 else "r01"
-KERNEL = "eval_decode_pairs"
+KERNELS = ("eval_decode_pairs", "eval_decode_runs")  # the bench line names the one it launched
 
 
 def rows(pattern):
@@ -40,7 +40,8 @@ def main():
             (ROOT / "profiles" / f"{ROUND}_{w}_kernel_stats.csv").write_text(Path(stats[0]).read_text())
         # the dominant kernel's own instantiation (K leaves): the bench's side legs launch
         # other instantiations of the same template (e.g. K = 1 for the equality query)
-        kname = f"{KERNEL}<{line['config']['bitvectors_read_K']}, "
+        kernel = next((k for k in KERNELS if k in line["roofline"]["kernel"]), KERNELS[0])
+        kname = f"{kernel}<{line['config']['bitvectors_read_K']}, "
         kt = [r for r in rows(f"{wdir}/kt/**/*kernel_trace.csv") if kname in r["Kernel_Name"]]
         fetch = [r for r in rows(f"{wdir}/fetch/**/*counter_collection.csv") if kname in r["Kernel_Name"]]
         write = [r for r in rows(f"{wdir}/write/**/*counter_collection.csv") if kname in r["Kernel_Name"]]
