@@ -1382,13 +1382,38 @@ extern "C" int cubit_table_set_inserts(cubit_table* t, const int64_t* row_begin,
 
 namespace {
 
+// The distinct values of v, ascending. Update lists hold millions of records over few
+// distinct values: a presence bitmap over [min, max] when that span is small, else sort.
+std::vector<int64_t> distinct_sorted(const int64_t* v, uint64_t n) {
+    std::vector<int64_t> out;
+    if (n == 0) return out;
+    const auto mm = std::minmax_element(v, v + n);
+    const uint64_t span = (uint64_t)*mm.second - (uint64_t)*mm.first;
+    if (span < (1ull << 26)) {
+        std::vector<uint64_t> bits(span / 64 + 1, 0);
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t d = (uint64_t)v[i] - (uint64_t)*mm.first;
+            bits[d >> 6] |= 1ull << (d & 63);
+        }
+        for (uint64_t w = 0; w < bits.size(); ++w)
+            for (uint64_t x = bits[w]; x; x &= x - 1)
+                out.push_back((int64_t)((uint64_t)*mm.first + w * 64 + (uint64_t)__builtin_ctzll(x)));
+        return out;
+    }
+    out.assign(v, v + n);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return out;
+}
+
 // store an update list (rows, values, versions) for col: records grouped by row, each row's
 // records kept in chronological order (UpdateInfo chains, update_info.hpp)
 int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values, const uint64_t* versions,
                   uint64_t n) {
     std::vector<uint64_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
+    if (!std::is_sorted(rows, rows + n))  // grouping keeps each row's records in list order
+        std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
     Updates u;
     u.n = n;
     for (uint64_t i : order) {
@@ -1396,13 +1421,13 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
         u.h_values.push_back(values[i]);
         u.h_versions.push_back(versions[i]);
     }
-    u.distinct_versions = u.h_versions;
-    std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
-    u.distinct_versions.erase(std::unique(u.distinct_versions.begin(), u.distinct_versions.end()),
-                              u.distinct_versions.end());
-    u.stat_values = u.h_values;
-    std::sort(u.stat_values.begin(), u.stat_values.end());
-    u.stat_values.erase(std::unique(u.stat_values.begin(), u.stat_values.end()), u.stat_values.end());
+    {
+        const auto dv = distinct_sorted(reinterpret_cast<const int64_t*>(u.h_versions.data()), n);
+        // versions are unsigned: distinct_sorted ordered them as signed, restore unsigned order
+        u.distinct_versions.assign(dv.begin(), dv.end());
+        std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
+    }
+    u.stat_values = distinct_sorted(u.h_values.data(), n);
     u.rows = std::make_unique<DevBuf>();
     u.values = std::make_unique<DevBuf>();
     u.versions = std::make_unique<DevBuf>();
@@ -1790,9 +1815,7 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
                                 const_cast<void*>(c.data), c.type, const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
     HIP_CHECK(hipStreamSynchronize(s));
     // statistics and exact keys for the merged values
-    std::vector<int64_t> added = m_vals;
-    std::sort(added.begin(), added.end());
-    added.erase(std::unique(added.begin(), added.end()), added.end());
+    const std::vector<int64_t> added = distinct_sorted(m_vals.data(), m_vals.size());
     for (Index* ix : ixs) {
         if (!ix) continue;
         const bool was_empty = ix->empty;

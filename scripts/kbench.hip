@@ -292,6 +292,23 @@ int main(int argc, char** argv) {
                   }, 3});
     // (S3072 x3/CU: the 80-VGPR cap spills 192 B per thread, 199 µs — not viable)
     DK4("K4 conj S3072 x2/CU", 3072, 2);
+    // larger grids: the hardware dispatcher hands out the work (WGs beyond the two resident
+    // per CU start as others finish) — load balance without atomics, no cross-tile prefetch
+#define K4G(NAME, DIV)                                                                                         \
+    vs.push_back({NAME, [&](EvalArgs& a, hipStream_t s) {                                                     \
+                      a.num_tiles = dtiles;                                                                   \
+                      a.prog.leaf[3] = leaf[4];                                                               \
+                      a.prog.n_leaves = 4;                                                                    \
+                      a.prog.negate = 0;                                                                      \
+                      a.prog.nops = 0;                                                                        \
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);                              \
+                      a.prog.ops = 0;                                                                         \
+                      hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 0, FORM_CONJ>),                  \
+                                         dim3((dtiles + DIV - 1) / DIV), dim3(512), 0, s, a, dir);            \
+                  }, 3})
+    K4G("K4 q6-density pairs grid=tiles/2", 2);
+    K4G("K4 q6-density pairs grid=tiles/4", 4);
+    K4G("K4 q6-density pairs grid=tiles/6", 6);
     vs.push_back({"K4 q6-density runs cap9984", [&](EvalArgs& a, hipStream_t s) {
                       a.num_tiles = dtiles;
                       a.prog.leaf[3] = leaf[4];
