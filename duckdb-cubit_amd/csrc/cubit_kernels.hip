@@ -1826,7 +1826,8 @@ unsigned grid_for(uint64_t n, unsigned cap = 4096) {
 // STAGE 4,096 staged ids (16 KiB LDS); count tiles of 256 threads × 8 pairs = 4,096 words.
 // Chosen from the interleaved variant sweep in scripts/kbench.hip.
 constexpr int kDecodeThreads = 512, kDecodePairs = 2, kDecodeStage = 4096;
-constexpr int kRunCap = 2 * kDecodeStage;  // eval_decode_runs: the same 64 KiB of LDS stages
+// eval_decode_runs: two stages of 9,984 entries (78 KiB; two workgroups per CU fill the 160 KiB)
+constexpr int kRunCap = 9984;
 // count tiles: 512 threads × 2 pairs = 2,048 words for K ≤ 4, × 1 pair above (two tiles in
 // flight must fit the 128-VGPR budget of 4 waves per SIMD)
 constexpr int count_pairs(uint32_t k) { return k <= 4 ? 2 : 1; }
@@ -1856,8 +1857,9 @@ uint32_t eval_form(const EvalProgram& p) {
 // and the pair kernel measured as fast or 1 % faster (73.2 vs 74.2 µs); the pair kernel for one
 // or two tiles per workgroup (small inputs: one claim per workgroup either way).
 int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel) {
+    (void)n_leaves;
     if (kernel == 1 || kernel == 2) return kernel;
-    return n_leaves != 4 && num_tiles > 2ull * grid ? 2 : 1;
+    return num_tiles > 2ull * grid ? 2 : 1;
 }
 
 template <int K, int FORM>

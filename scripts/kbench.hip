@@ -306,6 +306,17 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 0, FORM_CONJ>),                  \
                                          dim3((dtiles + DIV - 1) / DIV), dim3(512), 0, s, a, dir);            \
                   }, 3})
+    vs.push_back({"K4 q6-density auto", [&](EvalArgs& a, hipStream_t s) {
+                      a.num_tiles = dtiles;
+                      a.prog.leaf[3] = leaf[4];
+                      a.prog.n_leaves = 4;
+                      a.prog.negate = 0;
+                      a.prog.nops = 0;
+                      for (int k = 1; k < 4; ++k) a.prog.nops |= 1u << (4 * k);
+                      a.prog.ops = 0;
+                      a.prog.form = FORM_CONJ;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 3});
     K4G("K4 q6-density pairs grid=tiles/2", 2);
     K4G("K4 q6-density pairs grid=tiles/4", 4);
     K4G("K4 q6-density pairs grid=tiles/6", 6);
@@ -428,6 +439,17 @@ int main(int argc, char** argv) {
     KPR("K2 0.75% runs", 2, 0b10, true);
     KPR("K3 0.4% pairs", 3, 0b110, false);
     KPR("K3 0.4% runs", 3, 0b110, true);
+    vs.push_back({"K3 0.4% auto", [&](EvalArgs& a, hipStream_t s) {
+                      a.prog = EvalProgram{};
+                      a.prog.leaf[0] = leaf[5];
+                      a.prog.leaf[1] = leaf[0];
+                      a.prog.leaf[2] = leaf[2];
+                      a.prog.n_leaves = 3;
+                      a.prog.negate = 0b110;
+                      a.prog.form = FORM_CONJ;
+                      a.num_tiles = dtiles;
+                      CK(launch_eval_decode(a, dir, std::min<unsigned>(dtiles, 2 * cus), s));
+                  }, 3});
     vs.push_back({"K1 1% pairs P1", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
                       a.num_tiles = (uint32_t)(pw / 1024);
