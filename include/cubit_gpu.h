@@ -243,7 +243,10 @@ int cubit_table_set_inserts(cubit_table *t, const int64_t *row_begin, const int6
  * is maintained in place (bitvectors of the appended slice spliced in at bit n_rows; statistics
  * widened; an every-distinct-value index gains keys for values it has not seen). insert_id != 0
  * records [n_rows, n_rows+n_new) as an insert range of that transaction (see set_inserts);
- * 0 = visible to every snapshot. Storage grows geometrically when the padding runs out. */
+ * 0 = visible to every snapshot. Storage grows geometrically when the padding runs out.
+ * Columns registered as caller-owned device memory (add_column on_device = 1) are copied into
+ * table-owned storage on the first append or merge; the caller's buffer is no longer read.
+ * On an error the partition keeps its previous rows (a later append overwrites the slice). */
 int cubit_table_append(cubit_table *t, uint64_t n_new, const int *cols, const void *const *data,
                        const uint64_t *const *validity, uint32_t n_cols, uint64_t insert_id);
 /* Merge the update records of `col` with version < horizon into the base values and the

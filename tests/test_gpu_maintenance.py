@@ -327,3 +327,52 @@ def test_merge_into_int32_rejects_wide_values(ctx):
     with pytest.raises(L.CubitError):
         t.merge_updates(0, 10)
     t.close()
+
+
+def test_appends_concurrent_with_scans(ctx):
+    """A writer thread appends batches while a reader thread scans the same table on the same
+    context (the context mutex serialises the calls, DuckDB's pipeline threads share one
+    context the same way): every scan returns exactly the oracle's rows over some prefix of
+    the batches — never a torn state."""
+    import threading
+
+    rng = np.random.default_rng(99)
+    n0 = 200_003
+    batches = [rng.integers(0, 50, int(rng.integers(1, 300_000))).astype(np.int32) for _ in range(12)]
+    base = rng.integers(0, 50, n0).astype(np.int32)
+    t = CubitTable(ctx, n0)
+    t.add_column(0, base)
+    t.build_index(0, L.INDEX_RANGE)
+    fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 10), F.ConstantFilter("<", 13)])})
+    prefixes = [base]
+    for b in batches:
+        prefixes.append(np.concatenate([prefixes[-1], b]))
+    expected = {len(p): np.flatnonzero((p >= 10) & (p < 13)).astype(np.int64) for p in prefixes}
+    errors, seen = [], set()
+
+    def writer():
+        try:
+            for b in batches:
+                t.append({0: b})
+        except Exception as e:  # reported below
+            errors.append(repr(e))
+
+    def reader():
+        try:
+            for _ in range(40):
+                got = t.scan(fs, capacity=len(prefixes[-1]))  # the table grows under the reader
+                ok = [n for n, ref in expected.items() if len(ref) == len(got) and np.array_equal(got, ref)]
+                if not ok:
+                    errors.append(f"scan of {len(got)} rows matches no prefix")
+                seen.update(ok)
+        except Exception as e:
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=writer), threading.Thread(target=reader)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:3]
+    assert np.array_equal(t.scan(fs), expected[len(prefixes[-1])])
+    t.close()
