@@ -38,6 +38,20 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
     return x;
 }
 
+// Inclusive wave64 prefix sum of a uint32 with DPP (GFX9 row shifts, then row_bcast:15 / :31
+// across the four 16-lane rows): six v_add with a DPP operand, no LDS traffic (the 64-bit
+// __shfl_up scan above is twelve ds_bpermute). Lanes whose DPP source is outside the row, and
+// rows outside row_mask, add `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
@@ -98,15 +112,22 @@ template <int K, int NW, int FORM = FORM_POSTFIX>
 __device__ __forceinline__ void eval_words(const EvalProgram& prog, const u64x2 (&v)[K][NW / 2],
                                            uint64_t (&r)[NW]) {
     if (FORM == FORM_CONJ) {
-#pragma unroll
-        for (int j = 0; j < NW; ++j) r[j] = ~0ull;
+        // leaf 0 initialises r; each complemented leaf is a uniform branch, so a word costs
+        // one AND (or AND-NOT, v_bfi_b32) per 32 bits instead of an XOR and an AND
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const uint64_t neg = ((prog.negate >> k) & 1u) ? ~0ull : 0ull;
+            if ((prog.negate >> k) & 1u) {
 #pragma unroll
-            for (int j = 0; j < NW; ++j) {
-                const u64x2 p = v[k][j >> 1];
-                r[j] &= ((j & 1) ? p.y : p.x) ^ neg;
+                for (int j = 0; j < NW; ++j) {
+                    const uint64_t x = (j & 1) ? v[k][j >> 1].y : v[k][j >> 1].x;
+                    r[j] = k == 0 ? ~x : (r[j] & ~x);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NW; ++j) {
+                    const uint64_t x = (j & 1) ? v[k][j >> 1].y : v[k][j >> 1].x;
+                    r[j] = k == 0 ? x : (r[j] & x);
+                }
             }
         }
         return;
@@ -177,6 +198,8 @@ __device__ __forceinline__ uint64_t word_index(uint64_t tile_word0, int j, int t
 
 template <int NW, int THREADS>
 __device__ __forceinline__ void tail_mask(const EvalArgs& a, uint64_t tile_word0, int t, uint64_t (&r)[NW]) {
+    // uniform: only the tile that holds the last word (or lies past it) has bits to clear
+    if (tile_word0 + (uint64_t)THREADS * NW < a.n_words) return;
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
         const uint64_t gw = word_index<THREADS>(tile_word0, j, t);
@@ -704,17 +727,16 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     // STAMP (scripts/kbench.hip only): each workgroup's start / end (s_memrealtime) into g_diag_times
     if (STAMP && threadIdx.x == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     constexpr int NW = 2 * PAIRS;
-    constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
-    constexpr int FPW = 64 / FB;
-    constexpr uint64_t FMASK = (FB == 16) ? 0xffffull : 0xffffffffull;
-    constexpr int NPK = (PAIRS + FPW - 1) / FPW;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
     static_assert(MAXT <= 64, "directory entries per run");
     constexpr int NWAVES = THREADS / 64;
     constexpr bool EARLY = K <= 4;
     typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
-    __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
+    // per-wave totals of the pair counts, two 16-bit fields (a wave's total per pair is at most
+    // 64 lanes × 128 bits = 8,192)
+    static_assert(PAIRS <= 2, "pair counts are scanned as 16-bit fields of one uint32");
+    __shared__ uint32_t s_wave_tot[2][NWAVES];
     __shared__ uint64_t s_off;        // claimed base of the run being copied out
     __shared__ uint64_t s_dense_off;  // claimed base of a dense tile
     __shared__ uint32_t s_stage[2][RUN_CAP];
@@ -780,39 +802,33 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
         if (EARLY && next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
-        uint64_t packed[NPK], incl[NPK];
-#pragma unroll
-        for (int q = 0; q < NPK; ++q) packed[q] = 0;
+        uint32_t packed = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p)
-            packed[p / FPW] |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
-#pragma unroll
-        for (int q = 0; q < NPK; ++q) {
-            incl[q] = wave_incl_scan(packed[q], lane);
-            if (lane == 63) s_wave_tot[par][wave][q] = incl[q];
-        }
+            packed |= (uint32_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (16 * p);
+        const uint32_t incl = wave_incl_scan32(packed);
+        if (lane == 63) s_wave_tot[par][wave] = incl;
         if (pending && t == 0) s_off = pend_claim;  // the closed run's claim returned meanwhile
         __syncthreads();
-        uint64_t block_tot[NPK], wave_pre[NPK];
+        uint32_t wave_pre[2] = {0, 0}, block_tot[2] = {0, 0};
 #pragma unroll
-        for (int q = 0; q < NPK; ++q) {
-            uint64_t wp = 0, bt = 0;
-#pragma unroll
-            for (int w = 0; w < NWAVES; ++w) {
-                const uint64_t x = s_wave_tot[par][w][q];
-                if (w < wave) wp += x;
-                bt += x;
+        for (int w = 0; w < NWAVES; ++w) {
+            const uint32_t x = s_wave_tot[par][w];
+            const uint32_t lo = x & 0xffffu, hi = x >> 16;
+            if (w < wave) {
+                wave_pre[0] += lo;
+                wave_pre[1] += hi;
             }
-            block_tot[q] = bt;
-            wave_pre[q] = wp;
+            block_tot[0] += lo;
+            block_tot[1] += hi;
         }
+        const uint32_t excl = incl - packed;  // per field: no borrow (incl ≥ packed field-wise)
         uint32_t pair_off[PAIRS];
         uint32_t tile_count = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
-            pair_off[p] = tile_count +
-                          (uint32_t)(((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
-            tile_count += (uint32_t)((block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK);
+            pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
+            tile_count += block_tot[p];
         }
         const bool dense = tile_count > (uint32_t)RUN_CAP;
         // close the open run when this tile does not fit (claimed after the previous run's
