@@ -471,17 +471,14 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     // fake decode (same LDS traffic, no per-bit loop), bit 2 = record each workgroup's start
     // and end (s_memrealtime, 100 MHz) into g_diag_times[2·blockIdx + {0, 1}]
     constexpr int NW = 2 * PAIRS;
-    constexpr int FB = (THREADS * 128 < 65536) ? 16 : 32;
-    constexpr int FPW = 64 / FB;
-    constexpr uint64_t FMASK = (FB == 16) ? 0xffffull : 0xffffffffull;
-    constexpr int NPK = (PAIRS + FPW - 1) / FPW;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
     constexpr int NWAVES = THREADS / 64;
     constexpr bool EARLY = K <= 4;
     static_assert(TILE_WORDS * 64 < (1ull << 32), "tile-local offsets are 32-bit");
     typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
-    __shared__ uint64_t s_wave_tot[2][NWAVES][NPK];
+    static_assert(PAIRS <= 2, "pair counts are scanned as 16-bit fields of one uint32");
+    __shared__ uint32_t s_wave_tot[2][NWAVES];
     __shared__ uint64_t s_off;        // claimed base of the pair being copied out
     __shared__ uint64_t s_dense_off;  // claimed base of a dense tile
     __shared__ uint32_t s_stage[2][2 * STAGE];
@@ -532,39 +529,34 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
         if (EARLY && prefetch < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)prefetch * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
-        uint64_t packed[NPK], incl[NPK];
-#pragma unroll
-        for (int q = 0; q < NPK; ++q) packed[q] = 0;
+        // pair counts as 16-bit fields of one uint32 (a wave's total per pair ≤ 8,192), DPP scan
+        uint32_t packed = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p)
-            packed[p / FPW] |= (uint64_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (FB * (p % FPW));
-#pragma unroll
-        for (int q = 0; q < NPK; ++q) {
-            incl[q] = wave_incl_scan(packed[q], lane);
-            if (lane == 63) s_wave_tot[par][wave][q] = incl[q];
-        }
+            packed |= (uint32_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (16 * p);
+        const uint32_t incl = wave_incl_scan32(packed);
+        if (lane == 63) s_wave_tot[par][wave] = incl;
         if (publish_sp >= 0 && t == 0) publish(publish_sp);
         __syncthreads();
-        uint64_t block_tot[NPK], wave_pre[NPK];
+        uint32_t wave_pre[2] = {0, 0}, block_tot[2] = {0, 0};
 #pragma unroll
-        for (int q = 0; q < NPK; ++q) {
-            uint64_t wp = 0, bt = 0;
-#pragma unroll
-            for (int w = 0; w < NWAVES; ++w) {
-                const uint64_t x = s_wave_tot[par][w][q];
-                if (w < wave) wp += x;
-                bt += x;
+        for (int w = 0; w < NWAVES; ++w) {
+            const uint32_t x = s_wave_tot[par][w];
+            const uint32_t lo = x & 0xffffu, hi = x >> 16;
+            if (w < wave) {
+                wave_pre[0] += lo;
+                wave_pre[1] += hi;
             }
-            block_tot[q] = bt;
-            wave_pre[q] = wp;
+            block_tot[0] += lo;
+            block_tot[1] += hi;
         }
+        const uint32_t excl = incl - packed;
         // in-tile offsets and counts fit 32 bits (≤ TILE_WORDS·64 < 2^32, static_assert below)
         uint32_t tile_count = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
-            pair_off[p] = tile_count +
-                          (uint32_t)(((wave_pre[p / FPW] + incl[p / FPW] - packed[p / FPW]) >> (FB * (p % FPW))) & FMASK);
-            tile_count += (uint32_t)((block_tot[p / FPW] >> (FB * (p % FPW))) & FMASK);
+            pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
+            tile_count += block_tot[p];
         }
         return tile_count;
     };

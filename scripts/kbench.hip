@@ -464,13 +464,6 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<1, 2, 4096, 512, 0, FORM_CONJ, 2>),
                                          dim3(std::min<unsigned>((dtiles + 1) / 2, 2 * cus)), dim3(512), 0, s, a, dir);
                   }, 3});
-    vs.push_back({"K1 1% P4 grid=tiles/2", [&](EvalArgs& a, hipStream_t s) {
-                      k1(a);
-                      a.num_tiles = (uint32_t)(pw / 4096);
-                      hipLaunchKernelGGL((eval_decode_pairs<1, 4, 4096, 512, 0, FORM_CONJ, 2>),
-                                         dim3(std::min<unsigned>((a.num_tiles + 1) / 2, 2 * cus)), dim3(512), 0, s, a,
-                                         dir);
-                  }, 3});
     vs.push_back({"K1 1% tiles grid=tiles", [&](EvalArgs& a, hipStream_t s) {
                       k1(a);
                       a.num_tiles = dtiles;
