@@ -168,6 +168,8 @@ def run(ctx, seed, n_ops, n0):
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_maintenance_fuzz(seed):
     ctx = Context(0)
+    if seed % 2 == 0:
+        ctx.set_decode_kernel(L.DECODE_RUNS)  # the run-claimed decode at small sizes too
     try:
         counts = run(ctx, seed, 60, 150_001)
         assert counts["scan"] > 10

@@ -18,9 +18,12 @@ TXN_START = 4611686018427388000
 CMPS = ["=", "!=", "<", "<=", ">", ">="]
 
 
-@pytest.fixture(scope="module")
-def ctx():
+@pytest.fixture(scope="module", params=[L.DECODE_AUTO, L.DECODE_RUNS], ids=["auto", "runs"])
+def ctx(request):
+    """Both decode kernels: at these sizes the automatic policy picks the pair-claimed one, so
+    the run-claimed kernel (production above 2 tiles per workgroup) is forced once."""
     c = Context(0)
+    c.set_decode_kernel(request.param)
     yield c
     c.close()
 
