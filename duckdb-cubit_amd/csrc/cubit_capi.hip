@@ -325,6 +325,20 @@ int cubit_dev_free(cubit_ctx* ctx, void* dptr) {
     return CUBIT_OK;
 }
 
+int cubit_host_alloc(cubit_ctx* ctx, uint64_t bytes, void** hptr) {
+    if (!ctx || !hptr) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    if (hipHostMalloc(hptr, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
+    return CUBIT_OK;
+}
+
+int cubit_host_free(cubit_ctx* ctx, void* hptr) {
+    (void)ctx;  // page-locked memory is not tied to a context: NULL is accepted
+    if (hptr) HIP_CHECK(hipHostFree(hptr));
+    return CUBIT_OK;
+}
+
 int cubit_memcpy_h2d(cubit_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));

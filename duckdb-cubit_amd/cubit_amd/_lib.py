@@ -111,6 +111,8 @@ GPU_SIGNATURES = {
     "cubit_table_set_inserts": (C.c_int, [_P, _P, _P, _P, _U64]),
     "cubit_table_append": (C.c_int, [_P, _U64, _P, _P, _P, C.c_uint32, _U64]),
     "cubit_ctx_set_decode_kernel": (C.c_int, [_P, C.c_int]),
+    "cubit_host_alloc": (C.c_int, [_P, _U64, C.POINTER(_P)]),
+    "cubit_host_free": (C.c_int, [_P, _P]),
     "cubit_ctx_last_decode_kernel": (C.c_int, [_P, _P]),
     "cubit_table_merge_updates": (C.c_int, [_P, C.c_int, _U64, _P]),
     "cubit_table_save_index": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -24,6 +26,70 @@ void check(int rc, const char* what) {
     if (rc != CUBIT_OK) throw ScanError(rc, std::string(what) + ": " + cubit_last_error());
 }
 
+// Page-locked buffers outlive one scan: pinning ~100 MB costs milliseconds, more than its
+// copy, and DuckDB runs init_global once per query. Freed buffers wait here (≤ 4 GiB) and a
+// request takes the smallest one that fits without wasting more than half of it. Never
+// destroyed (the process exit releases the pages; a static destructor could run after the
+// HIP runtime's).
+class PinnedPool {
+  public:
+    static PinnedPool& get() {
+        static PinnedPool* pool = new PinnedPool();
+        return *pool;
+    }
+    void* take(cubit_ctx* ctx, size_t bytes, size_t* got) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = free_.lower_bound(bytes);
+            if (it != free_.end() && it->first <= 2 * bytes) {
+                void* p = it->second;
+                *got = it->first;
+                cached_ -= it->first;
+                free_.erase(it);
+                return p;
+            }
+        }
+        void* h = nullptr;
+        check(cubit_host_alloc(ctx, bytes, &h), "cubit_host_alloc");
+        *got = bytes;
+        return h;
+    }
+    void give(void* p, size_t bytes) {
+        std::lock_guard<std::mutex> lk(mu_);
+        free_.emplace(bytes, p);
+        cached_ += bytes;
+        while (cached_ > kMaxCached && !free_.empty()) {  // drop the largest first
+            auto it = std::prev(free_.end());
+            cached_ -= it->first;
+            cubit_host_free(nullptr, it->second);
+            free_.erase(it);
+        }
+    }
+
+  private:
+    static constexpr size_t kMaxCached = 4ull << 30;
+    std::mutex mu_;
+    std::multimap<size_t, void*> free_;
+    size_t cached_ = 0;
+};
+
+// Page-locked host staging (cubit_host_alloc via PinnedPool): device → host copies run at the
+// link's rate instead of through a pageable bounce buffer.
+struct PinnedBuffer {
+    int64_t* p = nullptr;
+    size_t bytes = 0;
+    PinnedBuffer() = default;
+    PinnedBuffer(const PinnedBuffer&) = delete;
+    PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+    PinnedBuffer(PinnedBuffer&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
+    void allocate(cubit_ctx* c, idx_t count);
+    int64_t* data() { return p; }
+    const int64_t* data() const { return p; }
+    ~PinnedBuffer() {
+        if (p) PinnedPool::get().give(p, bytes);
+    }
+};
+
 // Device result of one scan, copied to host once (the GPU work is one fused launch plus one
 // gather per emitted column; DataChunks are then served from host memory).
 struct CubitScanGlobalState : public GlobalTableFunctionState {
@@ -31,8 +97,8 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     std::vector<idx_t> emit;  // positions of column_ids that reach the output
     idx_t count = 0;
     idx_t rows_per_tile = 0;
-    std::vector<int64_t> rowids;                // tile-run order
-    std::vector<std::vector<int64_t>> columns;  // per emitted position (row ids or probed values)
+    PinnedBuffer rowids;                // tile-run order
+    std::vector<PinnedBuffer> columns;  // per emitted position (row ids or probed values)
     std::vector<uint32_t> tiles;                // non-empty tiles, ascending
     std::vector<uint64_t> dir;                  // {start, length} per tile
     std::atomic<uint32_t> next{0};
@@ -57,6 +123,10 @@ struct DeviceBuffer {
     }
 };
 
+void PinnedBuffer::allocate(cubit_ctx* c, idx_t count) {
+    p = static_cast<int64_t*>(PinnedPool::get().take(c, std::max<idx_t>(count, 1) * sizeof(int64_t), &bytes));
+}
+
 std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
     auto& bind = static_cast<const CubitScanBindData&>(*input.bind_data);
     auto g = std::make_unique<CubitScanGlobalState>();
@@ -67,10 +137,18 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         for (idx_t i = 0; i < input.column_ids.size(); ++i) g->emit.push_back(i);
     }
     cubit_ctx* ctx = bind.ctx;
-    const uint64_t cap = std::max<uint64_t>(bind.n_rows, 1);
-    DeviceBuffer d_ids(ctx, cap * 8), d_cnt(ctx, 16);
+    DeviceBuffer d_cnt(ctx, 16);
     const cubit_txn* txn = bind.has_txn ? &bind.txn : nullptr;
     const auto& nodes = input.filters ? input.filters->nodes : std::vector<cubit_filter_node>{};
+    // count first (one evaluate pass, no row ids), so the row-id and probe buffers are sized to
+    // the result rather than to the table (4.8 GB per query at SF100 otherwise)
+    check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn, nullptr,
+                           0, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_COUNT_ONLY),
+          "cubit_table_scan (count)");
+    uint64_t want = 0;
+    check(cubit_memcpy_d2h(ctx, &want, d_cnt.p, 8), "count");
+    const uint64_t cap = std::max<uint64_t>(want, 1);
+    DeviceBuffer d_ids(ctx, cap * 8);
     check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
                            static_cast<int64_t*>(d_ids.p), cap, static_cast<uint64_t*>(d_cnt.p), 0),
           "cubit_table_scan");
@@ -79,11 +157,11 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     const uint64_t* d_dir = nullptr;
     uint32_t n_tiles = 0;
     check(cubit_ctx_last_tiles(ctx, &d_dir, &n_tiles, &g->rows_per_tile), "tiles");
-    if (g->count > cap) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count exceeds the table's rows");
+    if (g->count > cap) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
     if (g->count == 0) n_tiles = 0;  // nothing qualified: no run to hand out, whatever the directory holds
     g->dir.resize(2 * (size_t)n_tiles);
     if (n_tiles) check(cubit_memcpy_d2h(ctx, g->dir.data(), d_dir, g->dir.size() * 8), "directory");
-    g->rowids.resize(g->count);
+    g->rowids.allocate(ctx, g->count);
     if (g->count) check(cubit_memcpy_d2h(ctx, g->rowids.data(), d_ids.p, g->count * 8), "row ids");
     uint64_t covered = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {
@@ -100,15 +178,16 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
                                                std::to_string(g->count) + " row ids");
     // probe every emitted storage column at the row ids (ColumnData::FilterScan semantics)
     g->columns.resize(g->emit.size());
+    std::unique_ptr<DeviceBuffer> d_vals;
     for (size_t e = 0; e < g->emit.size(); ++e) {
         const column_t col = g->column_ids[g->emit[e]];
         if (col == COLUMN_IDENTIFIER_ROW_ID || g->count == 0) continue;
-        DeviceBuffer d_vals(ctx, g->count * 8);
+        if (!d_vals) d_vals = std::make_unique<DeviceBuffer>(ctx, g->count * 8);
         check(cubit_table_probe(bind.table, (int)col, txn, static_cast<int64_t*>(d_ids.p),
-                                static_cast<uint64_t*>(d_cnt.p), g->count, static_cast<int64_t*>(d_vals.p)),
+                                static_cast<uint64_t*>(d_cnt.p), g->count, static_cast<int64_t*>(d_vals->p)),
               "cubit_table_probe");
-        g->columns[e].resize(g->count);
-        check(cubit_memcpy_d2h(ctx, g->columns[e].data(), d_vals.p, g->count * 8), "probe values");
+        g->columns[e].allocate(ctx, g->count);
+        check(cubit_memcpy_d2h(ctx, g->columns[e].data(), d_vals->p, g->count * 8), "probe values");
     }
     return g;
 }

@@ -137,6 +137,11 @@ int cubit_row_group_size(void);
 /* ------------------------------------------------------------------ device memory helpers */
 int cubit_dev_alloc(cubit_ctx *ctx, uint64_t bytes, void **dptr);
 int cubit_dev_free(cubit_ctx *ctx, void *dptr);
+/* Page-locked host memory: device ↔ host copies into it run at the link's rate (the
+ * table-function mirror stages its DataChunk columns here). cubit_host_free accepts a NULL
+ * context (the memory outlives contexts). */
+int cubit_host_alloc(cubit_ctx *ctx, uint64_t bytes, void **hptr);
+int cubit_host_free(cubit_ctx *ctx, void *hptr);
 int cubit_memcpy_h2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memcpy_d2h(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memset_d(cubit_ctx *ctx, void *dst, int value, uint64_t bytes);
