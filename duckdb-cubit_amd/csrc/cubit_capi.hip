@@ -954,9 +954,14 @@ int copy_column(cubit_table* t, Column& c, int type, const void* data, const uin
     return CUBIT_OK;
 }
 
+std::vector<int64_t> distinct_sorted(const int64_t* v, uint64_t n);
+
+// an exact index over a span ≥ 2^32 keeps at most this many keys (one bitvector each)
+constexpr size_t kMaxWideDistinct = 1 << 16;
+
 // Index-build statistics on the device: min / max / any valid, and (want_distinct) the
-// distinct valid values through a presence bitmap of vmax - vmin + 1 bits (≤ 2^32 values;
-// an index with more distinct keys than that is not a bitmap index anyone should build).
+// distinct valid values through a presence bitmap of vmax - vmin + 1 bits when the span is
+// below 2^32, else by sorting the valid values on the host.
 int value_stats(cubit_table* t, const void* data, int type, const uint64_t* validity, uint64_t n,
                 std::vector<int64_t>& distinct, bool want_distinct, int64_t& vmin, int64_t& vmax, bool& any) {
     const Column c{type, data, validity};
@@ -974,8 +979,28 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
     distinct.clear();
     if (!any) return CUBIT_OK;
     const uint64_t span = (uint64_t)vmax - (uint64_t)vmin;  // no signed overflow
-    if (span >= (1ull << 32))
-        return fail(CUBIT_ERR_UNSUPPORTED, "value range too wide for an all-distinct-values index; give keys");
+    if (span >= (1ull << 32)) {
+        // a wide span (TIMESTAMP microseconds, BIGINT ids) over few distinct values: sort the
+        // valid values on the host instead (only INT64 columns get here)
+        std::vector<int64_t> hv(n);
+        std::vector<uint64_t> hvalid(validity ? (n + 63) / 64 : 0);
+        HIP_CHECK(hipMemcpyAsync(hv.data(), data, n * 8, hipMemcpyDeviceToHost, t->ctx->stream));
+        if (validity)
+            HIP_CHECK(hipMemcpyAsync(hvalid.data(), validity, hvalid.size() * 8, hipMemcpyDeviceToHost,
+                                     t->ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+        if (validity) {
+            uint64_t k = 0;
+            for (uint64_t i = 0; i < n; ++i)
+                if ((hvalid[i >> 6] >> (i & 63)) & 1) hv[k++] = hv[i];
+            hv.resize(k);
+        }
+        distinct = distinct_sorted(hv.data(), hv.size());
+        if (distinct.size() > kMaxWideDistinct)
+            return fail(CUBIT_ERR_UNSUPPORTED, "%zu distinct values over a span of 2^32 or more; give keys",
+                        distinct.size());
+        return CUBIT_OK;
+    }
     const uint64_t range = span + 1;
     const uint64_t nw = (range + 63) / 64;
     DevBuf bits;

@@ -80,9 +80,28 @@ static void Check(int rc) {
 
 // ------------------------------------------------------------------ filters
 
+// Physical types whose values the GPU compares exactly as int64: the signed integers up to
+// 64 bits (DATE, TIME, TIMESTAMP*, DECIMAL(≤18) included), BOOLEAN and the unsigned integers
+// up to 32 bits. UBIGINT, HUGEINT, UHUGEINT, FLOAT, DOUBLE and VARCHAR stay on seq_scan.
 static bool IntegerPhysical(PhysicalType t) {
-    return t == PhysicalType::INT32 || t == PhysicalType::INT64 || t == PhysicalType::INT16 ||
-           t == PhysicalType::INT8;
+    switch (t) {
+    case PhysicalType::BOOL:
+    case PhysicalType::INT8:
+    case PhysicalType::INT16:
+    case PhysicalType::INT32:
+    case PhysicalType::INT64:
+    case PhysicalType::UINT8:
+    case PhysicalType::UINT16:
+    case PhysicalType::UINT32:
+        return true;
+    default:
+        return false;
+    }
+}
+
+// uploaded as CUBIT_TYPE_INT64 (else CUBIT_TYPE_INT32)
+static bool WidePhysical(PhysicalType t) {
+    return t == PhysicalType::INT64 || t == PhysicalType::UINT32;
 }
 
 static bool Supported(const TableFilter &f) {
@@ -128,6 +147,14 @@ static bool Supported(const TableFilter &f) {
 
 static int64_t ConstantAsInt64(const Value &v) {
     switch (v.type().InternalType()) {
+    case PhysicalType::BOOL:
+        return v.GetValueUnsafe<bool>() ? 1 : 0;
+    case PhysicalType::UINT8:
+        return v.GetValueUnsafe<uint8_t>();
+    case PhysicalType::UINT16:
+        return v.GetValueUnsafe<uint16_t>();
+    case PhysicalType::UINT32:
+        return v.GetValueUnsafe<uint32_t>();
     case PhysicalType::INT8:
         return v.GetValueUnsafe<int8_t>();
     case PhysicalType::INT16:
@@ -283,9 +310,29 @@ static unique_ptr<LocalTableFunctionState> CubitInitLocal(ExecutionContext &cont
     return std::move(l);
 }
 
+template <class T>
+static void Narrow(const int64_t *src, Vector &dst, idx_t n) {
+    auto d = FlatVector::GetData<T>(dst);
+    for (idx_t i = 0; i < n; i++) {
+        d[i] = (T)src[i];
+    }
+}
+
 // int64 staging → the column's physical type (DATE/INTEGER narrow, BIGINT/DECIMAL copy)
 static void CopyOut(const int64_t *src, Vector &dst, idx_t n) {
     switch (dst.GetType().InternalType()) {
+    case PhysicalType::BOOL:
+        Narrow<bool>(src, dst, n);
+        break;
+    case PhysicalType::UINT8:
+        Narrow<uint8_t>(src, dst, n);
+        break;
+    case PhysicalType::UINT16:
+        Narrow<uint16_t>(src, dst, n);
+        break;
+    case PhysicalType::UINT32:
+        Narrow<uint32_t>(src, dst, n);
+        break;
     case PhysicalType::INT8: {
         auto d = FlatVector::GetData<int8_t>(dst);
         for (idx_t i = 0; i < n; i++) {
@@ -426,7 +473,7 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
         if (!IntegerPhysical(phys)) {
             throw InvalidInputException("cubit_attach: column %s is not integer-backed", name);
         }
-        const bool wide = phys == PhysicalType::INT64;
+        const bool wide = WidePhysical(phys);
         vector<int32_t> v32(wide ? 0 : n_rows, 0);
         vector<int64_t> v64(wide ? n_rows : 0, 0);
         vector<uint64_t> valid((n_rows + 63) / 64, 0);
@@ -448,6 +495,18 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
                 }
                 valid[r >> 6] |= 1ull << (r & 63);
                 switch (phys) {
+                case PhysicalType::BOOL:
+                    v32[r] = FlatVector::GetData<bool>(vals)[i] ? 1 : 0;
+                    break;
+                case PhysicalType::UINT8:
+                    v32[r] = FlatVector::GetData<uint8_t>(vals)[i];
+                    break;
+                case PhysicalType::UINT16:
+                    v32[r] = FlatVector::GetData<uint16_t>(vals)[i];
+                    break;
+                case PhysicalType::UINT32:
+                    v64[r] = FlatVector::GetData<uint32_t>(vals)[i];
+                    break;
                 case PhysicalType::INT8:
                     v32[r] = FlatVector::GetData<int8_t>(vals)[i];
                     break;

@@ -77,8 +77,49 @@ def main():
              "expect": [1, 2, 3, 4, 5]},
         ],
     }
+    # test/sql/update/test_update.test: one row a=3; con1 updates it to 1 and commits, then
+    # updates it to 4 and rolls back. Each check: which connection, the WHERE (None = none),
+    # and the rows it sees.
+    upd = {
+        "source": "test/sql/update/test_update.test:11-104",
+        "rows": [3],
+        "steps": [
+            {"do": "con1 BEGIN; UPDATE test SET a=1",
+             "checks": [["con1", None, [1]], ["con1", 1, [1]], ["con2", None, [3]], ["con2", 3, [3]]]},
+            {"do": "con1 COMMIT", "checks": [["con1", None, [1]], ["con2", None, [1]]]},
+            {"do": "con1 BEGIN; UPDATE test SET a=4", "checks": [["con1", None, [4]], ["con2", None, [1]]]},
+            {"do": "con1 ROLLBACK", "checks": [["con1", None, [1]], ["con1", 1, [1]], ["con2", None, [1]]]},
+        ],
+    }
+    # test/optimizer/pushdown/table_filter_pushdown.test. The file asserts that these filters
+    # are pushed into the scan (no FILTER operator left); the rows each must return follow from
+    # the data it inserts. `types` are the <numeric> types whose physical type is an integer
+    # of at most 32 bits, or a signed 64-bit one (sqllogic_test_runner.cpp:180-203), with the
+    # physical width the shim uploads them at.
+    tfp = {
+        "source": "test/optimizer/pushdown/table_filter_pushdown.test:8-195",
+        "integers": {"rows": [[5, 5, 5], [10, 10, 10]],
+                     "queries": [{"where": [[1, "=", 5]], "k": [5]},
+                                 {"where": [[1, "=", 5], [0, "=", 10]], "k": []}]},
+        "numbers": {"types": {"tinyint": 32, "smallint": 32, "integer": 32, "bigint": 64,
+                              "utinyint": 32, "usmallint": 32, "uinteger": 64},
+                    "rows": [[0, 0, 0], [1, 1, 1], [2, 2, 2]],
+                    "queries": [{"where": [[1, "=", 1]], "k": [1]}, {"where": [[1, ">", 1]], "k": [2]},
+                                {"where": [[1, ">=", 1]], "k": [1, 2]}, {"where": [[1, "<", 1]], "k": [0]},
+                                {"where": [[1, "<=", 1]], "k": [0, 1]}]},
+        # create temporary table t as select range a, range % 10 b ... from range(100);
+        # count(*) where b <= 3 and b >= 0
+        "range_mod": {"n": 100, "mod": 10, "where": [[0, "<=", 3], [0, ">=", 0]], "count": 40},
+        # TIME as int64 microseconds; the fourth row is NULL
+        "time": {"micros": [60000000, 600000000, 3600000000, None], "eq": 60000000, "count": 1},
+        # BOOLEAN (i, j): (TRUE,TRUE),(TRUE,FALSE),(FALSE,TRUE),(NULL,NULL); SELECT i WHERE j = TRUE
+        "bool": {"i": [1, 1, 0, None], "j": [1, 0, 1, None], "eq": 1, "i_expect": [1, 0]},
+        # TIMESTAMP rows NOW() and NOW() - 10 years; ts >= NOW() - 1 year -> COUNT(*) = 1
+        "timestamp": {"count": 1},
+    }
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
-                                                          "table_or_pushdown": orp},
+                                                          "table_or_pushdown": orp, "update": upd,
+                                                          "table_filter_pushdown": tfp},
                                                          indent=1, sort_keys=True) + "\n")
 
 

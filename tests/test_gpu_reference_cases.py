@@ -5,8 +5,10 @@ import pytest
 
 from cubit_amd import _lib as L
 from cubit_amd import filters as F
+from cubit_amd.datagen import validity_from_mask
+from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import residual_from_json
+from test_oracle_tpch import filter_pushdown_tables, residual_from_json, update_case_views
 
 pytestmark = pytest.mark.gpu
 
@@ -67,3 +69,56 @@ def test_table_or_pushdown(ctx, golden, index):
     for q in c["queries"]:
         rows = t.scan(None, residual_from_json(q["tree"]))
         assert data[rows].tolist() == q["expect"], q["sql"]
+
+
+def select_all(t, fs, txn, col=0):
+    """SELECT col FROM t WHERE … through the cubit_scan table-function callbacks."""
+    fn = CubitScanFunction(t, [col], None, fs, txn=txn)
+    local = fn.init_local()
+    out = []
+    while True:
+        chunk = fn.function(local)[0]
+        if len(chunk) == 0:
+            return out
+        out += chunk.tolist()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_update(ctx, golden, encoding):
+    """test/sql/update/test_update.test through the table function; after the rollback the
+    committed update is merged into the base and the index, and every view stays the same."""
+    data = np.array(golden["cases"]["update"]["rows"], dtype=np.int32)
+    t = CubitTable(ctx, len(data))
+    t.add_column(0, data)
+    if encoding is not None:
+        t.build_index(0, encoding)
+    for step, upd, conns in update_case_views(golden):
+        t.set_updates(0, *upd)
+        for merged in ([False, True] if step is golden["cases"]["update"]["steps"][-1] else [False]):
+            if merged:
+                assert t.merge_updates(0, 8) == 1
+            for con, eq, expect in step["checks"]:
+                fs = F.TableFilterSet({0: F.ConstantFilter("=", eq)}) if eq is not None else F.TableFilterSet()
+                assert select_all(t, fs, L.Txn(*conns[con])) == expect, (step["do"], con, eq, merged)
+    t.close()
+
+
+@pytest.mark.parametrize("index", [False, True])
+def test_table_filter_pushdown(ctx, golden, index):
+    """test/optimizer/pushdown/table_filter_pushdown.test: the filters it expects pushed into
+    the scan, over every integer-backed type the shim attaches, with NULLs."""
+    for name, cols, queries in filter_pushdown_tables(golden):
+        n = len(cols[0][0])
+        t = CubitTable(ctx, n)
+        for j, (v, m) in enumerate(cols):
+            t.add_column(j, v, validity_from_mask(m) if m is not None else None)
+            if index:
+                t.build_index(j, L.INDEX_RANGE)
+        for fs, out_col, expect in queries:
+            rows = t.scan(fs)
+            if out_col is None:
+                assert len(rows) == expect, name
+                assert t.count(fs) == expect, name
+            else:
+                assert cols[out_col][0][rows].tolist() == expect, name
+        t.close()

@@ -201,3 +201,33 @@ def test_updates_outside_index_statistics(ctx):
 
 
 TXN_START_REG = 4611686018427388000
+
+
+def test_exact_index_over_a_wide_span(ctx):
+    """TIMESTAMP-like INT64 columns: few distinct values spread over more than 2^32. The
+    all-distinct-values index used to refuse them (the shim builds that index on attach);
+    now the distinct values are sorted on the host. Appends bring new wide values."""
+    rng = np.random.default_rng(5)
+    keys = np.array([-(1 << 50), 0, 1 << 40, (1 << 62) + 3], dtype=np.int64)
+    n = 70_001
+    a = keys[rng.integers(0, len(keys), n)]
+    valid = rng.random(n) > 0.05
+    from cubit_amd.datagen import validity_from_mask
+
+    t = CubitTable(ctx, n)
+    t.add_column(0, a, validity_from_mask(valid))
+    t.build_index(0, L.INDEX_RANGE)
+    extra = np.array([1 << 45, -(1 << 50), 7], dtype=np.int64)[rng.integers(0, 3, 5000)]
+    ev = rng.random(5000) > 0.05
+    for step in range(2):
+        data = a if step == 0 else np.concatenate([a, extra])
+        vm = valid if step == 0 else np.concatenate([valid, ev])
+        col = O.Column(data, validity_from_mask(vm))
+        for cmp in ("=", "<", ">=", "!="):
+            for k in list(keys) + [1 << 45, 7, 5]:
+                fs = F.TableFilterSet({0: F.ConstantFilter(cmp, int(k))})
+                ref = O.table_scan([col], F.serialize(fs), len(data))
+                assert np.array_equal(t.scan(fs), ref), (step, cmp, k)
+        if step == 0:
+            t.append({0: extra}, {0: validity_from_mask(ev)})
+    t.close()

@@ -187,3 +187,89 @@ def test_table_or_pushdown_reference_case(golden):
     for q in c["queries"]:
         rows = O.table_scan(cols, F.serialize(None, residual_from_json(q["tree"])), len(data))
         assert data[rows].tolist() == q["expect"], q["sql"]
+
+
+def where_filters(where):
+    """[[column, cmp, constant], …] (AND) → TableFilterSet; two filters on one column AND."""
+    per = {}
+    for col, cmp, c in where:
+        per.setdefault(col, []).append(F.ConstantFilter(cmp, c))
+    return F.TableFilterSet({c: fs[0] if len(fs) == 1 else F.ConjunctionAndFilter(fs) for c, fs in per.items()})
+
+
+def update_case_views(golden):
+    """test/sql/update/test_update.test as update lists and snapshots: yields (step, update
+    list, {connection: (start, transaction id)}). con1's update is uncommitted (its
+    transaction id) until COMMIT gives it commit id 6; the rolled-back update leaves the list."""
+    steps = golden["cases"]["update"]["steps"]
+    t1, t2, t3, t4, t5 = (TXN_START + k for k in range(1, 6))
+    u = lambda vals, vers: (np.zeros(len(vals), np.int64), np.array(vals, np.int64), np.array(vers, np.uint64))
+    yield steps[0], u([1], [t1]), {"con1": (5, t1), "con2": (5, t2)}
+    yield steps[1], u([1], [6]), {"con1": (7, t3), "con2": (7, t4)}
+    yield steps[2], u([1, 4], [6, t5]), {"con1": (7, t5), "con2": (7, t4)}
+    yield steps[3], u([1], [6]), {"con1": (8, TXN_START + 6), "con2": (8, TXN_START + 7)}
+
+
+def test_update_reference_case(golden):
+    """test/sql/update/test_update.test:11-104: an update seen by its writer only, then by all
+    after COMMIT; a rolled-back update seen by no one afterwards."""
+    data = np.array(golden["cases"]["update"]["rows"], dtype=np.int32)
+    for step, upd, conns in update_case_views(golden):
+        for con, eq, expect in step["checks"]:
+            fs = F.TableFilterSet({0: F.ConstantFilter("=", eq)}) if eq is not None else F.TableFilterSet()
+            start, tid = conns[con]
+            col = O.Column(data, updates=upd)
+            rows = O.table_scan([col], F.serialize(fs), 1, tx=O.Mvcc(start, tid))
+            seen = O.fetch(col, rows, tx=O.Mvcc(start, tid)).tolist() if len(rows) else []
+            assert list(seen) == expect, (step["do"], con, eq)
+
+
+def filter_pushdown_tables(golden):
+    """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
+    [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
+    expected values)])."""
+    c = golden["cases"]["table_filter_pushdown"]
+    out = []
+    rows = np.array(c["integers"]["rows"])
+    out.append(("integers", [(rows[:, j].astype(np.int32), None) for j in range(3)],
+                [(where_filters(q["where"]), 2, q["k"]) for q in c["integers"]["queries"]]))
+    nums = np.array(c["numbers"]["rows"])
+    for ty, width in c["numbers"]["types"].items():
+        dt = np.int32 if width == 32 else np.int64
+        out.append((ty, [(nums[:, j].astype(dt), None) for j in range(3)],
+                    [(where_filters(q["where"]), 2, q["k"]) for q in c["numbers"]["queries"]]))
+    rm = c["range_mod"]
+    b = (np.arange(rm["n"]) % rm["mod"]).astype(np.int64)
+    out.append(("range_mod", [(b, None)], [(where_filters(rm["where"]), None, rm["count"])]))
+    tm = c["time"]
+    valid = np.array([v is not None for v in tm["micros"]])
+    vals = np.array([v or 0 for v in tm["micros"]], dtype=np.int64)
+    out.append(("time", [(vals, valid)], [(where_filters([[0, "=", tm["eq"]]]), None, tm["count"])]))
+    bo = c["bool"]
+    cols = []
+    for name in ("i", "j"):
+        valid = np.array([v is not None for v in bo[name]])
+        cols.append((np.array([v or 0 for v in bo[name]], dtype=np.int32), valid))
+    out.append(("bool", cols, [(where_filters([[1, "=", bo["eq"]]]), 0, bo["i_expect"])]))
+    now = 1_760_000_000_000_000                       # a fixed NOW() in microseconds
+    year = 365 * 86_400_000_000
+    ts = np.array([now, now - 10 * year - 2 * 86_400_000_000], dtype=np.int64)
+    out.append(("timestamp", [(ts, None)],
+                [(where_filters([[0, ">=", now - year]]), None, c["timestamp"]["count"])]))
+    return out
+
+
+def test_table_filter_pushdown_reference_case(golden):
+    """test/optimizer/pushdown/table_filter_pushdown.test: every filter the file expects pushed
+    into the scan, over the integer-backed types, answered by the scan itself."""
+    from cubit_amd.datagen import validity_from_mask
+
+    for name, cols, queries in filter_pushdown_tables(golden):
+        ocols = [O.Column(v, validity_from_mask(m) if m is not None else None) for v, m in cols]
+        n = len(cols[0][0])
+        for fs, out_col, expect in queries:
+            rows = O.table_scan(ocols, F.serialize(fs), n)
+            if out_col is None:
+                assert len(rows) == expect, name
+            else:
+                assert cols[out_col][0][rows].tolist() == expect, name
