@@ -23,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cubit_gpu.h"
@@ -75,6 +76,13 @@ struct cubit_ctx {
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
     int decode_kernel = CUBIT_DECODE_AUTO;  // cubit_ctx_set_decode_kernel
     int last_decode = 0;                    // kernel of the last decode (CUBIT_DECODE_PAIRS / _RUNS)
+    // zonemap skip: the live-tile list of a launch, staged in page-locked memory and copied to
+    // the device on the stream; live_ev marks the copy done before the staging is rewritten
+    uint32_t* live_host = nullptr;
+    uint32_t* live_dev = nullptr;
+    uint64_t live_cap = 0;
+    hipEvent_t live_ev = nullptr;
+    bool live_pending = false;
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -135,14 +143,48 @@ int timing_events(cubit_ctx* ctx, hipEvent_t& start, hipEvent_t& stop) {
     return CUBIT_OK;
 }
 
+// Stage the live-tile list of a zonemap-skipping launch on the device (asynchronous on the
+// context stream): zone z becomes tiles z·per_zone … z·per_zone + per_zone - 1 of the kernel.
+int upload_live(cubit_ctx* ctx, const std::vector<uint32_t>& zones, uint32_t per_zone, const uint32_t** d_live,
+                uint32_t* n_live) {
+    const uint64_t n = (uint64_t)zones.size() * per_zone;
+    if (ctx->live_pending) {  // the previous list's copy must be done before its staging is reused
+        HIP_CHECK(hipEventSynchronize(ctx->live_ev));
+        ctx->live_pending = false;
+    }
+    if (n > ctx->live_cap) {
+        if (ctx->live_dev) HIP_CHECK(hipFree(ctx->live_dev));
+        if (ctx->live_host) HIP_CHECK(hipHostFree(ctx->live_host));
+        ctx->live_dev = nullptr;
+        ctx->live_host = nullptr;
+        ctx->live_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(n, 4096);
+        if (hipMalloc(&ctx->live_dev, cap * 4) != hipSuccess || hipHostMalloc(&ctx->live_host, cap * 4) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "live-tile list of %llu tiles failed", (unsigned long long)cap);
+        ctx->live_cap = cap;
+    }
+    if (!ctx->live_ev) HIP_CHECK(hipEventCreateWithFlags(&ctx->live_ev, hipEventDisableTiming));
+    uint64_t k = 0;
+    for (uint32_t z : zones)
+        for (uint32_t j = 0; j < per_zone; ++j) ctx->live_host[k++] = z * per_zone + j;
+    HIP_CHECK(hipMemcpyAsync(ctx->live_dev, ctx->live_host, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipEventRecord(ctx->live_ev, ctx->stream));
+    ctx->live_pending = true;
+    *d_live = ctx->live_dev;
+    *n_live = (uint32_t)n;
+    return CUBIT_OK;
+}
+
 enum class RunMode { kDecode, kCount };
 
 // Launch the evaluator over a compiled program (asynchronous on the context stream).
 //   kDecode: row ids as per-tile ascending runs + tile directory (ordered = lay them out in
 //            row order with one extra pass); kCount: count(*) and/or result words.
+// live_zones (optional, non-empty, ascending): evaluate only these zones (zonemap skip); the
+// other tiles hold no qualifying row. Not with result_words (the skipped words stay unwritten).
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
              uint64_t capacity, uint64_t* d_count, uint64_t* result_words, RunMode mode, bool timed = false,
-             bool ordered = false, bool check_capacity = false) {
+             bool ordered = false, bool check_capacity = false, const std::vector<uint32_t>* live_zones = nullptr) {
     // the directory describes only the decode launched here: a count, a failed launch or a
     // folded-away filter leaves no tiles behind for cubit_ctx_last_tiles to hand out
     ctx->last_tiles = 0;
@@ -157,11 +199,19 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.result_words = result_words;
     a.ticket = ctx->ticket;
     const uint64_t pw = padded_words(n_rows);
+    if (live_zones && (live_zones->empty() || result_words)) live_zones = nullptr;
     hipEvent_t start = nullptr, stop = nullptr;
     if (timed)
         if (int rc = timing_events(ctx, start, stop)) return rc;
     if (mode == RunMode::kCount) {
         a.num_tiles = (uint32_t)(pw / count_tile_words(prog.n_leaves));
+        if (live_zones) {
+            uint32_t n_live = 0;
+            if (int rc = upload_live(ctx, *live_zones, (uint32_t)(kZoneWords / count_tile_words(prog.n_leaves)),
+                                     &a.live, &n_live))
+                return rc;
+            a.num_tiles = n_live;
+        }
         HIP_CHECK(launch_eval_count(a, ctx->stream, start, stop));
         return CUBIT_OK;
     }
@@ -172,14 +222,23 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.num_tiles = (uint32_t)tiles;
     a.rowids = ordered && rowids ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
+    if (live_zones) {
+        static_assert(kZoneWords == 2048, "a zone is one decode tile");
+        uint32_t n_live = 0;
+        if (int rc = upload_live(ctx, *live_zones, 1, &a.live, &n_live)) return rc;
+        a.num_tiles = n_live;
+        // skipped tiles hold no rows: their directory entries are {0, 0}
+        HIP_CHECK(hipMemsetAsync(ctx->dir, 0, 2 * tiles * sizeof(uint64_t), ctx->stream));
+    }
     // persistent grid: two 512-thread workgroups per CU (VGPR-limited to 4 waves per SIMD).
     // Between one and two tiles per workgroup, every workgroup takes a whole pair instead
     // (grid = tiles / 2): the same critical path (one pair), a third fewer claims queued on
     // the ticket word at once (768 tiles: 384 instead of 512, ≈11 ns each).
+    const uint64_t work = a.num_tiles;
     const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
-    const unsigned grid = (unsigned)(tiles <= max_grid ? tiles : tiles <= 2 * max_grid ? (tiles + 1) / 2 : max_grid);
+    const unsigned grid = (unsigned)(work <= max_grid ? work : work <= 2 * max_grid ? (work + 1) / 2 : max_grid);
     HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel));
-    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel);
+    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel, a.live != nullptr);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (ordered && rowids)
@@ -237,6 +296,10 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (ctx->tmp_ids) (void)hipFree(ctx->tmp_ids);
     if (ctx->partials) (void)hipFree(ctx->partials);
     if (ctx->ticket) (void)hipFree(ctx->ticket);
+    if (ctx->live_pending) (void)hipEventSynchronize(ctx->live_ev);
+    if (ctx->live_dev) (void)hipFree(ctx->live_dev);
+    if (ctx->live_host) (void)hipHostFree(ctx->live_host);
+    if (ctx->live_ev) (void)hipEventDestroy(ctx->live_ev);
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -406,7 +469,14 @@ struct Leaf {
     int cmp = 0;
     int64_t constant = 0;
     int64_t constant2 = 0;
+    // where its zone classes (zonemaps) come from: kZoneBits = bv is a table-owned index leaf or
+    // validity bitvector, classified from its own bits; kZoneStats = bv holds exactly the valid
+    // rows whose base value passes (cmp, constant) — a K0 or candidate-check leaf — classified
+    // from the column's per-zone min / max like a ConstantFilter's CheckStatistics; kZoneNone
+    // = patched, visibility and materialised leaves (mixed everywhere)
+    int zsrc = 0;
 };
+enum { kZoneNone = 0, kZoneBits = 1, kZoneStats = 2 };
 
 struct Expr;
 using ExprP = std::shared_ptr<Expr>;
@@ -851,12 +921,43 @@ struct cubit_table {
     uint32_t last_decoded = 0;  // sum_product: values of b decoded from its index (0 = gathered)
     uint64_t* dummy_count = nullptr;
     std::unique_ptr<DevBuf> dummy;
+    // Zonemaps (RowGroup::CheckZonemap / CheckZonemapSegments, row_group.cpp:361-371, 407-445,
+    // over bitvector zones of kZoneRows rows): per table-owned bitvector (index leaf, bin,
+    // validity) a bit per zone for "no row set" (z) and "every row set" (o). Computed on the
+    // first scan that reads the bitvector; dropped (drop_zones) whenever a table-owned
+    // bitvector is written, grown or freed, so an entry always describes the current bits.
+    struct ZoneMap {
+        std::vector<uint64_t> z, o;
+        bool informative = false;  // some zone is all-zero or all-one
+    };
+    std::unordered_map<const uint64_t*, ZoneMap> zones;
+    std::unique_ptr<DevBuf> zone_dev;  // class bytes of the bitvectors being summarised
+    uint64_t zone_dev_bytes = 0;
+    // per-zone statistics of raw columns (min / max of the valid rows, any / every row valid),
+    // for leaves built from the column values (K0, candidate check), and the zone maps derived
+    // from them per predicate; dropped with the bitvector zone maps
+    struct ColZones {
+        std::vector<int64_t> mn, mx;
+        std::vector<uint8_t> fl;  // bit 0 = some row valid, bit 1 = every row valid
+    };
+    std::map<int, ColZones> col_zones;
+    std::map<std::tuple<int, int, int, int64_t, int64_t>, ZoneMap> pred_zones;
+    uint32_t last_live = 0, last_zones = 0;  // zones the last scan evaluated / the partition has
 };
 
 namespace {
 
+// A table-owned bitvector is about to be written, grown or freed: every zone map goes (they
+// are recomputed on the next scan that needs them).
+void drop_zones(cubit_table* t) {
+    t->zones.clear();
+    t->col_zones.clear();
+    t->pred_zones.clear();
+}
+
 // The column's values or indexes changed: its patched leaves are stale.
 void drop_patches(cubit_table* t, int col) {
+    drop_zones(t);
     auto it = t->upd.find(col);
     if (it != t->upd.end()) it->second.cache.clear();
 }
@@ -872,6 +973,7 @@ int alloc_table_bv(cubit_table* t, DevBuf& b) {
 // Everything derived from the row count (scratch / ones / visibility / patched leaves, all
 // nwp words): dropped when the table grows or its base changes.
 void drop_derived(cubit_table* t) {
+    drop_zones(t);
     t->scratch.clear();
     t->scratch_used = 0;
     t->ones.reset();
@@ -1504,6 +1606,7 @@ namespace {
 // nwp words in use, zero the rest. Index leaf pointers change, so everything derived from them
 // (patched leaves, scratch) is dropped by the caller.
 int grow_bitvectors(cubit_table* t, uint64_t words) {
+    drop_zones(t);
     hipStream_t s = t->ctx->stream;
     auto regrow = [&](void*& p) -> int {
         void* np = nullptr;
@@ -1667,6 +1770,7 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
     if (int rc = set_device(t->ctx)) return rc;
     hipStream_t s = t->ctx->stream;
     HIP_CHECK(hipStreamSynchronize(s));
+    drop_zones(t);  // every bitvector gains the appended rows
     // 1. capacity: bitvectors and columns grow together (×1.25 at least)
     const uint64_t need_words = padded_words(n_total);
     if (need_words > t->cap_words) {
@@ -1827,6 +1931,7 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     }
     if (m_rows.empty()) return CUBIT_OK;
     HIP_CHECK(hipStreamSynchronize(s));
+    drop_zones(t);  // the merge flips index bits in place
     if (int rc = own_column(t, c, std::max<uint64_t>(t->n_rows, c.cap_rows))) return rc;
     const uint64_t m = m_rows.size();
     DevBuf d_rows, d_vals;
@@ -1941,6 +2046,7 @@ struct Planner {
         l.bv = c.validity;
         l.column = col;
         l.pred = 1;
+        l.zsrc = kZoneBits;
         return mk_leaf(l);
     }
 
@@ -1959,6 +2065,7 @@ struct Planner {
         l.column = col;
         l.cmp = cmp;
         l.constant = c;
+        l.zsrc = kZoneStats;
         return mk_leaf(l);
     }
 
@@ -1973,6 +2080,7 @@ struct Planner {
             l.column = col;
             l.cmp = CUBIT_CMP_LT;
             l.constant = *it;
+            l.zsrc = kZoneBits;
             return mk_leaf(l);
         }
         return nullptr;
@@ -2008,6 +2116,7 @@ struct Planner {
         l.column = col;
         l.cmp = cmp;
         l.constant = c;
+        l.zsrc = kZoneStats;
         return mk_leaf(l);
     }
 
@@ -2020,6 +2129,7 @@ struct Planner {
             l.column = col;
             l.cmp = CUBIT_CMP_EQ;
             l.constant = c;
+            l.zsrc = kZoneBits;
             return mk_leaf(l);
         }
         if (ix.exact_all || ix.empty || c < ix.vmin || c > ix.vmax) return mk_false();
@@ -2093,6 +2203,7 @@ struct Planner {
                             l.column = col;
                             l.cmp = CUBIT_CMP_EQ;
                             l.constant = ix.keys[k];
+                            l.zsrc = kZoneBits;
                             acc = mk_bin(Expr::OR, acc, mk_leaf(l));
                         }
                         return acc;
@@ -2142,6 +2253,7 @@ struct Planner {
             l.pred = 2;
             l.constant = e[k];
             l.constant2 = e[k + 1];
+            l.zsrc = kZoneBits;
             acc = mk_bin(Expr::OR, acc, mk_leaf(l));
         }
         return acc;
@@ -2372,6 +2484,7 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
         }
         Leaf l = e->leaf;
         l.bv = copy;
+        l.zsrc = kZoneNone;  // the patched copy differs from the base at the updated rows
         e = mk_leaf(l, e->neg);
         return CUBIT_OK;
     }
@@ -2380,16 +2493,238 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
     return patch_updates(t, e->b, txn, patched);
 }
 
+// ---- zonemaps: the reference skips a row group (RowGroup::CheckZonemap, row_group.cpp:361-371)
+// or a run of vectors (CheckZonemapSegments, row_group.cpp:407-445) when a filter's
+// CheckStatistics (constant_filter.cpp:11-32) proves it false on the segment's min/max. Here the
+// statistics are the bitvectors themselves: per zone, "no row set" / "every row set". The
+// expression's zone classes follow three-valued logic, and zones it proves empty are skipped.
+
+using ZoneMap = cubit_table::ZoneMap;
+
+// zones that hold at least one row of the partition
+uint32_t real_zones(const cubit_table* t) { return (uint32_t)((t->n_rows + kZoneRows - 1) / kZoneRows); }
+
+// the table-owned bitvectors (kZoneBits) and the columns (kZoneStats) an expression's leaves
+// take their zone classes from
+void collect_zone_sources(const ExprP& e, std::vector<const uint64_t*>& bvs, std::vector<int>& cols) {
+    if (e->kind == Expr::LEAF) {
+        if (e->leaf.zsrc == kZoneBits && std::find(bvs.begin(), bvs.end(), e->leaf.bv) == bvs.end())
+            bvs.push_back(e->leaf.bv);
+        if (e->leaf.zsrc == kZoneStats && std::find(cols.begin(), cols.end(), e->leaf.column) == cols.end())
+            cols.push_back(e->leaf.column);
+        return;
+    }
+    if (e->a) collect_zone_sources(e->a, bvs, cols);
+    if (e->b) collect_zone_sources(e->b, bvs, cols);
+}
+
+// device scratch for zone summaries
+uint8_t* zone_scratch(cubit_table* t, uint64_t bytes) {
+    if (bytes > t->zone_dev_bytes) {
+        t->zone_dev = std::make_unique<DevBuf>();
+        t->zone_dev_bytes = 0;
+        if (hipMalloc(&t->zone_dev->p, bytes) != hipSuccess) return nullptr;
+        t->zone_dev_bytes = bytes;
+    }
+    return static_cast<uint8_t*>(t->zone_dev->p);
+}
+
+// Zone maps for the table-owned bitvectors `bvs` and zone statistics for the columns `cols`
+// that have none yet: one classification launch per bitvector (zone_class_kernel reads it
+// once), one statistics launch per column, one copy back.
+int ensure_zones(cubit_table* t, const std::vector<const uint64_t*>& bvs, const std::vector<int>& cols) {
+    std::vector<const uint64_t*> todo;
+    for (const uint64_t* b : bvs)
+        if (!t->zones.count(b)) todo.push_back(b);
+    std::vector<int> todo_c;
+    for (int c : cols)
+        if (!t->col_zones.count(c)) todo_c.push_back(c);
+    if (todo.empty() && todo_c.empty()) return CUBIT_OK;
+    const uint32_t nz = real_zones(t);
+    const uint64_t per_col = (uint64_t)nz * 17;  // min, max (int64) + flags per zone
+    const uint64_t bytes = (uint64_t)todo.size() * nz + (uint64_t)todo_c.size() * per_col + 16;
+    uint8_t* dev = zone_scratch(t, bytes);
+    if (!dev) return fail(CUBIT_ERR_OOM, "zone classes allocation failed");
+    hipStream_t s = t->ctx->stream;
+    for (size_t i = 0; i < todo.size(); ++i) HIP_CHECK(launch_zone_classes(todo[i], t->n_rows, 0, nz, dev + i * nz, s));
+    const uint64_t cbase = ((uint64_t)todo.size() * nz + 7) / 8 * 8;
+    for (size_t i = 0; i < todo_c.size(); ++i) {
+        const Column& c = t->cols.at(todo_c[i]);
+        uint8_t* p = dev + cbase + i * per_col;
+        HIP_CHECK(launch_column_zone_stats(c.data, c.type, c.validity, t->n_rows, nz, reinterpret_cast<int64_t*>(p),
+                                           reinterpret_cast<int64_t*>(p + 8ull * nz), p + 16ull * nz, s));
+    }
+    std::vector<uint8_t> host(cbase + todo_c.size() * per_col);
+    HIP_CHECK(hipMemcpyAsync(host.data(), dev, host.size(), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    const size_t nw = (nz + 63) / 64;
+    for (size_t i = 0; i < todo.size(); ++i) {
+        ZoneMap m;
+        m.z.assign(nw, 0);
+        m.o.assign(nw, 0);
+        for (uint32_t z = 0; z < nz; ++z) {
+            const uint8_t c = host[i * nz + z];
+            if (c & 1) m.z[z >> 6] |= 1ull << (z & 63);
+            if (c & 2) m.o[z >> 6] |= 1ull << (z & 63);
+            m.informative |= c != 0;
+        }
+        t->zones.emplace(todo[i], std::move(m));
+    }
+    for (size_t i = 0; i < todo_c.size(); ++i) {
+        const uint8_t* p = host.data() + cbase + i * per_col;
+        cubit_table::ColZones cz;
+        cz.mn.resize(nz);
+        cz.mx.resize(nz);
+        std::memcpy(cz.mn.data(), p, 8ull * nz);
+        std::memcpy(cz.mx.data(), p + 8ull * nz, 8ull * nz);
+        cz.fl.assign(p + 16ull * nz, p + 17ull * nz);
+        t->col_zones.emplace(todo_c[i], std::move(cz));
+    }
+    return CUBIT_OK;
+}
+
+// Zone map of the leaf {valid rows with v cmp c} of column col from the column's zone statistics:
+// ConstantFilter::CheckStatistics → NumericStats::CheckZonemap (constant_filter.cpp:11-32,
+// numeric_stats.cpp:157-228) — FILTER_ALWAYS_FALSE = every valid value fails (or no row is
+// valid), FILTER_ALWAYS_TRUE = every value passes and every row is valid.
+const ZoneMap& stats_zone_map(cubit_table* t, const Leaf& l) {
+    const auto key = std::make_tuple(l.column, l.pred, l.cmp, l.constant, l.constant2);
+    auto it = t->pred_zones.find(key);
+    if (it != t->pred_zones.end()) return it->second;
+    const cubit_table::ColZones& cz = t->col_zones.at(l.column);
+    const uint32_t nz = (uint32_t)cz.fl.size();
+    ZoneMap m;
+    m.z.assign((nz + 63) / 64, 0);
+    m.o.assign((nz + 63) / 64, 0);
+    const int64_t c = l.constant;
+    for (uint32_t z = 0; z < nz; ++z) {
+        const int64_t lo = cz.mn[z], hi = cz.mx[z];
+        bool none, all;
+        if (!(cz.fl[z] & 1)) {
+            none = true;
+            all = false;
+        } else {
+            switch (l.cmp) {
+            case CUBIT_CMP_EQ: none = c < lo || c > hi; all = lo == c && hi == c; break;
+            case CUBIT_CMP_NE: none = lo == c && hi == c; all = c < lo || c > hi; break;
+            case CUBIT_CMP_LT: none = lo >= c; all = hi < c; break;
+            case CUBIT_CMP_LE: none = lo > c; all = hi <= c; break;
+            case CUBIT_CMP_GT: none = hi <= c; all = lo > c; break;
+            default: none = hi < c; all = lo >= c; break;  // GE
+            }
+            all = all && (cz.fl[z] & 2);
+        }
+        if (none) m.z[z >> 6] |= 1ull << (z & 63);
+        if (all) m.o[z >> 6] |= 1ull << (z & 63);
+        m.informative |= none || all;
+    }
+    return t->pred_zones.emplace(key, std::move(m)).first->second;
+}
+
+struct ZoneSet {
+    std::vector<uint64_t> z, o;  // zones where the expression is false / true on every row
+};
+
+// three-valued evaluation of an expression over zone classes; leaves without zone classes are
+// mixed everywhere
+void zone_eval(cubit_table* t, const ExprP& e, size_t nw, ZoneSet& r) {
+    switch (e->kind) {
+    case Expr::LEAF: {
+        const ZoneMap* m = nullptr;
+        if (e->leaf.zsrc == kZoneBits) {
+            auto it = t->zones.find(e->leaf.bv);
+            if (it != t->zones.end()) m = &it->second;
+        } else if (e->leaf.zsrc == kZoneStats) {
+            m = &stats_zone_map(t, e->leaf);
+        }
+        if (m) {
+            r.z = m->z;
+            r.o = m->o;
+        } else {
+            r.z.assign(nw, 0);
+            r.o.assign(nw, 0);
+        }
+        if (e->neg) std::swap(r.z, r.o);
+        return;
+    }
+    case Expr::CONST_TRUE:
+        r.z.assign(nw, 0);
+        r.o.assign(nw, ~0ull);
+        return;
+    case Expr::CONST_FALSE:
+        r.z.assign(nw, ~0ull);
+        r.o.assign(nw, 0);
+        return;
+    default: break;
+    }
+    ZoneSet b;
+    zone_eval(t, e->a, nw, r);
+    zone_eval(t, e->b, nw, b);
+    for (size_t w = 0; w < nw; ++w) {
+        const uint64_t az = r.z[w], ao = r.o[w];
+        switch (e->kind) {
+        case Expr::AND: r.z[w] = az | b.z[w]; r.o[w] = ao & b.o[w]; break;
+        case Expr::OR: r.z[w] = az & b.z[w]; r.o[w] = ao | b.o[w]; break;
+        default: r.z[w] = az | b.o[w]; r.o[w] = ao & b.z[w]; break;  // ANDNOT
+        }
+    }
+}
+
+// does any leaf carry a zone class other than "mixed"?
+bool zone_informative(cubit_table* t, const ExprP& e) {
+    if (e->kind == Expr::LEAF) {
+        if (e->leaf.zsrc == kZoneBits) {
+            auto it = t->zones.find(e->leaf.bv);
+            return it != t->zones.end() && it->second.informative;
+        }
+        if (e->leaf.zsrc == kZoneStats) return stats_zone_map(t, e->leaf).informative;
+        return false;
+    }
+    return (e->a && zone_informative(t, e->a)) || (e->b && zone_informative(t, e->b));
+}
+
+// The zonemap skip of a planned expression. live = the zones a kernel must evaluate, when at
+// least one zone in 32 provably holds no qualifying row (below that the list and the cleared
+// directory cost about what the skipped reads save); left empty otherwise = every zone.
+// *none = no zone can hold a qualifying row.
+int zone_plan(cubit_table* t, const ExprP& e, std::vector<uint32_t>& live, bool* none) {
+    live.clear();
+    *none = false;
+    std::vector<const uint64_t*> bvs;
+    std::vector<int> cols;
+    collect_zone_sources(e, bvs, cols);
+    if (bvs.empty() && cols.empty()) return CUBIT_OK;
+    if (int rc = ensure_zones(t, bvs, cols)) return rc;
+    if (!zone_informative(t, e)) return CUBIT_OK;  // every zone of every leaf mixed: nothing to skip
+    const uint32_t nz = real_zones(t);
+    ZoneSet r;
+    zone_eval(t, e, (nz + 63) / 64, r);
+    uint32_t dead = 0;
+    for (uint32_t z = 0; z < nz; ++z) dead += (uint32_t)((r.z[z >> 6] >> (z & 63)) & 1);
+    if (dead == nz) {
+        *none = true;
+        return CUBIT_OK;
+    }
+    if (dead == 0 || (uint64_t)dead * 32 < nz) return CUBIT_OK;
+    live.reserve(nz - dead);
+    for (uint32_t z = 0; z < nz; ++z)
+        if (!((r.z[z >> 6] >> (z & 63)) & 1)) live.push_back(z);
+    return CUBIT_OK;
+}
+
 }  // namespace
 
 namespace {
 
 // Plan a pushed filter tree for a transaction into one program (front half of every scan):
 // planner → MVCC update patches → visibility leaf → constant folding → split until it fits
-// one pass → emit. *empty = the filter is FALSE (no kernel needed).
+// one pass → emit. *empty = the filter is FALSE (no kernel needed). live (optional) receives the
+// zonemap skip's live zones (empty = evaluate every zone); a filter false on every zone is
+// *empty too.
 int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes, const cubit_txn* txn,
-                 Emitter& em, bool* empty) {
+                 Emitter& em, bool* empty, std::vector<uint32_t>* live = nullptr) {
     *empty = false;
+    if (live) live->clear();
     cubit_ctx* ctx = t->ctx;
     t->scratch_used = 0;
     t->last_passes = 0;
@@ -2485,6 +2820,15 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
         l.bv = ones;
         e = mk_leaf(l);
     }
+    if (live) {
+        bool none = false;
+        if (int rc = zone_plan(t, e, *live, &none)) return rc;
+        if (none) {
+            *empty = true;
+            t->last_leaves = 0;
+            return CUBIT_OK;
+        }
+    }
     if (int rc = fit(t, e)) return rc;
     em.emit_top(e);
     if (!em.ok) return fail(CUBIT_ERR_UNSUPPORTED, "program does not fit one pass");
@@ -2557,20 +2901,27 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     t->ctx->last_tiles = 0;  // until this scan's decode is launched (a planning error leaves none)
     if (t->n_rows == 0) {  // empty partition
         t->last_leaves = t->last_passes = 0;
+        t->last_live = t->last_zones = 0;
         HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
         return CUBIT_OK;
     }
     Emitter em;
     bool empty = false;
-    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
-    if (empty) {  // the filter folded to FALSE: no launch, no tiles
+    std::vector<uint32_t> live;
+    const bool zonemap = (flags & CUBIT_SCAN_NO_ZONEMAP) == 0;
+    t->last_zones = real_zones(t);
+    t->last_live = 0;
+    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty, zonemap ? &live : nullptr)) return rc;
+    if (empty) {  // the filter folded to FALSE (or the zonemaps rule out every zone): no launch, no tiles
         t->ctx->last_tiles = 0;
         HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
         return CUBIT_OK;
     }
+    t->last_live = live.empty() ? t->last_zones : (uint32_t)live.size();
     return run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
                     nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
-                    (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0);
+                    (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0,
+                    live.empty() ? nullptr : &live);
 }
 
 extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
@@ -2616,12 +2967,17 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
     }
     Emitter em;
     bool empty = false;
-    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty)) return rc;
+    std::vector<uint32_t> live;
+    t->last_zones = real_zones(t);
+    t->last_live = 0;
+    if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty, (flags & CUBIT_SUM_NO_ZONEMAP) ? nullptr : &live))
+        return rc;
     if (empty) {
         HIP_CHECK(hipMemsetAsync(d_out, 0, 2 * sizeof(int64_t), ctx->stream));
         HIP_CHECK(hipMemsetAsync(count, 0, sizeof(uint64_t), ctx->stream));
         return CUBIT_OK;
     }
+    t->last_live = live.empty() ? t->last_zones : (uint32_t)live.size();
     SumArgs sa{};
     sa.a = static_cast<const int64_t*>(ait->second.data);
     sa.a_valid = ait->second.validity;
@@ -2650,6 +3006,11 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
     a.count = count;
     a.ticket = ctx->ticket;
     a.num_tiles = (uint32_t)(padded_words(t->n_rows) / decode_tile_words());
+    if (!live.empty()) {  // zonemap skip: a zone is one tile of the fused kernel
+        uint32_t n_live = 0;
+        if (int rc = upload_live(ctx, live, 1, &a.live, &n_live)) return rc;
+        a.num_tiles = n_live;
+    }
     const unsigned grid = std::min<unsigned>(a.num_tiles, sum_product_grid((unsigned)ctx->n_cus));
     HIP_CHECK(launch_eval_sum_product(a, sa, std::max(grid, 1u), d_out, ctx->stream));
     return CUBIT_OK;
@@ -2660,6 +3021,14 @@ extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_
     CUBIT_LOCK(t->ctx);
     if (n_leaves) *n_leaves = t->last_leaves;
     if (n_passes) *n_passes = t->last_passes;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_zones(cubit_table* t, uint32_t* evaluated, uint32_t* zones) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    if (evaluated) *evaluated = t->last_live;
+    if (zones) *zones = t->last_zones;
     return CUBIT_OK;
 }
 

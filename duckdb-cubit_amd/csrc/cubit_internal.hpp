@@ -66,7 +66,16 @@ struct EvalArgs {
     // counter + arrival counters. The last workgroup to finish publishes *count and re-zeroes
     // the ticket, so no memset launch precedes a scan (finish_ticket, cubit_kernels.hip).
     uint64_t* ticket;
+    // zonemap skip (device, ascending): the tiles to evaluate, num_tiles entries; null = every
+    // tile 0 … num_tiles-1. The planner leaves out the tiles whose zone classes prove the program
+    // false on every row (RowGroup::CheckZonemap, row_group.cpp:361-371, over bitvector zones).
+    const uint32_t* live;
 };
+// Zonemaps: one zone = one decode tile (2,048 words = 131,072 rows). Class byte per zone:
+// bit 0 = no row of the zone is set, bit 1 = every row of the zone is set (a zone past the
+// last row has both).
+constexpr uint64_t kZoneWords = 2048;
+constexpr uint64_t kZoneRows = kZoneWords * 64;
 constexpr uint32_t kTicketStride = 64;  // words (512 B) between ticket counters
 constexpr uint32_t kTicketGroups = 8;
 constexpr uint32_t kTicketWords = kTicketStride * (kTicketGroups + 2);
@@ -80,9 +89,15 @@ int decode_block_threads();
 // their elapsed time is the kernel's execution, as rocprofv3's kernel trace reports it
 // kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed;
 // decode_kernel_for resolves it (1 or 2) for a launch
-int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel);
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live = false);
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream,
                               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int kernel = 0);
+// zone classes of a bitvector (class byte per zone, see kZoneWords) for zones [z0, z0 + nz)
+hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0, uint32_t nz, uint8_t* out,
+                               hipStream_t stream);
+// per-zone min / max of a raw column's valid rows; fl bit 0 = some row valid, bit 1 = every row
+hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* validity, uint64_t n_rows, uint32_t nz,
+                                    int64_t* mn, int64_t* mx, uint8_t* fl, hipStream_t stream);
 // evaluate + count (and/or write the result bitvector)
 hipError_t launch_eval_count(const EvalArgs& a, hipStream_t stream, hipEvent_t ev0 = nullptr,
                              hipEvent_t ev1 = nullptr);

@@ -240,6 +240,10 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
     }
 }
 
+// The i-th tile of a launch: entry i of the planner's live-tile list (zonemap skip) or i itself.
+// i is uniform, so the list entry is a scalar load; callers fetch it one tile ahead.
+__device__ __forceinline__ uint32_t tile_at(const EvalArgs& a, uint32_t i) { return a.live ? a.live[i] : i; }
+
 // ------------------------------------------------------------------ K1: count / materialise
 
 // count(*) of the program and/or its result bitvector. Persistent: workgroup g takes tiles
@@ -254,26 +258,29 @@ __global__ __launch_bounds__(512, 4) void eval_count_kernel(EvalArgs a) {
     const uint32_t G = gridDim.x;
     uint64_t c = 0;
     u64x2 v0[K][PAIRS], v1[K][PAIRS];
-    uint32_t tile = blockIdx.x;
-    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v0);
-    if (tile + G < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)(tile + G) * TILE_WORDS, t, v1);
-    auto step = [&](u64x2 (&v)[K][PAIRS], uint32_t tl) {
-        const uint64_t tile_word0 = (uint64_t)tl * TILE_WORDS;
+    // i indexes the launch's tiles (tile_at: every tile, or the live-tile list)
+    uint32_t i = blockIdx.x;
+    const uint32_t n = a.num_tiles;
+    if (i < n) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile_at(a, i) * TILE_WORDS, t, v0);
+    if (i + G < n) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile_at(a, i + G) * TILE_WORDS, t, v1);
+    auto step = [&](u64x2 (&v)[K][PAIRS], uint32_t ii) {
+        const uint32_t ahead = ii + 2 * G;
+        const uint32_t ahead_tile = ahead < n ? tile_at(a, ahead) : 0;  // list entry fetched before the eval
+        const uint64_t tile_word0 = (uint64_t)tile_at(a, ii) * TILE_WORDS;
         uint64_t r[NW];
         eval_words<K, NW, FORM>(a.prog, v, r);
-        const uint32_t ahead = tl + 2 * G;
-        if (ahead < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)ahead * TILE_WORDS, t, v);
+        if (ahead < n) load_tile<K, PAIRS, THREADS>(a, (uint64_t)ahead_tile * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
 #pragma unroll
         for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
     };
-    while (tile < a.num_tiles) {
-        step(v0, tile);
-        tile += G;
-        if (tile >= a.num_tiles) break;
-        step(v1, tile);
-        tile += G;
+    while (i < n) {
+        step(v0, i);
+        i += G;
+        if (i >= n) break;
+        step(v1, i);
+        i += G;
     }
     __shared__ uint64_t s_part[THREADS / 64];
     c = wave_sum(c);
@@ -705,9 +712,11 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
 // next tile is evaluated, and the closed run is copied out (16-byte stores) after that tile's
 // scan barrier. The claim count follows the output volume (≈ q / RUN_CAP + workgroups) instead
 // of the tile count (pairs: one per two tiles), and a tile costs one block barrier instead of
-// one and a half. A stage entry is the row's offset from the run's first tile row (a unit is
-// G·TILE_ROWS further; a run spans at most MAXU units so that fits 32 bits), so the copy-out adds
-// one base per run. Tiles with more than RUN_CAP hits claim on
+// one and a half. A stage entry is the row's offset from the run's first tile row (a run spans
+// fewer than 2^32 / TILE_ROWS tiles so that fits 32 bits), so the copy-out adds one base per run.
+// With a live-tile list (zonemap skip) the workgroup walks list entries g, g+G, … instead of
+// tiles; runs, offsets and the directory are per tile as before, skipped tiles keep the {0, 0}
+// entries the host cleared. Tiles with more than RUN_CAP hits claim on
 // their own and write straight to the output (dense path). The directory gets {start, len} per
 // tile ({0, 0} for empty tiles) as with pairs.
 // Workgroup g takes tiles g, g+G, … (static striding). A dynamic hand-out of the last third of
@@ -739,17 +748,21 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     const int lane = t & 63;
     const int wave = t >> 6;
     const uint32_t G = gridDim.x;
-    // offsets (u - u_first)·G·TILE_ROWS + row must fit 32 bits
-    const uint32_t MAXU = (uint32_t)((1ull << 32) / ((uint64_t)G * TILE_ROWS)) < 64
-                              ? (uint32_t)((1ull << 32) / ((uint64_t)G * TILE_ROWS)) : 64u;
-    if (MAXU < 1) __builtin_trap();
+    // a stage entry (tile - run's first tile)·TILE_ROWS + row must fit 32 bits
+    constexpr uint32_t kMaxSpan = (uint32_t)((1ull << 32) / TILE_ROWS);
     const bool write_ids = a.rowids != nullptr;
     uint64_t pend_claim = 0;  // thread 0: the closed run's claimed base
     uint64_t mine = 0;        // thread 0: rows claimed by this workgroup
 
     u64x2 v[K][PAIRS];
-    uint32_t tile = blockIdx.x;
-    if (tile < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
+    // i indexes the launch's tiles (every tile, or the live-tile list of the zonemap skip);
+    // tile / next_tile are the current and the next tile, the list entry after them is fetched
+    // one unit ahead
+    const uint32_t n_idx = a.num_tiles;
+    uint32_t i = blockIdx.x;
+    uint32_t tile = i < n_idx ? tile_at(a, i) : 0;
+    uint32_t next_tile = i + G < n_idx ? tile_at(a, i + G) : 0;
+    if (i < n_idx) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
 
     // copy out closed run rs at s_off (published before the preceding barrier) and write its
     // directory entries
@@ -782,16 +795,17 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     };
 
     int rs = 0;              // the open run's stage
-    uint32_t fill = 0, rn = 0, u_first = 0;  // open run: entries, tiles, first unit (uniform)
+    uint32_t fill = 0, rn = 0, rfirst = 0;  // open run: entries, tiles, first tile (uniform)
     bool pending = false;    // a closed run (stage rs ^ 1) waits for its claim and copy-out
     uint32_t u = 0;
-    while (tile < a.num_tiles) {
+    while (i < n_idx) {
         const int par = (int)(u & 1);
         const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
-        const uint32_t next = tile + G;
+        const bool has_next = i + G < n_idx;
+        const uint32_t after = i + 2 * G < n_idx ? tile_at(a, i + 2 * G) : 0;
         uint64_t r[NW];
         eval_words<K, NW, FORM>(a.prog, v, r);
-        if (EARLY && next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        if (EARLY && has_next) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next_tile * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
         if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
         uint32_t packed = 0;
@@ -826,13 +840,13 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
         // close the open run when this tile does not fit (claimed after the previous run's
         // copy-out: issuing the claim before it measured 3 µs slower at K = 5)
         const bool close = !dense && rn > 0 &&
-                           (fill + tile_count > (uint32_t)RUN_CAP || rn == (uint32_t)MAXT || u - u_first >= MAXU);
+                           (fill + tile_count > (uint32_t)RUN_CAP || rn == (uint32_t)MAXT || tile - rfirst >= kMaxSpan);
         const bool copied = pending;
         if (pending) {
             copy_out(rs ^ 1);
             pending = false;
         }
-        if (!EARLY && next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        if (!EARLY && has_next) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next_tile * TILE_WORDS, t, v);
         const int64_t row0 = a.row_base + (int64_t)tile_word0 * 64;
         if (dense) {
             // dense tile: its own claim, direct writes
@@ -870,7 +884,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
                 if (t == 0) {
                     s_rn[rs] = rn;
                     s_rfill[rs] = fill;
-                    s_rfirst[rs] = blockIdx.x + u_first * G;
+                    s_rfirst[rs] = rfirst;
                     pend_claim = 0;
                     if (fill) {
                         pend_claim = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)fill);
@@ -884,9 +898,9 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
                 // the stage we switch to was copied out in this unit: every thread must be done
                 if (copied) __syncthreads();
             }
-            if (rn == 0) u_first = u;
+            if (rn == 0) rfirst = tile;
             if (tile_count && write_ids) {
-                const uint32_t delta = (u - u_first) * G * (uint32_t)TILE_ROWS;
+                const uint32_t delta = (tile - rfirst) * (uint32_t)TILE_ROWS;
 #pragma unroll
                 for (int p = 0; p < PAIRS; ++p) {
                     uint32_t off = fill + pair_off[p];
@@ -909,7 +923,9 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
             fill += tile_count;
             ++rn;
         }
-        tile = next;
+        i += G;
+        tile = next_tile;
+        next_tile = after;
         ++u;
     }
     // drain: the closed run (if any), then the open one
@@ -922,7 +938,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
         if (t == 0) {
             s_rn[rs] = rn;
             s_rfill[rs] = fill;
-            s_rfirst[rs] = blockIdx.x + u_first * G;
+            s_rfirst[rs] = rfirst;
             uint64_t c = 0;
             if (fill) {
                 c = atomicAdd(reinterpret_cast<unsigned long long*>(a.ticket), (unsigned long long)fill);
@@ -997,7 +1013,10 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
 
     u64x2 v[K][PAIRS];
     u64x2 dv[M > 0 ? M : 1][PAIRS];
-    uint32_t tile = blockIdx.x;
+    // i indexes the launch's tiles (every tile, or the zonemap skip's live-tile list)
+    const uint32_t n_idx = a.num_tiles;
+    uint32_t i = blockIdx.x;
+    uint32_t tile = i < n_idx ? tile_at(a, i) : 0;
     auto load_decode = [&](uint64_t tile_word0) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -1006,17 +1025,18 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             for (int p = 0; p < PAIRS; ++p) dv[m][p] = __builtin_nontemporal_load(base + p * THREADS + t);
         }
     };
-    if (tile < a.num_tiles) {
+    if (i < n_idx) {
         load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
         load_decode((uint64_t)tile * TILE_WORDS);
     }
-    while (tile < a.num_tiles) {
+    while (i < n_idx) {
         const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+        const bool has_next = i + gridDim.x < n_idx;
+        const uint32_t next = has_next ? tile_at(a, i + gridDim.x) : 0;
         uint64_t r[NW];
         eval_words<K, NW, FORM>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
-        const uint32_t next = tile + gridDim.x;
-        if (next < a.num_tiles) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
+        if (has_next) load_tile<K, PAIRS, THREADS>(a, (uint64_t)next * TILE_WORDS, t, v);
         uint64_t packed = 0;
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p)
@@ -1067,7 +1087,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                 }
             }
         }
-        if (M > 0 && next < a.num_tiles) load_decode((uint64_t)next * TILE_WORDS);
+        if (M > 0 && has_next) load_decode((uint64_t)next * TILE_WORDS);
         __syncthreads();  // stage complete
         if (staged) {
             // 4 gathers in flight per thread per round
@@ -1091,6 +1111,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             }
         }
         __syncthreads();  // stage / wave totals free
+        i += gridDim.x;
         tile = next;
     }
     // block reduce of the 128-bit partial sums
@@ -1658,6 +1679,83 @@ __global__ __launch_bounds__(64) void sum_partials_kernel(const int64_t* __restr
     }
 }
 
+// ------------------------------------------------------------------ zonemaps
+
+// Zone classes of a bitvector (the bitmap form of a segment's min/max statistics,
+// NumericStats::CheckZonemap, numeric_stats.cpp:157-228): one workgroup per zone of kZoneWords
+// words, each thread ANDs and ORs 8 words (4 coalesced 16-byte loads). Only rows < n_rows count:
+// words past the last row are skipped, the last word is masked. out[z - z0] bit 0 = no row set,
+// bit 1 = every row set (both for a zone past the last row).
+__global__ __launch_bounds__(256) void zone_class_kernel(const uint64_t* __restrict__ bv, uint64_t n_rows,
+                                                         uint32_t z0, uint8_t* __restrict__ out) {
+    const uint32_t z = z0 + blockIdx.x;
+    const int t = threadIdx.x;
+    const uint64_t n_words = (n_rows + 63) / 64;
+    const uint64_t last_mask = (n_rows & 63) ? (1ull << (n_rows & 63)) - 1 : ~0ull;
+    uint64_t all = ~0ull, any = 0;
+    const uint64_t w0 = (uint64_t)z * kZoneWords;
+#pragma unroll
+    for (int p = 0; p < (int)(kZoneWords / 512); ++p) {
+        const uint64_t gw = w0 + (uint64_t)(p * 256 + t) * 2;
+        if (gw >= n_words) continue;
+        const u64x2 x = reinterpret_cast<const u64x2*>(bv + w0)[p * 256 + t];
+        uint64_t a = x.x, b = x.y;
+        uint64_t ma = gw == n_words - 1 ? last_mask : ~0ull;
+        if (gw + 1 >= n_words) {  // b is past the last row (or a is the last word)
+            all &= a | ~ma;
+            any |= a & ma;
+            continue;
+        }
+        const uint64_t mb = gw + 1 == n_words - 1 ? last_mask : ~0ull;
+        all &= (a | ~ma) & (b | ~mb);
+        any |= (a & ma) | (b & mb);
+    }
+    const int none_set = __syncthreads_and(any == 0);
+    const int all_set = __syncthreads_and(all == ~0ull);
+    if (t == 0) out[blockIdx.x] = (uint8_t)((none_set ? 1 : 0) | (all_set ? 2 : 0));
+}
+
+// Per-zone statistics of a raw column (the segment statistics CheckZonemap consults,
+// numeric_stats.cpp:157-228): min / max over the zone's valid rows and whether any / every row
+// is valid. One workgroup per zone; consecutive threads read consecutive rows.
+template <typename T>
+__global__ __launch_bounds__(256) void column_zone_stats_kernel(const T* __restrict__ col,
+                                                                const uint64_t* __restrict__ validity, uint64_t n_rows,
+                                                                int64_t* __restrict__ mn, int64_t* __restrict__ mx,
+                                                                uint8_t* __restrict__ fl) {
+    __shared__ int64_t s_lo[256], s_hi[256];
+    __shared__ uint32_t s_n[256];
+    const int t = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * kZoneRows;
+    const uint64_t r1 = min(n_rows, r0 + kZoneRows);
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    uint32_t nv = 0;
+    for (uint64_t r = r0 + t; r < r1; r += 256) {
+        if (validity && !((validity[r >> 6] >> (r & 63)) & 1ull)) continue;
+        const int64_t v = (int64_t)col[r];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+        ++nv;
+    }
+    s_lo[t] = lo;
+    s_hi[t] = hi;
+    s_n[t] = nv;
+    __syncthreads();
+    for (int d = 128; d > 0; d >>= 1) {
+        if (t < d) {
+            s_lo[t] = s_lo[t + d] < s_lo[t] ? s_lo[t + d] : s_lo[t];
+            s_hi[t] = s_hi[t + d] > s_hi[t] ? s_hi[t + d] : s_hi[t];
+            s_n[t] += s_n[t + d];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        mn[blockIdx.x] = s_lo[0];
+        mx[blockIdx.x] = s_hi[0];
+        fl[blockIdx.x] = (uint8_t)((s_n[0] > 0 ? 1 : 0) | (r1 > r0 && s_n[0] == r1 - r0 ? 2 : 0));
+    }
+}
+
 // ------------------------------------------------------------------ K4: MVCC
 
 __global__ __launch_bounds__(256) void fill_valid_kernel(uint64_t* __restrict__ words, uint64_t n_rows,
@@ -1864,8 +1962,11 @@ uint32_t eval_form(const EvalProgram& p) {
 // µs; K = 5 at 1.9 %: 82 vs 84 µs) — except K = 4, where at Q6's density a run holds two tiles
 // and the pair kernel measured as fast or 1 % faster (73.2 vs 74.2 µs); the pair kernel for one
 // or two tiles per workgroup (small inputs: one claim per workgroup either way).
-int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel) {
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live) {
     (void)n_leaves;
+    // a live-tile list (zonemap skip) needs the run kernel: its stage offsets are taken from the
+    // run's first tile, while the pair kernel places tile B G tiles after tile A
+    if (live) return 2;
     if (kernel == 1 || kernel == 2) return kernel;
     return num_tiles > 2ull * grid ? 2 : 1;
 }
@@ -1873,7 +1974,7 @@ int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int 
 template <int K, int FORM>
 void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                       int kernel) {
-    if (decode_kernel_for(K, a.num_tiles, grid, kernel) == 2)
+    if (decode_kernel_for(K, a.num_tiles, grid, kernel, a.live != nullptr) == 2)
         hipExtLaunchKernelGGL((eval_decode_runs<K, kDecodePairs, kRunCap, kDecodeThreads, FORM>), dim3(grid),
                               dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
     else
@@ -2105,6 +2206,25 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
 hipError_t launch_fill_valid(uint64_t* words, uint64_t n_rows, hipStream_t stream) {
     const uint64_t nw = padded_words(n_rows);
     hipLaunchKernelGGL(fill_valid_kernel, dim3(grid_for(nw)), dim3(256), 0, stream, words, n_rows, nw);
+    return hipGetLastError();
+}
+
+hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0, uint32_t nz, uint8_t* out,
+                               hipStream_t stream) {
+    if (nz == 0) return hipSuccess;
+    hipLaunchKernelGGL(zone_class_kernel, dim3(nz), dim3(256), 0, stream, bv, n_rows, z0, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* validity, uint64_t n_rows, uint32_t nz,
+                                    int64_t* mn, int64_t* mx, uint8_t* fl, hipStream_t stream) {
+    if (nz == 0) return hipSuccess;
+    if (type == 0)
+        hipLaunchKernelGGL(column_zone_stats_kernel<int32_t>, dim3(nz), dim3(256), 0, stream,
+                           static_cast<const int32_t*>(col), validity, n_rows, mn, mx, fl);
+    else
+        hipLaunchKernelGGL(column_zone_stats_kernel<int64_t>, dim3(nz), dim3(256), 0, stream,
+                           static_cast<const int64_t*>(col), validity, n_rows, mn, mx, fl);
     return hipGetLastError();
 }
 

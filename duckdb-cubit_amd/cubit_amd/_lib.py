@@ -24,10 +24,12 @@ CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
 FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = range(5)
 INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2
 SUM_GATHER_B = 1
+SUM_NO_ZONEMAP = 2
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2
 SCAN_CHECK_CAPACITY = 4  # synchronise; ERR_CAPACITY when the count exceeds the buffer
+SCAN_NO_ZONEMAP = 8  # evaluate every zone (the zonemap skip off; results are identical)
 DECODE_AUTO, DECODE_PAIRS, DECODE_RUNS = 0, 1, 2
 
 
@@ -105,6 +107,7 @@ GPU_SIGNATURES = {
     ),
     "cubit_table_probe": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P]),
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
+    "cubit_table_last_zones": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
     "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),

@@ -278,24 +278,27 @@ class CubitTable:
 
     # ------------------------------------------------------------------ scan
     def scan_into(self, plan_nodes, rowids_dptr: int, capacity: int, count_dptr: int,
-                  txn: Optional[L.Txn] = None, count_only: bool = False, ordered: bool = False) -> None:
+                  txn: Optional[L.Txn] = None, count_only: bool = False, ordered: bool = False,
+                  zonemap: bool = True) -> None:
         """Asynchronous scan into caller-owned device buffers (the bench path)."""
         arr = plan_nodes if isinstance(plan_nodes, C.Array) else to_ctypes(plan_nodes)
         n = len(plan_nodes) if not isinstance(plan_nodes, C.Array) else len(arr)
         flags = (L.SCAN_COUNT_ONLY if count_only else 0) | (L.SCAN_ORDERED if ordered else 0)
+        flags |= 0 if zonemap else L.SCAN_NO_ZONEMAP
         L.check(self.lib.cubit_table_scan(self.handle, arr, n, C.byref(txn) if txn is not None else None,
                                           C.c_void_p(rowids_dptr) if rowids_dptr else None, capacity,
                                           C.c_void_p(count_dptr), flags))
 
     def scan(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
-             txn: Optional[L.Txn] = None, capacity: Optional[int] = None, ordered: bool = True) -> np.ndarray:
+             txn: Optional[L.Txn] = None, capacity: Optional[int] = None, ordered: bool = True,
+             zonemap: bool = True) -> np.ndarray:
         """Synchronous scan returning the global row ids as numpy int64: ascending with
         ordered=True (device ordered pass), else in tile-run order (see last_tiles())."""
         plan = serialize(filter_set, residual)
         cap = self.n_rows if capacity is None else capacity
         out = self.ctx.alloc(max(cap, 1) * 8)
         cnt = self.ctx.alloc(16)
-        self.scan_into(plan.nodes, out.addr, cap, cnt.addr, txn, ordered=ordered)
+        self.scan_into(plan.nodes, out.addr, cap, cnt.addr, txn, ordered=ordered, zonemap=zonemap)
         self.ctx.check()
         n = int(cnt.download(np.uint64, 1)[0])
         if n > cap:
@@ -303,10 +306,10 @@ class CubitTable:
         return out.download(np.int64, n)
 
     def count(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
-              txn: Optional[L.Txn] = None) -> int:
+              txn: Optional[L.Txn] = None, zonemap: bool = True) -> int:
         plan = serialize(filter_set, residual)
         cnt = self.ctx.alloc(16)
-        self.scan_into(plan.nodes, 0, 0, cnt.addr, txn, count_only=True)
+        self.scan_into(plan.nodes, 0, 0, cnt.addr, txn, count_only=True, zonemap=zonemap)
         self.ctx.check()
         return int(cnt.download(np.uint64, 1)[0])
 
@@ -318,7 +321,7 @@ class CubitTable:
 
     def sum_product(self, col_a: int, col_b: int, filter_set: Optional[TableFilterSet] = None,
                     residual: Optional[Residual] = None, txn: Optional[L.Txn] = None,
-                    gather_b: bool = False) -> Tuple[int, int]:
+                    gather_b: bool = False, zonemap: bool = True) -> Tuple[int, int]:
         """SELECT sum(a*b), count(*) WHERE <filter> in one fused pass → (sum as a Python int
         of the 128-bit DECIMAL storage, qualifying rows)."""
         plan = serialize(filter_set, residual)
@@ -328,7 +331,8 @@ class CubitTable:
         L.check(self.lib.cubit_table_sum_product(self.handle, arr, len(plan.nodes),
                                                  C.byref(txn) if txn is not None else None, col_a, col_b,
                                                  C.c_void_p(out.addr), C.c_void_p(cnt.addr),
-                                                 L.SUM_GATHER_B if gather_b else 0))
+                                                 (L.SUM_GATHER_B if gather_b else 0)
+                                                 | (0 if zonemap else L.SUM_NO_ZONEMAP)))
         self.ctx.check()
         lo, hi = (int(x) for x in out.download(np.int64, 2))
         n = int(cnt.download(np.uint64, 1)[0])
@@ -340,6 +344,14 @@ class CubitTable:
         v = C.c_uint32()
         L.check(self.lib.cubit_table_last_sum_decode(self.handle, C.byref(v)))
         return int(v.value)
+
+    def last_zones(self):
+        """(zones the last scan / sum_product evaluated, zones of the partition): fewer
+        evaluated when the zonemaps skipped zones its filter is false on."""
+        ev = C.c_uint32()
+        nz = C.c_uint32()
+        L.check(self.lib.cubit_table_last_zones(self.handle, C.byref(ev), C.byref(nz)))
+        return int(ev.value), int(nz.value)
 
     def last_plan(self):
         k = C.c_uint32()

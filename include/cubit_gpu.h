@@ -85,6 +85,13 @@ extern "C" {
 #define CUBIT_SCAN_COUNT_ONLY 1u     /* do not materialise row ids */
 #define CUBIT_SCAN_ORDERED 2u        /* one globally ascending array */
 #define CUBIT_SCAN_CHECK_CAPACITY 4u /* synchronise; CUBIT_ERR_CAPACITY when *d_count > capacity */
+/* Zonemaps (RowGroup::CheckZonemap / CheckZonemapSegments, src/storage/table/row_group.cpp:361-371,
+ * 407-445): every index and validity bitvector carries, per zone of 131,072 rows, whether no row
+ * or every row of the zone is set. A scan evaluates its filter over these classes (three-valued
+ * logic) and skips the zones where it is false on every row — as the reference skips row groups
+ * whose min/max statistics fail a filter. Results are identical either way; this flag turns the
+ * skip off. */
+#define CUBIT_SCAN_NO_ZONEMAP 8u
 
 typedef struct cubit_ctx cubit_ctx;
 typedef struct cubit_table cubit_table;
@@ -273,6 +280,9 @@ int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64
                       uint64_t max_n, int64_t *d_out);
 /* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
 int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
+/* Zones (131,072 rows each) the last scan or sum_product evaluated, out of the partition's
+ * zones; fewer when the zonemaps skipped some (0 when the filter folded to FALSE). */
+int cubit_table_last_zones(cubit_table *t, uint32_t *evaluated, uint32_t *zones);
 
 /* SELECT sum(a * b) WHERE <filter> as one fused pass (K1 + K3): evaluate the program,
  * gather a (and b) for the qualifying rows only, accumulate in 128 bits — no row ids are
@@ -284,6 +294,7 @@ int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes
  * sum; d_count (optional) = qualifying rows. Visible MVCC updates on a or b fall back to
  * scan + probe + sum (those columns must then be NOT NULL). */
 #define CUBIT_SUM_GATHER_B 1u
+#define CUBIT_SUM_NO_ZONEMAP 2u /* as CUBIT_SCAN_NO_ZONEMAP */
 int cubit_table_sum_product(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
                             int col_a, int col_b, int64_t *d_out, uint64_t *d_count, uint32_t flags);
 /* How the last sum_product read b: number of values decoded from the index (0 = gathered). */
