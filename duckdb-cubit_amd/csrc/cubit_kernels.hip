@@ -471,7 +471,8 @@ __device__ uint64_t* g_diag_times;  // DIAG & 4 builds only (scripts/kbench.hip)
 // Copy-out stores are issued before the prefetch they precede, so the wait for the prefetched
 // leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
 // STAGE hits claims on its own and writes straight to the output (dense path).
-template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX, int WG_PER_CU = 2>
+template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX, int WG_PER_CU = 2,
+          bool DSTAGE = true>
 __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decode_pairs(EvalArgs a,
                                                                                        uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
@@ -568,7 +569,27 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
         return tile_count;
     };
 
-    // decode r into stage sp at stage_base with row offsets + delta; dense tiles go direct.
+    // rowids[base + i] = row0 + st[i] for i < n: 16-byte stores (the first id alone when the
+    // output is not 16-byte aligned there), bounded by the capacity
+    auto emit = [&](const uint32_t* st, uint32_t n, uint64_t base, int64_t row0) {
+        int64_t* out = a.rowids + base;
+        const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
+        if (t == 0 && head && base < a.capacity) out[0] = row0 + (int64_t)st[0];
+        const uint64_t room = a.capacity > base ? a.capacity - base : 0;
+        for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
+            if (i + 1 < n && i + 1 < room) {
+                i64x2 val;
+                val.x = row0 + (int64_t)st[i];
+                val.y = row0 + (int64_t)st[i + 1];
+                *reinterpret_cast<i64x2*>(out + i) = val;
+            } else if (i < room) {
+                out[i] = row0 + (int64_t)st[i];
+            }
+        }
+    };
+
+    // decode r into stage sp at stage_base with row offsets + delta; a dense tile claims on its
+    // own and leaves through the other stage (copied out already) in rounds of 2·STAGE ids.
     // Returns the staged count (0 for a dense tile).
     auto decode = [&](uint32_t tl, int sp, uint32_t stage_base, uint32_t delta, const uint64_t (&r)[NW],
                       const uint32_t (&pair_off)[PAIRS], uint64_t tile_count) -> uint32_t {
@@ -603,9 +624,39 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
                 dir[2 * tl + 1] = tile_count;
             }
         }
-        __syncthreads();
+        __syncthreads();  // also: every thread is done with the copy-out of stage sp ^ 1
         const uint64_t base = s_dense_off;
-        if (write_ids) {
+        if (write_ids && DSTAGE) {
+            // stage sp ^ 1 was copied out before this pair's first barrier and is next written
+            // by the next pair, behind its own barrier
+            uint32_t* st = s_stage[sp ^ 1];
+            constexpr uint32_t CAP = 2 * STAGE;
+            for (uint32_t r0 = 0; r0 < (uint32_t)tile_count; r0 += CAP) {
+                const uint32_t r1 = min((uint32_t)tile_count, r0 + CAP);
+#pragma unroll
+                for (int p = 0; p < PAIRS; ++p) {
+                    uint32_t off = pair_off[p];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        uint64_t w = r[2 * p + e];
+                        const uint32_t c = (uint32_t)__popcll(w);
+                        const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                        if (off < r1 && off + c > r0) {
+                            uint32_t k = off;
+                            for (; k < r0; ++k) w &= w - 1;  // the word straddles the round's start
+                            for (; w && k < r1; ++k) {
+                                st[k - r0] = wrow + (uint32_t)__builtin_ctzll(w);
+                                w &= w - 1;
+                            }
+                        }
+                        off += c;
+                    }
+                }
+                __syncthreads();
+                emit(st, r1 - r0, base + r0, row0);
+                __syncthreads();
+            }
+        } else if (write_ids) {
 #pragma unroll
             for (int p = 0; p < PAIRS; ++p) {
                 uint64_t off = base + pair_off[p];
@@ -621,7 +672,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
                 }
             }
         }
-        __syncthreads();  // s_dense_off free again
+        __syncthreads();  // s_dense_off (and the scratch stage) free again
         return 0;
     };
 
@@ -723,7 +774,8 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
 // the tiles from per-XCD heads (scripts/kbench.hip) evened the workgroups' end
 // times (spread 25 → 14 µs) but slowed every workgroup more than that gained: its dequeue is a
 // returning atomic that the next wait on the leaf loads (vmcnt counts in order) also waits for.
-template <int K, int PAIRS, int RUN_CAP, int THREADS, int FORM = FORM_POSTFIX, int MAXT = 16, bool STAMP = false>
+template <int K, int PAIRS, int RUN_CAP, int THREADS, int FORM = FORM_POSTFIX, int MAXT = 16, bool STAMP = false,
+          bool DSTAGE = true>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(EvalArgs a, uint64_t* __restrict__ dir) {
     // STAMP (scripts/kbench.hip only): each workgroup's start / end (s_memrealtime) into g_diag_times
     if (STAMP && threadIdx.x == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -764,6 +816,25 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     uint32_t next_tile = i + G < n_idx ? tile_at(a, i + G) : 0;
     if (i < n_idx) load_tile<K, PAIRS, THREADS>(a, (uint64_t)tile * TILE_WORDS, t, v);
 
+    // rowids[base + i] = row0 + st[i] for i < n: 16-byte stores (the first id alone when the
+    // output is not 16-byte aligned there), bounded by the capacity
+    auto emit = [&](const uint32_t* st, uint32_t n, uint64_t base, int64_t row0) {
+        int64_t* out = a.rowids + base;
+        const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
+        auto id = [&](uint32_t i) -> int64_t { return row0 + (int64_t)st[i]; };
+        if (t == 0 && head && base < a.capacity) out[0] = id(0);
+        const uint64_t room = a.capacity > base ? a.capacity - base : 0;
+        for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
+            if (i + 1 < n && i + 1 < room) {
+                i64x2 val;
+                val.x = id(i);
+                val.y = id(i + 1);
+                *reinterpret_cast<i64x2*>(out + i) = val;
+            } else if (i < room) {
+                out[i] = id(i);
+            }
+        }
+    };
     // copy out closed run rs at s_off (published before the preceding barrier) and write its
     // directory entries
     auto copy_out = [&](int rs) {
@@ -774,24 +845,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
             dir[2 * s_rt[rs][t]] = s_rc[rs][t] ? base + s_ro[rs][t] : 0;
             dir[2 * s_rt[rs][t] + 1] = s_rc[rs][t];
         }
-        if (write_ids && n) {
-            const int64_t row0 = a.row_base + (int64_t)((uint64_t)s_rfirst[rs] * TILE_ROWS);
-            int64_t* out = a.rowids + base;
-            const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
-            auto id = [&](uint32_t i) -> int64_t { return row0 + (int64_t)s_stage[rs][i]; };
-            if (t == 0 && head && base < a.capacity) out[0] = id(0);
-            const uint64_t room = a.capacity > base ? a.capacity - base : 0;
-            for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
-                if (i + 1 < n && i + 1 < room) {
-                    i64x2 val;
-                    val.x = id(i);
-                    val.y = id(i + 1);
-                    *reinterpret_cast<i64x2*>(out + i) = val;
-                } else if (i < room) {
-                    out[i] = id(i);
-                }
-            }
-        }
+        if (write_ids && n) emit(s_stage[rs], n, base, a.row_base + (int64_t)((uint64_t)s_rfirst[rs] * TILE_ROWS));
     };
 
     int rs = 0;              // the open run's stage
@@ -859,9 +913,39 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
                     dir[2 * tile + 1] = tile_count;
                 }
             }
-            __syncthreads();
+            __syncthreads();  // also: every thread is done with the copy-out of stage rs ^ 1
             const uint64_t base = s_dense_off;
-            if (write_ids) {
+            if (write_ids && DSTAGE) {
+                // in rounds of RUN_CAP ids through the free stage (rs ^ 1; the open run keeps
+                // stage rs): each thread decodes its bits whose tile-local index falls in the
+                // round, then the round leaves as 16-byte stores
+                uint32_t* st = s_stage[rs ^ 1];
+                for (uint32_t r0 = 0; r0 < tile_count; r0 += (uint32_t)RUN_CAP) {
+                    const uint32_t r1 = min(tile_count, r0 + (uint32_t)RUN_CAP);
+#pragma unroll
+                    for (int p = 0; p < PAIRS; ++p) {
+                        uint32_t off = pair_off[p];
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            uint64_t w = r[2 * p + e];
+                            const uint32_t c = (uint32_t)__popcll(w);
+                            const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                            if (off < r1 && off + c > r0) {
+                                uint32_t k = off;
+                                for (; k < r0; ++k) w &= w - 1;  // the word straddles the round's start
+                                for (; w && k < r1; ++k) {
+                                    st[k - r0] = wrow + (uint32_t)__builtin_ctzll(w);
+                                    w &= w - 1;
+                                }
+                            }
+                            off += c;
+                        }
+                    }
+                    __syncthreads();
+                    emit(st, r1 - r0, base + r0, row0);
+                    __syncthreads();
+                }
+            } else if (write_ids) {
 #pragma unroll
                 for (int p = 0; p < PAIRS; ++p) {
                     uint64_t off = base + pair_off[p];
@@ -877,7 +961,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
                     }
                 }
             }
-            __syncthreads();  // s_dense_off free again
+            __syncthreads();  // s_dense_off (and the scratch stage) free again
         } else {
             if (close) {
                 // one claim for the whole run (returns during the next tile)
