@@ -473,8 +473,13 @@ struct Leaf {
     // validity bitvector, classified from its own bits; kZoneStats = bv holds exactly the valid
     // rows whose base value passes (cmp, constant) — a K0 or candidate-check leaf — classified
     // from the column's per-zone min / max like a ConstantFilter's CheckStatistics; kZoneNone
-    // = patched, visibility and materialised leaves (mixed everywhere)
+    // = visibility and materialised leaves (mixed everywhere)
     int zsrc = 0;
+    // a leaf patched with MVCC updates keeps the classes of the base leaf it was copied from
+    // (zbv: that bitvector, for kZoneBits) except in the zones that hold an update record of
+    // column zdirty (there: mixed)
+    const uint64_t* zbv = nullptr;
+    int zdirty = -1;
 };
 enum { kZoneNone = 0, kZoneBits = 1, kZoneStats = 2 };
 
@@ -873,6 +878,10 @@ struct Updates {
         std::unique_ptr<DevBuf> bv;
     };
     std::map<PatchKey, Patched> cache;
+    // zones holding an update record of any version (bit per zone), for the zone classes of
+    // patched leaves; computed on first use for dirty_nz zones
+    std::vector<uint64_t> dirty;
+    uint32_t dirty_nz = 0;
 };
 
 }  // namespace
@@ -2484,7 +2493,9 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
         }
         Leaf l = e->leaf;
         l.bv = copy;
-        l.zsrc = kZoneNone;  // the patched copy differs from the base at the updated rows
+        // the copy differs from the base only in zones holding an update record of the column
+        if (!l.zbv) l.zbv = e->leaf.bv;
+        l.zdirty = e->leaf.column;
         e = mk_leaf(l, e->neg);
         return CUBIT_OK;
     }
@@ -2508,8 +2519,8 @@ uint32_t real_zones(const cubit_table* t) { return (uint32_t)((t->n_rows + kZone
 // take their zone classes from
 void collect_zone_sources(const ExprP& e, std::vector<const uint64_t*>& bvs, std::vector<int>& cols) {
     if (e->kind == Expr::LEAF) {
-        if (e->leaf.zsrc == kZoneBits && std::find(bvs.begin(), bvs.end(), e->leaf.bv) == bvs.end())
-            bvs.push_back(e->leaf.bv);
+        const uint64_t* key = e->leaf.zbv ? e->leaf.zbv : e->leaf.bv;
+        if (e->leaf.zsrc == kZoneBits && std::find(bvs.begin(), bvs.end(), key) == bvs.end()) bvs.push_back(key);
         if (e->leaf.zsrc == kZoneStats && std::find(cols.begin(), cols.end(), e->leaf.column) == cols.end())
             cols.push_back(e->leaf.column);
         return;
@@ -2625,6 +2636,24 @@ struct ZoneSet {
     std::vector<uint64_t> z, o;  // zones where the expression is false / true on every row
 };
 
+// zones holding an update record of column col (any version), a bit per zone
+const std::vector<uint64_t>& dirty_zones(cubit_table* t, int col) {
+    static const std::vector<uint64_t> none;
+    auto it = t->upd.find(col);
+    if (it == t->upd.end()) return none;
+    Updates& u = it->second;
+    const uint32_t nz = real_zones(t);
+    if (u.dirty_nz != nz) {
+        u.dirty.assign((nz + 63) / 64, 0);
+        for (int64_t r : u.h_rows) {
+            const uint64_t z = (uint64_t)r / kZoneRows;
+            if (z < nz) u.dirty[z >> 6] |= 1ull << (z & 63);
+        }
+        u.dirty_nz = nz;
+    }
+    return u.dirty;
+}
+
 // three-valued evaluation of an expression over zone classes; leaves without zone classes are
 // mixed everywhere
 void zone_eval(cubit_table* t, const ExprP& e, size_t nw, ZoneSet& r) {
@@ -2632,7 +2661,7 @@ void zone_eval(cubit_table* t, const ExprP& e, size_t nw, ZoneSet& r) {
     case Expr::LEAF: {
         const ZoneMap* m = nullptr;
         if (e->leaf.zsrc == kZoneBits) {
-            auto it = t->zones.find(e->leaf.bv);
+            auto it = t->zones.find(e->leaf.zbv ? e->leaf.zbv : e->leaf.bv);
             if (it != t->zones.end()) m = &it->second;
         } else if (e->leaf.zsrc == kZoneStats) {
             m = &stats_zone_map(t, e->leaf);
@@ -2643,6 +2672,13 @@ void zone_eval(cubit_table* t, const ExprP& e, size_t nw, ZoneSet& r) {
         } else {
             r.z.assign(nw, 0);
             r.o.assign(nw, 0);
+        }
+        if (m && e->leaf.zdirty >= 0) {  // patched: zones with an update record are mixed
+            const std::vector<uint64_t>& d = dirty_zones(t, e->leaf.zdirty);
+            for (size_t w = 0; w < nw && w < d.size(); ++w) {
+                r.z[w] &= ~d[w];
+                r.o[w] &= ~d[w];
+            }
         }
         if (e->neg) std::swap(r.z, r.o);
         return;
@@ -2674,7 +2710,7 @@ void zone_eval(cubit_table* t, const ExprP& e, size_t nw, ZoneSet& r) {
 bool zone_informative(cubit_table* t, const ExprP& e) {
     if (e->kind == Expr::LEAF) {
         if (e->leaf.zsrc == kZoneBits) {
-            auto it = t->zones.find(e->leaf.bv);
+            auto it = t->zones.find(e->leaf.zbv ? e->leaf.zbv : e->leaf.bv);
             return it != t->zones.end() && it->second.informative;
         }
         if (e->leaf.zsrc == kZoneStats) return stats_zone_map(t, e->leaf).informative;
