@@ -3060,6 +3060,45 @@ extern "C" int cubit_table_last_plan(cubit_table* t, uint32_t* n_leaves, uint32_
     return CUBIT_OK;
 }
 
+// Column statistics (DataTable::GetStatistics, behind seq_scan's `statistics` callback
+// TableScanStatistics, table_scan.cpp:108-117): min / max of the valid values and whether the
+// column has NULL / non-NULL rows, from the per-zone statistics the zonemaps use (computed once,
+// cached until the column changes). As DuckDB's column statistics absorb every update
+// (UpdateSegment merges its values into the segment statistics), the bounds widen by the
+// column's update records of any version, and an updated row counts as a non-NULL one.
+extern "C" int cubit_table_column_statistics(cubit_table* t, int col, int64_t* vmin, int64_t* vmax,
+                                             int* has_null, int* has_no_null) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    bool any_null = false, any_valid = false;
+    if (t->n_rows) {
+        if (int rc = ensure_zones(t, {}, {col})) return rc;
+        const cubit_table::ColZones& cz = t->col_zones.at(col);
+        for (size_t z = 0; z < cz.fl.size(); ++z) {
+            if (cz.fl[z] & 1) {
+                any_valid = true;
+                lo = std::min(lo, cz.mn[z]);
+                hi = std::max(hi, cz.mx[z]);
+            }
+            if (!(cz.fl[z] & 2)) any_null = true;
+        }
+    }
+    auto uit = t->upd.find(col);
+    if (uit != t->upd.end() && !uit->second.stat_values.empty()) {
+        any_valid = true;
+        lo = std::min(lo, uit->second.stat_values.front());
+        hi = std::max(hi, uit->second.stat_values.back());
+    }
+    if (vmin) *vmin = any_valid ? lo : 0;
+    if (vmax) *vmax = any_valid ? hi : 0;
+    if (has_null) *has_null = any_null ? 1 : 0;
+    if (has_no_null) *has_no_null = any_valid ? 1 : 0;
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_table_last_zones(cubit_table* t, uint32_t* evaluated, uint32_t* zones) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     CUBIT_LOCK(t->ctx);

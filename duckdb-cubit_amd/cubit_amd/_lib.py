@@ -108,6 +108,8 @@ GPU_SIGNATURES = {
     "cubit_table_probe": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P]),
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_last_zones": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
+    "cubit_table_column_statistics": (C.c_int, [_P, C.c_int, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(C.c_int),
+                                                C.POINTER(C.c_int)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
     "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),
@@ -140,6 +142,9 @@ SCAN_SIGNATURES = {
     "cubit_scan_function": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_U64)]),
     "cubit_scan_batch_index": (C.c_int, [_P, _P, C.POINTER(_U64)]),
     "cubit_scan_progress": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "cubit_scan_cardinality": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
+    "cubit_scan_statistics": (C.c_int, [_P, _U64, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(C.c_int),
+                                        C.POINTER(C.c_int)]),
     "cubit_scan_local_destroy": (C.c_int, [_P]),
     "cubit_scan_destroy": (C.c_int, [_P]),
 }

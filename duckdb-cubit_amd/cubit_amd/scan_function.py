@@ -18,6 +18,27 @@ ROW_ID = 2 ** 64 - 1  # COLUMN_IDENTIFIER_ROW_ID
 VECTOR_SIZE = 2048
 
 
+def cardinality(table):
+    """TableScanCardinality: (estimated, max) rows of the partition (bind time)."""
+    lib = L.scan_lib()
+    e, m = C.c_uint64(), C.c_uint64()
+    L.check_scan(lib.cubit_scan_cardinality(table.handle, C.byref(e), C.byref(m)))
+    return int(e.value), int(m.value)
+
+
+def statistics(table, column_id: int):
+    """TableScanStatistics: (min, max, has_null, has_no_null) of a storage column, or None for
+    the row id (the reference returns no statistics)."""
+    lib = L.scan_lib()
+    lo, hi = C.c_int64(), C.c_int64()
+    hn, hv = C.c_int(), C.c_int()
+    rc = lib.cubit_scan_statistics(table.handle, column_id, C.byref(lo), C.byref(hi), C.byref(hn), C.byref(hv))
+    if rc == L.ERR_UNSUPPORTED and column_id == ROW_ID:
+        return None
+    L.check_scan(rc)
+    return int(lo.value), int(hi.value), bool(hn.value), bool(hv.value)
+
+
 class LocalState:
     def __init__(self, scan: "CubitScanFunction"):
         self.scan = scan

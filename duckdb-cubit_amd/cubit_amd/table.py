@@ -345,6 +345,15 @@ class CubitTable:
         L.check(self.lib.cubit_table_last_sum_decode(self.handle, C.byref(v)))
         return int(v.value)
 
+    def column_statistics(self, col: int):
+        """(min, max, has_null, has_no_null) of a column — DataTable::GetStatistics, widened by
+        the column's update records; min = max = 0 when no row is valid."""
+        lo, hi = C.c_int64(), C.c_int64()
+        hn, hv = C.c_int(), C.c_int()
+        L.check(self.lib.cubit_table_column_statistics(self.handle, col, C.byref(lo), C.byref(hi), C.byref(hn),
+                                                       C.byref(hv)))
+        return int(lo.value), int(hi.value), bool(hn.value), bool(hv.value)
+
     def last_zones(self):
         """(zones the last scan / sum_product evaluated, zones of the partition): fewer
         evaluated when the zonemaps skipped zones its filter is false on."""

@@ -247,6 +247,29 @@ double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gs
     return 100.0 * (double)g.emitted.load() / (double)g.count;
 }
 
+// TableScanCardinality (table_scan.cpp:201-208): NodeStatistics(table rows, table rows +
+// transaction-local rows); transaction-local rows stay on the CPU, so both are
+// the partition's rows
+NodeStatistics CubitScanCardinality(const FunctionData* bind_data) {
+    auto& bind = static_cast<const CubitScanBindData&>(*bind_data);
+    NodeStatistics st;
+    st.has_estimated_cardinality = st.has_max_cardinality = true;
+    st.estimated_cardinality = st.max_cardinality = bind.n_rows;
+    return st;
+}
+
+// TableScanStatistics (table_scan.cpp:108-117) → DataTable::GetStatistics: none for the row id
+bool CubitScanStatistics(const FunctionData* bind_data, column_t column_id, ColumnStatistics& out) {
+    auto& bind = static_cast<const CubitScanBindData&>(*bind_data);
+    if (column_id == COLUMN_IDENTIFIER_ROW_ID) return false;
+    int hn = 0, hv = 0;
+    check(cubit_table_column_statistics(bind.table, (int)column_id, &out.min, &out.max, &hn, &hv),
+          "cubit_table_column_statistics");
+    out.has_null = hn != 0;
+    out.has_no_null = hv != 0;
+    return true;
+}
+
 }  // namespace
 
 TableFunction GetCubitScanFunction() {
@@ -257,6 +280,8 @@ TableFunction GetCubitScanFunction() {
     f.init_local = CubitScanInitLocal;
     f.get_batch_index = CubitScanGetBatchIndex;
     f.table_scan_progress = CubitScanProgress;
+    f.cardinality = CubitScanCardinality;
+    f.statistics = CubitScanStatistics;
     f.projection_pushdown = true;  // as seq_scan (table_scan.cpp:436-438)
     f.filter_pushdown = true;
     f.filter_prune = true;
@@ -368,6 +393,42 @@ int cubit_scan_progress(cubit_scan* s, double* out) {
     if (!s || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
     *out = s->fn.table_scan_progress(&s->bind, s->gstate.get());
     return CUBIT_OK;
+}
+
+// bind-time callbacks: the bind data is the partition (no scan state needed)
+int cubit_scan_cardinality(cubit_table* table, uint64_t* estimated, uint64_t* max) {
+    if (!table) return scan_fail(CUBIT_ERR_INVALID, "null table");
+    try {
+        CubitScanBindData bind;
+        int64_t base = 0;
+        check(cubit_table_info(table, &bind.n_rows, &base, &bind.ctx), "cubit_table_info");
+        bind.table = table;
+        const NodeStatistics st = GetCubitScanFunction().cardinality(&bind);
+        if (estimated) *estimated = st.estimated_cardinality;
+        if (max) *max = st.max_cardinality;
+        return CUBIT_OK;
+    } catch (const ScanError& e) {
+        return scan_fail(e.code, e.what());
+    }
+}
+
+int cubit_scan_statistics(cubit_table* table, uint64_t column_id, int64_t* min, int64_t* max, int* has_null,
+                          int* has_no_null) {
+    if (!table) return scan_fail(CUBIT_ERR_INVALID, "null table");
+    try {
+        CubitScanBindData bind;
+        bind.table = table;
+        ColumnStatistics st;
+        if (!GetCubitScanFunction().statistics(&bind, column_id, st))
+            return scan_fail(CUBIT_ERR_UNSUPPORTED, "no statistics for the row-id column");
+        if (min) *min = st.min;
+        if (max) *max = st.max;
+        if (has_null) *has_null = st.has_null ? 1 : 0;
+        if (has_no_null) *has_no_null = st.has_no_null ? 1 : 0;
+        return CUBIT_OK;
+    } catch (const ScanError& e) {
+        return scan_fail(e.code, e.what());
+    }
 }
 
 int cubit_scan_local_destroy(cubit_scan_local* l) {

@@ -90,6 +90,22 @@ using table_function_get_batch_index_t = idx_t (*)(const FunctionData* bind_data
                                                    GlobalTableFunctionState* gstate);
 using table_function_progress_t = double (*)(const FunctionData* bind_data, const GlobalTableFunctionState* gstate);
 
+// NodeStatistics (src/include/duckdb/storage/statistics/node_statistics.hpp:16-33)
+struct NodeStatistics {
+    bool has_estimated_cardinality = false;
+    idx_t estimated_cardinality = 0;
+    bool has_max_cardinality = false;
+    idx_t max_cardinality = 0;
+};
+// the numeric part of BaseStatistics (NumericStats min / max, has_null / has_no_null)
+struct ColumnStatistics {
+    int64_t min = 0, max = 0;
+    bool has_null = false, has_no_null = false;
+};
+using table_function_cardinality_t = NodeStatistics (*)(const FunctionData* bind_data);
+// false = no statistics (the reference returns nullptr, e.g. for the row-id column)
+using table_statistics_t = bool (*)(const FunctionData* bind_data, column_t column_id, ColumnStatistics& out);
+
 struct TableFunction {
     std::string name;
     table_function_t function = nullptr;
@@ -97,6 +113,8 @@ struct TableFunction {
     table_function_init_local_t init_local = nullptr;
     table_function_get_batch_index_t get_batch_index = nullptr;
     table_function_progress_t table_scan_progress = nullptr;
+    table_function_cardinality_t cardinality = nullptr;
+    table_statistics_t statistics = nullptr;
     bool projection_pushdown = false;
     bool filter_pushdown = false;
     bool filter_prune = false;

@@ -280,6 +280,13 @@ int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64
                       uint64_t max_n, int64_t *d_out);
 /* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
 int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
+/* Column statistics — DataTable::GetStatistics behind seq_scan's `statistics` callback
+ * (TableScanStatistics, src/function/table/table_scan.cpp:108-117): min / max of the valid
+ * values (widened by the column's update records, as UpdateSegment merges updates into the
+ * segment statistics) and whether any row is NULL / non-NULL. min = max = 0 when no row is
+ * valid. */
+int cubit_table_column_statistics(cubit_table *t, int col, int64_t *min, int64_t *max, int *has_null,
+                                  int *has_no_null);
 /* Zones (131,072 rows each) the last scan or sum_product evaluated, out of the partition's
  * zones; fewer when the zonemaps skipped some (0 when the filter folded to FALSE). */
 int cubit_table_last_zones(cubit_table *t, uint32_t *evaluated, uint32_t *zones);

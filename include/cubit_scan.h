@@ -14,6 +14,11 @@
  *                             physical_table_scan.cpp:82-103)
  *   cubit_scan_batch_index  ← TableScanGetBatchIndex (table_scan.cpp:179-189)
  *   cubit_scan_progress     ← TableScanProgress     (table_scan.cpp:158-177)
+ *   cubit_scan_cardinality  ← TableScanCardinality  (table_scan.cpp:201-208): NodeStatistics of
+ *                             the partition (bind time, no scan state)
+ *   cubit_scan_statistics   ← TableScanStatistics   (table_scan.cpp:108-117): min / max /
+ *                             has_null / has_no_null of a storage column; CUBIT_ERR_UNSUPPORTED
+ *                             for the row id (the reference returns no statistics)
  * column_ids / projection_ids / filters mean what TableFunctionInitInput's members mean
  * (table_function.hpp:103-126): column_ids are storage columns (UINT64_MAX = row id), the
  * output holds column_ids[projection_ids[i]] (or every column_id when projection_ids is
@@ -47,6 +52,9 @@ int cubit_scan_init_local(cubit_scan *scan, cubit_scan_local **out);
 int cubit_scan_function(cubit_scan *scan, cubit_scan_local *local, int64_t *const *out_columns, uint64_t *out_count);
 int cubit_scan_batch_index(cubit_scan *scan, cubit_scan_local *local, uint64_t *out);
 int cubit_scan_progress(cubit_scan *scan, double *out);
+int cubit_scan_cardinality(cubit_table *table, uint64_t *estimated, uint64_t *max);
+int cubit_scan_statistics(cubit_table *table, uint64_t column_id, int64_t *min, int64_t *max, int *has_null,
+                          int *has_no_null);
 int cubit_scan_local_destroy(cubit_scan_local *local);
 int cubit_scan_destroy(cubit_scan *scan);
 

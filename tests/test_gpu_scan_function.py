@@ -125,3 +125,44 @@ def test_mvcc_views_through_table_function(ctx, golden):
         if txn.transaction_id == writer:
             exp[rows % 7 == 0] = 100
         assert np.array_equal(q, exp)
+
+
+def test_cardinality_and_statistics_callbacks(ctx):
+    """seq_scan's bind-time callbacks: TableScanCardinality (table_scan.cpp:201-208) and
+    TableScanStatistics (table_scan.cpp:108-117 → DataTable::GetStatistics): min / max of the
+    valid values widened by update records, has_null / has_no_null, none for the row id."""
+    from cubit_amd import scan_function as S
+    from cubit_amd.datagen import validity_from_mask
+
+    rng = np.random.default_rng(8)
+    n = 700_001
+    a = rng.integers(-1000, 1000, n).astype(np.int32)
+    b = rng.integers(0, 2 ** 40, n).astype(np.int64)
+    valid_b = rng.random(n) > 0.2
+    c = np.zeros(n, dtype=np.int64)
+    t = CubitTable(ctx, n, row_base=5)
+    t.add_column(0, a)
+    t.add_column(1, b, validity_from_mask(valid_b))
+    t.add_column(2, c, validity_from_mask(np.zeros(n, dtype=bool)))  # every row NULL
+    assert S.cardinality(t) == (n, n)
+    assert S.statistics(t, S.ROW_ID) is None
+    assert S.statistics(t, 0) == (int(a.min()), int(a.max()), False, True)
+    assert S.statistics(t, 1) == (int(b[valid_b].min()), int(b[valid_b].max()), True, True)
+    assert S.statistics(t, 2) == (0, 0, True, False)
+    assert t.column_statistics(0) == S.statistics(t, 0)
+    # update records widen the bounds (any version, as UpdateSegment merges its statistics)
+    t.set_updates(0, np.array([3, 9], dtype=np.int64), np.array([-5000, 7000], dtype=np.int64),
+                  np.array([2, TXN_START + 1], dtype=np.uint64))
+    assert S.statistics(t, 0) == (-5000, 7000, False, True)
+    # appends change the statistics (the cached zone statistics are dropped)
+    t.append({0: np.array([-9999], dtype=np.int32), 1: np.array([1], dtype=np.int64),
+              2: np.array([42], dtype=np.int64)}, validity={2: np.array([1], dtype=np.uint64)})
+    assert S.statistics(t, 0) == (-9999, 7000, False, True)
+    assert S.statistics(t, 2) == (42, 42, True, True)
+    assert S.cardinality(t) == (n + 1, n + 1)
+    t.close()
+    empty = CubitTable(ctx, 0)
+    empty.add_column(0, np.empty(0, dtype=np.int64))
+    assert S.statistics(empty, 0) == (0, 0, False, False)
+    assert S.cardinality(empty) == (0, 0)
+    empty.close()
