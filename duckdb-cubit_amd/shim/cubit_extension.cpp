@@ -390,12 +390,50 @@ static double CubitProgress(ClientContext &context, const FunctionData *bind_dat
     return p;
 }
 
+// TableScanCardinality (table_scan.cpp:201-208) over the attached partition
+static unique_ptr<NodeStatistics> CubitCardinality(ClientContext &context, const FunctionData *bind_data) {
+    auto &bind = bind_data->Cast<CubitBindData>();
+    uint64_t estimated = 0, max = 0;
+    if (cubit_scan_cardinality(bind.attached.table, &estimated, &max) != CUBIT_OK) {
+        return nullptr;
+    }
+    return make_uniq<NodeStatistics>(estimated, max);
+}
+
+// TableScanStatistics (table_scan.cpp:108-117): the column's min / max / NULL flags from the
+// GPU partition; none for the row id, as the reference
+static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const FunctionData *bind_data,
+                                                  column_t column_id) {
+    auto &bind = bind_data->Cast<CubitBindData>();
+    if (column_id == COLUMN_IDENTIFIER_ROW_ID) {
+        return nullptr;
+    }
+    int64_t lo = 0, hi = 0;
+    int has_null = 0, has_no_null = 0;
+    if (cubit_scan_statistics(bind.attached.table, column_id, &lo, &hi, &has_null, &has_no_null) != CUBIT_OK) {
+        return nullptr;
+    }
+    const auto &type = bind.table.GetColumn(LogicalIndex(column_id)).GetType();
+    auto stats = BaseStatistics::CreateEmpty(type);
+    if (has_no_null) {
+        NumericStats::SetMin(stats, Value::Numeric(type, lo));  // DECIMAL: lo is the storage value
+        NumericStats::SetMax(stats, Value::Numeric(type, hi));
+        stats.SetHasNoNull();
+    }
+    if (has_null) {
+        stats.SetHasNull();
+    }
+    return stats.ToUnique();
+}
+
 TableFunction GetCubitScanFunction() {
     TableFunction f("cubit_scan", {}, CubitScanFunc);
     f.init_global = CubitInitGlobal;
     f.init_local = CubitInitLocal;
     f.get_batch_index = CubitBatchIndex;
     f.table_scan_progress = CubitProgress;
+    f.cardinality = CubitCardinality;
+    f.statistics = CubitStatistics;
     f.projection_pushdown = true;  // as seq_scan (table_scan.cpp:436-438)
     f.filter_pushdown = true;
     f.filter_prune = true;
