@@ -47,8 +47,11 @@ class Model:
     """The table as the oracle sees it: base values and validity, per-row insert / delete
     ids, and per-column chronological update lists."""
 
-    def __init__(self, rng, n0):
+    def __init__(self, rng, n0, clustered=False):
         self.data = [rng.integers(0, 50, n0).astype(DTYPES[c]) for c in range(4)]
+        if clustered:  # columns 0 and 1 ascend with the row (zonemaps skip zones)
+            for c in (0, 1):
+                self.data[c] = clustered_values(rng, 0, n0, DTYPES[c])
         self.valid = [rng.random(n0) > (0.1 if c in (0, 2) else 0.0) for c in range(4)]
         self.inserted = np.zeros(n0, dtype=np.uint64)
         self.deleted = np.full(n0, NOT_DELETED, dtype=np.uint64)
@@ -88,9 +91,15 @@ class Model:
         return merged
 
 
-def run(ctx, seed, n_ops, n0):
+def clustered_values(rng, start, n, dtype):
+    """rows [start, start + n) of a column that ascends with the row (one value per 20,000
+    rows, ±1 jitter): the layout where zonemaps skip zones"""
+    return ((np.arange(start, start + n) // 20_000) + rng.integers(0, 2, n)).astype(dtype)
+
+
+def run(ctx, seed, n_ops, n0, clustered=False):
     rng = np.random.default_rng(seed)
-    m = Model(rng, n0)
+    m = Model(rng, n0, clustered)
     t = CubitTable(ctx, n0, row_base=int(rng.integers(0, 1 << 30)))
     for c in range(4):
         t.add_column(c, m.data[c], validity_from_mask(m.valid[c]) if c in (0, 2) else None)
@@ -100,13 +109,16 @@ def run(ctx, seed, n_ops, n0):
     t.build_index(2, L.INDEX_BINS, [0, 10, 20, 30, 40, 50])
     clock = 3          # last committed id
     floor = 0          # merges fold versions below this: snapshots start at or after it
-    counts = {"scan": 0, "append": 0, "updates": 0, "merge": 0, "deletes": 0, "rows_merged": 0}
+    counts = {"scan": 0, "append": 0, "updates": 0, "merge": 0, "deletes": 0, "rows_merged": 0, "zones_skipped": 0}
     for _ in range(n_ops):
         op = rng.choice(["scan", "scan", "scan", "append", "updates", "merge", "deletes"])
         if op == "append":
             nb = int(rng.choice([1, 7, 64, 65, 1000, int(rng.integers(1, 150_000))]))
             lo, hi = (-5, 55) if rng.random() < 0.5 else (0, 50)
             bd = [rng.integers(lo, hi, nb).astype(DTYPES[c]) for c in range(4)]
+            if clustered:
+                for c in (0, 1):
+                    bd[c] = clustered_values(rng, m.n, nb, DTYPES[c])
             bv = [rng.random(nb) > (0.1 if c in (0, 2, 3) else 0.0) for c in range(4)]
             iid = int(rng.choice([0, clock, WRITER]))
             t.append({c: bd[c] for c in range(4)}, {c: validity_from_mask(bv[c]) for c in range(4)}, insert_id=iid)
@@ -159,6 +171,8 @@ def run(ctx, seed, n_ops, n0):
             ref = O.table_scan(m.ocols(), plan, m.n, row_base=t.row_base, tx=tx)
             got = t.scan(fs, residual, txn=L.Txn(start, tid))
             assert np.array_equal(got, ref), ("scan", start, tid, fs, residual, len(got), len(ref))
+            live, nz = t.last_zones()
+            counts["zones_skipped"] += live < nz
         counts[op] += 1
     t.close()
     return counts
@@ -173,5 +187,18 @@ def test_maintenance_fuzz(seed):
     try:
         counts = run(ctx, seed, 60, 150_001)
         assert counts["scan"] > 10
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_maintenance_fuzz_clustered():
+    """The same sequence on a table whose indexed columns ascend with the row, so scans skip
+    zones while appends, merges and updates keep rewriting the bitvectors the zone classes are
+    computed from."""
+    ctx = Context(0)
+    try:
+        counts = run(ctx, 4, 60, 1_000_003, clustered=True)
+        assert counts["scan"] > 10 and counts["zones_skipped"] > 0, counts
     finally:
         ctx.close()
