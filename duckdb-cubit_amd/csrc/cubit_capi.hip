@@ -830,7 +830,17 @@ struct Column {
     const uint64_t* validity = nullptr;  // device, padded to the table's cap_words (null = no NULLs)
     uint64_t cap_rows = 0;  // rows the owned data buffer holds (0 = caller-owned device data)
     std::vector<std::unique_ptr<DevBuf>> owned;
-    // value statistics (zonemap-like), computed at index build
+    // a column registered as BITPACKING segments keeps them on the device (packed bytes + the
+    // group table): constant comparisons on it unpack and compare in one pass
+    // (bitpacked_compare_kernel) instead of reading the plain column. Dropped when the values
+    // change (appends, merges).
+    std::unique_ptr<DevBuf> bp_bytes, bp_groups;
+    uint64_t bp_n_groups = 0;
+    void drop_packed() {
+        bp_bytes.reset();
+        bp_groups.reset();
+        bp_n_groups = 0;
+    }
 };
 
 struct Index {
@@ -952,6 +962,8 @@ struct cubit_table {
     std::map<int, ColZones> col_zones;
     std::map<std::tuple<int, int, int, int64_t, int64_t>, ZoneMap> pred_zones;
     uint32_t last_live = 0, last_zones = 0;  // zones the last scan evaluated / the partition has
+    bool use_packed = true;  // cubit_table_use_packed_filter
+    uint32_t last_packed = 0;  // leaves the last plan built straight from packed segments
 };
 
 namespace {
@@ -1277,6 +1289,11 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     c.data = out->p;
     c.cap_rows = t->n_rows;
     c.owned.push_back(std::move(out));
+    c.bp_bytes = std::make_unique<DevBuf>();
+    c.bp_groups = std::make_unique<DevBuf>();
+    std::swap(c.bp_bytes->p, d_bytes.p);
+    std::swap(c.bp_groups->p, d_groups.p);
+    c.bp_n_groups = groups.size();
     if (validity) {
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
         HIP_CHECK(hipStreamSynchronize(s));
@@ -1800,6 +1817,7 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
     for (auto& kv : t->cols) {
         const int col = kv.first;
         Column& c = kv.second;
+        c.drop_packed();  // the segments do not hold the appended rows
         const uint32_t i = at[col];
         const uint64_t esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
         HIP_CHECK(hipMemcpyAsync(tmp_col.p, data[i], n_new * esz, hipMemcpyHostToDevice, s));
@@ -1942,6 +1960,7 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     HIP_CHECK(hipStreamSynchronize(s));
     drop_zones(t);  // the merge flips index bits in place
     if (int rc = own_column(t, c, std::max<uint64_t>(t->n_rows, c.cap_rows))) return rc;
+    c.drop_packed();  // merged values are not in the segments
     const uint64_t m = m_rows.size();
     DevBuf d_rows, d_vals;
     if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess)
@@ -2064,7 +2083,18 @@ struct Planner {
         const Column& cl = t->cols.at(col);
         uint64_t* bv = nullptr;
         if ((rc = scratch_bv(t, &bv))) return nullptr;
-        hipError_t e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, cmp, c, bv, t->ctx->stream);
+        hipError_t e;
+        if (cl.bp_n_groups && t->use_packed) {
+            // straight from the BITPACKING segments: w/8 bytes per row instead of sizeof(T)
+            e = hipMemsetAsync(bv, 0, t->nwp * 8, t->ctx->stream);
+            if (e == hipSuccess)
+                e = launch_bitpacked_compare(static_cast<const uint8_t*>(cl.bp_bytes->p),
+                                             static_cast<const BpGroup*>(cl.bp_groups->p), cl.bp_n_groups, cl.type,
+                                             cl.validity, cmp, c, 0, bv, t->ctx->stream);
+            t->last_packed++;
+        } else {
+            e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, cmp, c, bv, t->ctx->stream);
+        }
         if (e != hipSuccess) {
             rc = fail(CUBIT_ERR_HIP, "compare kernel: %s", hipGetErrorString(e));
             return nullptr;
@@ -2764,6 +2794,7 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     cubit_ctx* ctx = t->ctx;
     t->scratch_used = 0;
     t->last_passes = 0;
+    t->last_packed = 0;
     ExprP e;
     if (n_nodes == 0) {
         e = mk_true();
@@ -3096,6 +3127,20 @@ extern "C" int cubit_table_column_statistics(cubit_table* t, int col, int64_t* v
     if (vmax) *vmax = any_valid ? hi : 0;
     if (has_null) *has_null = any_null ? 1 : 0;
     if (has_no_null) *has_no_null = any_valid ? 1 : 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_use_packed_filter(cubit_table* t, int on) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    t->use_packed = on != 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_packed(cubit_table* t, uint32_t* n_leaves) {
+    if (!t || !n_leaves) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    *n_leaves = t->last_packed;
     return CUBIT_OK;
 }
 

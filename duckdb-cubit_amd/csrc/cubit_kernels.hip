@@ -1577,37 +1577,16 @@ __global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col
 // 4t..4t+3 and 1024+4t..1024+4t+3), so every wave store is a contiguous 16 B per lane
 // (HBM-write-bound: the output is 4–8 B per value, the input w/8). U = unsigned T, the
 // reference's wrap-around arithmetic.
-template <typename T, typename U>
-__global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restrict__ bytes,
-                                                        const BpGroup* __restrict__ groups, T* __restrict__ out) {
+constexpr uint32_t kBpMaxWords = 2048 * 64 / 32;  // packed 32-bit words of a 64-bit-wide group
+
+// Unpack one group with 256 threads: thread t produces the 4-value quads t and t + 256 (values
+// 4t..4t+3 and 1024+4t..1024+4t+3) and hands each to store_quad(c, v) (c = 0, 1). s_words
+// (kBpMaxWords + 8 words, 16-byte aligned) stages the packed words, s_tot holds wave totals.
+template <typename T, typename U, typename Store>
+__device__ __forceinline__ void unpack_group(const uint8_t* __restrict__ bytes, const BpGroup& g, uint32_t* s_words,
+                                             U* s_tot, Store&& store_quad) {
     constexpr int THREADS = 256, QUADS = 2;
-    constexpr uint32_t MAXW = 2048 * 64 / 32;  // packed words of a 64-bit-wide group
-    __shared__ __attribute__((aligned(16))) uint32_t s_words[MAXW + 8];  // + alignment shift + 3-word window
-    __shared__ U s_tot[THREADS / 64];
-    const BpGroup g = groups[blockIdx.x];
     const int t = threadIdx.x;
-    T* dst = out + g.row_start;
-    // store quad c of this thread: values 4·(t + 256c) + 0..3
-    auto store_quad = [&](int c, const U (&v)[4]) {
-        const uint32_t i0 = 4u * (uint32_t)(t + THREADS * c);
-        if (i0 + 4 <= g.count) {
-            if (sizeof(T) == 4) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 o;
-                o.x = (uint32_t)v[0], o.y = (uint32_t)v[1], o.z = (uint32_t)v[2], o.w = (uint32_t)v[3];
-                *reinterpret_cast<u32x4*>(dst + i0) = o;
-            } else {
-                u64x2 o0, o1;
-                o0.x = (uint64_t)v[0], o0.y = (uint64_t)v[1], o1.x = (uint64_t)v[2], o1.y = (uint64_t)v[3];
-                reinterpret_cast<u64x2*>(dst + i0)[0] = o0;
-                reinterpret_cast<u64x2*>(dst + i0)[1] = o1;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (i0 + j < g.count) dst[i0 + j] = (T)v[j];
-        }
-    };
     if (g.mode == 2 || g.mode == 3) {  // CONSTANT, CONSTANT_DELTA
         const U base = (U)g.base, d = g.mode == 3 ? (U)g.aux : (U)0;
 #pragma unroll
@@ -1690,6 +1669,103 @@ __global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restric
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[c][j] += pre;
         store_quad(c, v[c]);
+    }
+}
+
+template <typename T, typename U>
+__global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restrict__ bytes,
+                                                        const BpGroup* __restrict__ groups, T* __restrict__ out) {
+    constexpr int THREADS = 256;
+    __shared__ __attribute__((aligned(16))) uint32_t s_words[kBpMaxWords + 8];  // + alignment shift + 3-word window
+    __shared__ U s_tot[THREADS / 64];
+    const BpGroup g = groups[blockIdx.x];
+    const int t = threadIdx.x;
+    T* dst = out + g.row_start;
+    // store quad c of this thread: values 4·(t + 256c) + 0..3
+    unpack_group<T, U>(bytes, g, s_words, s_tot, [&](int c, const U (&v)[4]) {
+        const uint32_t i0 = 4u * (uint32_t)(t + THREADS * c);
+        if (i0 + 4 <= g.count) {
+            if (sizeof(T) == 4) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 o;
+                o.x = (uint32_t)v[0], o.y = (uint32_t)v[1], o.z = (uint32_t)v[2], o.w = (uint32_t)v[3];
+                *reinterpret_cast<u32x4*>(dst + i0) = o;
+            } else {
+                u64x2 o0, o1;
+                o0.x = (uint64_t)v[0], o0.y = (uint64_t)v[1], o1.x = (uint64_t)v[2], o1.y = (uint64_t)v[3];
+                reinterpret_cast<u64x2*>(dst + i0)[0] = o0;
+                reinterpret_cast<u64x2*>(dst + i0)[1] = o1;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j < g.count) dst[i0 + j] = (T)v[j];
+        }
+    });
+}
+
+// Filter straight from DuckDB BITPACKING segments (the reference's ColumnSegment::Scan →
+// BitpackingScanPartial → ColumnSegment::FilterSelection chain, column_segment.cpp:378-522 /
+// bitpacking.cpp:779-868, for one constant comparison): one workgroup per group unpacks into
+// LDS as bitunpack_kernel does, then thread t tests values t, t + 256, …: a wave's 64
+// consecutive values are one ballot = one 64-row bitvector word. NULL rows never pass
+// (validity, optional). Words wholly inside the group are stored; a word a group shares with
+// its neighbour (a group whose rows do not start or end on a 64-row boundary) is OR-ed
+// atomically, so `out` must be zero beforehand. cmp = CUBIT_CMP_* or kCmpBetween
+// (c <= v < c2). Reads the packed bytes once: w/8 bytes per row instead of the plain column's
+// sizeof(T).
+template <typename T, typename U, typename CT>
+__global__ __launch_bounds__(256) void bitpacked_compare_kernel(const uint8_t* __restrict__ bytes,
+                                                                const BpGroup* __restrict__ groups,
+                                                                const uint64_t* __restrict__ validity, int cmp, CT c,
+                                                                CT c2, uint64_t* __restrict__ out) {
+    constexpr int THREADS = 256;
+    __shared__ __attribute__((aligned(16))) uint32_t s_words[kBpMaxWords + 8];
+    __shared__ U s_tot[THREADS / 64];
+    __shared__ T s_vals[2048];
+    const BpGroup g = groups[blockIdx.x];
+    const int t = threadIdx.x;
+    unpack_group<T, U>(bytes, g, s_words, s_tot, [&](int q, const U (&v)[4]) {
+        const uint32_t i0 = 4u * (uint32_t)(t + THREADS * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s_vals[i0 + j] = (T)v[j];
+    });
+    __syncthreads();
+    const int lane = t & 63, wave = t >> 6;
+    const uint64_t end = g.row_start + g.count;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t i = 256u * (uint32_t)k + (uint32_t)t;
+        const uint64_t r = g.row_start + i;
+        bool p = false;
+        if (i < g.count) {
+            const CT v = (CT)s_vals[i];
+            switch (cmp) {
+            case 0: p = v == c; break;
+            case 1: p = v != c; break;
+            case 2: p = v < c; break;
+            case 3: p = v <= c; break;
+            case 4: p = v > c; break;
+            case 5: p = v >= c; break;
+            default: p = v >= c && v < c2; break;
+            }
+            if (validity && !((validity[r >> 6] >> (r & 63)) & 1ull)) p = false;
+        }
+        const uint64_t bits = __ballot(p);
+        if (lane == 0) {
+            const uint64_t r0 = g.row_start + 256u * (uint32_t)k + 64u * (uint32_t)wave;  // row of bit 0
+            if (r0 >= end) continue;
+            const uint32_t sh = (uint32_t)(r0 & 63);
+            const uint64_t w0 = r0 >> 6;
+            if (sh == 0) {
+                if (r0 >= g.row_start && r0 + 64 <= end) out[w0] = bits;  // only this group's rows
+                else atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)bits);
+            } else {
+                atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)(bits << sh));
+                const uint64_t hi = bits >> (64 - sh);
+                if (hi) atomicOr(reinterpret_cast<unsigned long long*>(&out[w0 + 1]), (unsigned long long)hi);
+            }
+        }
     }
 }
 
@@ -2284,6 +2360,25 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
     else
         hipExtLaunchKernelGGL((bitunpack_kernel<int64_t, uint64_t>), dim3((unsigned)n_groups), dim3(256), 0, stream,
                               start, stop, 0, bytes, groups, static_cast<int64_t*>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
+                                    const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
+                                    uint64_t* out, hipStream_t stream) {
+    if (n_groups == 0) return hipSuccess;
+    if (n_groups > 0x7fffffffull) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)n_groups), block(256);
+    const bool fits32 = constant >= INT32_MIN && constant <= INT32_MAX && constant2 >= INT32_MIN && constant2 <= INT32_MAX;
+    if (type == 0 && fits32)
+        hipLaunchKernelGGL((bitpacked_compare_kernel<int32_t, uint32_t, int32_t>), grid, block, 0, stream, bytes, groups,
+                           validity, cmp, (int32_t)constant, (int32_t)constant2, out);
+    else if (type == 0)
+        hipLaunchKernelGGL((bitpacked_compare_kernel<int32_t, uint32_t, int64_t>), grid, block, 0, stream, bytes, groups,
+                           validity, cmp, constant, constant2, out);
+    else
+        hipLaunchKernelGGL((bitpacked_compare_kernel<int64_t, uint64_t, int64_t>), grid, block, 0, stream, bytes, groups,
+                           validity, cmp, constant, constant2, out);
     return hipGetLastError();
 }
 

@@ -354,6 +354,16 @@ class CubitTable:
                                                        C.byref(hv)))
         return int(lo.value), int(hi.value), bool(hn.value), bool(hv.value)
 
+    def use_packed_filter(self, on: bool = True) -> None:
+        """Filter bitpacked columns straight from their segments (default) or from the plain
+        column."""
+        L.check(self.lib.cubit_table_use_packed_filter(self.handle, 1 if on else 0))
+
+    def last_packed(self) -> int:
+        v = C.c_uint32()
+        L.check(self.lib.cubit_table_last_packed(self.handle, C.byref(v)))
+        return int(v.value)
+
     def last_zones(self):
         """(zones the last scan / sum_product evaluated, zones of the partition): fewer
         evaluated when the zonemaps skipped zones its filter is false on."""

@@ -218,6 +218,14 @@ int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, 
 int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
                                      const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
                                      const uint64_t *validity);
+/* A column registered with cubit_table_add_bitpacked_column keeps its segments on the device:
+ * a constant comparison the index cannot answer (K0) then unpacks and compares in one pass over
+ * the packed bytes (w/8 bytes per row — the reference's ColumnSegment::Scan →
+ * BitpackingScanPartial → FilterSelection, column_segment.cpp:378-522) instead of reading the
+ * plain column. On by default; results are identical either way. Appends and merges drop the
+ * segments (the plain column stays). cubit_table_last_packed: leaves the last scan built so. */
+int cubit_table_use_packed_filter(cubit_table *t, int on);
+int cubit_table_last_packed(cubit_table *t, uint32_t *n_leaves);
 /* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
  * distinct values of the column" (exact for every constant). RANGE / EQUALITY replace the
  * column's primary index; BINS (n >= 2 edges) adds a secondary binned index. */

@@ -105,3 +105,52 @@ def test_bench_packer_lineitem(ctx, name):
     col = O.BitpackedColumn(b.data, b.seg_off, None, b.seg_count, v.dtype)
     assert np.array_equal(O.bp_decode(col), got)
     t.close()
+
+
+@pytest.mark.parametrize("mode", ["auto", "for", "delta_for", "constant_delta"])
+@pytest.mark.parametrize("name", ["rand32", "rand64", "sorted32", "dates", "wide64", "constant"])
+def test_filter_straight_from_segments(ctx, name, mode):
+    """Constant comparisons on an unindexed bitpacked column run unpack + compare in one pass
+    over the segments (bitpacked_compare_kernel): the rows must equal the plain-column K0's and
+    the oracle's, for every comparison, with NULLs, and with small segments whose row counts
+    leave groups off the 64-row word boundaries (words shared by two groups)."""
+    rng = np.random.default_rng(abs(hash((name, mode, "f"))) % 2 ** 32)
+    n = 300_017
+    v = CASES[name](rng, n)
+    valid = rng.random(n) > 0.1
+    # segments cut at ragged rows (100,003 and 170,001): groups that start and end off the 64-row
+    # word boundaries (the compressor's own segments always end on whole groups)
+    parts, offs, counts, pos = [], [], [], 0
+    for a, b in ((0, 100_003), (100_003, 170_001), (170_001, n)):
+        c = O.bp_compress(v[a:b], valid[a:b], mode, block_size=65536)
+        assert c is not None
+        data = np.concatenate([c.data, np.zeros((-len(c.data)) % 8, np.uint8)])
+        parts.append(data)
+        offs.append(c.seg_off + pos)
+        counts.append(c.seg_count)
+        pos += len(data)
+    vw = validity_from_mask(valid)
+    t = CubitTable(ctx, n, row_base=11)
+    t.add_bitpacked_column(0, np.concatenate(parts), np.concatenate(offs).astype(np.uint64),
+                           np.concatenate(counts).astype(np.uint64), v.dtype, validity=vw)
+    other = rng.integers(0, 4, n).astype(np.int64)
+    t.add_column(1, other)
+    t.build_index(1, L.INDEX_RANGE)
+    cols = [O.Column(v, vw), O.Column(other)]
+    picks = rng.choice(v[valid], size=6) if valid.any() else np.zeros(6, v.dtype)
+    consts = [int(x) for x in picks] + [int(v.min()) - 1, int(v.max()) + 1]
+    for i, k in enumerate(consts):
+        cmp = ["=", "!=", "<", "<=", ">", ">="][i % 6]
+        for fs in (F.TableFilterSet({0: F.ConstantFilter(cmp, k)}),
+                   F.TableFilterSet({0: F.ConstantFilter(cmp, k), 1: F.ConstantFilter("<", 2)})):
+            ref = O.table_scan(cols, F.serialize(fs), n, row_base=11)
+            t.use_packed_filter(True)
+            got = t.scan(fs)
+            packed = t.last_packed()
+            t.use_packed_filter(False)
+            plain = t.scan(fs)
+            assert np.array_equal(got, ref), (name, mode, cmp, k)
+            assert np.array_equal(plain, ref), (name, mode, cmp, k)
+            assert packed == 1, (name, mode, cmp, k, packed)  # the leaf came from the segments
+    t.use_packed_filter(True)
+    t.close()
