@@ -962,7 +962,7 @@ struct cubit_table {
     std::map<int, ColZones> col_zones;
     std::map<std::tuple<int, int, int, int64_t, int64_t>, ZoneMap> pred_zones;
     uint32_t last_live = 0, last_zones = 0;  // zones the last scan evaluated / the partition has
-    bool use_packed = true;  // cubit_table_use_packed_filter
+    bool use_packed = false;  // cubit_table_use_packed_filter (off by default: slower than K0)
     uint32_t last_packed = 0;  // leaves the last plan built straight from packed segments
 };
 
