@@ -11,7 +11,7 @@ timeout -k 10 400 $B --workload synth > gpurun_out/bench_synth.log 2>&1 && \
 timeout -k 10 400 $B --workload or4 > gpurun_out/bench_or4.log 2>&1 && \
 timeout -k 10 400 $B --workload q6_mvcc > gpurun_out/bench_q6_mvcc.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/q6kt -o kt -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-maintenance > gpurun_out/prof/bench_kt.log 2>&1 && \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-maintenance --no-zonemap-leg > gpurun_out/prof/bench_kt.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/mvcckt -o kt -- \
     python3 bench.py --workload q6_mvcc --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof/bench_mvcc_kt.log 2>&1
 rc=$?
