@@ -964,6 +964,8 @@ struct cubit_table {
     uint32_t last_live = 0, last_zones = 0;  // zones the last scan evaluated / the partition has
     bool use_packed = false;  // cubit_table_use_packed_filter (off by default: slower than K0)
     uint32_t last_packed = 0;  // leaves the last plan built straight from packed segments
+    bool use_narrowing = true;  // cubit_table_use_narrowing
+    uint32_t last_narrowed = 0;  // K0 leaves the last plan built only at the rows a mask kept
 };
 
 namespace {
@@ -2050,6 +2052,32 @@ IndexView view_of(const cubit_table* t, int col, const Index& ix) {
     return v;
 }
 
+// A K0 leaf whose bitvector is not built yet: {valid rows: v cmp c} of column col into bv.
+struct PendingK0 {
+    uint64_t* bv;
+    int col, cmp;
+    int64_t c;
+};
+
+// Build a K0 leaf over the whole column (from the BITPACKING segments when enabled).
+int compute_k0(cubit_table* t, const PendingK0& k) {
+    const Column& cl = t->cols.at(k.col);
+    hipError_t e;
+    if (cl.bp_n_groups && t->use_packed) {
+        // straight from the BITPACKING segments: w/8 bytes per row instead of sizeof(T)
+        e = hipMemsetAsync(k.bv, 0, t->nwp * 8, t->ctx->stream);
+        if (e == hipSuccess)
+            e = launch_bitpacked_compare(static_cast<const uint8_t*>(cl.bp_bytes->p),
+                                         static_cast<const BpGroup*>(cl.bp_groups->p), cl.bp_n_groups, cl.type,
+                                         cl.validity, k.cmp, k.c, 0, k.bv, t->ctx->stream);
+        t->last_packed++;
+    } else {
+        e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, k.cmp, k.c, k.bv, t->ctx->stream);
+    }
+    if (e != hipSuccess) return fail(CUBIT_ERR_HIP, "compare kernel: %s", hipGetErrorString(e));
+    return CUBIT_OK;
+}
+
 struct Planner {
     cubit_table* t;
     const cubit_filter_node* nodes;
@@ -2078,27 +2106,14 @@ struct Planner {
         return mk_leaf(l);
     }
 
-    // K0 fallback: build the comparison from the raw column into a scratch bitvector
+    // K0 fallback: the comparison from the raw column into a scratch bitvector. The launch is
+    // deferred (pending) until the plan is complete: inside a conjunction it may be narrowed to
+    // the rows the other filters keep (narrow_k0), as the reference's filter loop does.
+    std::vector<PendingK0> pending;
     ExprP raw_compare(int col, int cmp, int64_t c) {
-        const Column& cl = t->cols.at(col);
         uint64_t* bv = nullptr;
         if ((rc = scratch_bv(t, &bv))) return nullptr;
-        hipError_t e;
-        if (cl.bp_n_groups && t->use_packed) {
-            // straight from the BITPACKING segments: w/8 bytes per row instead of sizeof(T)
-            e = hipMemsetAsync(bv, 0, t->nwp * 8, t->ctx->stream);
-            if (e == hipSuccess)
-                e = launch_bitpacked_compare(static_cast<const uint8_t*>(cl.bp_bytes->p),
-                                             static_cast<const BpGroup*>(cl.bp_groups->p), cl.bp_n_groups, cl.type,
-                                             cl.validity, cmp, c, 0, bv, t->ctx->stream);
-            t->last_packed++;
-        } else {
-            e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, cmp, c, bv, t->ctx->stream);
-        }
-        if (e != hipSuccess) {
-            rc = fail(CUBIT_ERR_HIP, "compare kernel: %s", hipGetErrorString(e));
-            return nullptr;
-        }
+        pending.push_back({bv, col, cmp, c});
         Leaf l;
         l.bv = bv;
         l.column = col;
@@ -2401,6 +2416,113 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
     if (int rc = scratch_bv(t, out)) return rc;
     t->last_passes++;
     return run_eval(t->ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, *out, RunMode::kCount);
+}
+
+bool fits(const ExprP& e);
+
+// Selection narrowing of K0 leaves (RowGroup::TemplatedScan's filter loop, row_group.cpp:537-550:
+// each filter column after the first is read only at the rows the earlier ones kept). When the
+// planned expression is a conjunction of literals holding non-negated K0 leaves, the other
+// literals are materialised into a mask (with none, the first K0 leaf is built in full and is
+// the mask). If the mask keeps at most one row in 32, each K0 leaf is built by
+// masked_compare_kernel — its column read only at the mask's rows, the result already the AND
+// with the mask — and the conjunction becomes that one leaf; a denser mask keeps the full K0
+// leaves (gathering most lines costs more than reading the column in order) and replaces the
+// literals it was made of. allow = false (visible MVCC updates, whose patches need whole
+// leaves) builds every leaf in full. Every pending leaf is built on return.
+int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool allow) {
+    auto compute_rest = [&]() -> int {
+        for (const PendingK0& k : pending)
+            if (int rc = compute_k0(t, k)) return rc;
+        pending.clear();
+        return CUBIT_OK;
+    };
+    auto take = [&](const uint64_t* bv, PendingK0* out) {
+        for (size_t i = 0; i < pending.size(); ++i)
+            if (pending[i].bv == bv) {
+                if (out) *out = pending[i];
+                pending.erase(pending.begin() + (long)i);
+                return true;
+            }
+        return false;
+    };
+    auto is_pending = [&](const uint64_t* bv) {
+        return std::any_of(pending.begin(), pending.end(), [&](const PendingK0& k) { return k.bv == bv; });
+    };
+    if (pending.empty()) return CUBIT_OK;
+    Emitter::Lits lits;
+    if (!allow || t->n_rows == 0 || e->kind == Expr::LEAF || !Emitter::conj_leaves(e, lits)) return compute_rest();
+    std::vector<const uint64_t*> narrow_bvs;
+    Emitter::Lits rest;
+    for (const auto& lit : lits) {
+        if (!lit.second && is_pending(lit.first.bv) &&
+            std::find(narrow_bvs.begin(), narrow_bvs.end(), lit.first.bv) == narrow_bvs.end())
+            narrow_bvs.push_back(lit.first.bv);
+        else
+            rest.push_back(lit);
+    }
+    for (const auto& lit : rest)  // a narrowed leaf must not also be read whole
+        if (std::find(narrow_bvs.begin(), narrow_bvs.end(), lit.first.bv) != narrow_bvs.end()) return compute_rest();
+    if (narrow_bvs.empty()) return compute_rest();
+    for (const auto& lit : rest) {  // complemented K0 leaves of the other literals: in full
+        PendingK0 k;
+        if (take(lit.first.bv, &k))
+            if (int rc = compute_k0(t, k)) return rc;
+    }
+    std::vector<PendingK0> narrow;
+    for (const uint64_t* bv : narrow_bvs) {
+        PendingK0 k;
+        take(bv, &k);
+        narrow.push_back(k);
+    }
+    uint64_t* mask = nullptr;
+    cubit_ctx* ctx = t->ctx;
+    if (!rest.empty()) {
+        ExprP r = mk_true();
+        for (const auto& lit : rest) r = mk_bin(Expr::AND, r, mk_leaf(lit.first, lit.second));
+        if (!fits(r)) {
+            for (const PendingK0& k : narrow) pending.push_back(k);
+            return compute_rest();
+        }
+        if (int rc = materialize(t, r, &mask)) return rc;  // counts its rows into dummy_count
+    } else {
+        const PendingK0 first = narrow.front();
+        narrow.erase(narrow.begin());
+        if (int rc = compute_k0(t, first)) return rc;
+        mask = first.bv;
+        Emitter em;
+        Leaf l;
+        l.bv = mask;
+        em.leaf(l, false);
+        if (int rc = run_eval(ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, nullptr, RunMode::kCount))
+            return rc;
+        t->last_passes++;
+    }
+    uint64_t kept = 0;
+    HIP_CHECK(hipMemcpyAsync(&kept, t->dummy_count, sizeof(kept), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    Leaf ml;
+    ml.bv = mask;
+    if (narrow.empty() || kept * 32 > t->n_rows) {
+        ExprP acc = mk_leaf(ml);
+        for (const PendingK0& k : narrow) {
+            if (int rc = compute_k0(t, k)) return rc;
+            Leaf l;
+            l.bv = k.bv;
+            acc = mk_bin(Expr::AND, acc, mk_leaf(l));
+        }
+        e = acc;
+        return compute_rest();
+    }
+    for (const PendingK0& k : narrow) {
+        const Column& cl = t->cols.at(k.col);
+        HIP_CHECK(launch_masked_compare(cl.data, cl.type, cl.validity, mask, t->n_rows, k.cmp, k.c, k.bv, ctx->stream));
+        mask = k.bv;
+        t->last_narrowed++;
+    }
+    ml.bv = mask;
+    e = mk_leaf(ml);
+    return compute_rest();
 }
 
 bool fits(const ExprP& e) {
@@ -2795,7 +2917,9 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     t->scratch_used = 0;
     t->last_passes = 0;
     t->last_packed = 0;
+    t->last_narrowed = 0;
     ExprP e;
+    std::vector<PendingK0> pending;  // K0 leaves not built yet (narrow_k0)
     if (n_nodes == 0) {
         e = mk_true();
     } else {
@@ -2803,6 +2927,16 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
         if (p.subtree_end(0) != (int)n_nodes) return fail(CUBIT_ERR_INVALID, "malformed filter tree");
         e = p.plan(0);
         if (!e) return p.rc ? p.rc : fail(CUBIT_ERR_INVALID, "planning failed");
+        pending = std::move(p.pending);
+    }
+    // a transaction that sees updates patches whole leaves: build the K0 leaves in full first
+    bool visible_updates = false;
+    if (txn)
+        for (auto& kv : t->upd) visible_updates |= kv.second.any_visible(txn);
+    if (visible_updates) {
+        for (const PendingK0& k : pending)
+            if (int rc = compute_k0(t, k)) return rc;
+        pending.clear();
     }
     if (txn) {
         std::map<const uint64_t*, uint64_t*> patched;
@@ -2896,6 +3030,8 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
             return CUBIT_OK;
         }
     }
+    // the K0 leaves last: narrowed to the rows the rest of a conjunction keeps, or in full
+    if (int rc = narrow_k0(t, e, pending, t->use_narrowing)) return rc;
     if (int rc = fit(t, e)) return rc;
     em.emit_top(e);
     if (!em.ok) return fail(CUBIT_ERR_UNSUPPORTED, "program does not fit one pass");
@@ -3134,6 +3270,20 @@ extern "C" int cubit_table_use_packed_filter(cubit_table* t, int on) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     CUBIT_LOCK(t->ctx);
     t->use_packed = on != 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_use_narrowing(cubit_table* t, int on) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    t->use_narrowing = on != 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_narrowed(cubit_table* t, uint32_t* n_leaves) {
+    if (!t || !n_leaves) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    *n_leaves = t->last_narrowed;
     return CUBIT_OK;
 }
 

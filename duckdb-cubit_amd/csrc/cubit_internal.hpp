@@ -114,6 +114,9 @@ hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* v
 hipError_t launch_candidate_check(const void* col, int type, const uint64_t* validity, const uint64_t* lo_bv,
                                   const uint64_t* hi_bv, uint64_t n_rows, int cmp, int64_t constant,
                                   uint64_t* out_words, hipStream_t stream);
+// selection narrowing: out = mask ∩ valid ∩ {v cmp constant}, the column read at mask rows only
+hipError_t launch_masked_compare(const void* col, int type, const uint64_t* validity, const uint64_t* mask,
+                                 uint64_t n_rows, int cmp, int64_t constant, uint64_t* out, hipStream_t stream);
 // K0 over several keys in one pass of the column (index build): out[k] = cmp(v, c[k], c2[k]),
 // cmp ∈ {EQ, LT, between}
 constexpr int kMultiKeys = 16;

@@ -1465,6 +1465,45 @@ __global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restric
     }
 }
 
+// Selection narrowing: RowGroup::TemplatedScan evaluates each filter column after the first
+// only at the rows the earlier ones kept (ColumnData::Select over the shared SelectionVector,
+// row_group.cpp:537-550). For a constant comparison on a column without a usable index inside a
+// conjunction: out = mask ∩ valid ∩ {r : lo <= v[r] <= hi, complemented when neg}, the column
+// read only at the mask's rows (line-granular gathers, as the candidate check). Each thread owns
+// two consecutive words (16-byte loads and stores).
+template <typename T>
+__global__ __launch_bounds__(256) void masked_compare_kernel(const T* __restrict__ col,
+                                                             const uint64_t* __restrict__ validity,
+                                                             const uint64_t* __restrict__ mask, uint64_t n_words_padded,
+                                                             T lo, T hi, int neg, uint64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * p < n_words_padded; p += stride) {
+        const uint64_t w0 = 2 * p;
+        u64x2 m = reinterpret_cast<const u64x2*>(mask)[p];
+        if (validity) {
+            const u64x2 vw = reinterpret_cast<const u64x2*>(validity)[p];
+            m.x &= vw.x;
+            m.y &= vw.y;
+        }
+        u64x2 res = {0ull, 0ull};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            uint64_t cand = e ? m.y : m.x;
+            uint64_t hit = 0;
+            const T* base = col + (w0 + e) * 64;
+            while (cand) {
+                const int b = __builtin_ctzll(cand);
+                const T v = base[b];
+                if (((v >= lo) & (v <= hi)) != (neg != 0)) hit |= 1ull << b;
+                cand &= cand - 1;
+            }
+            if (e) res.y = hit;
+            else res.x = hit;
+        }
+        reinterpret_cast<u64x2*>(out)[p] = res;
+    }
+}
+
 template <typename T, typename CT>
 hipError_t launch_candidate_t(const T* col, const uint64_t* validity, const uint64_t* lo_bv, const uint64_t* hi_bv,
                               uint64_t n_rows, int cmp, CT c, uint64_t* out, hipStream_t stream) {
@@ -2479,32 +2518,63 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
     return hipGetLastError();
 }
 
+// A comparison (CUBIT_CMP_* or kCmpBetween) as the inclusive range [lo, hi] of passing values,
+// complemented when neg (!=); empty: lo > hi. clamp32 narrows it to INT32 values.
+struct CmpRange {
+    int64_t lo = INT64_MIN, hi = INT64_MAX;
+    int neg = 0;
+    void clamp32(int32_t& lo32, int32_t& hi32) const {
+        const bool empty = lo > hi || lo > INT32_MAX || hi < INT32_MIN;
+        lo32 = empty ? 1 : (int32_t)std::max<int64_t>(lo, INT32_MIN);
+        hi32 = empty ? 0 : (int32_t)std::min<int64_t>(hi, INT32_MAX);
+    }
+};
+CmpRange cmp_range(int cmp, int64_t constant, int64_t constant2) {
+    CmpRange r;
+    switch (cmp) {
+    case 0: r.lo = r.hi = constant; break;                                            // =
+    case 1: r.lo = r.hi = constant; r.neg = 1; break;                                 // !=
+    case 2: if (constant == INT64_MIN) { r.lo = 1; r.hi = 0; } else r.hi = constant - 1; break;  // <
+    case 3: r.hi = constant; break;                                                   // <=
+    case 4: if (constant == INT64_MAX) { r.lo = 1; r.hi = 0; } else r.lo = constant + 1; break;  // >
+    case 5: r.lo = constant; break;                                                   // >=
+    default:                                                                          // c <= v < c2
+        r.lo = constant;
+        if (constant2 == INT64_MIN) { r.lo = 1; r.hi = 0; } else r.hi = constant2 - 1;
+        break;
+    }
+    return r;
+}
+
+hipError_t launch_masked_compare(const void* col, int type, const uint64_t* validity, const uint64_t* mask,
+                                 uint64_t n_rows, int cmp, int64_t constant, uint64_t* out, hipStream_t stream) {
+    const uint64_t nw = padded_words(n_rows);
+    const CmpRange r = cmp_range(cmp, constant, 0);
+    const dim3 grid(grid_for(nw / 2)), block(256);
+    if (type == 0) {
+        int32_t lo32, hi32;
+        r.clamp32(lo32, hi32);
+        hipLaunchKernelGGL(masked_compare_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
+                           validity, mask, nw, lo32, hi32, r.neg, out);
+    } else {
+        hipLaunchKernelGGL(masked_compare_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, mask, nw, r.lo, r.hi, r.neg, out);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
                                     uint64_t* out, hipStream_t stream) {
     if (n_groups == 0) return hipSuccess;
     if (n_groups > 0x7fffffffull) return hipErrorInvalidValue;
-    // the comparison as an inclusive range [lo, hi], complemented for != (empty: lo > hi)
-    int64_t lo = INT64_MIN, hi = INT64_MAX;
-    int neg = 0;
-    switch (cmp) {
-    case 0: lo = hi = constant; break;                                       // =
-    case 1: lo = hi = constant; neg = 1; break;                              // !=
-    case 2: if (constant == INT64_MIN) { lo = 1; hi = 0; } else hi = constant - 1; break;  // <
-    case 3: hi = constant; break;                                            // <=
-    case 4: if (constant == INT64_MAX) { lo = 1; hi = 0; } else lo = constant + 1; break;  // >
-    case 5: lo = constant; break;                                            // >=
-    default:                                                                 // constant <= v < constant2
-        lo = constant;
-        if (constant2 == INT64_MIN) { lo = 1; hi = 0; } else hi = constant2 - 1;
-        break;
-    }
+    const CmpRange rg = cmp_range(cmp, constant, constant2);
+    const int64_t lo = rg.lo, hi = rg.hi;
+    const int neg = rg.neg;
     const uint32_t ng = (uint32_t)n_groups;
     if (type == 0) {
-        // clamp to INT32 (an empty range stays empty: lo > hi after clamping, or lo > INT32_MAX)
-        const bool empty = lo > hi || lo > INT32_MAX || hi < INT32_MIN;
-        const int32_t lo32 = empty ? 1 : (int32_t)std::max<int64_t>(lo, INT32_MIN);
-        const int32_t hi32 = empty ? 0 : (int32_t)std::min<int64_t>(hi, INT32_MAX);
+        int32_t lo32, hi32;
+        rg.clamp32(lo32, hi32);
         constexpr int GPW = 4;  // groups per workgroup, their loads all in flight together
         hipLaunchKernelGGL((bitpacked_compare_kernel<int32_t, uint32_t, GPW>), dim3((ng + GPW - 1) / GPW), dim3(256),
                            0, stream, bytes, groups, ng, validity, lo32, hi32, neg, out);

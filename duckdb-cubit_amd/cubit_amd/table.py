@@ -364,6 +364,16 @@ class CubitTable:
         L.check(self.lib.cubit_table_last_packed(self.handle, C.byref(v)))
         return int(v.value)
 
+    def use_narrowing(self, on: bool = True) -> None:
+        """Read unindexed (K0) comparison columns of a conjunction only at the rows its other
+        filters keep, when they keep few (the default), or always in full."""
+        L.check(self.lib.cubit_table_use_narrowing(self.handle, 1 if on else 0))
+
+    def last_narrowed(self) -> int:
+        v = C.c_uint32()
+        L.check(self.lib.cubit_table_last_narrowed(self.handle, C.byref(v)))
+        return int(v.value)
+
     def last_zones(self):
         """(zones the last scan / sum_product evaluated, zones of the partition): fewer
         evaluated when the zonemaps skipped zones its filter is false on."""

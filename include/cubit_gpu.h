@@ -228,6 +228,14 @@ int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const ui
  * plain column stays). cubit_table_last_packed: leaves the last scan built so. */
 int cubit_table_use_packed_filter(cubit_table *t, int on);
 int cubit_table_last_packed(cubit_table *t, uint32_t *n_leaves);
+/* Selection narrowing (on by default): in a conjunction, a constant comparison on a column the
+ * index cannot answer (K0) reads its column only at the rows the rest of the conjunction keeps,
+ * when that is at most one row in 32 — the reference's filter loop reading each later filter
+ * column through the selection of the earlier ones (RowGroup::TemplatedScan, row_group.cpp:
+ * 537-550). Results are identical either way. cubit_table_last_narrowed: K0 leaves the last
+ * scan built so. */
+int cubit_table_use_narrowing(cubit_table *t, int on);
+int cubit_table_last_narrowed(cubit_table *t, uint32_t *n_leaves);
 /* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
  * distinct values of the column" (exact for every constant). RANGE / EQUALITY replace the
  * column's primary index; BINS (n >= 2 edges) adds a secondary binned index. */
