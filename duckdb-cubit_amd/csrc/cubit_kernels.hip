@@ -240,6 +240,58 @@ __device__ __forceinline__ void load_tile(const EvalArgs& a, uint64_t tile_word0
     }
 }
 
+// rowids[base + i] = row0 + st[i] for i < n, ids at or past `capacity` dropped (base and n are
+// workgroup-uniform; n ≤ 2^28 so the byte range fits a buffer descriptor). 16-byte stores from
+// the first ALIGN-byte boundary on, the ids before it one per thread. SAUX >= 0: buffer stores through
+// a descriptor built from SGPRs with cache-policy bits SAUX — sc1 (16, write-through) measured
+// 64.4 µs against 70.1 µs for plain global stores in the decode's read/write floor at SF100 Q6
+// (scripts/balbench.hip, profiles/r02e_balbench_cache_policy.txt); SAUX < 0: plain stores.
+template <int THREADS, int SAUX, int ALIGN = 16>
+__device__ __forceinline__ void emit_ids(int64_t* rowids, uint64_t capacity, const uint32_t* st, uint32_t n,
+                                         uint64_t base, int64_t row0, int t) {
+    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t room = capacity > base ? capacity - base : 0;
+    const uint32_t lim = (uint32_t)(room < (uint64_t)n ? room : (uint64_t)n);
+    if (lim == 0) return;
+    int64_t* out = rowids + base;
+    static_assert(ALIGN == 16 || ALIGN == 128, "16-byte stores, optionally from a 128-byte line boundary on");
+    const uint32_t head = min(lim, (uint32_t)(((ALIGN - (reinterpret_cast<uintptr_t>(out) & (ALIGN - 1))) & (ALIGN - 1)) >> 3));
+    if (SAUX < 0) {
+        if (t < (int)head) out[t] = row0 + (int64_t)st[t];
+        for (uint32_t i = head + 2 * t; i < lim; i += 2 * THREADS) {
+            if (i + 1 < lim) {
+                i64x2 val;
+                val.x = row0 + (int64_t)st[i];
+                val.y = row0 + (int64_t)st[i + 1];
+                *reinterpret_cast<i64x2*>(out + i) = val;
+            } else {
+                out[i] = row0 + (int64_t)st[i];
+            }
+        }
+        return;
+    }
+    const uint64_t ob = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)out >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)out);
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane(lim) * 8u;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)ob, (short)0, (int)nb, 0x00020000);
+    if (t < (int)head)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, row0 + (int64_t)st[t]), rs, (int)(t * 8), 0,
+                                              SAUX < 0 ? 0 : SAUX);
+    for (uint32_t i = head + 2 * t; i < lim; i += 2 * THREADS) {
+        if (i + 1 < lim) {
+            i64x2 val;
+            val.x = row0 + (int64_t)st[i];
+            val.y = row0 + (int64_t)st[i + 1];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rs, (int)(i * 8u), 0, SAUX < 0 ? 0 : SAUX);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, row0 + (int64_t)st[i]), rs, (int)(i * 8u), 0,
+                                                  SAUX < 0 ? 0 : SAUX);
+        }
+    }
+}
+
 // The i-th tile of a launch: entry i of the planner's live-tile list (zonemap skip) or i itself.
 // i is uniform, so the list entry is a scalar load; callers fetch it one tile ahead.
 __device__ __forceinline__ uint32_t tile_at(const EvalArgs& a, uint32_t i) { return a.live ? a.live[i] : i; }
@@ -472,7 +524,7 @@ __device__ uint64_t* g_diag_times;  // DIAG & 4 builds only (scripts/kbench.hip)
 // leaves (vmcnt counts stores too) does not add a store round trip. A tile with more than
 // STAGE hits claims on its own and writes straight to the output (dense path).
 template <int K, int PAIRS, int STAGE, int THREADS, int DIAG = 0, int FORM = FORM_POSTFIX, int WG_PER_CU = 2,
-          bool DSTAGE = true>
+          bool DSTAGE = true, int SAUX = 16>
 __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decode_pairs(EvalArgs a,
                                                                                        uint64_t* __restrict__ dir) {
     // DIAG (scripts/kbench.hip only): bit 0 = no claim (fixed pair offsets), bit 1 = uniform
@@ -484,7 +536,6 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     constexpr int NWAVES = THREADS / 64;
     constexpr bool EARLY = K <= 4;
     static_assert(TILE_WORDS * 64 < (1ull << 32), "tile-local offsets are 32-bit");
-    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
     static_assert(PAIRS <= 2, "pair counts are scanned as 16-bit fields of one uint32");
     __shared__ uint32_t s_wave_tot[2][NWAVES];
     __shared__ uint64_t s_off;        // claimed base of the pair being copied out
@@ -572,20 +623,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     // rowids[base + i] = row0 + st[i] for i < n: 16-byte stores (the first id alone when the
     // output is not 16-byte aligned there), bounded by the capacity
     auto emit = [&](const uint32_t* st, uint32_t n, uint64_t base, int64_t row0) {
-        int64_t* out = a.rowids + base;
-        const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
-        if (t == 0 && head && base < a.capacity) out[0] = row0 + (int64_t)st[0];
-        const uint64_t room = a.capacity > base ? a.capacity - base : 0;
-        for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
-            if (i + 1 < n && i + 1 < room) {
-                i64x2 val;
-                val.x = row0 + (int64_t)st[i];
-                val.y = row0 + (int64_t)st[i + 1];
-                *reinterpret_cast<i64x2*>(out + i) = val;
-            } else if (i < room) {
-                out[i] = row0 + (int64_t)st[i];
-            }
-        }
+        emit_ids<THREADS, SAUX>(a.rowids, a.capacity, st, n, base, row0, t);
     };
 
     // decode r into stage sp at stage_base with row offsets + delta; a dense tile claims on its
@@ -683,24 +721,9 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
     auto copy_out = [&](int sp) {
         const uint64_t base = s_off;
         const uint32_t n = s_cnt_a[sp] + s_cnt_b[sp];
-        if (write_ids && n) {
-            const int64_t row0 = a.row_base + (int64_t)((uint64_t)s_tile_a[sp] * TILE_ROWS);
-            int64_t* out = a.rowids + base;
-            // a leading element when the run starts off a 16-byte boundary
-            const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
-            if (t == 0 && head && base < a.capacity) out[0] = row0 + (int64_t)s_stage[sp][0];
-            const uint64_t room = a.capacity > base ? a.capacity - base : 0;
-            for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
-                if (i + 1 < n && i + 1 < room) {
-                    i64x2 val;
-                    val.x = row0 + (int64_t)s_stage[sp][i];
-                    val.y = row0 + (int64_t)s_stage[sp][i + 1];
-                    *reinterpret_cast<i64x2*>(out + i) = val;
-                } else if (i < room) {
-                    out[i] = row0 + (int64_t)s_stage[sp][i];
-                }
-            }
-        }
+        if (write_ids && n)
+            emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage[sp], n, base,
+                                    a.row_base + (int64_t)((uint64_t)s_tile_a[sp] * TILE_ROWS), t);
     };
 
     bool pending = false;  // a claimed pair waits for copy-out (uniform)
@@ -775,7 +798,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
 // times (spread 25 → 14 µs) but slowed every workgroup more than that gained: its dequeue is a
 // returning atomic that the next wait on the leaf loads (vmcnt counts in order) also waits for.
 template <int K, int PAIRS, int RUN_CAP, int THREADS, int FORM = FORM_POSTFIX, int MAXT = 16, bool STAMP = false,
-          bool DSTAGE = true>
+          bool DSTAGE = true, int SAUX = 16, int ALIGN = 16>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(EvalArgs a, uint64_t* __restrict__ dir) {
     // STAMP (scripts/kbench.hip only): each workgroup's start / end (s_memrealtime) into g_diag_times
     if (STAMP && threadIdx.x == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -785,7 +808,6 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     static_assert(MAXT <= 64, "directory entries per run");
     constexpr int NWAVES = THREADS / 64;
     constexpr bool EARLY = K <= 4;
-    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
     // per-wave totals of the pair counts, two 16-bit fields (a wave's total per pair is at most
     // 64 lanes × 128 bits = 8,192)
     static_assert(PAIRS <= 2, "pair counts are scanned as 16-bit fields of one uint32");
@@ -819,21 +841,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     // rowids[base + i] = row0 + st[i] for i < n: 16-byte stores (the first id alone when the
     // output is not 16-byte aligned there), bounded by the capacity
     auto emit = [&](const uint32_t* st, uint32_t n, uint64_t base, int64_t row0) {
-        int64_t* out = a.rowids + base;
-        const uint32_t head = (uint32_t)((reinterpret_cast<uintptr_t>(out) >> 3) & 1);
-        auto id = [&](uint32_t i) -> int64_t { return row0 + (int64_t)st[i]; };
-        if (t == 0 && head && base < a.capacity) out[0] = id(0);
-        const uint64_t room = a.capacity > base ? a.capacity - base : 0;
-        for (uint32_t i = head + 2 * t; i < n; i += 2 * THREADS) {
-            if (i + 1 < n && i + 1 < room) {
-                i64x2 val;
-                val.x = id(i);
-                val.y = id(i + 1);
-                *reinterpret_cast<i64x2*>(out + i) = val;
-            } else if (i < room) {
-                out[i] = id(i);
-            }
-        }
+        emit_ids<THREADS, SAUX, ALIGN>(a.rowids, a.capacity, st, n, base, row0, t);
     };
     // copy out closed run rs at s_off (published before the preceding barrier) and write its
     // directory entries
@@ -1737,17 +1745,30 @@ __global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restric
     __shared__ U s_tot[THREADS / 64];
     const BpGroup g = groups[blockIdx.x];
     const int t = threadIdx.x;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    // 4-byte values leave through a descriptor over dst[0, count) built from SGPRs, as sc1
+    // (write-through) 16-byte buffer stores — the store policy the decode's copy-out measured
+    // fastest (emit_ids, profiles/r02e_balbench_cache_policy.txt); each store instruction then
+    // covers 1 KiB contiguously
     T* dst = out + g.row_start;
+    const uintptr_t dp = reinterpret_cast<uintptr_t>(dst);
+    const uint64_t db = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(dp >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dp);
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(g.count);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)db, (short)0, (int)(cnt * (uint32_t)sizeof(T)), 0x00020000);
     // store quad c of this thread: values 4·(t + 256c) + 0..3
     unpack_group<T, U>(bytes, g, s_words, s_tot, [&](int c, const U (&v)[4]) {
         const uint32_t i0 = 4u * (uint32_t)(t + THREADS * c);
-        if (i0 + 4 <= g.count) {
+        if (i0 + 4 <= cnt) {
             if (sizeof(T) == 4) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                 u32x4 o;
                 o.x = (uint32_t)v[0], o.y = (uint32_t)v[1], o.z = (uint32_t)v[2], o.w = (uint32_t)v[3];
-                *reinterpret_cast<u32x4*>(dst + i0) = o;
+                __builtin_amdgcn_raw_buffer_store_b128(o, rs, (int)(i0 * 4u), 0, 16);
             } else {
+                // 8-byte values: a lane's quad is 32 bytes, so each store instruction covers every
+                // other 16 bytes; write-through (sc1) of those half lines measured 3.3 ms instead of
+                // 1.0 ms for l_discount, so these stay plain (write-back merges the halves in L2)
                 u64x2 o0, o1;
                 o0.x = (uint64_t)v[0], o0.y = (uint64_t)v[1], o1.x = (uint64_t)v[2], o1.y = (uint64_t)v[3];
                 reinterpret_cast<u64x2*>(dst + i0)[0] = o0;
@@ -1755,8 +1776,13 @@ __global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restric
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (i0 + j < g.count) dst[i0 + j] = (T)v[j];
+            for (int j = 0; j < 4; ++j) {
+                if (i0 + j >= cnt) continue;
+                if (sizeof(T) == 4)
+                    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[j], rs, (int)((i0 + j) * 4u), 0, 16);
+                else
+                    dst[i0 + j] = (T)v[j];
+            }
         }
     });
 }

@@ -207,6 +207,16 @@ int main(int argc, char** argv) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ>), dim3(grid), dim3(512), 0, s, a, dir);
                   }, false});
+    vs.push_back({"runs K4 sc1 align128", [&](hipStream_t s) {
+                      EvalArgs a = base;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 16, 128>), dim3(grid),
+                                         dim3(512), 0, s, a, dir);
+                  }, false});
+    vs.push_back({"runs K4 plain align128", [&](hipStream_t s) {
+                      EvalArgs a = base;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, -1, 128>), dim3(grid),
+                                         dim3(512), 0, s, a, dir);
+                  }, false});
     vs.push_back({"runs K4 plain stores", [&](hipStream_t s) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, -1>), dim3(grid),
