@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __rest
             for (int j = 0; j < JB; ++j) {
                 const uint64_t row = (w0 + jb + j) * 64 + lane;
                 ok[j] = row < n_rows;
-                v[j] = ok[j] ? (CT)col[row] : (CT)0;
+                v[j] = ok[j] ? (CT)__builtin_nontemporal_load(col + row) : (CT)0;  // streamed once: nt
                 if (validity) ok[j] = ok[j] && ((validity[w0 + jb + j] >> lane) & 1ull);
             }
 #pragma unroll
@@ -1437,9 +1437,9 @@ __global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restric
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; 2 * p < n_words_padded; p += stride) {
         const uint64_t w0 = 2 * p;
         u64x2 lo = {0ull, 0ull}, hi;
-        if (lo_bv) lo = reinterpret_cast<const u64x2*>(lo_bv)[p];
+        if (lo_bv) lo = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(lo_bv) + p);
         if (hi_bv) {
-            hi = reinterpret_cast<const u64x2*>(hi_bv)[p];
+            hi = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(hi_bv) + p);
         } else {
             // every valid row of the partition: full words, the tail word's rows, nothing past it
             hi.x = w0 < n_words ? ~0ull : 0ull;
@@ -1677,7 +1677,7 @@ __device__ __forceinline__ void unpack_group(const uint8_t* __restrict__ bytes, 
     if (!STAGED) {
         const bp_u32x4* src = reinterpret_cast<const bp_u32x4*>(bytes + sp.a0);
         bp_u32x4* sw = reinterpret_cast<bp_u32x4*>(s_words);
-        for (uint32_t i = t; i < sp.nvec; i += THREADS) sw[i] = src[i];
+        for (uint32_t i = t; i < sp.nvec; i += THREADS) sw[i] = __builtin_nontemporal_load(src + i);
         // (a value's window may read one word past its last bit: those bits are masked off)
         __syncthreads();
     }
@@ -2063,11 +2063,11 @@ __global__ __launch_bounds__(256) void column_zone_stats_kernel(const T* __restr
         if (b + 4 <= r1) {
             int64_t x[4];
             if (sizeof(T) == 4) {
-                const bp_u32x4 q = *reinterpret_cast<const bp_u32x4*>(col + b);
+                const bp_u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const bp_u32x4*>(col + b));
                 x[0] = (int32_t)q.x, x[1] = (int32_t)q.y, x[2] = (int32_t)q.z, x[3] = (int32_t)q.w;
             } else {
-                const u64x2 q0 = reinterpret_cast<const u64x2*>(col + b)[0];
-                const u64x2 q1 = reinterpret_cast<const u64x2*>(col + b)[1];
+                const u64x2 q0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(col + b));
+                const u64x2 q1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(col + b) + 1);
                 x[0] = (int64_t)q0.x, x[1] = (int64_t)q0.y, x[2] = (int64_t)q1.x, x[3] = (int64_t)q1.y;
             }
 #pragma unroll
