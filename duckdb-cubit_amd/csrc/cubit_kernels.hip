@@ -1192,8 +1192,9 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                     ok[u] = k < (uint32_t)tile_count;
                     const uint32_t sr = ok[u] ? s_row[k] : 0u;
                     const uint64_t rr = (uint64_t)(row0 - a.row_base) + (sr & ((1u << kMissShift) - 1));
-                    av[u] = ok[u] ? s.a[rr] : 0;
-                    bvv[u] = M > 0 ? (ok[u] ? decoded_b(sr >> kMissShift) : 0) : (ok[u] ? s.b[rr] : 0);
+                    // line-granular gathers, no reuse: nontemporal like the leaf loads
+                    av[u] = ok[u] ? __builtin_nontemporal_load(s.a + rr) : 0;
+                    bvv[u] = M > 0 ? (ok[u] ? decoded_b(sr >> kMissShift) : 0) : (ok[u] ? __builtin_nontemporal_load(s.b + rr) : 0);
                     if (ok[u] && s.a_valid && !((s.a_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
                     if (M == 0 && ok[u] && s.b_valid && !((s.b_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
                 }
@@ -1938,7 +1939,7 @@ __global__ __launch_bounds__(256) void gather_kernel(const T* __restrict__ col, 
     const uint64_t n = min(*d_count, max_n);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        out[i] = (int64_t)col[rowids[i] - row_base];
+        out[i] = (int64_t)__builtin_nontemporal_load(col + (__builtin_nontemporal_load(rowids + i) - row_base));
 }
 
 __global__ __launch_bounds__(256) void gather_sum_product_kernel(const int64_t* __restrict__ x,
@@ -1951,8 +1952,8 @@ __global__ __launch_bounds__(256) void gather_sum_product_kernel(const int64_t* 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     __int128 acc = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int64_t r = rowids[i] - row_base;
-        acc += (__int128)x[r] * (__int128)y[r];
+        const int64_t r = __builtin_nontemporal_load(rowids + i) - row_base;
+        acc += (__int128)__builtin_nontemporal_load(x + r) * (__int128)__builtin_nontemporal_load(y + r);
     }
     // wave reduce on the two halves
     uint64_t lo = (uint64_t)acc;

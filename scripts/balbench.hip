@@ -207,6 +207,11 @@ int main(int argc, char** argv) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ>), dim3(grid), dim3(512), 0, s, a, dir);
                   }, false});
+    vs.push_back({"runs K4 st18 (nt+sc1)", [&](hipStream_t s) {
+                      EvalArgs a = base;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 18>), dim3(grid),
+                                         dim3(512), 0, s, a, dir);
+                  }, false});
     vs.push_back({"runs K4 sc1 align128", [&](hipStream_t s) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 16, 128>), dim3(grid),
@@ -255,6 +260,9 @@ int main(int argc, char** argv) {
     FW("ldsnext ld18 st-", 1, 18, -1);
     FW("ldsnext ld3 st-", 1, 3, -1);
     FW("ldsnext ld0 st2", 1, 0, 2);
+    FW("ldsnext ld2 st18", 1, 2, 18);
+    FW("ldsnext ld18 st16", 1, 18, 16);
+    FW("ldsnext ld3 st16", 1, 3, 16);
     FW("reads only ld2", 1, 2, -1, true);
     FW("reads only ld0", 1, 0, -1, true);
 
