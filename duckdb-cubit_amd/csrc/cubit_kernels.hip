@@ -1761,15 +1761,39 @@ __global__ __launch_bounds__(256) void bitunpack_kernel(const uint8_t* __restric
     // store quad c of this thread: values 4·(t + 256c) + 0..3
     unpack_group<T, U>(bytes, g, s_words, s_tot, [&](int c, const U (&v)[4]) {
         const uint32_t i0 = 4u * (uint32_t)(t + THREADS * c);
+        if (sizeof(T) == 8 && cnt == 2048u) {
+            // 8-byte values of a full group (uniform; store_quad runs with every lane active): a
+            // wave's 256 values are 2 KiB, lane l owns bytes [32l, 32l + 32). Two lane exchanges
+            // make each store instruction cover 1 KiB contiguously — lane l writes wave values
+            // 2l, 2l + 1 (from lane l/2) and 128 + 2l, 129 + 2l (from lane 32 + l/2) — so the
+            // stores can be sc1 (write-through) without half-line writes
+            const int lane = t & 63;
+            const bool odd = (lane & 1) != 0;
+            const uint32_t wbase = 32u * (uint32_t)(THREADS * c + (t & ~63));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int src = 32 * h + (lane >> 1);
+                const unsigned long long e0 = __shfl((unsigned long long)(uint64_t)v[0], src, 64);
+                const unsigned long long e1 = __shfl((unsigned long long)(uint64_t)v[1], src, 64);
+                const unsigned long long f0 = __shfl((unsigned long long)(uint64_t)v[2], src, 64);
+                const unsigned long long f1 = __shfl((unsigned long long)(uint64_t)v[3], src, 64);
+                u64x2 o;
+                o.x = odd ? f0 : e0;
+                o.y = odd ? f1 : e1;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (int)(wbase + 1024u * h + 16u * lane),
+                                                       0, 16);
+            }
+            return;
+        }
         if (i0 + 4 <= cnt) {
             if (sizeof(T) == 4) {
                 u32x4 o;
                 o.x = (uint32_t)v[0], o.y = (uint32_t)v[1], o.z = (uint32_t)v[2], o.w = (uint32_t)v[3];
                 __builtin_amdgcn_raw_buffer_store_b128(o, rs, (int)(i0 * 4u), 0, 16);
             } else {
-                // 8-byte values: a lane's quad is 32 bytes, so each store instruction covers every
-                // other 16 bytes; write-through (sc1) of those half lines measured 3.3 ms instead of
-                // 1.0 ms for l_discount, so these stay plain (write-back merges the halves in L2)
+                // 8-byte values of a partial group: a lane's quad is 32 bytes, so each store
+                // instruction covers every other 16 bytes; write-through (sc1) of those half lines
+                // measured 3.3 ms instead of 1.0 ms for l_discount, so these stay plain
                 u64x2 o0, o1;
                 o0.x = (uint64_t)v[0], o0.y = (uint64_t)v[1], o1.x = (uint64_t)v[2], o1.y = (uint64_t)v[3];
                 reinterpret_cast<u64x2*>(dst + i0)[0] = o0;
