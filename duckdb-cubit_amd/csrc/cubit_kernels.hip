@@ -1270,6 +1270,9 @@ __global__ __launch_bounds__(256) void sum_product_arrays_kernel(const int64_t* 
 // reads from the directory itself (16 B per tile, L2-resident: ≤ 37 KB at SF100, read with
 // every thread's loads in flight), so no separate scan launch and no single-workgroup scan
 // precede the copy. The copy keeps four 8-byte loads in flight per thread.
+// MODE (scripts/balbench.hip compares them): 0 plain loads and stores, 1 nontemporal loads and
+// sc1 (write-through) buffer stores, 2 nontemporal loads and plain stores.
+template <int MODE = 0>
 __global__ __launch_bounds__(256) void order_runs_kernel(const uint64_t* __restrict__ dir, uint32_t n_tiles,
                                                          uint32_t tpw, const int64_t* __restrict__ src,
                                                          uint64_t capacity, int64_t* __restrict__ dst) {
@@ -1287,19 +1290,32 @@ __global__ __launch_bounds__(256) void order_runs_kernel(const uint64_t* __restr
 #pragma unroll
     for (int w = 0; w < THREADS / 64; ++w) d += s_part[w];
     const uint32_t t1 = t0 + tpw < n_tiles ? t0 + tpw : n_tiles;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     for (uint32_t tile = t0; tile < t1; ++tile) {
         const uint64_t so = dir[2 * tile], n = dir[2 * tile + 1];
+        // MODE 1: this tile's destination run through a descriptor from SGPRs (≤ 131,072 ids)
+        const uint64_t lim = d < capacity ? min(n, capacity - d) : 0;
+        const uintptr_t dp = reinterpret_cast<uintptr_t>(dst + d);
+        const uint64_t db = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(dp >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)dp);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)db, (short)0, (int)((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)lim) * 8u), 0x00020000);
         for (uint64_t i = t; i < n; i += 4 * THREADS) {
             int64_t v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint64_t j = i + (uint64_t)u * THREADS;
-                v[u] = (j < n && so + j < capacity) ? src[so + j] : 0;
+                v[u] = (j < n && so + j < capacity) ? (MODE ? __builtin_nontemporal_load(src + so + j) : src[so + j]) : 0;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint64_t j = i + (uint64_t)u * THREADS;
-                if (j < n && so + j < capacity && d + j < capacity) dst[d + j] = v[u];
+                if (j < n && so + j < capacity && d + j < capacity) {
+                    if (MODE == 1)
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[u]), rs, (int)(j * 8u), 0, 16);
+                    else
+                        dst[d + j] = v[u];
+                }
             }
         }
         d += n;
@@ -2412,7 +2428,7 @@ hipError_t launch_order_runs(const uint64_t* dir, uint32_t n_tiles, uint64_t* ds
     if (n_tiles == 0) return hipSuccess;
     const uint32_t tpw = std::max<uint32_t>(1, std::min<uint32_t>(8, n_tiles / 1024));
     const unsigned grid = (n_tiles + tpw - 1) / tpw;
-    hipLaunchKernelGGL(order_runs_kernel, dim3(grid), dim3(256), 0, s, dir, n_tiles, tpw, src, capacity, dst);
+    hipLaunchKernelGGL(order_runs_kernel<0>, dim3(grid), dim3(256), 0, s, dir, n_tiles, tpw, src, capacity, dst);
     return hipGetLastError();
 }
 

@@ -241,6 +241,18 @@ int main(int argc, char** argv) {
                       hipLaunchKernelGGL((eval_decode_pairs<4, 2, 4096, 512, 0, FORM_CONJ, 2, true, -1>), dim3(grid), dim3(512), 0,
                                          s, a, dir);
                   }, false});
+    // the ordered output pass over the directory and ids the variants above left
+    int64_t* ord;
+    CK(hipMalloc(&ord, cap * 8));
+#define OR(NAME, MODE)                                                                                          \
+    vs.push_back({NAME, [&](hipStream_t s) {                                                                   \
+                      const uint32_t tpw = std::max<uint32_t>(1, std::min<uint32_t>(8, dtiles / 1024));        \
+                      hipLaunchKernelGGL(order_runs_kernel<MODE>, dim3((dtiles + tpw - 1) / tpw), dim3(256), 0, s, dir, \
+                                         dtiles, tpw, ids, cap, ord);                                           \
+                  }, false})
+    OR("order pass plain", 0);
+    OR("order pass nt+sc1", 1);
+    OR("order pass nt", 2);
 #define FW(NAME, MODE, ...)                                                                                        \
     vs.push_back({NAME, [&](hipStream_t s) {                                                                   \
                       CK(hipMemsetAsync(heads, 0, 8 * kHeadStride * 8, s));                                    \
@@ -277,7 +289,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < rounds + 2; ++r) {
         for (size_t i = 0; i < vs.size(); ++i) {
             CK(hipMemsetAsync(done, 0, 8, s));
-            if (!vs[i].floor) CK(hipMemsetAsync(dir, 0, dtiles * 16, s));
+            if (!vs[i].floor && vs[i].name.rfind("order", 0) != 0) CK(hipMemsetAsync(dir, 0, dtiles * 16, s));
             CK(hipEventRecord(e0, s));
             vs[i].launch(s);
             CK(hipEventRecord(e1, s));
