@@ -74,7 +74,7 @@ __device__ __forceinline__ void load_tile_aux(const EvalArgs& a, uint64_t tile_w
 
 // MODE 0 static, 1 ldsnext, 2 xcd heads, 3 one global head; LAUX / SAUX: cache-policy bits of
 // the leaf loads / the id stores (SAUX < 0: plain stores)
-template <int K, int WR, int MODE, int LAUX = 2, int SAUX = -1, bool NOWR = false>
+template <int K, int WR, int MODE, int LAUX = 2, int SAUX = -1, bool NOWR = false, bool NORD = false>
 __global__ __launch_bounds__(512, 4) void floor_walk(EvalArgs a, int64_t* out, unsigned long long* heads,
                                                       unsigned long long* done, uint64_t* stamps) {
     constexpr int THREADS = 512, PAIRS = 2;
@@ -93,7 +93,13 @@ __global__ __launch_bounds__(512, 4) void floor_walk(EvalArgs a, int64_t* out, u
         if (lane == 0) pend = atomicAdd(&heads[cx * kHeadStride], 1ull);
     };
     uint32_t tile = blockIdx.x, count = 0, u = 0;
-    if (tile < n) load_tile_aux<K, PAIRS, THREADS, LAUX>(a, (uint64_t)tile * TILE_WORDS, t, v);
+    if (NORD) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int p = 0; p < PAIRS; ++p) v[k][p] = u64x2{(uint64_t)t, (uint64_t)blockIdx.x};
+    }
+    if (tile < n && !NORD) load_tile_aux<K, PAIRS, THREADS, LAUX>(a, (uint64_t)tile * TILE_WORDS, t, v);
     if (MODE >= 2 && wave == 7) dequeue();
     while (tile < n) {
         uint64_t x = 0;
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(512, 4) void floor_walk(EvalArgs a, int64_t* out, u
             __syncthreads();
             next = s_next[u & 1];
         }
-        if (next < n) load_tile_aux<K, PAIRS, THREADS, LAUX>(a, (uint64_t)next * TILE_WORDS, t, v);
+        if (next < n && !NORD) load_tile_aux<K, PAIRS, THREADS, LAUX>(a, (uint64_t)next * TILE_WORDS, t, v);
         i64x2* o = reinterpret_cast<i64x2*>(out + (uint64_t)tile * (WR + 6));
         if (NOWR) {
             if (x == 0x123456789ull) out[tile] = 1;  // keep the loads
@@ -276,6 +282,8 @@ int main(int argc, char** argv) {
     FW("ldsnext ld18 st16", 1, 18, 16);
     FW("ldsnext ld3 st16", 1, 3, 16);
     FW("reads only ld2", 1, 2, -1, true);
+    FW("writes only st-", 1, 2, -1, false, true);
+    FW("writes only st16", 1, 2, 16, false, true);
     FW("reads only ld0", 1, 0, -1, true);
 
     hipStream_t s;
