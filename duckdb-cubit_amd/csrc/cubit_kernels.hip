@@ -798,7 +798,7 @@ __global__ __launch_bounds__(THREADS, WG_PER_CU * THREADS / 256) void eval_decod
 // times (spread 25 → 14 µs) but slowed every workgroup more than that gained: its dequeue is a
 // returning atomic that the next wait on the leaf loads (vmcnt counts in order) also waits for.
 template <int K, int PAIRS, int RUN_CAP, int THREADS, int FORM = FORM_POSTFIX, int MAXT = 16, bool STAMP = false,
-          bool DSTAGE = true, int SAUX = 16, int ALIGN = 16>
+          bool DSTAGE = true, int SAUX = 16, int ALIGN = 16, int EARLY_AT = 4>
 __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(EvalArgs a, uint64_t* __restrict__ dir) {
     // STAMP (scripts/kbench.hip only): each workgroup's start / end (s_memrealtime) into g_diag_times
     if (STAMP && threadIdx.x == 0) g_diag_times[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     constexpr uint64_t TILE_ROWS = TILE_WORDS * 64;
     static_assert(MAXT <= 64, "directory entries per run");
     constexpr int NWAVES = THREADS / 64;
-    constexpr bool EARLY = K <= 4;
+    constexpr bool EARLY = K <= EARLY_AT;  // next tile's loads before the copy-out (K <= 4) or after it
     // per-wave totals of the pair counts, two 16-bit fields (a wave's total per pair is at most
     // 64 lanes × 128 bits = 8,192)
     static_assert(PAIRS <= 2, "pair counts are scanned as 16-bit fields of one uint32");

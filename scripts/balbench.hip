@@ -213,6 +213,11 @@ int main(int argc, char** argv) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ>), dim3(grid), dim3(512), 0, s, a, dir);
                   }, false});
+    vs.push_back({"runs K4 late loads", [&](hipStream_t s) {
+                      EvalArgs a = base;
+                      hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 16, 16, 3>), dim3(grid),
+                                         dim3(512), 0, s, a, dir);
+                  }, false});
     vs.push_back({"runs K4 st18 (nt+sc1)", [&](hipStream_t s) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 18>), dim3(grid),
