@@ -208,8 +208,27 @@ __device__ __forceinline__ void tail_mask(const EvalArgs& a, uint64_t tile_word0
     }
 }
 
-template <int PAIRS, int THREADS>
+// A tile's result words (materialised subtrees, narrowing masks). SAUX >= 0: buffer stores with
+// those cache-policy bits through a descriptor over the tile (tile_word0 is uniform), as the
+// decode's copy-out (emit_ids); SAUX < 0: plain stores.
+template <int PAIRS, int THREADS, int SAUX = -1>
 __device__ __forceinline__ void store_words(uint64_t* out, uint64_t tile_word0, int t, const uint64_t (&r)[2 * PAIRS]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if (SAUX >= 0) {
+        const uint64_t tw = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tile_word0 >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tile_word0);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(out + tw), (short)0, PAIRS * THREADS * 16, 0x00020000);
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            u64x2 o;
+            o.x = r[2 * p];
+            o.y = r[2 * p + 1];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (int)((uint32_t)(p * THREADS + t) * 16u),
+                                                   0, SAUX < 0 ? 0 : SAUX);
+        }
+        return;
+    }
 #pragma unroll
     for (int p = 0; p < PAIRS; ++p) {
         u64x2 o;
@@ -302,7 +321,7 @@ __device__ __forceinline__ uint32_t tile_at(const EvalArgs& a, uint32_t i) { ret
 // g, g+G, …, two tiles in flight (register double buffer: the loads of tile i+2 are issued
 // as soon as tile i is evaluated), keeps its count in registers and claims once at the end
 // (one returning atomic per workgroup).
-template <int K, int PAIRS, int FORM = FORM_POSTFIX>
+template <int K, int PAIRS, int FORM = FORM_POSTFIX, int SAUX = -1>
 __global__ __launch_bounds__(512, 4) void eval_count_kernel(EvalArgs a) {
     constexpr int THREADS = 512, NW = 2 * PAIRS;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
@@ -323,7 +342,7 @@ __global__ __launch_bounds__(512, 4) void eval_count_kernel(EvalArgs a) {
         eval_words<K, NW, FORM>(a.prog, v, r);
         if (ahead < n) load_tile<K, PAIRS, THREADS>(a, (uint64_t)ahead_tile * TILE_WORDS, t, v);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);
-        if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+        if (a.result_words) store_words<PAIRS, THREADS, SAUX>(a.result_words, tile_word0, t, r);
 #pragma unroll
         for (int j = 0; j < NW; ++j) c += __popcll(r[j]);
     };

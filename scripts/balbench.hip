@@ -213,6 +213,21 @@ int main(int argc, char** argv) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ>), dim3(grid), dim3(512), 0, s, a, dir);
                   }, false});
+    // materialise one leaf AND another into a result bitvector (count kernel + result words)
+    uint64_t* res;
+    CK(hipMalloc(&res, pw * 8));
+#define MAT(NAME, SA)                                                                                           \
+    vs.push_back({NAME, [&](hipStream_t s) {                                                                   \
+                      EvalArgs a = base;                                                                      \
+                      a.prog.n_leaves = 2;                                                                    \
+                      a.prog.nops = 1u << 4;                                                                  \
+                      a.result_words = res;                                                                   \
+                      a.num_tiles = (uint32_t)(pw / (512 * 2 * 2));                                           \
+                      hipLaunchKernelGGL((eval_count_kernel<2, 2, FORM_CONJ, SA>), dim3(std::min<unsigned>(a.num_tiles, 4 * cus)), \
+                                         dim3(512), 0, s, a);                                                 \
+                  }, false})
+    MAT("materialise K2 plain", -1);
+    MAT("materialise K2 sc1", 16);
     vs.push_back({"runs K4 late loads", [&](hipStream_t s) {
                       EvalArgs a = base;
                       hipLaunchKernelGGL((eval_decode_runs<4, 2, 9984, 512, FORM_CONJ, 16, false, true, 16, 16, 3>), dim3(grid),
