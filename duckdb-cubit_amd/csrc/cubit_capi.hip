@@ -74,6 +74,8 @@ struct cubit_ctx {
     uint64_t tmp_cap = 0;
     int64_t* partials = nullptr;
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
+    uint64_t* flags = nullptr;   // look-back flag words of eval_decode_lookback (EvalArgs::flags)
+    uint64_t epoch = 0;          // the last look-back launch's epoch (EvalArgs::epoch)
     int decode_kernel = CUBIT_DECODE_AUTO;  // cubit_ctx_set_decode_kernel
     int last_decode = 0;                    // kernel of the last decode (CUBIT_DECODE_PAIRS / _RUNS)
     // zonemap skip: the live-tile list of a launch, staged in page-locked memory and copied to
@@ -215,11 +217,15 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         HIP_CHECK(launch_eval_count(a, ctx->stream, start, stop));
         return CUBIT_OK;
     }
-    const uint64_t tiles = pw / decode_tile_words();
-    if (int rc = ensure_dir(ctx, tiles)) return rc;
+    // the tiles that hold rows (the padding past the last word needs no workgroup); the
+    // directory is sized for every padded tile, as a live-tile list may name any of them
+    const uint64_t tiles = (a.n_words + decode_tile_words() - 1) / decode_tile_words();
+    if (int rc = ensure_dir(ctx, pw / decode_tile_words())) return rc;
     if (ordered && rowids)
         if (int rc = ensure_tmp(ctx, capacity)) return rc;
     a.num_tiles = (uint32_t)tiles;
+    a.flags = ctx->flags;
+    a.epoch = ++ctx->epoch;
     a.rowids = ordered && rowids ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
     if (live_zones) {
@@ -237,8 +243,15 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     const uint64_t work = a.num_tiles;
     const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
     const unsigned grid = (unsigned)(work <= max_grid ? work : work <= 2 * max_grid ? (work + 1) / 2 : max_grid);
-    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel));
-    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel, a.live != nullptr);
+    if (tiles == 0) {  // no row: the count is 0 and no kernel runs
+        if (start) ctx->n_timed--;
+        HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), ctx->stream));
+        ctx->last_decode = 0;
+        return CUBIT_OK;
+    }
+    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel, ctx->n_cus));
+    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel, a.live != nullptr,
+                                         ctx->n_cus);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (ordered && rowids)
@@ -248,6 +261,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         uint64_t n = 0;
         HIP_CHECK(hipMemcpyAsync(&n, d_count, sizeof(n), hipMemcpyDeviceToHost, ctx->stream));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        if (n == ~0ull) return fail(CUBIT_ERR_DEVICE, "decode look-back did not complete (bounded wait expired)");
         if (n > capacity)
             return fail(CUBIT_ERR_CAPACITY, "%llu qualifying rows exceed the capacity of %llu row ids",
                         (unsigned long long)n, (unsigned long long)capacity);
@@ -278,9 +292,13 @@ int cubit_ctx_create(int device, cubit_ctx** out) {
         ctx->n_cus = prop.multiProcessorCount;
     if (hipMalloc(&ctx->partials, 2 * kSumBlocks * sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&ctx->ticket, kTicketWords * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(ctx->ticket, 0, kTicketWords * sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        hipMemset(ctx->ticket, 0, kTicketWords * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&ctx->flags, kLookbackMaxTiles * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(ctx->flags, 0, kLookbackMaxTiles * sizeof(uint64_t)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
         if (ctx->partials) (void)hipFree(ctx->partials);
         if (ctx->ticket) (void)hipFree(ctx->ticket);
+        if (ctx->flags) (void)hipFree(ctx->flags);
         delete ctx;
         return fail(CUBIT_ERR_OOM, "context workspace allocation failed");
     }
@@ -296,6 +314,7 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (ctx->tmp_ids) (void)hipFree(ctx->tmp_ids);
     if (ctx->partials) (void)hipFree(ctx->partials);
     if (ctx->ticket) (void)hipFree(ctx->ticket);
+    if (ctx->flags) (void)hipFree(ctx->flags);
     if (ctx->live_pending) (void)hipEventSynchronize(ctx->live_ev);
     if (ctx->live_dev) (void)hipFree(ctx->live_dev);
     if (ctx->live_host) (void)hipHostFree(ctx->live_host);
@@ -325,7 +344,7 @@ int cubit_ctx_set_stream(cubit_ctx* ctx, void* stream) {
 
 int cubit_ctx_set_decode_kernel(cubit_ctx* ctx, int kernel) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "null context");
-    if (kernel < CUBIT_DECODE_AUTO || kernel > CUBIT_DECODE_RUNS) return fail(CUBIT_ERR_INVALID, "decode kernel %d", kernel);
+    if (kernel < CUBIT_DECODE_AUTO || kernel > CUBIT_DECODE_LOOKBACK) return fail(CUBIT_ERR_INVALID, "decode kernel %d", kernel);
     CUBIT_LOCK(ctx);
     ctx->decode_kernel = kernel;
     return CUBIT_OK;

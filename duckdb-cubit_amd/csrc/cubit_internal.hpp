@@ -70,7 +70,13 @@ struct EvalArgs {
     // tile 0 … num_tiles-1. The planner leaves out the tiles whose zone classes prove the program
     // false on every row (RowGroup::CheckZonemap, row_group.cpp:361-371, over bitvector zones).
     const uint32_t* live;
+    // eval_decode_lookback: context-owned flag words (kLookbackMaxTiles, zeroed once) and the
+    // launch's epoch (> 0, one per launch on the context), which tags every flag it publishes
+    uint64_t* flags;
+    uint64_t epoch;
 };
+// eval_decode_lookback: one workgroup per tile, at most this many tiles per launch
+constexpr uint32_t kLookbackMaxTiles = 4096;
 // Zonemaps: one zone = one decode tile (2,048 words = 131,072 rows). Class byte per zone:
 // bit 0 = no row of the zone is set, bit 1 = every row of the zone is set (a zone past the
 // last row has both).
@@ -89,9 +95,13 @@ int decode_block_threads();
 // their elapsed time is the kernel's execution, as rocprofv3's kernel trace reports it
 // kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed;
 // decode_kernel_for resolves it (1 or 2) for a launch
-int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live = false);
+// 3 = look-back (one tile per workgroup, small partitions: lookback_max_tiles)
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live = false,
+                      int n_cus = 256);
+// the largest tile count the measured policy decodes with the look-back kernel (grid = tiles)
+uint32_t lookback_max_tiles(uint32_t n_leaves, int n_cus);
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream,
-                              hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int kernel = 0);
+                              hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int kernel = 0, int n_cus = 256);
 // zone classes of a bitvector (class byte per zone, see kZoneWords) for zones [z0, z0 + nz)
 hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0, uint32_t nz, uint8_t* out,
                                hipStream_t stream);

@@ -1066,6 +1066,159 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
     if (STAMP && t == 0) g_diag_times[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+// ------------------------------------------------------------------ K1+K2 for small partitions
+
+// One tile per workgroup, output offsets by look-back instead of a claim. For partitions whose
+// tiles fit the co-resident grid (WPC workgroups per CU: SF100 split over 8 GPUs = 572 tiles,
+// SURVEY config 2 = 768), where the claim kernels are latency-bound: every workgroup of those
+// takes its one claim at about the same moment, and one word serves ≈ 88 returning atomics per µs
+// (MI355X_MICROARCH.md "dequeue"), so the last claim of 572 returns ≈ 6.5 µs after the first.
+// Here each workgroup
+//   loads and evaluates its tile → block scan → publishes the tile's count in its own flag word
+//   (agent-scope store; the word carries the launch's epoch in its high bits, so flags are never
+//   reset) → decodes its rows into LDS (the flags of its predecessors land meanwhile) → sums the
+//   counts of every earlier workgroup, each thread polling one or two flags (agent-scope loads,
+//   MI355X_MICROARCH.md hand-off table row 1; the whole window in one round trip once they are
+//   published) → copies its run out at that offset and writes its directory entry. The last
+//   workgroup writes the count: no arrival ticket either. A workgroup waits only on lower block
+//   indices, which are dispatched before it, so the walk completes whatever the residency.
+// A tile with more rows than the stage leaves through it in rounds after the offset is known.
+// A poll that exceeds kLookbackSpins marks the count ~0 (the host reports CUBIT_ERR_DEVICE).
+constexpr int kFlagCntBits = 20;  // a tile holds ≤ 131,072 rows
+constexpr uint32_t kLookbackSpins = 1u << 22;
+template <int K, int FORM, int STAGE, int WPC, int SAUX = 16>
+__global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a, uint64_t* __restrict__ dir) {
+    constexpr int THREADS = 512, PAIRS = 2, NW = 2 * PAIRS, NWAVES = THREADS / 64;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr uint64_t kCntMask = (1ull << kFlagCntBits) - 1;
+    __shared__ uint32_t s_wave_tot[NWAVES];
+    __shared__ uint64_t s_pre[NWAVES];
+    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_stage[STAGE];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tile = tile_at(a, b);
+    const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+    const bool write_ids = a.rowids != nullptr;
+    if (t == 0) s_bad = 0;
+    u64x2 v[K][PAIRS];
+    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+    uint64_t r[NW];
+    eval_words<K, NW, FORM>(a.prog, v, r);
+    tail_mask<NW, THREADS>(a, tile_word0, t, r);
+    if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p)
+        packed |= (uint32_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (16 * p);
+    const uint32_t incl = wave_incl_scan32(packed);
+    if (lane == 63) s_wave_tot[wave] = incl;
+    __syncthreads();
+    uint32_t wave_pre[2] = {0, 0}, block_tot[2] = {0, 0};
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) {
+        const uint32_t x = s_wave_tot[w];
+        const uint32_t lo = x & 0xffffu, hi = x >> 16;
+        if (w < wave) {
+            wave_pre[0] += lo;
+            wave_pre[1] += hi;
+        }
+        block_tot[0] += lo;
+        block_tot[1] += hi;
+    }
+    const uint32_t excl = incl - packed;
+    uint32_t pair_off[PAIRS];
+    uint32_t tile_count = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p) {
+        pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
+        tile_count += block_tot[p];
+    }
+    if (t == 0)
+        __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBits) | (uint64_t)tile_count, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const bool staged = tile_count <= (uint32_t)STAGE;
+    if (staged && write_ids && tile_count) {
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            uint32_t off = pair_off[p];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                uint64_t w = r[2 * p + e];
+                const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                while (w) {
+                    s_stage[off++] = wrow + (uint32_t)__builtin_ctzll(w);
+                    w &= w - 1;
+                }
+            }
+        }
+    }
+    // look-back over every earlier workgroup's flag
+    uint64_t pre = 0;
+    for (uint32_t j = t; j < b; j += THREADS) {
+        uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while ((f >> kFlagCntBits) != a.epoch) {
+            if (++spins == kLookbackSpins) {
+                s_bad = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        pre += f & kCntMask;
+    }
+    pre = wave_sum(pre);
+    if (lane == 0) s_pre[wave] = pre;
+    __syncthreads();  // also: the stage is complete
+    uint64_t base = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) base += s_pre[w];
+    if (s_bad) {
+        if (t == 0) *a.count = ~0ull;
+        return;
+    }
+    const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
+    if (t == 0) {
+        if (dir) {
+            dir[2 * tile] = tile_count ? base : 0;
+            dir[2 * tile + 1] = tile_count;
+        }
+        if (b == gridDim.x - 1) *a.count = base + tile_count;
+    }
+    if (!write_ids || !tile_count) return;
+    if (staged) {
+        emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, tile_count, base, row0, t);
+        return;
+    }
+    // dense tile: rounds of STAGE ids through the stage
+    for (uint32_t r0 = 0; r0 < tile_count; r0 += (uint32_t)STAGE) {
+        const uint32_t r1 = min(tile_count, r0 + (uint32_t)STAGE);
+        if (r0) __syncthreads();  // the previous round's copy-out is done
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            uint32_t off = pair_off[p];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                uint64_t w = r[2 * p + e];
+                const uint32_t c = (uint32_t)__popcll(w);
+                const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                if (off < r1 && off + c > r0) {
+                    uint32_t k = off;
+                    for (; k < r0; ++k) w &= w - 1;  // the word straddles the round's start
+                    for (; w && k < r1; ++k) {
+                        s_stage[k - r0] = wrow + (uint32_t)__builtin_ctzll(w);
+                        w &= w - 1;
+                    }
+                }
+                off += c;
+            }
+        }
+        __syncthreads();
+        emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, r1 - r0, base + r0, row0, t);
+    }
+}
+
 // ------------------------------------------------------------------ K1+K3: fused filter + probe-sum
 
 __device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, __int128 x) {
@@ -2363,8 +2516,17 @@ uint32_t eval_form(const EvalProgram& p) {
 // µs; K = 5 at 1.9 %: 82 vs 84 µs) — except K = 4, where at Q6's density a run holds two tiles
 // and the pair kernel measured as fast or 1 % faster (73.2 vs 74.2 µs); the pair kernel for one
 // or two tiles per workgroup (small inputs: one claim per workgroup either way).
-int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live) {
-    (void)n_leaves;
+// look-back kernel geometry: workgroups per CU (the grid is co-resident up to WPC·CUs tiles) and
+// stage entries (32 KiB of LDS per workgroup)
+constexpr int lookback_wpc(uint32_t) { return 3; }  // 80 VGPRs: no spill for K ≤ 8 (4 per CU: 64, spills)
+constexpr int kLookbackStage = 8192;
+uint32_t lookback_max_tiles(uint32_t n_leaves, int n_cus) {
+    return std::min<uint32_t>(kLookbackMaxTiles, (uint32_t)lookback_wpc(n_leaves) * (uint32_t)n_cus);
+}
+
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live, int n_cus) {
+    if (kernel == 3 && num_tiles <= kLookbackMaxTiles) return 3;
+    if (kernel == 0 && num_tiles <= lookback_max_tiles(n_leaves, n_cus)) return 3;
     // a live-tile list (zonemap skip) needs the run kernel: its stage offsets are taken from the
     // run's first tile, while the pair kernel places tile B G tiles after tile A
     if (live) return 2;
@@ -2374,8 +2536,12 @@ int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int 
 
 template <int K, int FORM>
 void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
-                      int kernel) {
-    if (decode_kernel_for(K, a.num_tiles, grid, kernel, a.live != nullptr) == 2)
+                      int kernel, int n_cus) {
+    const int which = decode_kernel_for(K, a.num_tiles, grid, kernel, a.live != nullptr, n_cus);
+    if (which == 3)
+        hipExtLaunchKernelGGL((eval_decode_lookback<K, FORM, kLookbackStage, lookback_wpc(K)>), dim3(a.num_tiles),
+                              dim3(512), 0, s, e0, e1, 0, a, dir);
+    else if (which == 2)
         hipExtLaunchKernelGGL((eval_decode_runs<K, kDecodePairs, kRunCap, kDecodeThreads, FORM>), dim3(grid),
                               dim3(kDecodeThreads), 0, s, e0, e1, 0, a, dir);
     else
@@ -2385,12 +2551,12 @@ void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream
 
 template <int K>
 hipError_t launch_decode_k(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
-                           hipEvent_t e1, int kernel) {
+                           hipEvent_t e1, int kernel, int n_cus) {
     switch (eval_form(a.prog)) {
-    case FORM_CONJ: launch_decode_kf<K, FORM_CONJ>(a, dir, grid, s, e0, e1, kernel); break;
-    case FORM_DNF: launch_decode_kf<K, FORM_DNF>(a, dir, grid, s, e0, e1, kernel); break;
-    case FORM_CNF: launch_decode_kf<K, FORM_CNF>(a, dir, grid, s, e0, e1, kernel); break;
-    default: launch_decode_kf<K, FORM_POSTFIX>(a, dir, grid, s, e0, e1, kernel); break;
+    case FORM_CONJ: launch_decode_kf<K, FORM_CONJ>(a, dir, grid, s, e0, e1, kernel, n_cus); break;
+    case FORM_DNF: launch_decode_kf<K, FORM_DNF>(a, dir, grid, s, e0, e1, kernel, n_cus); break;
+    case FORM_CNF: launch_decode_kf<K, FORM_CNF>(a, dir, grid, s, e0, e1, kernel, n_cus); break;
+    default: launch_decode_kf<K, FORM_POSTFIX>(a, dir, grid, s, e0, e1, kernel, n_cus); break;
     }
     return hipGetLastError();
 }
@@ -2416,16 +2582,19 @@ hipError_t launch_count_k(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEv
 }
 
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1, int kernel) {
+                              hipEvent_t e1, int kernel, int n_cus) {
+    if (decode_kernel_for(a.prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, n_cus) == 3 &&
+        (a.flags == nullptr || a.epoch == 0 || a.num_tiles == 0))
+        return hipErrorInvalidValue;  // the look-back kernel needs the context's flags and an epoch
     switch (a.prog.n_leaves) {
-    case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1, kernel);
-    case 2: return launch_decode_k<2>(a, dir, grid, s, e0, e1, kernel);
-    case 3: return launch_decode_k<3>(a, dir, grid, s, e0, e1, kernel);
-    case 4: return launch_decode_k<4>(a, dir, grid, s, e0, e1, kernel);
-    case 5: return launch_decode_k<5>(a, dir, grid, s, e0, e1, kernel);
-    case 6: return launch_decode_k<6>(a, dir, grid, s, e0, e1, kernel);
-    case 7: return launch_decode_k<7>(a, dir, grid, s, e0, e1, kernel);
-    case 8: return launch_decode_k<8>(a, dir, grid, s, e0, e1, kernel);
+    case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 2: return launch_decode_k<2>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 3: return launch_decode_k<3>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 4: return launch_decode_k<4>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 5: return launch_decode_k<5>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 6: return launch_decode_k<6>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 7: return launch_decode_k<7>(a, dir, grid, s, e0, e1, kernel, n_cus);
+    case 8: return launch_decode_k<8>(a, dir, grid, s, e0, e1, kernel, n_cus);
     default: return hipErrorInvalidValue;
     }
 }

@@ -30,7 +30,7 @@ SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2
 SCAN_CHECK_CAPACITY = 4  # synchronise; ERR_CAPACITY when the count exceeds the buffer
 SCAN_NO_ZONEMAP = 8  # evaluate every zone (the zonemap skip off; results are identical)
-DECODE_AUTO, DECODE_PAIRS, DECODE_RUNS = 0, 1, 2
+DECODE_AUTO, DECODE_PAIRS, DECODE_RUNS, DECODE_LOOKBACK = 0, 1, 2, 3
 
 
 class FilterNode(C.Structure):

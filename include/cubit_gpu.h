@@ -121,13 +121,18 @@ int cubit_ctx_destroy(cubit_ctx *ctx);
 int cubit_ctx_set_stream(cubit_ctx *ctx, void *stream);
 const char *cubit_last_error(void);
 /* Which evaluate + decode kernel the context's scans launch: AUTO (the measured policy: the
- * run-claimed kernel when a workgroup walks three or more tiles and K != 4, else the
- * pair-claimed one), or one of them always (tests and benchmarks). Results are identical. */
+ * look-back kernel — one workgroup per 131,072-row tile, output offsets by look-back over the
+ * earlier tiles' counts — when the partition's tiles fit the co-resident grid; else the
+ * run-claimed kernel when a workgroup walks three or more tiles, else the pair-claimed one),
+ * or one of them always (tests and benchmarks; LOOKBACK up to 4,096 tiles). Results are
+ * identical. */
 #define CUBIT_DECODE_AUTO 0
 #define CUBIT_DECODE_PAIRS 1
 #define CUBIT_DECODE_RUNS 2
+#define CUBIT_DECODE_LOOKBACK 3
 int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
-/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS or CUBIT_DECODE_RUNS). */
+/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS or _LOOKBACK; 0 when
+ * the partition had no row and nothing was launched). */
 int cubit_ctx_last_decode_kernel(cubit_ctx *ctx, int *kernel);
 /* Filter-kernel durations measured with HIP events recorded around each launch on the
  * context stream (ms); requires cubit_ctx_enable_timing(ctx, 1). */

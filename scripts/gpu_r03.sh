@@ -1,0 +1,26 @@
+# Round-3 GPU check on one box: parity suite, smallbench (small-partition decode), headline
+# bench at N = 1 (strong-scaling default). Each GPU step under its own limit; stops at the
+# first failure. STEPS selects the steps to run (default all): tests,small,bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+STEPS="${STEPS:-tests,small,bench}"
+rc=0
+if [[ ",$STEPS," == *",tests,"* ]]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  tail -4 gpurun_out/pytest_gpu.log
+  [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" gpurun_out/pytest_gpu.log | head -30; exit $rc; }
+fi
+if [[ ",$STEPS," == *",small,"* ]]; then
+  timeout -k 10 300 ./scripts/smallbench ${SMALL_REPS:-50} > gpurun_out/smallbench.log 2>&1; rc=$?
+  cat gpurun_out/smallbench.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [[ ",$STEPS," == *",bench,"* ]]; then
+  timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 5 $BENCH_ARGS > gpurun_out/bench.log 2>&1; rc=$?
+  tail -c 3000 gpurun_out/bench.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+exit 0

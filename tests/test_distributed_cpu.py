@@ -43,13 +43,35 @@ def _worker(rank, world, port, sf, result_path):
         cols = [O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity)]
         local = O.table_scan(cols, F.serialize(F.q6_filter_set()), li.n_rows, li.row_base)
         out = P.gather_rowids(torch.from_numpy(local), dst=0)
+        # the bench's form: fixed-size slots posted without reading any count on the host,
+        # the counts gathered beside them and read once at the end; a buffer larger than its
+        # count (as the scan's capacity-sized row-id buffer) and a few repeated posts
+        q = torch.tensor([len(local)], dtype=torch.int64)
+        qmax = q.clone()
+        dist.all_reduce(qmax, op=dist.ReduceOp.MAX)
+        buf = torch.full((int(qmax.item()) + 100,), -1, dtype=torch.int64)
+        buf[: len(local)] = torch.from_numpy(local)
+        ex = P.RowIdExchange(int(qmax.item()) + 7)
+        for _ in range(3):
+            ex.post(buf, torch.tensor([len(local), 0], dtype=torch.int64))
+        slots = ex.result()
+        # a slot below some rank's count is refused on every rank
+        small = P.RowIdExchange(1)
+        small.post(buf, q)
+        refused = False
+        try:
+            small.runs()
+        except RuntimeError:
+            refused = True
         if rank == 0:
             np.save(result_path, out.numpy())
+            np.save(str(result_path) + ".slots.npy", slots.numpy())
+            np.save(str(result_path) + ".refused.npy", np.array([refused]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_partitioned_q6_gathers_to_whole_table_result(tmp_path, world, li01):
     from cubit_amd import filters as F
     from oracle import oracle as O
@@ -60,6 +82,8 @@ def test_partitioned_q6_gathers_to_whole_table_result(tmp_path, world, li01):
     ref = O.table_scan([O.Column(li01.l_shipdate), O.Column(li01.l_discount), O.Column(li01.l_quantity)],
                        F.serialize(F.q6_filter_set()), li01.n_rows)
     assert np.array_equal(got, ref)
+    assert np.array_equal(np.load(str(res) + ".slots.npy"), ref)
+    assert bool(np.load(str(res) + ".refused.npy")[0])
 
 
 def test_partition_range_alignment_and_cover():

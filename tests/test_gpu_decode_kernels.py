@@ -1,6 +1,9 @@
-"""The two evaluate + decode kernels — pair-claimed (eval_decode_pairs) and run-claimed
-(eval_decode_runs) — against the oracle's CPU bitmap evaluator, forced one at a time through
-cubit_ctx_set_decode_kernel and under the automatic policy.
+"""The three evaluate + decode kernels — pair-claimed (eval_decode_pairs), run-claimed
+(eval_decode_runs) and look-back (eval_decode_lookback: one tile per workgroup, offsets from
+the earlier tiles' published counts) — against the oracle's CPU bitmap evaluator, forced one at
+a time through cubit_ctx_set_decode_kernel and under the automatic policy. At 140 M rows the
+look-back grid (1,069 workgroups) exceeds what is co-resident, so its waits span workgroups
+that start only after others finish.
 
 The run-claimed kernel keeps decoding a workgroup's tiles into one LDS stage until the next
 tile does not fit, so its interesting cases need workgroups that walk many tiles: tables of
@@ -77,7 +80,7 @@ def run_program(ctx, dleaves, k, neg, prog, n, base, out, cnt, ordered):
     return got
 
 
-@pytest.mark.parametrize("n", [1_000_003, 140_000_001])
+@pytest.mark.parametrize("n", [1_000_003, 100_000_000, 140_000_001])
 def test_pairs_and_runs_match_oracle(ctx, n):
     rng = np.random.default_rng(n % 1000)
     pw = padded_words(n)
@@ -109,7 +112,7 @@ def test_pairs_and_runs_match_oracle(ctx, n):
                     ol[j][-1] &= np.uint64((1 << (n & 63)) - 1)
         ref, _ = O.bitmap_eval(ol, prog, n, 1_000_000_007)
         assert len(ref) <= out.nbytes // 8
-        for kernel in (L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_AUTO):
+        for kernel in (L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_LOOKBACK, L.DECODE_AUTO):
             ctx.set_decode_kernel(kernel)
             for ordered in (False, True):
                 got = run_program(ctx, dleaves, k, neg, prog, n, 1_000_000_007, out, cnt, ordered)

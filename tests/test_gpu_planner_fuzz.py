@@ -18,7 +18,7 @@ TXN_START = 4611686018427388000
 CMPS = ["=", "!=", "<", "<=", ">", ">="]
 
 
-@pytest.fixture(scope="module", params=[L.DECODE_AUTO, L.DECODE_RUNS], ids=["auto", "runs"])
+@pytest.fixture(scope="module", params=[L.DECODE_AUTO, L.DECODE_RUNS, L.DECODE_PAIRS], ids=["auto", "runs", "pairs"])
 def ctx(request):
     """Both decode kernels: at these sizes the automatic policy picks the pair-claimed one, so
     the run-claimed kernel (production above 2 tiles per workgroup) is forced once."""
