@@ -149,6 +149,7 @@ SCAN_SIGNATURES = {
     "cubit_scan_cardinality": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
     "cubit_scan_statistics": (C.c_int, [_P, _U64, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(C.c_int),
                                         C.POINTER(C.c_int)]),
+    "cubit_scan_release_cached": (C.c_int, [C.POINTER(_U64), C.POINTER(_U64)]),
     "cubit_scan_local_destroy": (C.c_int, [_P]),
     "cubit_scan_destroy": (C.c_int, [_P]),
 }

@@ -3,6 +3,7 @@
 #include "cubit_scan_function.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -26,106 +27,164 @@ void check(int rc, const char* what) {
     if (rc != CUBIT_OK) throw ScanError(rc, std::string(what) + ": " + cubit_last_error());
 }
 
-// Page-locked buffers outlive one scan: pinning ~100 MB costs milliseconds, more than its
-// copy, and DuckDB runs init_global once per query. Freed buffers wait here (≤ 4 GiB) and a
-// request takes the smallest one that fits without wasting more than half of it. Never
-// destroyed (the process exit releases the pages; a static destructor could run after the
-// HIP runtime's).
-class PinnedPool {
+// Buffers outlive one scan: pinning or allocating ~100 MB costs milliseconds, more than the
+// work, and DuckDB runs init_global once per query. Freed buffers wait here and a request takes
+// the smallest one that fits without wasting more than half of it. The cap bounds what an idle
+// process keeps (CUBIT_SCAN_CACHE_MB, default 256 MiB of page-locked and 4 GiB of device
+// memory); cubit_scan_release_cached() frees everything cached. Never destroyed (the process
+// exit releases the pages; a static destructor could run after the HIP runtime's).
+class BufferPool {
   public:
-    static PinnedPool& get() {
-        static PinnedPool* pool = new PinnedPool();
-        return *pool;
-    }
+    BufferPool(bool pinned, size_t cap) : pinned_(pinned), cap_(cap) {}
     void* take(cubit_ctx* ctx, size_t bytes, size_t* got) {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            auto it = free_.lower_bound(bytes);
-            if (it != free_.end() && it->first <= 2 * bytes) {
+            auto it = free_.lower_bound(Key{ctx, bytes});
+            if (it != free_.end() && it->first.ctx == ctx && it->first.bytes <= 2 * bytes) {
                 void* p = it->second;
-                *got = it->first;
-                cached_ -= it->first;
+                *got = it->first.bytes;
+                cached_ -= it->first.bytes;
                 free_.erase(it);
                 return p;
             }
         }
         void* h = nullptr;
-        check(cubit_host_alloc(ctx, bytes, &h), "cubit_host_alloc");
+        if (pinned_) check(cubit_host_alloc(ctx, bytes, &h), "cubit_host_alloc");
+        else check(cubit_dev_alloc(ctx, bytes, &h), "cubit_dev_alloc");
         *got = bytes;
         return h;
     }
-    void give(void* p, size_t bytes) {
+    void give(cubit_ctx* ctx, void* p, size_t bytes) {
         std::lock_guard<std::mutex> lk(mu_);
-        free_.emplace(bytes, p);
+        free_.emplace(Key{pinned_ ? nullptr : ctx, bytes}, p);
         cached_ += bytes;
-        while (cached_ > kMaxCached && !free_.empty()) {  // drop the largest first
+        while (cached_ > cap_ && !free_.empty()) {  // drop the largest first
             auto it = std::prev(free_.end());
-            cached_ -= it->first;
-            cubit_host_free(nullptr, it->second);
-            free_.erase(it);
+            drop(it);
         }
+    }
+    void release_all() {
+        std::lock_guard<std::mutex> lk(mu_);
+        while (!free_.empty()) drop(free_.begin());
+    }
+    // device buffers of a context that is going away
+    void release_ctx(cubit_ctx* ctx) {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto it = free_.begin(); it != free_.end();) {
+            auto nx = std::next(it);
+            if (it->first.ctx == ctx) drop(it);
+            it = nx;
+        }
+    }
+    size_t cached() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return cached_;
     }
 
   private:
-    static constexpr size_t kMaxCached = 4ull << 30;
+    struct Key {
+        cubit_ctx* ctx;  // owning context of device memory (pinned memory: nullptr, any context)
+        size_t bytes;
+        bool operator<(const Key& o) const { return ctx != o.ctx ? ctx < o.ctx : bytes < o.bytes; }
+    };
+    void drop(std::multimap<Key, void*>::iterator it) {
+        cached_ -= it->first.bytes;
+        if (pinned_) cubit_host_free(nullptr, it->second);
+        else cubit_dev_free(it->first.ctx, it->second);
+        free_.erase(it);
+    }
+    const bool pinned_;
+    const size_t cap_;
     std::mutex mu_;
-    std::multimap<size_t, void*> free_;
+    std::multimap<Key, void*> free_;
     size_t cached_ = 0;
 };
 
-// Page-locked host staging (cubit_host_alloc via PinnedPool): device → host copies run at the
-// link's rate instead of through a pageable bounce buffer.
-struct PinnedBuffer {
-    int64_t* p = nullptr;
+size_t cache_cap_mb(size_t dflt) {
+    const char* e = std::getenv("CUBIT_SCAN_CACHE_MB");
+    return (e && *e ? std::strtoull(e, nullptr, 10) : dflt) << 20;
+}
+BufferPool& pinned_pool() {
+    static BufferPool* p = new BufferPool(true, cache_cap_mb(256));
+    return *p;
+}
+BufferPool& device_pool() {
+    static BufferPool* p = new BufferPool(false, cache_cap_mb(256) * 16);
+    return *p;
+}
+
+// A buffer from one of the pools, returned on destruction.
+struct PooledBuffer {
+    BufferPool* pool = nullptr;
+    cubit_ctx* ctx = nullptr;
+    void* p = nullptr;
     size_t bytes = 0;
-    PinnedBuffer() = default;
-    PinnedBuffer(const PinnedBuffer&) = delete;
-    PinnedBuffer& operator=(const PinnedBuffer&) = delete;
-    PinnedBuffer(PinnedBuffer&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; }
-    void allocate(cubit_ctx* c, idx_t count);
-    int64_t* data() { return p; }
-    const int64_t* data() const { return p; }
-    ~PinnedBuffer() {
-        if (p) PinnedPool::get().give(p, bytes);
+    PooledBuffer() = default;
+    PooledBuffer(const PooledBuffer&) = delete;
+    PooledBuffer& operator=(const PooledBuffer&) = delete;
+    PooledBuffer(PooledBuffer&& o) noexcept : pool(o.pool), ctx(o.ctx), p(o.p), bytes(o.bytes) { o.p = nullptr; }
+    void allocate(BufferPool& pl, cubit_ctx* c, size_t want) {
+        reset();
+        pool = &pl;
+        ctx = c;
+        p = pl.take(c, std::max<size_t>(want, 16), &bytes);
     }
+    void reset() {
+        if (p) pool->give(ctx, p, bytes);
+        p = nullptr;
+    }
+    int64_t* i64() { return static_cast<int64_t*>(p); }
+    ~PooledBuffer() { reset(); }
 };
 
-// Device result of one scan, copied to host once (the GPU work is one fused launch plus one
-// gather per emitted column; DataChunks are then served from host memory).
+// Streaming result of one scan. init_global runs the GPU work — one decode (ordered: the runs
+// laid out in tile order, so consecutive tiles are one contiguous range of ids) and the probe
+// of every emitted column, all on the device — and copies only the count and the tile
+// directory to the host. The ids and values then reach the host per *window* (consecutive
+// non-empty tiles of about kWindowRows rows): the local state that claims a window copies its
+// range of every emitted column into its own page-locked buffer and hands the window's tiles
+// out as DataChunks. The reference hands out one row group per NextParallelScan and produces
+// its chunks on demand (table_scan.cpp:119-156); a window is the unit a GPU→host copy is worth.
+constexpr idx_t kWindowRows = 1u << 18;
+constexpr idx_t kWindowTiles = 64;
+
+struct Window {
+    uint32_t first, last;  // index range [first, last) into the non-empty tiles
+    idx_t off, len;        // the window's rows in the ordered output
+};
+
 struct CubitScanGlobalState : public GlobalTableFunctionState {
+    cubit_ctx* ctx = nullptr;
     std::vector<column_t> column_ids;
     std::vector<idx_t> emit;  // positions of column_ids that reach the output
     idx_t count = 0;
     idx_t rows_per_tile = 0;
-    PinnedBuffer rowids;                // tile-run order
-    std::vector<PinnedBuffer> columns;  // per emitted position (row ids or probed values)
-    std::vector<uint32_t> tiles;                // non-empty tiles, ascending
-    std::vector<uint64_t> dir;                  // {start, length} per tile
+    PooledBuffer d_ids;                  // device: ordered row ids
+    std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
+    std::vector<uint32_t> tiles;         // non-empty tiles, ascending
+    std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
+    std::vector<Window> windows;
+    idx_t max_window = 0;
     std::atomic<uint32_t> next{0};
     std::atomic<idx_t> emitted{0};
     idx_t MaxThreads() const override {
         const idx_t hw = std::max<unsigned>(1, std::thread::hardware_concurrency());
-        return std::max<idx_t>(1, std::min<idx_t>(tiles.size(), hw));
+        return std::max<idx_t>(1, std::min<idx_t>(windows.size(), hw));
+    }
+    ~CubitScanGlobalState() override {
+        // probes launched by init_global may still read the buffers returned to the pool
+        if (ctx) cubit_sync(ctx);
     }
 };
 
 struct CubitScanLocalState : public LocalTableFunctionState {
-    int64_t tile_slot = -1;  // index into tiles, -1 = none yet
-    idx_t pos = 0;           // next row of the tile's run to emit
+    int64_t window = -1;           // claimed window, -1 = none yet
+    uint32_t tile_slot = 0;        // current tile (index into tiles)
+    idx_t pos = 0;                 // next row of the tile's run to emit
+    std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
 };
 
-struct DeviceBuffer {
-    cubit_ctx* ctx;
-    void* p = nullptr;
-    DeviceBuffer(cubit_ctx* c, uint64_t bytes) : ctx(c) { check(cubit_dev_alloc(c, bytes, &p), "cubit_dev_alloc"); }
-    ~DeviceBuffer() {
-        if (p) cubit_dev_free(ctx, p);
-    }
-};
-
-void PinnedBuffer::allocate(cubit_ctx* c, idx_t count) {
-    p = static_cast<int64_t*>(PinnedPool::get().take(c, std::max<idx_t>(count, 1) * sizeof(int64_t), &bytes));
-}
+int64_t* device_ptr(PooledBuffer& b) { return b.i64(); }
 
 std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
     auto& bind = static_cast<const CubitScanBindData&>(*input.bind_data);
@@ -137,58 +196,71 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         for (idx_t i = 0; i < input.column_ids.size(); ++i) g->emit.push_back(i);
     }
     cubit_ctx* ctx = bind.ctx;
-    DeviceBuffer d_cnt(ctx, 16);
+    g->ctx = ctx;
+    PooledBuffer d_cnt;
+    d_cnt.allocate(device_pool(), ctx, 16);
     const cubit_txn* txn = bind.has_txn ? &bind.txn : nullptr;
     const auto& nodes = input.filters ? input.filters->nodes : std::vector<cubit_filter_node>{};
-    // count first (one evaluate pass, no row ids), so the row-id and probe buffers are sized to
-    // the result rather than to the table (4.8 GB per query at SF100 otherwise)
-    check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn, nullptr,
-                           0, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_COUNT_ONLY),
-          "cubit_table_scan (count)");
-    uint64_t want = 0;
-    check(cubit_memcpy_d2h(ctx, &want, d_cnt.p, 8), "count");
-    const uint64_t cap = std::max<uint64_t>(want, 1);
-    DeviceBuffer d_ids(ctx, cap * 8);
-    check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
-                           static_cast<int64_t*>(d_ids.p), cap, static_cast<uint64_t*>(d_cnt.p), 0),
-          "cubit_table_scan");
-    check(cubit_ctx_check(ctx), "scan kernel");
-    check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
+    // one decode into a buffer sized by a guess (an eighth of the rows); only a filter that
+    // keeps more rows than that runs a second time, with the exact count
+    uint64_t cap = std::max<uint64_t>(bind.n_rows / 8 + 4096, 1);
+    for (int pass = 0; pass < 2; ++pass) {
+        g->d_ids.allocate(device_pool(), ctx, cap * 8);
+        cap = g->d_ids.bytes / 8;
+        check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
+                               device_ptr(g->d_ids), cap, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_ORDERED),
+              "cubit_table_scan");
+        check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
+        if (g->count == ~0ull) throw ScanError(CUBIT_ERR_DEVICE, "cubit_table_scan: device failure");
+        if (g->count <= cap) break;
+        if (pass == 1) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
+        cap = g->count;
+    }
     const uint64_t* d_dir = nullptr;
     uint32_t n_tiles = 0;
     check(cubit_ctx_last_tiles(ctx, &d_dir, &n_tiles, &g->rows_per_tile), "tiles");
-    if (g->count > cap) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
     if (g->count == 0) n_tiles = 0;  // nothing qualified: no run to hand out, whatever the directory holds
-    g->dir.resize(2 * (size_t)n_tiles);
-    if (n_tiles) check(cubit_memcpy_d2h(ctx, g->dir.data(), d_dir, g->dir.size() * 8), "directory");
-    g->rowids.allocate(ctx, g->count);
-    if (g->count) check(cubit_memcpy_d2h(ctx, g->rowids.data(), d_ids.p, g->count * 8), "row ids");
-    uint64_t covered = 0;
+    std::vector<uint64_t> dir(2 * (size_t)n_tiles);
+    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), d_dir, dir.size() * 8), "directory");
+    // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
+    idx_t off = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {
-        const uint64_t start = g->dir[2 * t], len = g->dir[2 * t + 1];
+        const uint64_t len = dir[2 * t + 1];
         if (!len) continue;
-        // every run lies inside this scan's output (a directory of another launch would not)
-        if (start > g->count || len > g->count - start)
+        if (len > g->count - off)
             throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile directory does not describe this scan's output");
-        covered += len;
         g->tiles.push_back(t);
+        g->tile_off.push_back(off);
+        g->tile_len.push_back(len);
+        off += len;
     }
-    if (covered != g->count)
-        throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(covered) + " of " +
+    if (off != g->count)
+        throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(off) + " of " +
                                                std::to_string(g->count) + " row ids");
-    // probe every emitted storage column at the row ids (ColumnData::FilterScan semantics)
-    g->columns.resize(g->emit.size());
-    std::unique_ptr<DeviceBuffer> d_vals;
+    for (uint32_t i = 0; i < g->tiles.size();) {
+        Window w{i, i, g->tile_off[i], 0};
+        while (w.last < g->tiles.size() && (w.last == w.first || (w.len + g->tile_len[w.last] <= kWindowRows &&
+                                                                   w.last - w.first < kWindowTiles))) {
+            w.len += g->tile_len[w.last];
+            ++w.last;
+        }
+        g->max_window = std::max(g->max_window, w.len);
+        g->windows.push_back(w);
+        i = w.last;
+    }
+    // probe every emitted storage column at the ordered row ids (ColumnData::FilterScan
+    // semantics), on the device; the copies of the first window wait for them in stream order
+    g->d_cols.resize(g->emit.size());
     for (size_t e = 0; e < g->emit.size(); ++e) {
         const column_t col = g->column_ids[g->emit[e]];
         if (col == COLUMN_IDENTIFIER_ROW_ID || g->count == 0) continue;
-        if (!d_vals) d_vals = std::make_unique<DeviceBuffer>(ctx, g->count * 8);
-        check(cubit_table_probe(bind.table, (int)col, txn, static_cast<int64_t*>(d_ids.p),
-                                static_cast<uint64_t*>(d_cnt.p), g->count, static_cast<int64_t*>(d_vals->p)),
+        g->d_cols[e].allocate(device_pool(), ctx, g->count * 8);
+        check(cubit_table_probe(bind.table, (int)col, txn, device_ptr(g->d_ids), static_cast<uint64_t*>(d_cnt.p),
+                                g->count, device_ptr(g->d_cols[e])),
               "cubit_table_probe");
-        g->columns[e].allocate(ctx, g->count);
-        check(cubit_memcpy_d2h(ctx, g->columns[e].data(), d_vals->p, g->count * 8), "probe values");
     }
+    // d_cnt goes back to the pool while the probes may still read it: stream order on this
+    // context keeps a later user of the buffer behind them; other contexts never get it
     return g;
 }
 
@@ -196,15 +268,25 @@ std::unique_ptr<LocalTableFunctionState> CubitScanInitLocal(TableFunctionInitInp
     return std::make_unique<CubitScanLocalState>();
 }
 
-// TableScanParallelStateNext analogue: take the next non-empty tile (row_group_collection.cpp
-// hands out row groups under a mutex; one atomic suffices here).
-bool NextTile(CubitScanGlobalState& g, CubitScanLocalState& l) {
-    const uint32_t s = g.next.fetch_add(1);
-    if (s >= g.tiles.size()) {
-        l.tile_slot = (int64_t)g.tiles.size();
+// TableScanParallelStateNext analogue: take the next window (row_group_collection.cpp hands
+// out row groups under a mutex; one atomic suffices here) and copy its rows of every emitted
+// column to this state's page-locked buffers.
+bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
+    const uint32_t w = g.next.fetch_add(1);
+    if (w >= g.windows.size()) {
+        l.window = (int64_t)g.windows.size();
         return false;
     }
-    l.tile_slot = s;
+    const Window& win = g.windows[w];
+    if (l.host.size() != g.emit.size()) l.host.resize(g.emit.size());
+    for (size_t e = 0; e < g.emit.size(); ++e) {
+        if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
+        const column_t col = g.column_ids[g.emit[e]];
+        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
+        check(cubit_memcpy_d2h(g.ctx, l.host[e].p, device_ptr(src) + win.off, win.len * 8), "window copy");
+    }
+    l.window = w;
+    l.tile_slot = win.first;
     l.pos = 0;
     return true;
 }
@@ -214,33 +296,37 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
     auto& l = static_cast<CubitScanLocalState&>(*data.local_state);
     output.Reset();
     for (;;) {
-        if (l.tile_slot < 0 && !NextTile(g, l)) return;
-        if ((size_t)l.tile_slot >= g.tiles.size()) return;
-        const uint32_t tile = g.tiles[l.tile_slot];
-        const uint64_t start = g.dir[2 * tile], len = g.dir[2 * tile + 1];
+        if (l.window < 0 && !NextWindow(g, l)) return;
+        if ((size_t)l.window >= g.windows.size()) return;
+        const Window& win = g.windows[l.window];
+        if (l.tile_slot >= win.last) {
+            if (!NextWindow(g, l)) return;
+            continue;
+        }
+        const idx_t len = g.tile_len[l.tile_slot];
         if (l.pos < len) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
-            for (size_t e = 0; e < g.emit.size(); ++e) {
-                const column_t col = g.column_ids[g.emit[e]];
-                const int64_t* src = col == COLUMN_IDENTIFIER_ROW_ID ? g.rowids.data() : g.columns[e].data();
-                std::memcpy(output.data[e].data(), src + start + l.pos, n * sizeof(int64_t));
-            }
+            const idx_t at = g.tile_off[l.tile_slot] - win.off + l.pos;
+            for (size_t e = 0; e < g.emit.size(); ++e)
+                std::memcpy(output.data[e].data(), l.host[e].i64() + at, n * sizeof(int64_t));
             l.pos += n;
             output.SetCardinality(n);
             g.emitted.fetch_add(n);
             return;
         }
-        if (!NextTile(g, l)) return;
+        ++l.tile_slot;
+        l.pos = 0;
     }
 }
 
+// batch index = tile index: a local state's tiles ascend (windows are claimed in order and
+// hold consecutive tiles), as PipelineExecutor::NextBatch requires (pipeline_executor.cpp:132)
 idx_t CubitScanGetBatchIndex(const FunctionData*, LocalTableFunctionState* lstate, GlobalTableFunctionState* gstate) {
     auto& g = static_cast<CubitScanGlobalState&>(*gstate);
     auto& l = static_cast<CubitScanLocalState&>(*lstate);
-    if (l.tile_slot < 0 || (size_t)l.tile_slot >= g.tiles.size()) return 0;
+    if (l.window < 0 || (size_t)l.window >= g.windows.size() || l.tile_slot >= g.tiles.size()) return 0;
     return g.tiles[l.tile_slot];
 }
-
 double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gstate) {
     auto& g = static_cast<const CubitScanGlobalState&>(*gstate);
     if (g.count == 0) return 100.0;
@@ -429,6 +515,14 @@ int cubit_scan_statistics(cubit_table* table, uint64_t column_id, int64_t* min, 
     } catch (const ScanError& e) {
         return scan_fail(e.code, e.what());
     }
+}
+
+int cubit_scan_release_cached(uint64_t* pinned_bytes, uint64_t* device_bytes) {
+    if (pinned_bytes) *pinned_bytes = pinned_pool().cached();
+    if (device_bytes) *device_bytes = device_pool().cached();
+    pinned_pool().release_all();
+    device_pool().release_all();
+    return CUBIT_OK;
 }
 
 int cubit_scan_local_destroy(cubit_scan_local* l) {

@@ -7,9 +7,17 @@
 // Linking it needs libduckdb, which this repository does not build.
 //
 //   PRAGMA cubit_attach('lineitem', 'l_shipdate,l_discount,l_quantity,l_extendedprice');
-//     copies those columns to the GPU (one partition per call) and builds an exact range
-//     index on each; from then on the optimizer swaps seq_scan for cubit_scan whenever every
-//     pushed filter of the scan is supported and every scanned column is attached.
+//     copies those columns to the GPU (one partition per call), builds an exact range index on
+//     each, and adds a CUBIT index (CubitIndex, a BoundIndex) to the table so DuckDB hands it
+//     every committed append and every index removal from then on;
+//   PRAGMA cubit_sync('lineitem');
+//     brings the partition to the table's committed state (uploads the appends the index
+//     buffered, records committed deletes) and stamps it with the last commit.
+//   The optimizer swaps seq_scan for cubit_scan when every pushed filter of the scan is
+//   supported, every scanned column is attached, and the partition is exactly the state the
+//   scanning transaction sees: no transaction-local rows or deletes on the table (those stay
+//   on seq_scan, which scans them after the persistent rows: DataTable::Scan,
+//   data_table.cpp:277-287), no commit since the stamp, and a snapshot that includes it.
 //
 // Reference interfaces used (src/include/duckdb/…):
 //   OptimizerExtension::optimize_function          optimizer/optimizer_extension.hpp:31-41
@@ -33,6 +41,16 @@
 #include "duckdb/planner/operator/logical_get.hpp"
 #include "duckdb/planner/table_filter.hpp"
 #include "duckdb/transaction/duck_transaction.hpp"
+#include "duckdb/transaction/duck_transaction_manager.hpp"
+#include "duckdb/transaction/local_storage.hpp"
+#include "duckdb/execution/index/bound_index.hpp"
+#include "duckdb/execution/index/index_type.hpp"
+#include "duckdb/execution/index/index_type_set.hpp"
+#include "duckdb/planner/expression/bound_reference_expression.hpp"
+#include "duckdb/storage/data_table.hpp"
+#include "duckdb/storage/table_io_manager.hpp"
+#include "duckdb/storage/table/append_state.hpp"
+#include "duckdb/storage/table_storage_info.hpp"
 
 #include "cubit_gpu.h"
 #include "cubit_scan.h"
@@ -49,6 +67,23 @@ struct CubitAttached {
     cubit_ctx *ctx = nullptr;
     cubit_table *table = nullptr;
     unordered_map<column_t, PhysicalType> columns;
+    vector<column_t> column_order;  // attached storage columns, in the CubitIndex's key order
+    uint64_t gpu_rows = 0;          // rows of the GPU partition (row ids 0 … gpu_rows-1)
+    // the last commit the partition reflects (DuckTransactionManager::GetLastCommit at the
+    // attach / sync that produced it); the swap needs GetLastCommit() == stamp
+    transaction_t stamp = 0;
+    // committed appends handed to the CubitIndex since the last sync: first row id + one
+    // buffer per attached column (int64 values, DuckDB validity), uploaded by cubit_sync
+    struct Pending {
+        row_t first = 0;
+        idx_t count = 0;
+        vector<vector<int64_t>> values;
+        vector<vector<uint64_t>> validity;
+    };
+    vector<Pending> pending;
+    vector<int64_t> deleted;  // row ids removed through the index (cleanup of committed deletes)
+    bool index_added = false; // the table's index list holds this partition's CubitIndex
+    mutex lock;               // the hooks run on DuckDB's commit / cleanup threads
 };
 
 class CubitRegistry {
@@ -142,6 +177,28 @@ static bool Supported(const TableFilter &f) {
         return true;
     default:
         return false;  // STRUCT_EXTRACT and anything newer stay on seq_scan
+    }
+}
+
+// one value of a flat vector of an integer-backed physical type, as int64
+static int64_t PhysicalAsInt64(Vector &v, idx_t i) {
+    switch (v.GetType().InternalType()) {
+    case PhysicalType::BOOL:
+        return FlatVector::GetData<bool>(v)[i] ? 1 : 0;
+    case PhysicalType::UINT8:
+        return FlatVector::GetData<uint8_t>(v)[i];
+    case PhysicalType::UINT16:
+        return FlatVector::GetData<uint16_t>(v)[i];
+    case PhysicalType::UINT32:
+        return FlatVector::GetData<uint32_t>(v)[i];
+    case PhysicalType::INT8:
+        return FlatVector::GetData<int8_t>(v)[i];
+    case PhysicalType::INT16:
+        return FlatVector::GetData<int16_t>(v)[i];
+    case PhysicalType::INT32:
+        return FlatVector::GetData<int32_t>(v)[i];
+    default:
+        return FlatVector::GetData<int64_t>(v)[i];
     }
 }
 
@@ -442,6 +499,26 @@ TableFunction GetCubitScanFunction() {
 
 // ------------------------------------------------------------------ optimizer swap
 
+// The GPU partition holds exactly what the scanning transaction's seq_scan would read:
+//  * no transaction-local storage on the table: DataTable::Scan reads the persistent row groups
+//    and then the transaction's LocalStorage (data_table.cpp:277-287, local_storage.cpp:326-341),
+//    and local deletes hide persistent rows; none of that is on the GPU;
+//  * no commit since the partition's stamp (a DELETE reaches no index hook until cleanup, so
+//    any later commit may have changed rows the partition shows) and every appended row synced;
+//  * the transaction's snapshot includes the stamp (start_time > stamp: an older snapshot
+//    must not see commits the partition already shows).
+static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
+    auto &tx = DuckTransaction::Get(context, table.catalog);
+    auto &storage = table.GetStorage();
+    if (LocalStorage::Get(tx).Find(storage)) {
+        return false;
+    }
+    auto &tm = DuckTransactionManager::Get(table.catalog.GetAttached());
+    lock_guard<mutex> g(attached.lock);
+    return attached.pending.empty() && tm.GetLastCommit() == attached.stamp && tx.start_time > attached.stamp &&
+           storage.GetTotalRows() == attached.gpu_rows;
+}
+
 static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOperator> &plan) {
     for (auto &child : plan->children) {
         CubitOptimize(input, child);
@@ -461,6 +538,9 @@ static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOper
     if (!attached) {
         return;
     }
+    if (!CubitPartitionIsCurrent(input.context, table->Cast<DuckTableEntry>(), *attached)) {
+        return;  // seq_scan reads what the GPU partition does not hold
+    }
     for (auto c : get.column_ids) {
         if (c != COLUMN_IDENTIFIER_ROW_ID && !attached->columns.count(c)) {
             return;  // a scanned column is not on the GPU
@@ -473,6 +553,204 @@ static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOper
     }
     get.function = GetCubitScanFunction();
     get.bind_data = make_uniq<CubitBindData>(table->Cast<DuckTableEntry>(), *attached);
+}
+
+// ------------------------------------------------------------------ index maintenance
+
+// CUBIT's bitmap index as a DuckDB index type ("CUBIT"; DBConfig::GetIndexTypes, registered as
+// IndexTypeSet registers ART, index_type_set.cpp:7-13). cubit_attach adds one instance to the
+// table (DataTable::AddIndex), and from then on DuckDB calls it like any BoundIndex
+// (bound_index.hpp:67-126):
+//   Append  ← DataTable::AppendToIndexes (data_table.cpp:1000-1040), once per committed chunk
+//             (LocalStorage::Flush at commit), and for the insert half of an UPDATE of an
+//             attached column (an UPDATE of an indexed column runs as delete + insert,
+//             table_catalog_entry.cpp:288-308). The chunk's attached columns are buffered; the
+//             next cubit_sync uploads them with cubit_table_append (every bitmap index on the
+//             GPU maintained in place) — until then the swap is refused.
+//   Delete  ← DataTable::RemoveFromIndexes: the revert of a failed append (data_table.cpp:
+//             1032-1037) and the cleanup of committed deletes (cleanup_state.cpp:93); the rows
+//             become deletes of the partition (cubit_table_set_deletes at the next sync).
+//   Insert  ← an index build over existing rows (not used: cubit_attach uploads them itself).
+// Constraint checks pass (CUBIT is not a constraint index), and the index holds no DuckDB-side
+// storage (GetStorageInfo: nothing to persist; the GPU index is rebuilt by cubit_attach).
+class CubitIndex : public BoundIndex {
+public:
+    static constexpr const char *TYPE_NAME = "CUBIT";
+
+    CubitIndex(const string &name, const vector<column_t> &column_ids, TableIOManager &io,
+               const vector<unique_ptr<Expression>> &exprs, AttachedDatabase &db, CubitAttached *attached_p)
+        : BoundIndex(name, TYPE_NAME, IndexConstraintType::NONE, column_ids, io, exprs, db), attached(attached_p) {
+    }
+
+    // IndexType::create_instance: a CUBIT index bound to the table's attached partition
+    static unique_ptr<BoundIndex> Create(CreateIndexInput &input) {
+        return make_uniq<CubitIndex>(input.name, input.column_ids, input.table_io_manager, input.unbound_expressions,
+                                     input.db, nullptr);
+    }
+
+    ErrorData Append(IndexLock &, DataChunk &entries, Vector &row_identifiers) override {
+        if (!attached || entries.size() == 0) {
+            return ErrorData();
+        }
+        DataChunk keys;
+        keys.Initialize(Allocator::DefaultAllocator(), logical_types);
+        ExecuteExpressions(entries, keys);  // the attached columns, in key order
+        keys.Flatten();
+        row_identifiers.Flatten(entries.size());
+        auto rows = FlatVector::GetData<row_t>(row_identifiers);
+        CubitAttached::Pending p;
+        p.first = rows[0];
+        p.count = entries.size();
+        for (idx_t c = 0; c < keys.ColumnCount(); c++) {
+            vector<int64_t> v(p.count, 0);
+            vector<uint64_t> valid((p.count + 63) / 64, 0);
+            auto &vec = keys.data[c];
+            auto &mask = FlatVector::Validity(vec);
+            for (idx_t i = 0; i < p.count; i++) {
+                if (!mask.RowIsValid(i)) {
+                    continue;
+                }
+                valid[i >> 6] |= 1ull << (i & 63);
+                v[i] = PhysicalAsInt64(vec, i);
+            }
+            p.values.push_back(std::move(v));
+            p.validity.push_back(std::move(valid));
+        }
+        lock_guard<mutex> g(attached->lock);
+        attached->pending.push_back(std::move(p));
+        return ErrorData();
+    }
+
+    void Delete(IndexLock &, DataChunk &entries, Vector &row_identifiers) override {
+        if (!attached) {
+            return;
+        }
+        row_identifiers.Flatten(entries.size());
+        auto rows = FlatVector::GetData<row_t>(row_identifiers);
+        lock_guard<mutex> g(attached->lock);
+        for (idx_t i = 0; i < entries.size(); i++) {
+            attached->deleted.push_back(rows[i]);
+        }
+    }
+
+    ErrorData Insert(IndexLock &state, DataChunk &input, Vector &row_identifiers) override {
+        return Append(state, input, row_identifiers);
+    }
+    void VerifyAppend(DataChunk &) override {
+    }
+    void VerifyAppend(DataChunk &, ConflictManager &) override {
+    }
+    void CheckConstraintsForChunk(DataChunk &, ConflictManager &) override {
+    }
+    void CommitDrop(IndexLock &) override {
+        attached = nullptr;
+    }
+    bool MergeIndexes(IndexLock &, BoundIndex &) override {
+        return true;  // local (transaction) indexes are never CUBIT: nothing to merge
+    }
+    void Vacuum(IndexLock &) override {
+    }
+    idx_t GetInMemorySize(IndexLock &) override {
+        return 0;  // the bitvectors live in GPU memory (cubit_table_index_info)
+    }
+    string VerifyAndToString(IndexLock &, const bool) override {
+        return "CUBIT index (GPU partition)";
+    }
+    string GetConstraintViolationMessage(VerifyExistenceType, idx_t, DataChunk &) override {
+        return "CUBIT indexes enforce no constraint";
+    }
+    IndexStorageInfo GetStorageInfo(const bool) override {
+        IndexStorageInfo info(name);
+        return info;
+    }
+
+    CubitAttached *attached;
+};
+
+// Upload what the CubitIndex buffered and record the committed deletes, under a snapshot that
+// no commit overtakes (stamp taken before the row-id scan, checked unchanged after it).
+static void SyncPartition(ClientContext &context, TableCatalogEntry &entry, CubitAttached &attached,
+                          const string &table_name) {
+    auto &tm = DuckTransactionManager::Get(entry.catalog.GetAttached());
+    for (int attempt = 0; attempt < 3; attempt++) {
+        const transaction_t t0 = tm.GetLastCommit();
+        Connection con(*context.db);
+        auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name));
+        if (res->HasError()) {
+            res->ThrowError();
+        }
+        vector<bool> present;
+        while (auto chunk = res->Fetch()) {
+            chunk->Flatten();
+            auto rows = FlatVector::GetData<int64_t>(chunk->data[0]);
+            for (idx_t i = 0; i < chunk->size(); i++) {
+                const uint64_t r = (uint64_t)rows[i];
+                if (r >= present.size()) {
+                    present.resize(r + 1, false);
+                }
+                present[r] = true;
+            }
+        }
+        if (tm.GetLastCommit() != t0) {
+            continue;  // a commit landed during the scan: take a new snapshot
+        }
+        lock_guard<mutex> g(attached.lock);
+        // appends in row order, each continuing the partition
+        std::sort(attached.pending.begin(), attached.pending.end(),
+                  [](const CubitAttached::Pending &a, const CubitAttached::Pending &b) { return a.first < b.first; });
+        for (auto &p : attached.pending) {
+            if ((uint64_t)p.first != attached.gpu_rows) {
+                throw InvalidInputException("cubit_sync: appended rows start at %lld, the partition holds %llu rows; "
+                                            "run cubit_attach again",
+                                            (long long)p.first, (unsigned long long)attached.gpu_rows);
+            }
+            vector<int> cols;
+            vector<const void *> data;
+            vector<const uint64_t *> valid;
+            vector<vector<int32_t>> narrow;
+            narrow.reserve(attached.column_order.size());
+            for (idx_t c = 0; c < attached.column_order.size(); c++) {
+                const column_t col = attached.column_order[c];
+                cols.push_back((int)col);
+                if (WidePhysical(attached.columns[col])) {
+                    data.push_back(p.values[c].data());
+                } else {
+                    narrow.emplace_back(p.values[c].begin(), p.values[c].end());
+                    data.push_back(narrow.back().data());
+                }
+                valid.push_back(p.validity[c].data());
+            }
+            Check(cubit_table_append(attached.table, p.count, cols.data(), data.data(), valid.data(),
+                                     (uint32_t)cols.size(), 0));
+            attached.gpu_rows += p.count;
+        }
+        attached.pending.clear();
+        // committed deletes: rows of the partition the snapshot does not see (and the rows the
+        // index was told to remove), committed before every later snapshot
+        vector<int64_t> gone;
+        for (uint64_t r = 0; r < attached.gpu_rows; r++) {
+            if (r >= present.size() || !present[r]) {
+                gone.push_back((int64_t)r);
+            }
+        }
+        attached.deleted.clear();
+        vector<uint64_t> ids(gone.size(), 0);
+        Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
+        attached.stamp = t0;
+        return;
+    }
+    throw InvalidInputException("cubit_sync: commits kept landing during the sync of %s; retry", table_name);
+}
+
+// PRAGMA cubit_sync(table)
+static void CubitSync(ClientContext &context, const FunctionParameters &parameters) {
+    const auto table_name = parameters.values[0].ToString();
+    auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
+    auto attached = CubitRegistry::Find(entry);
+    if (!attached || !attached->table) {
+        throw InvalidInputException("cubit_sync: %s is not attached", table_name);
+    }
+    SyncPartition(context, entry, *attached, table_name);
 }
 
 // ------------------------------------------------------------------ attach
@@ -501,6 +779,7 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
     if (attached.table) {
         cubit_table_destroy(attached.table);
         attached.columns.clear();
+        attached.column_order.clear();
     }
     Check(cubit_table_create(attached.ctx, n_rows, 0, &attached.table));
     vector<bool> present(n_rows, false);
@@ -532,31 +811,10 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
                     continue;
                 }
                 valid[r >> 6] |= 1ull << (r & 63);
-                switch (phys) {
-                case PhysicalType::BOOL:
-                    v32[r] = FlatVector::GetData<bool>(vals)[i] ? 1 : 0;
-                    break;
-                case PhysicalType::UINT8:
-                    v32[r] = FlatVector::GetData<uint8_t>(vals)[i];
-                    break;
-                case PhysicalType::UINT16:
-                    v32[r] = FlatVector::GetData<uint16_t>(vals)[i];
-                    break;
-                case PhysicalType::UINT32:
-                    v64[r] = FlatVector::GetData<uint32_t>(vals)[i];
-                    break;
-                case PhysicalType::INT8:
-                    v32[r] = FlatVector::GetData<int8_t>(vals)[i];
-                    break;
-                case PhysicalType::INT16:
-                    v32[r] = FlatVector::GetData<int16_t>(vals)[i];
-                    break;
-                case PhysicalType::INT32:
-                    v32[r] = FlatVector::GetData<int32_t>(vals)[i];
-                    break;
-                default:
-                    v64[r] = FlatVector::GetData<int64_t>(vals)[i];
-                    break;
+                if (wide) {
+                    v64[r] = PhysicalAsInt64(vals, i);
+                } else {
+                    v32[r] = (int32_t)PhysicalAsInt64(vals, i);
                 }
             }
         }
@@ -565,17 +823,27 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
                                      wide ? (const void *)v64.data() : (const void *)v32.data(), valid.data(), 0));
         Check(cubit_table_build_index(attached.table, (int)storage, CUBIT_INDEX_RANGE, nullptr, 0));
         attached.columns[storage] = phys;
+        attached.column_order.push_back(storage);
     }
-    vector<int64_t> gone;
-    for (uint64_t r = 0; r < n_rows; r++) {
-        if (!present[r]) {
-            gone.push_back((int64_t)r);
+    attached.gpu_rows = n_rows;
+    attached.pending.clear();
+    attached.deleted.clear();
+    // from here DuckDB reports every committed append and index removal to the CubitIndex; the
+    // deletes and the stamp come from a snapshot no commit overtook (SyncPartition)
+    auto &duck = entry.Cast<DuckTableEntry>();
+    auto &storage = duck.GetStorage();
+    if (!attached.index_added) {
+        vector<unique_ptr<Expression>> exprs;
+        vector<column_t> ids;
+        for (auto c : attached.column_order) {
+            exprs.push_back(make_uniq<BoundReferenceExpression>(duck.GetColumn(LogicalIndex(c)).GetType(), c));
+            ids.push_back(c);
         }
+        storage.AddIndex(make_uniq<CubitIndex>("cubit_" + table_name, ids, TableIOManager::Get(storage), exprs,
+                                               entry.catalog.GetAttached(), &attached));
+        attached.index_added = true;
     }
-    if (!gone.empty()) {
-        vector<uint64_t> ids(gone.size(), 0);  // committed before every later transaction
-        Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
-    }
+    SyncPartition(context, entry, attached, table_name);
 }
 
 } // namespace duckdb
@@ -590,6 +858,13 @@ DUCKDB_EXTENSION_API void cubit_init(duckdb::DatabaseInstance &db) {
     duckdb::ExtensionUtil::RegisterFunction(
         db, duckdb::PragmaFunction::PragmaCall("cubit_attach", duckdb::CubitAttach,
                                                {duckdb::LogicalType::VARCHAR, duckdb::LogicalType::VARCHAR}));
+    duckdb::ExtensionUtil::RegisterFunction(
+        db, duckdb::PragmaFunction::PragmaCall("cubit_sync", duckdb::CubitSync, {duckdb::LogicalType::VARCHAR}));
+    // the index type (index_type_set.cpp:7-13 registers ART the same way)
+    duckdb::IndexType cubit_index;
+    cubit_index.name = duckdb::CubitIndex::TYPE_NAME;
+    cubit_index.create_instance = duckdb::CubitIndex::Create;
+    config.GetIndexTypes().RegisterIndexType(cubit_index);
 }
 
 DUCKDB_EXTENSION_API const char *cubit_version() {

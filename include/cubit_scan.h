@@ -5,7 +5,12 @@
  * Each entry point replaces one seq_scan callback (src/function/table/table_scan.cpp) and
  * keeps its contract:
  *   cubit_scan_init_global  ← TableScanInitGlobal   (table_scan.cpp:88-106)
- *                             (bind data = table partition + TransactionData)
+ *                             (bind data = table partition + TransactionData): runs the GPU
+ *                             scan (one ordered decode + the probes, on the device) and copies
+ *                             only the count and tile directory to the host
+ *   (the ids and probed values reach the host window by window — consecutive non-empty tiles,
+ *    about 262,144 rows — when a local state claims the window, as seq_scan materialises a row
+ *    group only when a thread takes its morsel)
  *   cubit_scan_max_threads  ← GlobalTableFunctionState::MaxThreads (DataTable::MaxThreads,
  *                             data_table.cpp:247-254)
  *   cubit_scan_init_local   ← TableScanInitLocal    (table_scan.cpp:67-86)
@@ -55,6 +60,11 @@ int cubit_scan_progress(cubit_scan *scan, double *out);
 int cubit_scan_cardinality(cubit_table *table, uint64_t *estimated, uint64_t *max);
 int cubit_scan_statistics(cubit_table *table, uint64_t column_id, int64_t *min, int64_t *max, int *has_null,
                           int *has_no_null);
+/* Buffers of finished scans are kept for the next one (page-locked host windows and device
+ * result buffers; at most CUBIT_SCAN_CACHE_MB MiB pinned — default 256 — and 16x that on the
+ * device). This frees every cached buffer and reports what was cached (either pointer may be
+ * NULL); call it before destroying a context whose scans are done. */
+int cubit_scan_release_cached(uint64_t *pinned_bytes, uint64_t *device_bytes);
 int cubit_scan_local_destroy(cubit_scan_local *local);
 int cubit_scan_destroy(cubit_scan *scan);
 

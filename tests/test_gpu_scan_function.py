@@ -166,3 +166,66 @@ def test_cardinality_and_statistics_callbacks(ctx):
     assert S.statistics(empty, 0) == (0, 0, False, False)
     assert S.cardinality(empty) == (0, 0)
     empty.close()
+
+
+def test_windows_stream_in_batch_order_per_task(ctx):
+    """A result of several copy windows (262,144 rows each) drained by 4 tasks: every task's
+    batch indexes never decrease (PipelineExecutor::NextBatch refuses a lower one,
+    pipeline_executor.cpp:132-136), every chunk's rows lie in its batch's tile, and the rows
+    equal numpy's predicate. The filter keeps half the rows, more than init_global's first
+    guess (an eighth), so the decode runs a second time with the exact count."""
+    from cubit_amd import scan_function as S
+
+    n = 3_000_017
+    rng = np.random.default_rng(21)
+    a = rng.integers(0, 1000, n).astype(np.int64)
+    b = rng.integers(-50, 50, n).astype(np.int32)
+    t = CubitTable(ctx, n, row_base=1_000)
+    t.add_column(0, a)
+    t.add_column(1, b)
+    t.build_index(0, L.INDEX_RANGE)
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 500)})
+    fn = CubitScanFunction(t, [1, 0, ROW_ID], [2, 0], fs)
+    assert fn.max_threads() >= 4
+    per_task, lock = {}, threading.Lock()
+
+    def task(k):
+        local = fn.init_local()
+        seen = []
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                break
+            seen.append((fn.get_batch_index(local), cols))
+        with lock:
+            per_task[k] = seen
+
+    th = [threading.Thread(target=task, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    chunks = []
+    for k, seen in per_task.items():
+        idx = [bi for bi, _ in seen]
+        assert idx == sorted(idx), k
+        for bi, cols in seen:
+            assert np.all((cols[0] - 1_000) // 131072 == bi)
+        chunks += seen
+    want = np.flatnonzero(a < 500)
+    assert np.array_equal(ordered(chunks, 0), want + 1_000)
+    assert np.array_equal(ordered(chunks, 1), b[want])
+    assert fn.progress() == pytest.approx(100.0)
+    fn.close()
+    pinned, device = C_release()
+    assert pinned > 0 and device > 0  # the finished scan's buffers were cached, now freed
+    assert C_release() == (0, 0)
+    t.close()
+
+
+def C_release():
+    import ctypes as C
+
+    p, d = C.c_uint64(), C.c_uint64()
+    L.check_scan(L.scan_lib().cubit_scan_release_cached(C.byref(p), C.byref(d)))
+    return int(p.value), int(d.value)
