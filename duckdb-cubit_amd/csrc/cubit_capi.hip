@@ -985,6 +985,7 @@ struct cubit_table {
     uint32_t last_packed = 0;  // leaves the last plan built straight from packed segments
     bool use_narrowing = true;  // cubit_table_use_narrowing
     uint32_t last_narrowed = 0;  // K0 leaves the last plan built only at the rows a mask kept
+    std::vector<int32_t> last_narrow_cols;  // columns of the last plan's K0 leaves, in build order
 };
 
 namespace {
@@ -2438,21 +2439,30 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
 }
 
 bool fits(const ExprP& e);
+double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc);
 
 // Selection narrowing of K0 leaves (RowGroup::TemplatedScan's filter loop, row_group.cpp:537-550:
 // each filter column after the first is read only at the rows the earlier ones kept). When the
 // planned expression is a conjunction of literals holding non-negated K0 leaves, the other
-// literals are materialised into a mask (with none, the first K0 leaf is built in full and is
-// the mask). If the mask keeps at most one row in 32, each K0 leaf is built by
+// literals are materialised into a mask; with none, the most selective K0 comparison is built in
+// full and is the mask. Each remaining K0 leaf, most selective first, is then built by
 // masked_compare_kernel — its column read only at the mask's rows, the result already the AND
-// with the mask — and the conjunction becomes that one leaf; a denser mask keeps the full K0
-// leaves (gathering most lines costs more than reading the column in order) and replaces the
-// literals it was made of. allow = false (visible MVCC updates, whose patches need whole
-// leaves) builds every leaf in full. Every pending leaf is built on return.
+// with the mask, and the next leaf's mask — and the conjunction becomes that one leaf. The order
+// and the decision come from selectivity estimates of every literal over the columns' per-zone
+// min / max (literal_selectivity; the statistics the zonemaps use, computed once per table
+// version), the reference's AdaptiveFilter ordering its filters by observed cost
+// (adaptive_filter.cpp:21-88) made up front: when the mask is estimated to keep more than one
+// row in 32, the K0 leaves are built in full (gathering most lines costs more than reading the
+// column in order). No count is read back: planning never waits for the device. allow = false
+// (visible MVCC updates, whose patches need whole leaves) builds every leaf in full. Every
+// pending leaf is built on return; t->last_narrow_cols lists the K0 columns in build order.
 int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool allow) {
+    t->last_narrow_cols.clear();
     auto compute_rest = [&]() -> int {
-        for (const PendingK0& k : pending)
+        for (const PendingK0& k : pending) {
             if (int rc = compute_k0(t, k)) return rc;
+            t->last_narrow_cols.push_back(k.col);
+        }
         pending.clear();
         return CUBIT_OK;
     };
@@ -2483,62 +2493,78 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
     for (const auto& lit : rest)  // a narrowed leaf must not also be read whole
         if (std::find(narrow_bvs.begin(), narrow_bvs.end(), lit.first.bv) != narrow_bvs.end()) return compute_rest();
     if (narrow_bvs.empty()) return compute_rest();
-    for (const auto& lit : rest) {  // complemented K0 leaves of the other literals: in full
-        PendingK0 k;
-        if (take(lit.first.bv, &k))
-            if (int rc = compute_k0(t, k)) return rc;
+    // selectivity estimates: the mask of the other literals (independent columns: the
+    // product), each K0 comparison
+    int rc = CUBIT_OK;
+    double rest_sel = 1.0;
+    for (const auto& lit : rest) {
+        rest_sel *= literal_selectivity(t, lit.first, lit.second, &rc);
+        if (rc) return rc;
     }
-    std::vector<PendingK0> narrow;
+    std::vector<std::pair<double, PendingK0>> narrow;
     for (const uint64_t* bv : narrow_bvs) {
+        Leaf l;
+        for (const auto& lit : lits)
+            if (lit.first.bv == bv) l = lit.first;
+        const double s = literal_selectivity(t, l, false, &rc);
+        if (rc) return rc;
         PendingK0 k;
         take(bv, &k);
-        narrow.push_back(k);
+        narrow.push_back({s, k});
     }
+    // most selective first (ties: column order, so the plan does not depend on the text order)
+    std::sort(narrow.begin(), narrow.end(), [](const auto& x, const auto& y) {
+        return x.first != y.first ? x.first < y.first
+                                  : (x.second.col != y.second.col ? x.second.col < y.second.col : x.second.c < y.second.c);
+    });
+    for (const auto& lit : rest) {  // complemented K0 leaves of the other literals: in full
+        PendingK0 k;
+        if (take(lit.first.bv, &k)) {
+            if (int rc2 = compute_k0(t, k)) return rc2;
+            t->last_narrow_cols.push_back(k.col);
+        }
+    }
+    const double mask_sel = rest.empty() ? narrow.front().first : rest_sel;
     uint64_t* mask = nullptr;
     cubit_ctx* ctx = t->ctx;
     if (!rest.empty()) {
         ExprP r = mk_true();
         for (const auto& lit : rest) r = mk_bin(Expr::AND, r, mk_leaf(lit.first, lit.second));
-        if (!fits(r)) {
-            for (const PendingK0& k : narrow) pending.push_back(k);
+        if (!fits(r) || mask_sel * 32 > 1.0) {
+            for (const auto& kv : narrow) pending.push_back(kv.second);
             return compute_rest();
         }
-        if (int rc = materialize(t, r, &mask)) return rc;  // counts its rows into dummy_count
+        if (int rc2 = materialize(t, r, &mask)) return rc2;
     } else {
-        const PendingK0 first = narrow.front();
+        const PendingK0 first = narrow.front().second;
         narrow.erase(narrow.begin());
-        if (int rc = compute_k0(t, first)) return rc;
+        if (int rc2 = compute_k0(t, first)) return rc2;
+        t->last_narrow_cols.push_back(first.col);
         mask = first.bv;
-        Emitter em;
-        Leaf l;
-        l.bv = mask;
-        em.leaf(l, false);
-        if (int rc = run_eval(ctx, em.prog, t->n_rows, 0, nullptr, 0, t->dummy_count, nullptr, RunMode::kCount))
-            return rc;
-        t->last_passes++;
-    }
-    uint64_t kept = 0;
-    HIP_CHECK(hipMemcpyAsync(&kept, t->dummy_count, sizeof(kept), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    Leaf ml;
-    ml.bv = mask;
-    if (narrow.empty() || kept * 32 > t->n_rows) {
-        ExprP acc = mk_leaf(ml);
-        for (const PendingK0& k : narrow) {
-            if (int rc = compute_k0(t, k)) return rc;
-            Leaf l;
-            l.bv = k.bv;
-            acc = mk_bin(Expr::AND, acc, mk_leaf(l));
+        if (mask_sel * 32 > 1.0) {  // too dense a mask: every other K0 leaf in full
+            Leaf ml;
+            ml.bv = mask;
+            ExprP acc = mk_leaf(ml);
+            for (const auto& kv : narrow) {
+                if (int rc2 = compute_k0(t, kv.second)) return rc2;
+                t->last_narrow_cols.push_back(kv.second.col);
+                Leaf l;
+                l.bv = kv.second.bv;
+                acc = mk_bin(Expr::AND, acc, mk_leaf(l));
+            }
+            e = acc;
+            return compute_rest();
         }
-        e = acc;
-        return compute_rest();
     }
-    for (const PendingK0& k : narrow) {
+    for (const auto& kv : narrow) {
+        const PendingK0& k = kv.second;
         const Column& cl = t->cols.at(k.col);
         HIP_CHECK(launch_masked_compare(cl.data, cl.type, cl.validity, mask, t->n_rows, k.cmp, k.c, k.bv, ctx->stream));
         mask = k.bv;
         t->last_narrowed++;
+        t->last_narrow_cols.push_back(k.col);
     }
+    Leaf ml;
     ml.bv = mask;
     e = mk_leaf(ml);
     return compute_rest();
@@ -2723,7 +2749,8 @@ int ensure_zones(cubit_table* t, const std::vector<const uint64_t*>& bvs, const 
         if (!t->col_zones.count(c)) todo_c.push_back(c);
     if (todo.empty() && todo_c.empty()) return CUBIT_OK;
     const uint32_t nz = real_zones(t);
-    const uint64_t per_col = (uint64_t)nz * 17;  // min, max (int64) + flags per zone
+    // min, max (int64) + flags per zone, each column's block 8-byte aligned
+    const uint64_t per_col = ((uint64_t)nz * 17 + 7) / 8 * 8;
     const uint64_t bytes = (uint64_t)todo.size() * nz + (uint64_t)todo_c.size() * per_col + 16;
     uint8_t* dev = zone_scratch(t, bytes);
     if (!dev) return fail(CUBIT_ERR_OOM, "zone classes allocation failed");
@@ -2801,6 +2828,43 @@ const ZoneMap& stats_zone_map(cubit_table* t, const Leaf& l) {
         m.informative |= none || all;
     }
     return t->pred_zones.emplace(key, std::move(m)).first->second;
+}
+
+// Estimated fraction of the partition's rows a literal keeps, from the column's per-zone min /
+// max (values uniform between them in each zone): the planner's cost model for narrowing. Leaves
+// not derived from a column value (visibility, materialised subtrees) count as keeping every row.
+// Exactness never depends on it.
+double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc) {
+    if (l.column < 0 || !t->cols.count(l.column) || t->n_rows == 0) return 1.0;
+    if ((*rc = ensure_zones(t, {}, {l.column}))) return 1.0;
+    const cubit_table::ColZones& cz = t->col_zones.at(l.column);
+    const uint32_t nz = (uint32_t)cz.fl.size();
+    double kept = 0.0;
+    for (uint32_t z = 0; z < nz; ++z) {
+        const double rows = (double)std::min<uint64_t>(kZoneRows, t->n_rows - (uint64_t)z * kZoneRows);
+        if (!(cz.fl[z] & 1)) continue;  // no valid row: no comparison passes (and NN keeps none)
+        const double lo = (double)cz.mn[z], hi = (double)cz.mx[z], span = hi - lo + 1.0;
+        const double c = (double)l.constant, c2 = (double)l.constant2;
+        auto clip = [](double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); };
+        double f = 1.0;
+        if (l.pred == 1) {
+            f = 1.0;
+        } else if (l.pred == 2) {
+            f = clip((std::min(c2, hi + 1.0) - std::max(c, lo)) / span);
+        } else {
+            switch (l.cmp) {
+            case CUBIT_CMP_EQ: f = (c < lo || c > hi) ? 0.0 : 1.0 / span; break;
+            case CUBIT_CMP_NE: f = (c < lo || c > hi) ? 1.0 : 1.0 - 1.0 / span; break;
+            case CUBIT_CMP_LT: f = clip((c - lo) / span); break;
+            case CUBIT_CMP_LE: f = clip((c - lo + 1.0) / span); break;
+            case CUBIT_CMP_GT: f = clip((hi - c) / span); break;
+            default: f = clip((hi - c + 1.0) / span); break;  // GE
+            }
+        }
+        kept += f * rows;  // NULL rows of a mixed zone counted as valid: an over-estimate
+    }
+    const double s = kept / (double)t->n_rows;
+    return neg ? 1.0 - s : s;
 }
 
 struct ZoneSet {
@@ -2937,6 +3001,7 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     t->last_passes = 0;
     t->last_packed = 0;
     t->last_narrowed = 0;
+    t->last_narrow_cols.clear();
     ExprP e;
     std::vector<PendingK0> pending;  // K0 leaves not built yet (narrow_k0)
     if (n_nodes == 0) {
@@ -2953,8 +3018,10 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     if (txn)
         for (auto& kv : t->upd) visible_updates |= kv.second.any_visible(txn);
     if (visible_updates) {
-        for (const PendingK0& k : pending)
+        for (const PendingK0& k : pending) {
             if (int rc = compute_k0(t, k)) return rc;
+            t->last_narrow_cols.push_back(k.col);
+        }
         pending.clear();
     }
     if (txn) {
@@ -3296,6 +3363,23 @@ extern "C" int cubit_table_use_narrowing(cubit_table* t, int on) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     CUBIT_LOCK(t->ctx);
     t->use_narrowing = on != 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_column_changed(cubit_table* t, int col) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null table");
+    CUBIT_LOCK(t->ctx);
+    if (!t->cols.count(col)) return fail(CUBIT_ERR_INVALID, "column %d is not registered", col);
+    // statistics and zone classes derived from the values, and leaves patched from them
+    drop_patches(t, col);
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_k0_order(cubit_table* t, int32_t* cols, uint32_t cap, uint32_t* n) {
+    if (!t || !n || (cap && !cols)) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    *n = (uint32_t)t->last_narrow_cols.size();
+    for (uint32_t i = 0; i < *n && i < cap; ++i) cols[i] = t->last_narrow_cols[i];
     return CUBIT_OK;
 }
 

@@ -112,6 +112,8 @@ GPU_SIGNATURES = {
     "cubit_table_last_packed": (C.c_int, [_P, C.POINTER(_U32)]),
     "cubit_table_use_narrowing": (C.c_int, [_P, C.c_int]),
     "cubit_table_last_narrowed": (C.c_int, [_P, C.POINTER(_U32)]),
+    "cubit_table_last_k0_order": (C.c_int, [_P, C.POINTER(C.c_int32), _U32, C.POINTER(_U32)]),
+    "cubit_table_column_changed": (C.c_int, [_P, C.c_int]),
     "cubit_table_column_statistics": (C.c_int, [_P, C.c_int, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(C.c_int),
                                                 C.POINTER(C.c_int)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),

@@ -374,6 +374,20 @@ class CubitTable:
         L.check(self.lib.cubit_table_last_narrowed(self.handle, C.byref(v)))
         return int(v.value)
 
+    def last_k0_order(self):
+        """Columns of the K0 comparisons the last scan built, in build order (most selective
+        first when narrowed)."""
+        cap = 64
+        arr = (C.c_int32 * cap)()
+        n = C.c_uint32()
+        L.check(self.lib.cubit_table_last_k0_order(self.handle, arr, cap, C.byref(n)))
+        return [int(arr[i]) for i in range(min(cap, n.value))]
+
+    def column_changed(self, col: int) -> None:
+        """A caller-owned (device) column's values were rewritten: drop the statistics and zone
+        classes the table derived from them."""
+        L.check(self.lib.cubit_table_column_changed(self.handle, col))
+
     def last_zones(self):
         """(zones the last scan / sum_product evaluated, zones of the partition): fewer
         evaluated when the zonemaps skipped zones its filter is false on."""

@@ -208,9 +208,15 @@ int cubit_table_info(cubit_table *t, uint64_t *n_rows, int64_t *row_base, cubit_
  * src/storage/table/column_data.cpp:135-188). */
 int cubit_table_column_data(cubit_table *t, int col, const void **data, int *type);
 /* Register column `col`. data/validity are host pointers unless on_device = 1 (then the
- * table only references them). validity may be NULL (no NULLs). */
+ * table only references them). validity may be NULL (no NULLs). A caller-owned (on_device = 1)
+ * buffer must not change while registered unless the caller says so with
+ * cubit_table_column_changed: the table caches per-zone statistics of the values (zonemaps,
+ * column statistics, selectivity estimates) and would otherwise skip zones by stale bounds.
+ * Index bitvectors are not rebuilt by it (rebuild with cubit_table_build_index). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
+/* The values of a caller-owned column changed: drop what the table derived from them. */
+int cubit_table_column_changed(cubit_table *t, int col);
 /* Register a column given as DuckDB BITPACKING segments (K5; the reference's persistent
  * integer storage, src/storage/compression/bitpacking.cpp): `bytes` holds the segment images
  * (each: 8-byte header = end of its metadata words, group data, metadata words of the
@@ -241,6 +247,13 @@ int cubit_table_last_packed(cubit_table *t, uint32_t *n_leaves);
  * scan built so. */
 int cubit_table_use_narrowing(cubit_table *t, int on);
 int cubit_table_last_narrowed(cubit_table *t, uint32_t *n_leaves);
+/* The columns of the K0 comparisons the last scan built, in build order (cols[i] for i <
+ * min(cap, *n)). Narrowing orders them by estimated selectivity — every literal's fraction of
+ * kept rows from its column's per-zone min / max, the reference's AdaptiveFilter ordering
+ * (src/execution/adaptive_filter.cpp:21-88) decided up front — most selective first, so the
+ * order does not depend on the order of the filters; the estimate also decides whether to
+ * narrow, without waiting for the device. */
+int cubit_table_last_k0_order(cubit_table *t, int32_t *cols, uint32_t cap, uint32_t *n);
 /* Build a bitmap index on `col` (K0). edges/values sorted ascending; n = 0 means "all
  * distinct values of the column" (exact for every constant). RANGE / EQUALITY replace the
  * column's primary index; BINS (n >= 2 edges) adds a secondary binned index. */

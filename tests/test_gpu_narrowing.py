@@ -209,3 +209,55 @@ def test_random_conjunctions(ctx):
         narrowed_total += narrowed
     assert narrowed_total >= 5, narrowed_total
     t.close()
+
+
+def test_order_by_estimated_selectivity(ctx):
+    """Two unindexed comparisons in both textual orders (and behind an index leaf): the plan
+    builds the most selective one first — full-column, as the mask — and reads the other only at
+    its rows, whatever the order the filters came in (the reference's AdaptiveFilter reorders
+    its filters by measured cost, adaptive_filter.cpp:21-88); rows equal the oracle either way.
+    The estimate comes from per-zone min / max, so no count is read back while planning."""
+    t, cols, vw = make(ctx)
+    oc = ocols(cols, vw)
+    sel1 = F.ConstantFilter("<", -990_000)        # col 1: ≈ 0.5 % (the more selective)
+    sel2 = F.ConstantFilter("<", -2 ** 62 + 2 ** 59)  # col 2: ≈ 6 %
+    orders = []
+    for fs in (F.TableFilterSet({1: sel1, 2: sel2}), F.TableFilterSet({2: sel2, 1: sel1})):
+        ref, narrowed = check(t, oc, fs)
+        assert len(ref) > 0 and narrowed == 1
+        t.scan(fs)
+        orders.append(t.last_k0_order())
+    assert orders[0] == orders[1] == [1, 2], orders
+    # behind an index leaf keeping 2 % (the mask), both chained, most selective first
+    for fs in (F.TableFilterSet({0: F.ConstantFilter("<", 20), 1: sel1, 2: sel2}),
+               F.TableFilterSet({2: sel2, 0: F.ConstantFilter("<", 20), 1: sel1})):
+        t.build_index(0, L.INDEX_RANGE)
+        ref, narrowed = check(t, oc, fs)
+        assert narrowed == 2
+        t.scan(fs)
+        assert t.last_k0_order() == [1, 2]
+    t.close()
+
+
+def test_caller_owned_column_changed(ctx):
+    """A caller-owned device column rewritten in place: after cubit_table_column_changed the
+    zonemaps and statistics follow the new values (stale per-zone bounds would skip zones that
+    now qualify)."""
+    import torch
+
+    from cubit_amd.table import CubitTable
+
+    n = 1_000_003
+    a = torch.arange(n, dtype=torch.int64, device="cuda")  # ascending: zones with disjoint bounds
+    t = CubitTable(ctx, n)
+    t.add_device_column(0, a.data_ptr(), L.TYPE_INT64)
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 1000)})
+    assert t.count(fs) == 1000
+    assert t.last_zones()[0] < t.last_zones()[1]  # the zonemap skipped zones
+    a.copy_(torch.flip(a, [0]))  # now the small values sit in the last zone
+    torch.cuda.synchronize()
+    t.column_changed(0)
+    assert t.count(fs) == 1000
+    assert t.scan(fs)[0] == n - 1000
+    assert t.column_statistics(0)[:2] == (0, n - 1)
+    t.close()
