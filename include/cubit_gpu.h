@@ -294,7 +294,11 @@ int cubit_table_set_inserts(cubit_table *t, const int64_t *row_begin, const int6
  * 0 = visible to every snapshot. Storage grows geometrically when the padding runs out.
  * Columns registered as caller-owned device memory (add_column on_device = 1) are copied into
  * table-owned storage on the first append or merge; the caller's buffer is no longer read.
- * On an error the partition keeps its previous rows (a later append overwrites the slice). */
+ * On an error the partition keeps its previous rows: scans and counts are those of the state
+ * before the call (a later append overwrites the slice). What the failed call already did to
+ * the indexes stays but never changes a result: bits spliced past the last row (masked by every
+ * scan), statistics widened (bounds the values still lie within) and keys added to an
+ * every-distinct-value index (exact leaves of values no row holds). */
 int cubit_table_append(cubit_table *t, uint64_t n_new, const int *cols, const void *const *data,
                        const uint64_t *const *validity, uint32_t n_cols, uint64_t insert_id);
 /* Merge the update records of `col` with version < horizon into the base values and the

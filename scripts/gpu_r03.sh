@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-STEPS="${STEPS:-tests,small,bench}"
+STEPS="${STEPS:-tests,small,bench}"  # also: probe
 rc=0
 if [[ ",$STEPS," == *",tests,"* ]]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread \
@@ -16,6 +16,11 @@ fi
 if [[ ",$STEPS," == *",small,"* ]]; then
   timeout -k 10 300 ./scripts/smallbench ${SMALL_REPS:-50} > gpurun_out/smallbench.log 2>&1; rc=$?
   cat gpurun_out/smallbench.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [[ ",$STEPS," == *",probe,"* ]]; then
+  timeout -k 10 300 ./scripts/probebench ${PROBE_REPS:-10} > gpurun_out/probebench.log 2>&1; rc=$?
+  cat gpurun_out/probebench.log
   [ $rc -eq 0 ] || exit $rc
 fi
 if [[ ",$STEPS," == *",bench,"* ]]; then
