@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -2440,6 +2441,7 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
 
 bool fits(const ExprP& e);
 double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc);
+double conj_selectivity(cubit_table* t, const Emitter::Lits& lits, int* rc);
 
 // Selection narrowing of K0 leaves (RowGroup::TemplatedScan's filter loop, row_group.cpp:537-550:
 // each filter column after the first is read only at the rows the earlier ones kept). When the
@@ -2496,11 +2498,8 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
     // selectivity estimates: the mask of the other literals (independent columns: the
     // product), each K0 comparison
     int rc = CUBIT_OK;
-    double rest_sel = 1.0;
-    for (const auto& lit : rest) {
-        rest_sel *= literal_selectivity(t, lit.first, lit.second, &rc);
-        if (rc) return rc;
-    }
+    const double rest_sel = conj_selectivity(t, rest, &rc);
+    if (rc) return rc;
     std::vector<std::pair<double, PendingK0>> narrow;
     for (const uint64_t* bv : narrow_bvs) {
         Leaf l;
@@ -2830,41 +2829,92 @@ const ZoneMap& stats_zone_map(cubit_table* t, const Leaf& l) {
     return t->pred_zones.emplace(key, std::move(m)).first->second;
 }
 
-// Estimated fraction of the partition's rows a literal keeps, from the column's per-zone min /
-// max (values uniform between them in each zone): the planner's cost model for narrowing. Leaves
-// not derived from a column value (visibility, materialised subtrees) count as keeping every row.
-// Exactness never depends on it.
-double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc) {
-    if (l.column < 0 || !t->cols.count(l.column) || t->n_rows == 0) return 1.0;
-    if ((*rc = ensure_zones(t, {}, {l.column}))) return 1.0;
-    const cubit_table::ColZones& cz = t->col_zones.at(l.column);
+// Estimated fraction of the partition's rows whose value of column col lies in [lo, hi) (valid
+// rows only), from the column's per-zone min / max (values uniform between them in each zone):
+// the planner's cost model for narrowing. Exactness never depends on it.
+double interval_selectivity(cubit_table* t, int col, double lo_c, double hi_c, int* rc) {
+    if (!t->cols.count(col) || t->n_rows == 0) return 1.0;
+    if ((*rc = ensure_zones(t, {}, {col}))) return 1.0;
+    const cubit_table::ColZones& cz = t->col_zones.at(col);
     const uint32_t nz = (uint32_t)cz.fl.size();
-    double kept = 0.0;
+    // a zone whose value span is far wider than the typical zone's holds a few outliers (one
+    // extreme value stretches the uniform assumption over the whole type range): it counts at
+    // the other zones' mean fraction instead
+    std::vector<double> spans;
+    for (uint32_t z = 0; z < nz; ++z)
+        if (cz.fl[z] & 1) spans.push_back((double)cz.mx[z] - (double)cz.mn[z] + 1.0);
+    double median_span = 0.0;
+    if (!spans.empty()) {
+        std::nth_element(spans.begin(), spans.begin() + spans.size() / 2, spans.end());
+        median_span = spans[spans.size() / 2];
+    }
+    double kept = 0.0, normal_rows = 0.0, outlier_rows = 0.0;
     for (uint32_t z = 0; z < nz; ++z) {
         const double rows = (double)std::min<uint64_t>(kZoneRows, t->n_rows - (uint64_t)z * kZoneRows);
-        if (!(cz.fl[z] & 1)) continue;  // no valid row: no comparison passes (and NN keeps none)
-        const double lo = (double)cz.mn[z], hi = (double)cz.mx[z], span = hi - lo + 1.0;
-        const double c = (double)l.constant, c2 = (double)l.constant2;
-        auto clip = [](double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); };
-        double f = 1.0;
-        if (l.pred == 1) {
-            f = 1.0;
-        } else if (l.pred == 2) {
-            f = clip((std::min(c2, hi + 1.0) - std::max(c, lo)) / span);
+        if (!(cz.fl[z] & 1)) continue;  // no valid row passes a comparison
+        const double lo = (double)cz.mn[z], hi = (double)cz.mx[z] + 1.0, span = hi - lo;
+        if (median_span > 1.0 && span > 8.0 * median_span) {
+            outlier_rows += rows;
+            continue;
+        }
+        const double f = std::max(0.0, std::min(hi, hi_c) - std::max(lo, lo_c)) / span;
+        kept += f * rows;  // NULL rows of a mixed zone counted as valid: an over-estimate
+        normal_rows += rows;
+    }
+    if (outlier_rows > 0.0) kept += outlier_rows * (normal_rows > 0.0 ? kept / normal_rows : 0.5);
+    return std::min(1.0, kept / (double)t->n_rows);
+}
+
+// Estimated fraction of rows a conjunction of literals keeps: the literals of one column fold
+// into one interval (a range index answers `a <= v < b` as L(b) AND NOT L(a): two literals of
+// one predicate, not independent ones), the columns multiply (independence), literals that
+// fold into no interval (NOT (v = c), NOT of a bin) multiply as 1 - their own fraction, and
+// leaves not derived from a column value (visibility, materialised subtrees) keep every row.
+double conj_selectivity(cubit_table* t, const Emitter::Lits& lits, int* rc) {
+    const double inf = std::numeric_limits<double>::infinity();
+    std::map<int, std::pair<double, double>> iv;
+    double sel = 1.0;
+    for (const auto& lit : lits) {
+        const Leaf& l = lit.first;
+        const bool neg = lit.second;
+        if (l.column < 0 || l.pred == 1) continue;
+        auto& r = iv.emplace(l.column, std::make_pair(-inf, inf)).first->second;
+        const double c = (double)l.constant;
+        double lo = -inf, hi = inf;  // the literal as [lo, hi), when it is one interval
+        bool interval = true;
+        if (l.pred == 2) {
+            lo = c;
+            hi = (double)l.constant2;
+            interval = !neg;
         } else {
             switch (l.cmp) {
-            case CUBIT_CMP_EQ: f = (c < lo || c > hi) ? 0.0 : 1.0 / span; break;
-            case CUBIT_CMP_NE: f = (c < lo || c > hi) ? 1.0 : 1.0 - 1.0 / span; break;
-            case CUBIT_CMP_LT: f = clip((c - lo) / span); break;
-            case CUBIT_CMP_LE: f = clip((c - lo + 1.0) / span); break;
-            case CUBIT_CMP_GT: f = clip((hi - c) / span); break;
-            default: f = clip((hi - c + 1.0) / span); break;  // GE
+            case CUBIT_CMP_EQ: lo = c; hi = c + 1; interval = !neg; break;
+            case CUBIT_CMP_NE: lo = c; hi = c + 1; interval = neg; break;  // NOT (v != c) = (v = c)
+            case CUBIT_CMP_LT: (neg ? lo : hi) = c; break;
+            case CUBIT_CMP_LE: (neg ? lo : hi) = c + 1; break;
+            case CUBIT_CMP_GT: (neg ? hi : lo) = c + 1; break;
+            default: (neg ? hi : lo) = c; break;  // GE
             }
         }
-        kept += f * rows;  // NULL rows of a mixed zone counted as valid: an over-estimate
+        if (interval) {
+            r.first = std::max(r.first, lo);
+            r.second = std::min(r.second, hi);
+        } else {
+            sel *= 1.0 - interval_selectivity(t, l.column, lo, hi, rc);
+            if (*rc) return 1.0;
+        }
     }
-    const double s = kept / (double)t->n_rows;
-    return neg ? 1.0 - s : s;
+    for (const auto& kv : iv) {
+        if (kv.second.first == -inf && kv.second.second == inf) continue;
+        sel *= interval_selectivity(t, kv.first, kv.second.first, kv.second.second, rc);
+        if (*rc) return 1.0;
+    }
+    return sel;
+}
+
+double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc) {
+    Emitter::Lits one{{l, neg}};
+    return conj_selectivity(t, one, rc);
 }
 
 struct ZoneSet {

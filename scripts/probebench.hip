@@ -74,6 +74,28 @@ __global__ __launch_bounds__(256) void gather_sum(const int64_t* __restrict__ a,
     if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
 }
 
+__global__ void iota_ids(int64_t* ids, uint64_t m, uint64_t stride) {
+    const uint64_t st = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += st) ids[i] = (int64_t)(i * stride);
+}
+
+// contiguous read of a column, 16 B per lane (the streaming rate the gathers compare with)
+__global__ __launch_bounds__(256) void stream_sum(const int64_t* __restrict__ a, uint64_t n, unsigned long long* out) {
+    typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+    const i64x2* p = reinterpret_cast<const i64x2*>(a);
+    const uint64_t m = n / 2, st = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += 4 * st) {
+        i64x2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i + u * st < m ? __builtin_nontemporal_load(p + i + u * st) : i64x2{0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += (uint64_t)(v[u].x + v[u].y);
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 10;
     CK(hipSetDevice(0));
@@ -184,11 +206,28 @@ int main(int argc, char** argv) {
              CK(launch_gather_sum_product(a, b, ids, cnt, cap, 0, partials, out, s));
          }, 4 * leaf_b + 8.0 * q + 24.0 * q},
     };
+    // fetch-granularity calibration: one gather per 128-B line (every 16th int64) and one per
+    // two lines (every 32nd), against the contiguous read of the whole column
+    vs.push_back({"calib: stream the whole column a", [&] {
+                      hipLaunchKernelGGL(stream_sum, dim3(4096), dim3(256), 0, s, a, n, gsum);
+                  }, 8.0 * n});
+    vs.push_back({"calib: gather every 16th row (1/line)", [&] {
+                      hipLaunchKernelGGL(gather_sum<4>, dim3(2048), dim3(256), 0, s, a, ids, n / 16, gsum);
+                  }, 8.0 * (n / 16)});
+    vs.push_back({"calib: gather every 32nd row (1/2 lines)", [&] {
+                      hipLaunchKernelGGL(gather_sum<4>, dim3(2048), dim3(256), 0, s, a, ordered, n / 32, gsum);
+                  }, 8.0 * (n / 32)});
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     printf("%-40s %10s %12s %10s %12s\n", "variant", "us", "alg GB/s", "frac", "w/ sectors");
+    bool calib_ids = false;
     for (auto& v : vs) {
+        if (!calib_ids && v.name.rfind("calib:", 0) == 0) {
+            hipLaunchKernelGGL(iota_ids, dim3(4096), dim3(256), 0, s, ids, n / 16, 16ull);
+            hipLaunchKernelGGL(iota_ids, dim3(4096), dim3(256), 0, s, ordered, n / 32, 32ull);
+            calib_ids = true;
+        }
         for (int i = 0; i < 3; ++i) v.f();
         std::vector<float> t;
         for (int r = 0; r < 5; ++r) {
@@ -207,8 +246,9 @@ int main(int argc, char** argv) {
         const double gathered = v.name.find("gather a only") != std::string::npos ? 1.0
                                 : v.name.find("unfused") != std::string::npos  ? 2.0
                                 : v.name.find("b gathered") != std::string::npos ? 2.0 : 1.0;
-        const double sect = v.name.find("count") != std::string::npos ? v.bytes
-                                                                       : v.bytes - gathered * 8.0 * q + gathered * 64.0 * sectors64;
+        const double sect = (v.name.find("count") != std::string::npos || v.name.rfind("calib:", 0) == 0)
+                                ? v.bytes
+                                : v.bytes - gathered * 8.0 * q + gathered * 64.0 * sectors64;
         printf("%-40s %10.1f %12.0f %10.3f %12.0f\n", v.name.c_str(), us, v.bytes / (us * 1e-6) / 1e9,
                v.bytes / (us * 1e-6) / 8e12, sect / (us * 1e-6) / 1e9);
     }
