@@ -855,10 +855,12 @@ struct Column {
     // (bitpacked_compare_kernel) instead of reading the plain column. Dropped when the values
     // change (appends, merges).
     std::unique_ptr<DevBuf> bp_bytes, bp_groups;
+    std::unique_ptr<DevBuf> bp_vgroup;  // per 2,048-row vector: the group holding its first row
     uint64_t bp_n_groups = 0;
     void drop_packed() {
         bp_bytes.reset();
         bp_groups.reset();
+        bp_vgroup.reset();
         bp_n_groups = 0;
     }
 };
@@ -987,6 +989,7 @@ struct cubit_table {
     bool use_narrowing = true;  // cubit_table_use_narrowing
     uint32_t last_narrowed = 0;  // K0 leaves the last plan built only at the rows a mask kept
     std::vector<int32_t> last_narrow_cols;  // columns of the last plan's K0 leaves, in build order
+    bool last_sum_packed = false;  // the last sum_product read a from its BITPACKING segments
 };
 
 namespace {
@@ -1292,15 +1295,24 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     if (row != t->n_rows)
         return fail(CUBIT_ERR_INVALID, "segments hold %llu rows, partition has %llu", (unsigned long long)row,
                     (unsigned long long)t->n_rows);
+    // the probe's random access (SumArgs::a_vgroup): the group of each vector's first row
+    const uint64_t n_vec = (t->n_rows + 2047) / 2048;
+    std::vector<uint32_t> vgroup(std::max<uint64_t>(n_vec, 1), 0);
+    for (uint64_t v = 0, g = 0; v < n_vec; ++v) {
+        while (g + 1 < groups.size() && groups[g].row_start + groups[g].count <= v * 2048) ++g;
+        vgroup[v] = (uint32_t)g;
+    }
     hipStream_t s = t->ctx->stream;
-    DevBuf d_bytes, d_groups;
+    DevBuf d_bytes, d_groups, d_vgroup;
     auto out = std::make_unique<DevBuf>();
     // +16: the kernel stages packed words with 16-byte-aligned loads that may run past the end
     if (hipMalloc(&d_bytes.p, (n_bytes + 15) / 16 * 16 + 16) != hipSuccess ||
         hipMalloc(&d_groups.p, groups.size() * sizeof(BpGroup)) != hipSuccess ||
-        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * tsz, 16)) != hipSuccess)
+        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * tsz, 16)) != hipSuccess ||
+        hipMalloc(&d_vgroup.p, vgroup.size() * 4) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "bitpacked column allocation failed");
     HIP_CHECK(hipMemcpyAsync(d_bytes.p, bytes, n_bytes, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d_vgroup.p, vgroup.data(), vgroup.size() * 4, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_groups.p, groups.data(), groups.size() * sizeof(BpGroup), hipMemcpyHostToDevice, s));
     hipEvent_t e0, e1;
     if (int rc = timing_events(t->ctx, e0, e1)) return rc;
@@ -1316,6 +1328,8 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     c.bp_groups = std::make_unique<DevBuf>();
     std::swap(c.bp_bytes->p, d_bytes.p);
     std::swap(c.bp_groups->p, d_groups.p);
+    c.bp_vgroup = std::make_unique<DevBuf>();
+    std::swap(c.bp_vgroup->p, d_vgroup.p);
     c.bp_n_groups = groups.size();
     if (validity) {
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
@@ -3320,6 +3334,14 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
     SumArgs sa{};
     sa.a = static_cast<const int64_t*>(ait->second.data);
     sa.a_valid = ait->second.validity;
+    t->last_sum_packed = false;
+    if ((flags & CUBIT_SUM_PACKED_A) && ait->second.bp_n_groups) {
+        sa.a_bytes = static_cast<const uint8_t*>(ait->second.bp_bytes->p);
+        sa.a_groups = static_cast<const BpGroup*>(ait->second.bp_groups->p);
+        sa.a_vgroup = static_cast<const uint32_t*>(ait->second.bp_vgroup->p);
+        sa.a_plain = sa.a;
+        t->last_sum_packed = true;
+    }
     sa.partials = ctx->partials;
     std::vector<int64_t> vals;
     std::vector<const uint64_t*> dl;
@@ -3452,6 +3474,13 @@ extern "C" int cubit_table_last_zones(cubit_table* t, uint32_t* evaluated, uint3
     CUBIT_LOCK(t->ctx);
     if (evaluated) *evaluated = t->last_live;
     if (zones) *zones = t->last_zones;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_last_sum_packed(cubit_table* t, int* packed) {
+    if (!t || !packed) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    *packed = t->last_sum_packed ? 1 : 0;
     return CUBIT_OK;
 }
 

@@ -185,6 +185,16 @@ struct SumArgs {
     int64_t v0;
     uint32_t n_decode;
     int64_t* partials;  // 2 int64 (lo, hi) per workgroup
+    // a read from its DuckDB BITPACKING segments instead of the plain column (null = plain):
+    // the packed bytes, the group records (BpGroup, row order) and per 2,048-row vector the
+    // index of the group holding its first row. CONSTANT / CONSTANT_DELTA / FOR groups are
+    // random-accessible (value i = base (+ aux·i | + its w bits at bit i·w)); a row of a
+    // DELTA_FOR group is read from a_plain (the unpacked column), as its value needs the prefix
+    // of its group.
+    const uint8_t* a_bytes;
+    const BpGroup* a_groups;
+    const uint32_t* a_vgroup;
+    const int64_t* a_plain;
 };
 // grid = persistent workgroups; partials must hold 2·grid int64; out = {lo, hi}
 hipError_t launch_eval_sum_product(const EvalArgs& a, const SumArgs& s, unsigned grid, int64_t* out, hipStream_t stream);

@@ -1264,6 +1264,34 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             if ((miss >> m) & 1u) v += (uint64_t)s.delta[m];
         return (int64_t)v;
     };
+    // a[r], from the plain column or from its BITPACKING group (row → group record → packed bits)
+    auto load_a = [&](uint64_t r) -> int64_t {
+        if (!s.a_bytes) return __builtin_nontemporal_load(s.a + r);
+        uint32_t g = s.a_vgroup[r >> 11];
+        uint64_t rs = s.a_groups[g].row_start;
+        uint32_t cnt = s.a_groups[g].count;
+        while (r >= rs + cnt) {  // a vector that starts in the tail of a segment's last group
+            ++g;
+            rs = s.a_groups[g].row_start;
+            cnt = s.a_groups[g].count;
+        }
+        const BpGroup& gr = s.a_groups[g];
+        const uint64_t i = r - rs;
+        const uint32_t mode = gr.mode;
+        if (mode == 2) return (int64_t)gr.base;
+        if (mode == 3) return (int64_t)(gr.base + gr.aux * i);
+        if (mode != 5) return __builtin_nontemporal_load(s.a_plain + r);  // DELTA_FOR: needs its prefix
+        const uint32_t w = gr.width;
+        if (w == 0) return (int64_t)gr.base;
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(s.a_bytes + gr.words_off);
+        const uint64_t bit = i * w;
+        const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
+        uint64_t x = ((uint64_t)__builtin_nontemporal_load(words + wi) |
+                      (off + w > 32 ? (uint64_t)__builtin_nontemporal_load(words + wi + 1) << 32 : 0ull)) >> off;
+        if (off + w > 64) x |= (uint64_t)__builtin_nontemporal_load(words + wi + 2) << (64 - off);
+        if (w < 64) x &= (1ull << w) - 1;
+        return (int64_t)(x + gr.base);
+    };
     auto accumulate = [&](int64_t row, int64_t bval_decoded) {
         const uint64_t r = (uint64_t)(row - a.row_base);
         if (s.a_valid && !((s.a_valid[r >> 6] >> (r & 63)) & 1ull)) return;
@@ -1272,7 +1300,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             if (s.b_valid && !((s.b_valid[r >> 6] >> (r & 63)) & 1ull)) return;
             bv = s.b[r];
         }
-        add128(acc_lo, acc_hi, (__int128)s.a[r] * (__int128)bv);
+        add128(acc_lo, acc_hi, (__int128)load_a(r) * (__int128)bv);
     };
 
     u64x2 v[K][PAIRS];
@@ -1365,7 +1393,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                     const uint32_t sr = ok[u] ? s_row[k] : 0u;
                     const uint64_t rr = (uint64_t)(row0 - a.row_base) + (sr & ((1u << kMissShift) - 1));
                     // line-granular gathers, no reuse: nontemporal like the leaf loads
-                    av[u] = ok[u] ? __builtin_nontemporal_load(s.a + rr) : 0;
+                    av[u] = ok[u] ? load_a(rr) : 0;
                     bvv[u] = M > 0 ? (ok[u] ? decoded_b(sr >> kMissShift) : 0) : (ok[u] ? __builtin_nontemporal_load(s.b + rr) : 0);
                     if (ok[u] && s.a_valid && !((s.a_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;
                     if (M == 0 && ok[u] && s.b_valid && !((s.b_valid[rr >> 6] >> (rr & 63)) & 1ull)) ok[u] = false;

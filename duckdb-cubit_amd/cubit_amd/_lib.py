@@ -25,6 +25,7 @@ FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = ran
 INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2
 SUM_GATHER_B = 1
 SUM_NO_ZONEMAP = 2
+SUM_PACKED_A = 4
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2
@@ -118,6 +119,7 @@ GPU_SIGNATURES = {
                                                 C.POINTER(C.c_int)]),
     "cubit_table_sum_product": (C.c_int, [_P, _P, _U32, _P, C.c_int, C.c_int, _P, _P, _U32]),
     "cubit_table_last_sum_decode": (C.c_int, [_P, C.POINTER(_U32)]),
+    "cubit_table_last_sum_packed": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "cubit_table_column_data": (C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(C.c_int)]),
     "cubit_table_set_inserts": (C.c_int, [_P, _P, _P, _P, _U64]),
     "cubit_table_append": (C.c_int, [_P, _U64, _P, _P, _P, C.c_uint32, _U64]),

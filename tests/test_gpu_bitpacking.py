@@ -157,3 +157,42 @@ def test_filter_straight_from_segments(ctx, name, mode):
             assert packed == (1 if live else 0), (name, mode, cmp, k, packed, live)
     t.use_packed_filter(True)
     t.close()
+
+
+@pytest.mark.parametrize("mode", ["auto", "for", "delta_for", "constant_delta"])
+def test_fused_sum_reads_packed_column(ctx, mode):
+    """SELECT sum(a * b) WHERE <filter> with a read at the qualifying rows straight from its
+    BITPACKING segments (CUBIT_SUM_PACKED_A: row → group record → the value's w bits; DELTA_FOR
+    rows from the unpacked column): equal to the same sum over the plain column and to numpy,
+    for every group mode, with NULLs in a, several segments and a row base."""
+    rng = np.random.default_rng({"auto": 1, "for": 2, "delta_for": 3, "constant_delta": 4}[mode])
+    n = 600_011
+    a = rng.integers(-2 ** 23, 2 ** 23, n).astype(np.int64)
+    if mode == "constant_delta":
+        a = (np.arange(n, dtype=np.int64) * 3 - 5)
+    elif mode == "delta_for":
+        a = np.cumsum(rng.integers(0, 100, n)).astype(np.int64)
+    a[100_000:104_096] = 42  # a constant group or two
+    b = rng.integers(0, 11, n).astype(np.int64)
+    key = rng.integers(0, 100, n).astype(np.int32)
+    valid_a = np.ones(n, dtype=bool)  # NULLs in a few groups (the delta modes need all-valid groups)
+    valid_a[200_000:220_000] = rng.random(20_000) > 0.3
+    c = O.bp_compress(a, valid_a, mode)
+    modes = set(O.bp_group_modes(c))
+    assert {"auto": "for", "for": "for", "delta_for": "delta_for", "constant_delta": "constant_delta"}[mode] in modes
+    t = CubitTable(ctx, n, row_base=11)
+    t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, np.int64, validity=validity_from_mask(valid_a))
+    t.add_column(1, b)
+    t.add_column(2, key)
+    t.build_index(2, L.INDEX_RANGE)
+    for f in (F.ConstantFilter("<", 3), F.ConstantFilter(">=", 60), F.ConstantFilter("=", 50)):
+        fs = F.TableFilterSet({2: f})
+        keep = {"<": key < 3, ">=": key >= 60, "=": key == 50}[f.comparison] & valid_a
+        want = int((a[keep].astype(object) * b[keep].astype(object)).sum())
+        s_plain, n_plain = t.sum_product(0, 1, fs, gather_b=True)
+        assert not t.last_sum_packed()
+        s_packed, n_packed = t.sum_product(0, 1, fs, gather_b=True, packed_a=True)
+        assert t.last_sum_packed()
+        assert s_plain == want and s_packed == want, (mode, f.comparison)
+        assert n_plain == n_packed
+    t.close()
