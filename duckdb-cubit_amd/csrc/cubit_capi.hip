@@ -3335,11 +3335,12 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
     sa.a = static_cast<const int64_t*>(ait->second.data);
     sa.a_valid = ait->second.validity;
     t->last_sum_packed = false;
-    if ((flags & CUBIT_SUM_PACKED_A) && ait->second.bp_n_groups) {
+    if (!(flags & CUBIT_SUM_PLAIN_A) && ait->second.bp_n_groups) {
         sa.a_bytes = static_cast<const uint8_t*>(ait->second.bp_bytes->p);
         sa.a_groups = static_cast<const BpGroup*>(ait->second.bp_groups->p);
         sa.a_vgroup = static_cast<const uint32_t*>(ait->second.bp_vgroup->p);
         sa.a_plain = sa.a;
+        sa.a_n_groups = ait->second.bp_n_groups;
         t->last_sum_packed = true;
     }
     sa.partials = ctx->partials;

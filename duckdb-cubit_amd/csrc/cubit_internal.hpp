@@ -195,6 +195,7 @@ struct SumArgs {
     const BpGroup* a_groups;
     const uint32_t* a_vgroup;
     const int64_t* a_plain;
+    uint64_t a_n_groups;
 };
 // grid = persistent workgroups; partials must hold 2·grid int64; out = {lo, hi}
 hipError_t launch_eval_sum_product(const EvalArgs& a, const SumArgs& s, unsigned grid, int64_t* out, hipStream_t stream);

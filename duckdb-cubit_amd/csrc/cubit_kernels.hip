@@ -1264,33 +1264,61 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             if ((miss >> m) & 1u) v += (uint64_t)s.delta[m];
         return (int64_t)v;
     };
-    // a[r], from the plain column or from its BITPACKING group (row → group record → packed bits)
+    // a from its BITPACKING segments: the group records of the current tile (the groups from the
+    // one holding the tile's first row on; 2,048 rows each inside a segment, so a tile of 131,072
+    // rows spans 64 of them, a few more where segments end mid-vector) are staged in LDS at the
+    // start of the tile, so a gathered value costs one load of its packed words, like the plain
+    // column's one load of its value
+    constexpr int NREC = 96;
+    __shared__ int32_t s_gst[NREC];   // group's first row - the tile's first row
+    __shared__ uint32_t s_gcnt[NREC];
+    __shared__ uint64_t s_gbase[NREC], s_gaux[NREC], s_goff[NREC];
+    __shared__ uint8_t s_gmode[NREC], s_gw[NREC];
+    uint32_t tile_g0 = 0, tile_ng = 0;  // staged records: groups tile_g0 … tile_g0 + tile_ng - 1
+    uint64_t tile_row0 = 0;
+    auto stage_groups = [&](uint64_t row0) {
+        tile_row0 = row0;
+        const uint64_t n_vec = (a.n_rows + 2047) / 2048;
+        const uint64_t v0 = row0 >> 11;
+        tile_g0 = s.a_vgroup[v0 < n_vec ? v0 : n_vec - 1];
+        tile_ng = (uint32_t)min<uint64_t>((uint64_t)NREC, s.a_n_groups - tile_g0);
+        if (t < (int)tile_ng) {
+            const BpGroup& gr = s.a_groups[tile_g0 + t];
+            s_gst[t] = (int32_t)((int64_t)gr.row_start - (int64_t)row0);
+            s_gcnt[t] = gr.count;
+            s_gbase[t] = gr.base;
+            s_gaux[t] = gr.aux;
+            s_goff[t] = gr.words_off;
+            s_gmode[t] = (uint8_t)gr.mode;
+            s_gw[t] = (uint8_t)gr.width;
+        }
+    };
+    // a[r], from the plain column or from its BITPACKING group (group record → packed bits)
     auto load_a = [&](uint64_t r) -> int64_t {
         if (!s.a_bytes) return __builtin_nontemporal_load(s.a + r);
-        uint32_t g = s.a_vgroup[r >> 11];
-        uint64_t rs = s.a_groups[g].row_start;
-        uint32_t cnt = s.a_groups[g].count;
-        while (r >= rs + cnt) {  // a vector that starts in the tail of a segment's last group
-            ++g;
-            rs = s.a_groups[g].row_start;
-            cnt = s.a_groups[g].count;
-        }
-        const BpGroup& gr = s.a_groups[g];
-        const uint64_t i = r - rs;
-        const uint32_t mode = gr.mode;
-        if (mode == 2) return (int64_t)gr.base;
-        if (mode == 3) return (int64_t)(gr.base + gr.aux * i);
+        const int64_t rl = (int64_t)r - (int64_t)tile_row0;
+        int32_t g = (int32_t)((rl - (int64_t)s_gst[0]) >> 11);  // exact inside one segment
+        if (g >= (int32_t)tile_ng) g = (int32_t)tile_ng - 1;
+        while (g > 0 && rl < (int64_t)s_gst[g]) --g;
+        while (g + 1 < (int32_t)tile_ng && rl >= (int64_t)s_gst[g] + (int64_t)s_gcnt[g]) ++g;
+        if (rl < (int64_t)s_gst[g] || rl >= (int64_t)s_gst[g] + (int64_t)s_gcnt[g])
+            return __builtin_nontemporal_load(s.a_plain + r);  // past the staged groups
+        const uint64_t i = (uint64_t)(rl - (int64_t)s_gst[g]);
+        const uint32_t mode = s_gmode[g];
+        const uint64_t base = s_gbase[g];
+        if (mode == 2) return (int64_t)base;
+        if (mode == 3) return (int64_t)(base + s_gaux[g] * i);
         if (mode != 5) return __builtin_nontemporal_load(s.a_plain + r);  // DELTA_FOR: needs its prefix
-        const uint32_t w = gr.width;
-        if (w == 0) return (int64_t)gr.base;
-        const uint32_t* words = reinterpret_cast<const uint32_t*>(s.a_bytes + gr.words_off);
+        const uint32_t w = s_gw[g];
+        if (w == 0) return (int64_t)base;
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(s.a_bytes + s_goff[g]);
         const uint64_t bit = i * w;
         const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
         uint64_t x = ((uint64_t)__builtin_nontemporal_load(words + wi) |
                       (off + w > 32 ? (uint64_t)__builtin_nontemporal_load(words + wi + 1) << 32 : 0ull)) >> off;
         if (off + w > 64) x |= (uint64_t)__builtin_nontemporal_load(words + wi + 2) << (64 - off);
         if (w < 64) x &= (1ull << w) - 1;
-        return (int64_t)(x + gr.base);
+        return (int64_t)(x + base);
     };
     auto accumulate = [&](int64_t row, int64_t bval_decoded) {
         const uint64_t r = (uint64_t)(row - a.row_base);
@@ -1325,6 +1353,9 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
         const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
         const bool has_next = i + gridDim.x < n_idx;
         const uint32_t next = has_next ? tile_at(a, i + gridDim.x) : 0;
+        // (read at the gathers, behind the "stage complete" barrier; the previous tile's gathers
+        // finished behind the barrier that ends its iteration)
+        if (s.a_bytes) stage_groups(tile_word0 * 64);
         uint64_t r[NW];
         eval_words<K, NW, FORM>(a.prog, v, r);
         tail_mask<NW, THREADS>(a, tile_word0, t, r);

@@ -26,6 +26,7 @@ INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2
 SUM_GATHER_B = 1
 SUM_NO_ZONEMAP = 2
 SUM_PACKED_A = 4
+SUM_PLAIN_A = 8
 OP_AND, OP_OR, OP_ANDNOT = -1, -2, -3
 SCAN_COUNT_ONLY = 1
 SCAN_ORDERED = 2

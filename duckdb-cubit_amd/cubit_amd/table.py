@@ -321,7 +321,7 @@ class CubitTable:
 
     def sum_product(self, col_a: int, col_b: int, filter_set: Optional[TableFilterSet] = None,
                     residual: Optional[Residual] = None, txn: Optional[L.Txn] = None,
-                    gather_b: bool = False, zonemap: bool = True, packed_a: bool = False) -> Tuple[int, int]:
+                    gather_b: bool = False, zonemap: bool = True, packed_a: bool = True) -> Tuple[int, int]:
         """SELECT sum(a*b), count(*) WHERE <filter> in one fused pass → (sum as a Python int
         of the 128-bit DECIMAL storage, qualifying rows)."""
         plan = serialize(filter_set, residual)
@@ -333,7 +333,7 @@ class CubitTable:
                                                  C.c_void_p(out.addr), C.c_void_p(cnt.addr),
                                                  (L.SUM_GATHER_B if gather_b else 0)
                                                  | (0 if zonemap else L.SUM_NO_ZONEMAP)
-                                                 | (L.SUM_PACKED_A if packed_a else 0)))
+                                                 | (0 if packed_a else L.SUM_PLAIN_A)))
         self.ctx.check()
         lo, hi = (int(x) for x in out.download(np.int64, 2))
         n = int(cnt.download(np.uint64, 1)[0])

@@ -342,18 +342,21 @@ int cubit_table_last_zones(cubit_table *t, uint32_t *evaluated, uint32_t *zones)
  * scan + probe + sum (those columns must then be NOT NULL). */
 #define CUBIT_SUM_GATHER_B 1u
 #define CUBIT_SUM_NO_ZONEMAP 2u /* as CUBIT_SCAN_NO_ZONEMAP */
-/* read a at the qualifying rows straight from its DuckDB BITPACKING segments (a column registered
- * with cubit_table_add_bitpacked_column; otherwise ignored): BitpackingScanPartial +
+/* When a was registered as DuckDB BITPACKING segments (cubit_table_add_bitpacked_column), the
+ * fused pass reads it at the qualifying rows straight from them: BitpackingScanPartial +
  * ColumnData::FilterScan (src/storage/compression/bitpacking.cpp:779-868, column_data.cpp:305-309)
  * as one pass that touches only the packed lines holding a qualifying row (a FOR value is its
  * group's base + w bits at bit i·w; rows of DELTA_FOR groups come from the unpacked column). The
- * gathers move whole 128-byte lines, so w-bit values touch fewer lines than 8-byte ones. */
+ * gathers move whole 128-byte lines, so w-bit values touch fewer lines than 8-byte ones (SF100 Q6,
+ * 24-bit l_extendedprice: 0.223 vs 0.245 ms). CUBIT_SUM_PLAIN_A reads the unpacked column instead;
+ * CUBIT_SUM_PACKED_A names the default. */
 #define CUBIT_SUM_PACKED_A 4u
+#define CUBIT_SUM_PLAIN_A 8u
 int cubit_table_sum_product(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
                             int col_a, int col_b, int64_t *d_out, uint64_t *d_count, uint32_t flags);
 /* How the last sum_product read b: number of values decoded from the index (0 = gathered). */
 int cubit_table_last_sum_decode(cubit_table *t, uint32_t *n_values);
-/* Whether the last sum_product read a from its BITPACKING segments (CUBIT_SUM_PACKED_A). */
+/* Whether the last sum_product read a from its BITPACKING segments. */
 int cubit_table_last_sum_packed(cubit_table *t, int *packed);
 
 #ifdef __cplusplus

@@ -162,8 +162,9 @@ def test_filter_straight_from_segments(ctx, name, mode):
 @pytest.mark.parametrize("mode", ["auto", "for", "delta_for", "constant_delta"])
 def test_fused_sum_reads_packed_column(ctx, mode):
     """SELECT sum(a * b) WHERE <filter> with a read at the qualifying rows straight from its
-    BITPACKING segments (CUBIT_SUM_PACKED_A: row → group record → the value's w bits; DELTA_FOR
-    rows from the unpacked column): equal to the same sum over the plain column and to numpy,
+    BITPACKING segments (the default for such a column: group record → the value's w bits;
+    DELTA_FOR rows from the unpacked column): equal to the same sum over the plain column
+    (CUBIT_SUM_PLAIN_A) and to numpy,
     for every group mode, with NULLs in a, several segments and a row base."""
     rng = np.random.default_rng({"auto": 1, "for": 2, "delta_for": 3, "constant_delta": 4}[mode])
     n = 600_011
@@ -189,9 +190,9 @@ def test_fused_sum_reads_packed_column(ctx, mode):
         fs = F.TableFilterSet({2: f})
         keep = {"<": key < 3, ">=": key >= 60, "=": key == 50}[f.comparison] & valid_a
         want = int((a[keep].astype(object) * b[keep].astype(object)).sum())
-        s_plain, n_plain = t.sum_product(0, 1, fs, gather_b=True)
+        s_plain, n_plain = t.sum_product(0, 1, fs, gather_b=True, packed_a=False)
         assert not t.last_sum_packed()
-        s_packed, n_packed = t.sum_product(0, 1, fs, gather_b=True, packed_a=True)
+        s_packed, n_packed = t.sum_product(0, 1, fs, gather_b=True)
         assert t.last_sum_packed()
         assert s_plain == want and s_packed == want, (mode, f.comparison)
         assert n_plain == n_packed
