@@ -87,7 +87,7 @@ def smallbench_summary(summary):
     cases = {"lookback_sf100_over_8": (573, 75004738, 4, 1435604), "lookback_cfg2_1e8": (763, 100000000, 1, 1001343)}
     for key, (tiles, n, k, q) in cases.items():
         grid = str(tiles * 512)
-        sel = lambda rs: [r for r in rs if "eval_decode_lookback" in r["Kernel_Name"] and r["Grid_Size"] == grid]
+        sel = lambda rs: [r for r in rs if "eval_decode_lookback" in r["Kernel_Name"] and (r.get("Grid_Size") or r.get("Grid_Size_X")) == grid]
         ff, ww, dd = sel(fetch), sel(write), sel(kt)
         if not ff or not ww:
             continue
