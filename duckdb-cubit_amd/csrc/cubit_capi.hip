@@ -86,6 +86,11 @@ struct cubit_ctx {
     uint64_t live_cap = 0;
     hipEvent_t live_ev = nullptr;
     bool live_pending = false;
+    // cubit_ctx_set_repeat: the next decode launch is issued `repeat` times back to back
+    // between two stream events (rep_ev); rep_launches of them went into the last measurement
+    uint32_t repeat = 0;
+    uint32_t rep_launches = 0;
+    hipEvent_t rep_ev[2] = {nullptr, nullptr};
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -250,7 +255,31 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         ctx->last_decode = 0;
         return CUBIT_OK;
     }
+    if (ctx->repeat) {
+        // steady-state kernel time: the same launch `repeat` times back to back, bracketed by two
+        // stream events (a dispatch-stamped pair adds a marker and its gap to each sample). Every
+        // repeat rewrites the same outputs from the same inputs; the look-back takes a new epoch.
+        if (start) {
+            ctx->n_timed--;
+            start = stop = nullptr;
+        }
+        if (!ctx->rep_ev[0]) {
+            HIP_CHECK(hipEventCreate(&ctx->rep_ev[0]));
+            HIP_CHECK(hipEventCreate(&ctx->rep_ev[1]));
+        }
+        HIP_CHECK(hipEventRecord(ctx->rep_ev[0], ctx->stream));
+        for (uint32_t i = 1; i < ctx->repeat; ++i) {
+            HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, nullptr, nullptr, ctx->decode_kernel,
+                                         ctx->n_cus));
+            a.epoch = ++ctx->epoch;
+        }
+    }
     HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel, ctx->n_cus));
+    if (ctx->repeat) {
+        HIP_CHECK(hipEventRecord(ctx->rep_ev[1], ctx->stream));
+        ctx->rep_launches = ctx->repeat;
+        ctx->repeat = 0;
+    }
     ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel, a.live != nullptr,
                                          ctx->n_cus);
     ctx->last_tiles = (uint32_t)tiles;
@@ -320,6 +349,8 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (ctx->live_dev) (void)hipFree(ctx->live_dev);
     if (ctx->live_host) (void)hipHostFree(ctx->live_host);
     if (ctx->live_ev) (void)hipEventDestroy(ctx->live_ev);
+    for (hipEvent_t e : ctx->rep_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -391,6 +422,27 @@ int cubit_ctx_kernel_times(cubit_ctx* ctx, float* ms, uint32_t cap, uint32_t* n)
         HIP_CHECK(hipEventElapsedTime(&ms[i], ctx->evs[i].first, ctx->evs[i].second));
     }
     *n = (uint32_t)ctx->n_timed;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_set_repeat(cubit_ctx* ctx, uint32_t reps) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (reps > 100000) return fail(CUBIT_ERR_INVALID, "%u repeats", reps);
+    CUBIT_LOCK(ctx);
+    ctx->repeat = reps;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_repeat_time(cubit_ctx* ctx, double* ms_per_launch, uint32_t* launches) {
+    if (!ctx || !ms_per_launch) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    if (!ctx->rep_launches) return fail(CUBIT_ERR_INVALID, "no repeated decode launch recorded (cubit_ctx_set_repeat)");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipEventSynchronize(ctx->rep_ev[1]));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, ctx->rep_ev[0], ctx->rep_ev[1]));
+    *ms_per_launch = (double)ms / ctx->rep_launches;
+    if (launches) *launches = ctx->rep_launches;
     return CUBIT_OK;
 }
 

@@ -79,6 +79,8 @@ GPU_SIGNATURES = {
     "cubit_last_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_float)]),
     "cubit_ctx_timing_reset": (C.c_int, [_P]),
     "cubit_ctx_kernel_times": (C.c_int, [_P, C.POINTER(C.c_float), _U32, C.POINTER(_U32)]),
+    "cubit_ctx_set_repeat": (C.c_int, [_P, _U32]),
+    "cubit_ctx_repeat_time": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(_U32)]),
     "cubit_ctx_check": (C.c_int, [_P]),
     "cubit_ctx_last_tiles": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_U32), C.POINTER(_U64)]),
     "cubit_dev_alloc": (C.c_int, [_P, _U64, C.POINTER(_P)]),

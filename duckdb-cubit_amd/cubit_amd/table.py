@@ -56,6 +56,17 @@ class Context:
         L.check(self.lib.cubit_ctx_kernel_times(self.handle, arr, cap, C.byref(n)))
         return [float(arr[i]) for i in range(min(cap, n.value))]
 
+    def set_repeat(self, reps: int) -> None:
+        """Issue the next decode launch `reps` times back to back between two stream events."""
+        L.check(self.lib.cubit_ctx_set_repeat(self.handle, int(reps)))
+
+    def repeat_time(self):
+        """(mean ms per launch, launches) of the last repeated decode."""
+        ms = C.c_double()
+        n = C.c_uint32()
+        L.check(self.lib.cubit_ctx_repeat_time(self.handle, C.byref(ms), C.byref(n)))
+        return float(ms.value), int(n.value)
+
     def sync(self) -> None:
         L.check(self.lib.cubit_sync(self.handle))
 

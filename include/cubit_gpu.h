@@ -141,6 +141,14 @@ int cubit_last_kernel_ms(cubit_ctx *ctx, float *ms);
 /* Every timed filter-kernel launch since the last reset: ms[i] for i < min(cap, *n). */
 int cubit_ctx_timing_reset(cubit_ctx *ctx);
 int cubit_ctx_kernel_times(cubit_ctx *ctx, float *ms, uint32_t cap, uint32_t *n);
+/* Steady-state decode time: the context's next decode launch is issued `reps` times back to
+ * back on its stream between two stream events (reps <= 100000; 0 disarms). Every repeat
+ * rewrites the same outputs from the same inputs, so results are unchanged. Afterwards
+ * cubit_ctx_repeat_time gives the mean ms per launch and the number of launches bracketed.
+ * A dispatch-stamped pair (cubit_ctx_enable_timing) puts a marker and its gap inside each
+ * sample, which matters for kernels of a few microseconds. */
+int cubit_ctx_set_repeat(cubit_ctx *ctx, uint32_t reps);
+int cubit_ctx_repeat_time(cubit_ctx *ctx, double *ms_per_launch, uint32_t *launches);
 /* Compile-time contract checks (vector 2048 = 32 words, row group 122880 = 1920 words). */
 int cubit_abi_version(void);
 int cubit_vector_size(void);

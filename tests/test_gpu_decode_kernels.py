@@ -148,3 +148,31 @@ def test_auto_policy_large_table_scan(ctx):
             assert np.array_equal(got, ref)
         assert t.count(fs) == len(ref)
     t.close()
+
+
+def test_repeated_launch_timing_keeps_results(ctx):
+    """cubit_ctx_set_repeat (the bench's kernel timing): the next decode is launched `reps` times
+    back to back between two stream events; each repeat rewrites the same outputs from the same
+    inputs (the look-back under a new epoch each time), so the row ids equal the oracle's."""
+    rng = np.random.default_rng(9)
+    n = 100_000_000
+    pw, nw = padded_words(n), (n + 63) // 64
+    host = [shaped_leaf(rng, n), rand_words(rng, nw, 1)]  # n is a multiple of 64: no tail mask
+    dleaves = [ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])) for w in host]
+    out = ctx.alloc(n // 2 * 8)
+    cnt = ctx.alloc(16)
+    prog = [0, 1, L.OP_AND]
+    ref, _ = O.bitmap_eval(host, prog, n, 5)
+    with pytest.raises(L.CubitError):
+        ctx.repeat_time()  # nothing repeated yet on this context
+    for kernel in (L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_LOOKBACK):
+        ctx.set_decode_kernel(kernel)
+        for ordered in (False, True):
+            ctx.set_repeat(7)
+            got = run_program(ctx, dleaves, 2, 0, prog, n, 5, out, cnt, ordered)
+            assert np.array_equal(got, ref), (kernel, ordered)
+            ms, launches = ctx.repeat_time()
+            assert launches == 7 and 0 < ms < 10
+            # disarmed after one decode: the next call launches once
+            assert np.array_equal(run_program(ctx, dleaves, 2, 0, prog, n, 5, out, cnt, ordered), ref)
+    ctx.set_decode_kernel(L.DECODE_AUTO)
