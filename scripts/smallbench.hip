@@ -77,6 +77,13 @@ __global__ __launch_bounds__(512, 6) void floor_kernel(EvalArgs a, int64_t* out)
     }
 }
 
+// look-back variants with the kernel's diagnostic switches (DBG: 1 no wait, 2 no ids, 4 no sleep)
+template <int K, int SAUX, int DBG>
+void lookback_variant(EvalArgs& a, uint64_t* dir, hipStream_t st) {
+    hipLaunchKernelGGL((eval_decode_lookback<K, FORM_CONJ, kLookbackStage, lookback_wpc(K), SAUX, DBG>), dim3(a.num_tiles),
+                       dim3(512), 0, st, a, dir);
+}
+
 struct Variant {
     std::string name;
     std::function<void(EvalArgs&, hipStream_t)> launch;
@@ -157,6 +164,22 @@ int main(int argc, char** argv) {
                               a.epoch = ++epoch;
                               CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 3, cus));
                           }, true});
+        if (tiles <= kLookbackMaxTiles && getenv("SMALLBENCH_LB_VARIANTS")) {
+            auto add = [&](const char* nm, void (*f1)(EvalArgs&, uint64_t*, hipStream_t),
+                           void (*f4)(EvalArgs&, uint64_t*, hipStream_t), bool chk) {
+                vs.push_back({std::string("lookback ") + nm, [&, f1, f4](EvalArgs& a, hipStream_t st) {
+                                  a.epoch = ++epoch;
+                                  (c.k == 4 ? f4 : f1)(a, dir, st);
+                              }, chk});
+            };
+            add("SAUX plain", lookback_variant<1, -1, 0>, lookback_variant<4, -1, 0>, true);
+            add("SAUX nt", lookback_variant<1, 2, 0>, lookback_variant<4, 2, 0>, true);
+            add("SAUX 0", lookback_variant<1, 0, 0>, lookback_variant<4, 0, 0>, true);
+            add("no sleep", lookback_variant<1, 16, 4>, lookback_variant<4, 16, 4>, true);
+            add("DBG no wait", lookback_variant<1, 16, 1>, lookback_variant<4, 16, 1>, false);
+            add("DBG no ids", lookback_variant<1, 16, 2>, lookback_variant<4, 16, 2>, false);
+            add("DBG no wait, no ids", lookback_variant<1, 16, 3>, lookback_variant<4, 16, 3>, false);
+        }
         vs.push_back({"AUTO (library policy)", [&](EvalArgs& a, hipStream_t st) {
                           a.epoch = ++epoch;
                           CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 0, cus));
