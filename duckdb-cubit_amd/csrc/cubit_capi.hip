@@ -187,7 +187,8 @@ enum class RunMode { kDecode, kCount };
 
 // Launch the evaluator over a compiled program (asynchronous on the context stream).
 //   kDecode: row ids as per-tile ascending runs + tile directory (ordered = lay them out in
-//            row order with one extra pass); kCount: count(*) and/or result words.
+//            row order: the look-back decode writes them so, up to kLookbackMaxTiles tiles;
+//            past that, one extra pass); kCount: count(*) and/or result words.
 // live_zones (optional, non-empty, ascending): evaluate only these zones (zonemap skip); the
 // other tiles hold no qualifying row. Not with result_words (the skipped words stay unwritten).
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
@@ -227,12 +228,15 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     // directory is sized for every padded tile, as a live-tile list may name any of them
     const uint64_t tiles = (a.n_words + decode_tile_words() - 1) / decode_tile_words();
     if (int rc = ensure_dir(ctx, pw / decode_tile_words())) return rc;
-    if (ordered && rowids)
+    // an ordered scan takes the look-back decode (runs in tile order) unless a kernel is forced
+    const int kernel = ordered && rowids && ctx->decode_kernel == 0 && tiles <= kLookbackMaxTiles ? 3 : ctx->decode_kernel;
+    const bool order_pass = ordered && rowids && !(kernel == 3 && tiles <= kLookbackMaxTiles);
+    if (order_pass)
         if (int rc = ensure_tmp(ctx, capacity)) return rc;
     a.num_tiles = (uint32_t)tiles;
     a.flags = ctx->flags;
     a.epoch = ++ctx->epoch;
-    a.rowids = ordered && rowids ? ctx->tmp_ids : rowids;
+    a.rowids = order_pass ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
     if (live_zones) {
         static_assert(kZoneWords == 2048, "a zone is one decode tile");
@@ -269,22 +273,20 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         }
         HIP_CHECK(hipEventRecord(ctx->rep_ev[0], ctx->stream));
         for (uint32_t i = 1; i < ctx->repeat; ++i) {
-            HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, nullptr, nullptr, ctx->decode_kernel,
-                                         ctx->n_cus));
+            HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, nullptr, nullptr, kernel, ctx->n_cus));
             a.epoch = ++ctx->epoch;
         }
     }
-    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, ctx->decode_kernel, ctx->n_cus));
+    HIP_CHECK(launch_eval_decode(a, ctx->dir, grid, ctx->stream, start, stop, kernel, ctx->n_cus));
     if (ctx->repeat) {
         HIP_CHECK(hipEventRecord(ctx->rep_ev[1], ctx->stream));
         ctx->rep_launches = ctx->repeat;
         ctx->repeat = 0;
     }
-    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, ctx->decode_kernel, a.live != nullptr,
-                                         ctx->n_cus);
+    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, ctx->n_cus);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
-    if (ordered && rowids)
+    if (order_pass)
         HIP_CHECK(launch_order_runs(ctx->dir, (uint32_t)tiles, ctx->dst_off, ctx->tmp_ids, capacity, rowids,
                                     ctx->stream));
     if (check_capacity && rowids) {

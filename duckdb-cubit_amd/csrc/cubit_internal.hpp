@@ -75,8 +75,10 @@ struct EvalArgs {
     uint64_t* flags;
     uint64_t epoch;
 };
-// eval_decode_lookback: one workgroup per tile, at most this many tiles per launch
-constexpr uint32_t kLookbackMaxTiles = 4096;
+// eval_decode_lookback: one workgroup per tile, at most this many tiles per launch (1.07e9 rows;
+// every workgroup reads the counts of all earlier tiles, so the flag reads grow with the square of
+// the tile count: 4,578 tiles (SF100) cost 68.5 µs against 64.7 µs for the run-claimed decode)
+constexpr uint32_t kLookbackMaxTiles = 8192;
 // Zonemaps: one zone = one decode tile (2,048 words = 131,072 rows). Class byte per zone:
 // bit 0 = no row of the zone is set, bit 1 = every row of the zone is set (a zone past the
 // last row has both).
@@ -93,9 +95,10 @@ int decode_block_threads();
 // evaluate + decode into per-tile runs; dir (optional) gets {start, length} per tile
 // ev0 / ev1 (optional): events stamped by the kernel dispatch itself (hipExtLaunchKernel), so
 // their elapsed time is the kernel's execution, as rocprofv3's kernel trace reports it
-// kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed;
-// decode_kernel_for resolves it (1 or 2) for a launch
-// 3 = look-back (one tile per workgroup, small partitions: lookback_max_tiles)
+// kernel: 0 = by the measured policy (launch_decode_kf), 1 = pair-claimed, 2 = run-claimed,
+// 3 = look-back (one tile per workgroup, runs in tile order: small partitions by policy —
+// lookback_max_tiles — and ordered scans up to kLookbackMaxTiles); decode_kernel_for resolves
+// it for a launch
 int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live = false,
                       int n_cus = 256);
 // the largest tile count the measured policy decodes with the look-back kernel (grid = tiles)

@@ -52,6 +52,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
     return x;
 }
 
+// Sum over the wave of values below 2^41 (look-back counts): two DPP scans of 24-bit low and high
+// parts, the totals read from lane 63 — no ds_bpermute round trips. Every lane must be active.
+__device__ __forceinline__ uint64_t wave_sum_flags(uint64_t x) {
+    const uint32_t lo = wave_incl_scan32((uint32_t)x & 0xffffffu);
+    const uint32_t hi = wave_incl_scan32((uint32_t)(x >> 24));
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
+           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+}
+
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
@@ -1084,9 +1093,19 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
 //   indices, which are dispatched before it, so the walk completes whatever the residency.
 // A tile with more rows than the stage leaves through it in rounds after the offset is known.
 // A poll that exceeds kLookbackSpins marks the count ~0 (the host reports CUBIT_ERR_DEVICE).
+// Runs land in tile order, so the output is one ascending array: ordered scans take this kernel
+// at any size up to kLookbackMaxTiles (SF100, 4,578 tiles: 68.5 µs against 95 µs for the
+// run-claimed decode plus the ordering pass; scripts/smallbench.hip).
 constexpr int kFlagCntBits = 20;  // a tile holds ≤ 131,072 rows
 constexpr uint32_t kLookbackSpins = 1u << 22;
-template <int K, int FORM, int STAGE, int WPC, int SAUX = 16>
+// DBG (diagnostic builds, scripts/smallbench.hip; 0 in the library): 1 no spin, 2 no ids, 4 no
+// sleep, 8 no flag loads, 16 no LDS decode.
+// Measured and not kept (scripts/smallbench.hip; profiles/r03e_*, r03g_*, r03h_*): eight copies of
+// every flag, each reader on its own; a two-level walk (groups of 64 tiles + group totals); flag
+// loads issued before the LDS decode; a decoupled look-back (aggregate, then inclusive-prefix flags,
+// walks that stop at the nearest prefix) — slower at every size measured, 573 to 4,578 tiles (at
+// 4,578 the sum over every earlier flag costs 68.5 µs, the decoupled walk 91 µs).
+template <int K, int FORM, int STAGE, int WPC, int SAUX = 16, int DBG = 0>
 __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a, uint64_t* __restrict__ dir) {
     constexpr int THREADS = 512, PAIRS = 2, NW = 2 * PAIRS, NWAVES = THREADS / 64;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
@@ -1138,7 +1157,7 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBits) | (uint64_t)tile_count, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     const bool staged = tile_count <= (uint32_t)STAGE;
-    if (staged && write_ids && tile_count) {
+    if (!(DBG & 16) && staged && write_ids && tile_count) {
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
             uint32_t off = pair_off[p];
@@ -1155,20 +1174,20 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     }
     // look-back over every earlier workgroup's flag
     uint64_t pre = 0;
-    for (uint32_t j = t; j < b; j += THREADS) {
+    for (uint32_t j = t; j < b && !(DBG & 8); j += THREADS) {
         uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t spins = 0;
-        while ((f >> kFlagCntBits) != a.epoch) {
+        while (!(DBG & 1) && (f >> kFlagCntBits) != a.epoch) {
             if (++spins == kLookbackSpins) {
                 s_bad = 1;
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            if (!(DBG & 4)) __builtin_amdgcn_s_sleep(2);
             f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         pre += f & kCntMask;
     }
-    pre = wave_sum(pre);
+    pre = wave_sum_flags(pre);
     if (lane == 0) s_pre[wave] = pre;
     __syncthreads();  // also: the stage is complete
     uint64_t base = 0;
@@ -1186,7 +1205,7 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         }
         if (b == gridDim.x - 1) *a.count = base + tile_count;
     }
-    if (!write_ids || !tile_count) return;
+    if (!write_ids || !tile_count || (DBG & 2)) return;
     if (staged) {
         emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, tile_count, base, row0, t);
         return;

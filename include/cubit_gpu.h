@@ -76,7 +76,10 @@ extern "C" {
  * parallel table scan, whose morsels reach the sink in nondeterministic order with a batch
  * index (src/function/table/table_scan.cpp:179-189). cubit_ctx_last_tiles() returns the
  * tile directory ({start, length} per tile) that restores row order for free.
- * CUBIT_SCAN_ORDERED lays the runs out ascending with one extra device pass.
+ * CUBIT_SCAN_ORDERED lays the runs out ascending: the look-back decode places each tile's run at
+ * the sum of the earlier tiles' counts, so no extra pass (partitions up to 8,192 tiles = 1.07e9
+ * rows; larger ones take one extra device pass). The small partitions that AUTO decodes with the
+ * look-back kernel are ascending without the flag, too.
  * Capacity: *d_count is always the full number of qualifying rows. When it exceeds
  * `capacity` the calls still return CUBIT_OK (they do not wait for the kernel) and the
  * buffer holds an unspecified subset of the ids (runs are claimed in nondeterministic order;
@@ -124,14 +127,15 @@ const char *cubit_last_error(void);
  * look-back kernel — one workgroup per 131,072-row tile, output offsets by look-back over the
  * earlier tiles' counts — when the partition's tiles fit the co-resident grid; else the
  * run-claimed kernel when a workgroup walks three or more tiles, else the pair-claimed one),
- * or one of them always (tests and benchmarks; LOOKBACK up to 4,096 tiles). Results are
- * identical. */
+ * or one of them always (tests and benchmarks; LOOKBACK up to 8,192 tiles). Results are
+ * identical. Under AUTO a CUBIT_SCAN_ORDERED scan takes the look-back kernel at any size up to
+ * 8,192 tiles (its runs land in tile order). */
 #define CUBIT_DECODE_AUTO 0
 #define CUBIT_DECODE_PAIRS 1
 #define CUBIT_DECODE_RUNS 2
 #define CUBIT_DECODE_LOOKBACK 3
 int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
-/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS or _LOOKBACK; 0 when
+/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS, or _LOOKBACK; 0 when
  * the partition had no row and nothing was launched). */
 int cubit_ctx_last_decode_kernel(cubit_ctx *ctx, int *kernel);
 /* Filter-kernel durations measured with HIP events recorded around each launch on the

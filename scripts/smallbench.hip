@@ -77,7 +77,145 @@ __global__ __launch_bounds__(512, 6) void floor_kernel(EvalArgs a, int64_t* out)
     }
 }
 
-// look-back variants with the kernel's diagnostic switches (DBG: 1 no wait, 2 no ids, 4 no sleep)
+// the look-back kernel as it stood before its wave sum moved to DPP, for comparison (a copy of
+// the kernel text, diagnostic only)
+constexpr int kFlagCntBitsR03 = 20;
+template <int K, int FORM, int STAGE, int WPC, int SAUX = 16>
+__global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback_r03(EvalArgs a, uint64_t* __restrict__ dir) {
+    constexpr int THREADS = 512, PAIRS = 2, NW = 2 * PAIRS, NWAVES = THREADS / 64;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
+    constexpr uint64_t kCntMask = (1ull << kFlagCntBitsR03) - 1;
+    __shared__ uint32_t s_wave_tot[NWAVES];
+    __shared__ uint64_t s_pre[NWAVES];
+    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_stage[STAGE];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t tile = tile_at(a, b);
+    const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
+    const bool write_ids = a.rowids != nullptr;
+    if (t == 0) s_bad = 0;
+    u64x2 v[K][PAIRS];
+    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+    uint64_t r[NW];
+    eval_words<K, NW, FORM>(a.prog, v, r);
+    tail_mask<NW, THREADS>(a, tile_word0, t, r);
+    if (a.result_words) store_words<PAIRS, THREADS>(a.result_words, tile_word0, t, r);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p)
+        packed |= (uint32_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1])) << (16 * p);
+    const uint32_t incl = wave_incl_scan32(packed);
+    if (lane == 63) s_wave_tot[wave] = incl;
+    __syncthreads();
+    uint32_t wave_pre[2] = {0, 0}, block_tot[2] = {0, 0};
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) {
+        const uint32_t x = s_wave_tot[w];
+        const uint32_t lo = x & 0xffffu, hi = x >> 16;
+        if (w < wave) {
+            wave_pre[0] += lo;
+            wave_pre[1] += hi;
+        }
+        block_tot[0] += lo;
+        block_tot[1] += hi;
+    }
+    const uint32_t excl = incl - packed;
+    uint32_t pair_off[PAIRS];
+    uint32_t tile_count = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p) {
+        pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
+        tile_count += block_tot[p];
+    }
+    if (t == 0)
+        __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBitsR03) | (uint64_t)tile_count, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const bool staged = tile_count <= (uint32_t)STAGE;
+    if (staged && write_ids && tile_count) {
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            uint32_t off = pair_off[p];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                uint64_t w = r[2 * p + e];
+                const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                while (w) {
+                    s_stage[off++] = wrow + (uint32_t)__builtin_ctzll(w);
+                    w &= w - 1;
+                }
+            }
+        }
+    }
+    // look-back over every earlier workgroup's flag
+    uint64_t pre = 0;
+    for (uint32_t j = t; j < b; j += THREADS) {
+        uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while ((f >> kFlagCntBitsR03) != a.epoch) {
+            if (++spins == kLookbackSpins) {
+                s_bad = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        pre += f & kCntMask;
+    }
+    pre = wave_sum(pre);
+    if (lane == 0) s_pre[wave] = pre;
+    __syncthreads();  // also: the stage is complete
+    uint64_t base = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) base += s_pre[w];
+    if (s_bad) {
+        if (t == 0) *a.count = ~0ull;
+        return;
+    }
+    const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
+    if (t == 0) {
+        if (dir) {
+            dir[2 * tile] = tile_count ? base : 0;
+            dir[2 * tile + 1] = tile_count;
+        }
+        if (b == gridDim.x - 1) *a.count = base + tile_count;
+    }
+    if (!write_ids || !tile_count) return;
+    if (staged) {
+        emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, tile_count, base, row0, t);
+        return;
+    }
+    // dense tile: rounds of STAGE ids through the stage
+    for (uint32_t r0 = 0; r0 < tile_count; r0 += (uint32_t)STAGE) {
+        const uint32_t r1 = min(tile_count, r0 + (uint32_t)STAGE);
+        if (r0) __syncthreads();  // the previous round's copy-out is done
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            uint32_t off = pair_off[p];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                uint64_t w = r[2 * p + e];
+                const uint32_t c = (uint32_t)__popcll(w);
+                const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                if (off < r1 && off + c > r0) {
+                    uint32_t k = off;
+                    for (; k < r0; ++k) w &= w - 1;  // the word straddles the round's start
+                    for (; w && k < r1; ++k) {
+                        s_stage[k - r0] = wrow + (uint32_t)__builtin_ctzll(w);
+                        w &= w - 1;
+                    }
+                }
+                off += c;
+            }
+        }
+        __syncthreads();
+        emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, r1 - r0, base + r0, row0, t);
+    }
+}
+
+
+// look-back variants: the kernel's diagnostic switches (DBG: 1 no spin, 2 no ids, 4 no sleep,
+// 8 no flag loads, 16 no LDS decode)
 template <int K, int SAUX, int DBG>
 void lookback_variant(EvalArgs& a, uint64_t* dir, hipStream_t st) {
     hipLaunchKernelGGL((eval_decode_lookback<K, FORM_CONJ, kLookbackStage, lookback_wpc(K), SAUX, DBG>), dim3(a.num_tiles),
@@ -113,6 +251,9 @@ int main(int argc, char** argv) {
     uint64_t* flags;
     CK(hipMalloc(&flags, kLookbackMaxTiles * 8));
     CK(hipMemset(flags, 0, kLookbackMaxTiles * 8));
+    uint64_t* flags_r03;
+    CK(hipMalloc(&flags_r03, kLookbackMaxTiles * 8));
+    CK(hipMemset(flags_r03, 0, kLookbackMaxTiles * 8));
     uint64_t* ticket;
     CK(hipMalloc(&ticket, kTicketWords * 8));
     CK(hipMemset(ticket, 0, kTicketWords * 8));
@@ -134,6 +275,10 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&ids, cap * 8));
         CK(hipMalloc(&ids_ref, cap * 8));
         CK(hipMalloc(&fl_out, cap * 8));
+        int64_t* ids_ord;
+        uint64_t* dst_off;
+        CK(hipMalloc(&ids_ord, cap * 8));
+        CK(hipMalloc(&dst_off, (uint64_t)tiles * 8 + 64));
         CK(hipMalloc(&cnt, 16));
         CK(hipMalloc(&dir, 2 * (uint64_t)tiles * 8 + 64));
         CK(hipMalloc(&dir_ref, 2 * (uint64_t)tiles * 8 + 64));
@@ -159,6 +304,10 @@ int main(int argc, char** argv) {
         vs.push_back({"runs", [&](EvalArgs& a, hipStream_t st) {
                           CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 2, cus));
                       }, true});
+        vs.push_back({"runs + order pass (one ascending array)", [&](EvalArgs& a, hipStream_t st) {
+                          CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 2, cus));
+                          CK(launch_order_runs(dir, tiles, dst_off, a.rowids, a.capacity, ids_ord, st));
+                      }, false});
         if (tiles <= kLookbackMaxTiles)
             vs.push_back({"lookback (grid " + std::to_string(tiles) + ")", [&](EvalArgs& a, hipStream_t st) {
                               a.epoch = ++epoch;
@@ -172,12 +321,22 @@ int main(int argc, char** argv) {
                                   (c.k == 4 ? f4 : f1)(a, dir, st);
                               }, chk});
             };
-            add("SAUX plain", lookback_variant<1, -1, 0>, lookback_variant<4, -1, 0>, true);
-            add("SAUX nt", lookback_variant<1, 2, 0>, lookback_variant<4, 2, 0>, true);
-            add("SAUX 0", lookback_variant<1, 0, 0>, lookback_variant<4, 0, 0>, true);
-            add("no sleep", lookback_variant<1, 16, 4>, lookback_variant<4, 16, 4>, true);
-            add("DBG no wait", lookback_variant<1, 16, 1>, lookback_variant<4, 16, 1>, false);
+            // flag copies (read copy b % R), a two-level look-back (groups of 64 tiles + group
+            // totals) and flag loads issued before the LDS decode measured no faster:
+            // profiles/r03e_smallbench_flag_copies_two_level.txt
+            vs.push_back({"lookback r03 kernel (shfl wave sum)", [&](EvalArgs& a, hipStream_t st) {
+                              a.epoch = ++epoch;
+                              EvalArgs a2 = a;
+                              a2.flags = flags_r03;
+                              if (c.k == 4)
+                                  hipLaunchKernelGGL((eval_decode_lookback_r03<4, FORM_CONJ, kLookbackStage, 3>), dim3(a.num_tiles),
+                                                     dim3(512), 0, st, a2, dir);
+                              else
+                                  hipLaunchKernelGGL((eval_decode_lookback_r03<1, FORM_CONJ, kLookbackStage, 3>), dim3(a.num_tiles),
+                                                     dim3(512), 0, st, a2, dir);
+                          }, true});
             add("DBG no ids", lookback_variant<1, 16, 2>, lookback_variant<4, 16, 2>, false);
+            add("DBG no flag loads, no ids", lookback_variant<1, 16, 10>, lookback_variant<4, 16, 10>, false);
             add("DBG no wait, no ids", lookback_variant<1, 16, 3>, lookback_variant<4, 16, 3>, false);
         }
         vs.push_back({"AUTO (library policy)", [&](EvalArgs& a, hipStream_t st) {
@@ -271,6 +430,8 @@ int main(int argc, char** argv) {
         CK(hipFree(ids));
         CK(hipFree(ids_ref));
         CK(hipFree(fl_out));
+        CK(hipFree(ids_ord));
+        CK(hipFree(dst_off));
         CK(hipFree(cnt));
         CK(hipFree(dir));
         CK(hipFree(dir_ref));

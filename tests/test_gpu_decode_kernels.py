@@ -3,7 +3,8 @@
 the earlier tiles' published counts) — against the oracle's CPU bitmap evaluator, forced one at
 a time through cubit_ctx_set_decode_kernel and under the automatic policy. At 140 M rows the
 look-back grid (1,069 workgroups) exceeds what is co-resident, so its waits span workgroups
-that start only after others finish.
+that start only after others finish. The look-back runs land in tile order, so its default
+output is already the ascending array, and ordered scans take it up to 8,192 tiles.
 
 The run-claimed kernel keeps decoding a workgroup's tiles into one LDS stage until the next
 tile does not fit, so its interesting cases need workgroups that walk many tiles: tables of
@@ -117,6 +118,8 @@ def test_pairs_and_runs_match_oracle(ctx, n):
             for ordered in (False, True):
                 got = run_program(ctx, dleaves, k, neg, prog, n, 1_000_000_007, out, cnt, ordered)
                 assert np.array_equal(got, ref), (kernel, ordered, k, neg, prog)
+                if ctx.last_decode_kernel() == L.DECODE_LOOKBACK:
+                    assert np.array_equal(out.download(np.int64, len(ref)), ref), (kernel, ordered)
     ctx.set_decode_kernel(L.DECODE_AUTO)
 
 
@@ -176,3 +179,26 @@ def test_repeated_launch_timing_keeps_results(ctx):
             # disarmed after one decode: the next call launches once
             assert np.array_equal(run_program(ctx, dleaves, 2, 0, prog, n, 5, out, cnt, ordered), ref)
     ctx.set_decode_kernel(L.DECODE_AUTO)
+
+
+def test_ordered_scan_past_the_old_lookback_limit(ctx):
+    """540 M rows = 4,120 tiles: CUBIT_SCAN_ORDERED under AUTO takes the look-back decode (no
+    ordering pass) at a size where the unordered scan takes the run-claimed kernel; both equal
+    the oracle."""
+    rng = np.random.default_rng(11)
+    n = 540_000_001
+    pw, nw = padded_words(n), (n + 63) // 64
+    host = [shaped_leaf(rng, n), rand_words(rng, nw, 1)]
+    host[1][-1] &= np.uint64((1 << (n & 63)) - 1)
+    dleaves = [ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])) for w in host]
+    prog = [0, 1, L.OP_AND]
+    ref, _ = O.bitmap_eval(host, prog, n, 3)
+    out = ctx.alloc((len(ref) + 1024) * 8)
+    cnt = ctx.alloc(16)
+    ctx.set_decode_kernel(L.DECODE_AUTO)
+    got = run_program(ctx, dleaves, 2, 0, prog, n, 3, out, cnt, True)
+    assert ctx.last_decode_kernel() == L.DECODE_LOOKBACK
+    assert np.array_equal(got, ref)
+    got = run_program(ctx, dleaves, 2, 0, prog, n, 3, out, cnt, False)
+    assert ctx.last_decode_kernel() == L.DECODE_RUNS
+    assert np.array_equal(got, ref)
