@@ -91,6 +91,10 @@ struct cubit_ctx {
     uint32_t repeat = 0;
     uint32_t rep_launches = 0;
     hipEvent_t rep_ev[2] = {nullptr, nullptr};
+    // copy streams handed back by cubit_copy_stream_destroy, each with its ordering event
+    // (creating a HIP stream costs milliseconds; the table function's tasks take one per scan)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> copy_pool;
+    std::unordered_map<hipStream_t, hipEvent_t> copy_live;
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -353,6 +357,11 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
     if (ctx->live_ev) (void)hipEventDestroy(ctx->live_ev);
     for (hipEvent_t e : ctx->rep_ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& se : ctx->copy_live) ctx->copy_pool.push_back(se);
+    for (auto& se : ctx->copy_pool) {
+        (void)hipStreamDestroy(se.first);
+        (void)hipEventDestroy(se.second);
+    }
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -487,6 +496,51 @@ int cubit_memcpy_d2h(cubit_ctx* ctx, void* dst, const void* src, uint64_t bytes)
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return CUBIT_OK;
+}
+
+int cubit_copy_stream_create(cubit_ctx* ctx, void** stream) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    if (int rc = set_device(ctx)) return rc;
+    std::pair<hipStream_t, hipEvent_t> se{nullptr, nullptr};
+    if (!ctx->copy_pool.empty()) {
+        se = ctx->copy_pool.back();
+        ctx->copy_pool.pop_back();
+    } else {
+        HIP_CHECK(hipStreamCreateWithFlags(&se.first, hipStreamNonBlocking));
+        if (hipEventCreateWithFlags(&se.second, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(se.first);
+            return fail(CUBIT_ERR_DEVICE, "copy stream: event creation failed");
+        }
+    }
+    ctx->copy_live[se.first] = se.second;
+    // the stream starts behind the context stream's enqueued work (the scan and its probes)
+    HIP_CHECK(hipEventRecord(se.second, ctx->stream));
+    HIP_CHECK(hipStreamWaitEvent(se.first, se.second, 0));
+    *stream = se.first;
+    return CUBIT_OK;
+}
+
+int cubit_copy_stream_destroy(cubit_ctx* ctx, void* stream) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (!stream) return CUBIT_OK;
+    CUBIT_LOCK(ctx);
+    auto it = ctx->copy_live.find(static_cast<hipStream_t>(stream));
+    if (it == ctx->copy_live.end()) return fail(CUBIT_ERR_INVALID, "not a copy stream of this context");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipStreamSynchronize(it->first));  // its copies are done before another task reuses it
+    ctx->copy_pool.push_back(*it);
+    ctx->copy_live.erase(it);
+    return CUBIT_OK;
+}
+
+int cubit_memcpy_d2h_stream(cubit_ctx* ctx, void* stream, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
     return CUBIT_OK;
 }
 

@@ -2,7 +2,7 @@
  * q6_scan — TPC-H Q6 through the C ABI alone (no Python, no PyTorch): what a C/C++ host such
  * as a DuckDB extension does with libcubitgpu.so and libcubit_scan.so.
  *
- *   q6_scan <sf>      e.g. q6_scan 1
+ *   q6_scan <sf> [threads]      e.g. q6_scan 1, q6_scan 100 16
  *
  * 1. generates lineitem's Q6 columns with libcubit_datagen (the repo's dbgen restatement);
  * 2. registers them on the GPU and builds the bitmap indexes (cubit_table_add_column /
@@ -12,10 +12,17 @@
  *    (init_global / init_local / function until an empty chunk);
  * 4. prints one line: rows, rows from the table function, Σ row ids, revenue.
  * tests/test_gpu_c_example.py checks that line against the reference's answer files.
+ * 5. with [threads]: the whole query through the callbacks as a DuckDB pipeline runs it —
+ *    init_global, then `threads` pipeline tasks (pthreads), each with its own local state,
+ *    draining 2,048-row chunks of (l_extendedprice, l_discount) into a partial revenue —
+ *    timed end to end (best of 3) and checked against the fused revenue; one more line.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <inttypes.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 
 #include "cubit_gpu.h"
 #include "cubit_scan.h"
@@ -51,6 +58,42 @@ static int32_t date_of(int y, int m) {
     days += cum[m - 1];
     if (m > 2 && (y % 4 == 0 && (y % 100 != 0 || y % 400 == 0))) days += 1;
     return days;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* one pipeline task: TableScanInitLocal, then TableScanFunc until an empty chunk, aggregating
+ * sum(l_extendedprice * l_discount) of its chunks (DuckDB's PhysicalUngroupedAggregate sink) */
+typedef struct {
+    cubit_scan *scan;
+    uint64_t rows;
+    __int128 revenue;
+    int rc;
+} task_t;
+
+static void *pipeline_task(void *arg) {
+    task_t *tk = (task_t *)arg;
+    cubit_scan_local *local;
+    tk->rc = cubit_scan_init_local(tk->scan, &local);
+    if (tk->rc != CUBIT_OK) return NULL;
+    int64_t *cols[2] = {malloc(2048 * 8), malloc(2048 * 8)};
+    uint64_t got = 0;
+    do {
+        tk->rc = cubit_scan_function(tk->scan, local, cols, &got);
+        if (tk->rc != CUBIT_OK) break;
+        __int128 s = 0;
+        for (uint64_t i = 0; i < got; ++i) s += (__int128)cols[0][i] * cols[1][i];
+        tk->revenue += s;
+        tk->rows += got;
+    } while (got);
+    cubit_scan_local_destroy(local);
+    free(cols[0]);
+    free(cols[1]);
+    return NULL;
 }
 
 int main(int argc, char **argv) {
@@ -150,6 +193,49 @@ int main(int argc, char **argv) {
     printf("rows %" PRIu64 " table_function_rows %" PRIu64 " sum_rowid %" PRIu64 " table_function_sum_rowid %" PRIu64
            " revenue %" PRId64 ".%04" PRId64 "\n",
            q, rows_tf, sum_ids, sum_tf, whole, frac);
+
+    /* 5. the query as a pipeline of `threads` tasks over the callbacks */
+    const int threads = argc > 2 ? atoi(argv[2]) : 0;
+    if (threads > 0) {
+        const uint64_t proj_ids[] = {3, 1};
+        double best = 1e30, best_init = 0;
+        uint64_t rows_p = 0;
+        __int128 rev_p = 0;
+        task_t *tasks = calloc((size_t)threads, sizeof(task_t));
+        pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
+        for (int rep = 0; rep < 3; ++rep) {
+            const double t0 = now_s();
+            cubit_scan *ps;
+            CHECK_SCAN(cubit_scan_init_global(t, proj_ids, 2, NULL, 0, q6, nn, NULL, &ps));
+            const double t1 = now_s();
+            for (int i = 0; i < threads; ++i) {
+                tasks[i] = (task_t){ps, 0, 0, 0};
+                if (pthread_create(&th[i], NULL, pipeline_task, &tasks[i]) != 0) return 1;
+            }
+            rows_p = 0;
+            rev_p = 0;
+            for (int i = 0; i < threads; ++i) {
+                pthread_join(th[i], NULL);
+                CHECK_SCAN(tasks[i].rc);
+                rows_p += tasks[i].rows;
+                rev_p += tasks[i].revenue;
+            }
+            const double t2 = now_s();
+            CHECK_SCAN(cubit_scan_destroy(ps));
+            if (t2 - t0 < best) {
+                best = t2 - t0;
+                best_init = t1 - t0;
+            }
+            if (rows_p != q || rev_p != rev) {
+                fprintf(stderr, "pipeline: %" PRIu64 " rows, revenue differs from the fused sum\n", rows_p);
+                return 1;
+            }
+        }
+        printf("pipeline threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64 " rows_per_s %.4e revenue_match 1\n",
+               threads, best_init * 1e3, best * 1e3, rows_p, rows_p / best);
+        free(tasks);
+        free(th);
+    }
     CHECK(cubit_dev_free(ctx, d_ids));
     CHECK(cubit_dev_free(ctx, d_cnt));
     CHECK(cubit_dev_free(ctx, d_sum));

@@ -182,6 +182,13 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     uint32_t tile_slot = 0;        // current tile (index into tiles)
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
+    // this task's copy stream (ordered after init_global's device work): the tasks' window
+    // copies run side by side instead of queueing on the context stream
+    cubit_ctx* ctx = nullptr;
+    void* copy_stream = nullptr;
+    ~CubitScanLocalState() override {
+        if (copy_stream) cubit_copy_stream_destroy(ctx, copy_stream);
+    }
 };
 
 int64_t* device_ptr(PooledBuffer& b) { return b.i64(); }
@@ -278,12 +285,17 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         return false;
     }
     const Window& win = g.windows[w];
+    if (!l.copy_stream) {
+        check(cubit_copy_stream_create(g.ctx, &l.copy_stream), "copy stream");
+        l.ctx = g.ctx;
+    }
     if (l.host.size() != g.emit.size()) l.host.resize(g.emit.size());
     for (size_t e = 0; e < g.emit.size(); ++e) {
         if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
         const column_t col = g.column_ids[g.emit[e]];
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
-        check(cubit_memcpy_d2h(g.ctx, l.host[e].p, device_ptr(src) + win.off, win.len * 8), "window copy");
+        check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
+              "window copy");
     }
     l.window = w;
     l.tile_slot = win.first;

@@ -170,6 +170,14 @@ int cubit_memcpy_h2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes)
 int cubit_memcpy_d2h(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memset_d(cubit_ctx *ctx, void *dst, int value, uint64_t bytes);
 int cubit_sync(cubit_ctx *ctx);
+/* Copy streams: a stream of the context's device whose work starts after everything enqueued
+ * on the context stream before the call (one pipeline task of the table-function mirror copies
+ * its windows on its own, so the tasks' copies overlap instead of queueing on one stream).
+ * cubit_memcpy_d2h_stream copies on it and waits for the copy. Destroyed streams go back to a
+ * pool of the context (creating a HIP stream costs milliseconds) and are freed with it. */
+int cubit_copy_stream_create(cubit_ctx *ctx, void **stream);
+int cubit_copy_stream_destroy(cubit_ctx *ctx, void *stream);
+int cubit_memcpy_d2h_stream(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
 /* Synchronise the context stream and report any pending HIP error. */
 int cubit_ctx_check(cubit_ctx *ctx);
 /* Tile directory of the last row-id materialisation on this context (device pointer, valid

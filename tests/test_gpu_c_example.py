@@ -1,7 +1,8 @@
 """The C ABI from a plain-C host (duckdb-cubit_amd/examples/q6_scan.c, built by
 __graft_entry__.build()): TPC-H SF1 Q6 through cubit_table_scan, the fused
 cubit_table_sum_product and the seq_scan-shaped callbacks of cubit_scan.h, with no Python or
-PyTorch in the process. Its output must equal the reference's SF1 fingerprint and answer."""
+PyTorch in the process, and the whole query as four pthread pipeline tasks over the callbacks.
+Its output must equal the reference's SF1 fingerprint and answer."""
 import subprocess
 from pathlib import Path
 
@@ -11,14 +12,24 @@ ROOT = Path(__file__).resolve().parents[1]
 EXE = ROOT / "duckdb-cubit_amd" / "lib" / "q6_scan"
 
 
+def fp_count(golden):
+    return golden["tpch"]["fingerprints"]["sf1_q6"]["count"]
+
+
 @pytest.mark.gpu
 def test_q6_from_c(golden):
     if not EXE.exists():
         pytest.fail(f"{EXE} is missing: run __graft_entry__.build()")
-    out = subprocess.run([str(EXE), "1"], capture_output=True, text=True, timeout=120)
+    out = subprocess.run([str(EXE), "1", "4"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
-    f = out.stdout.split()
+    lines = out.stdout.splitlines()
+    f = lines[0].split()
     got = dict(zip(f[0::2], f[1::2]))
+    # the query as four pipeline tasks over the callbacks: every row, the fused revenue
+    p = lines[1].split()[1:]  # "pipeline" then name value pairs
+    pipe = dict(zip(p[0::2], p[1::2]))
+    assert int(pipe["threads"]) == 4 and int(pipe["rows"]) == fp_count(golden)
+    assert pipe["revenue_match"] == "1"
     fp = golden["tpch"]["fingerprints"]["sf1_q6"]
     assert int(got["rows"]) == fp["count"]
     assert int(got["table_function_rows"]) == fp["count"]
