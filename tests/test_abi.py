@@ -44,6 +44,15 @@ def test_errors_are_status_codes_not_exceptions():
     assert b"null" in lib.cubit_last_error()
 
 
+def test_copy_stream_calls_reject_null_arguments():
+    """The table function's per-task copy streams (cubit_copy_stream_*): status codes, no GPU."""
+    lib = L.gpu_lib()
+    assert lib.cubit_copy_stream_create(None, None) == L.ERR_INVALID
+    assert lib.cubit_copy_stream_destroy(None, None) == L.ERR_INVALID
+    assert lib.cubit_memcpy_d2h_stream(None, None, None, None, 0) == L.ERR_INVALID
+    assert b"null" in lib.cubit_last_error()
+
+
 def test_validity_words_layout():
     from cubit_amd.datagen import mask_from_words, validity_from_mask
 
