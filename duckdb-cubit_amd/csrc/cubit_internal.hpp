@@ -75,10 +75,12 @@ struct EvalArgs {
     uint64_t* flags;
     uint64_t epoch;
 };
-// eval_decode_lookback: one workgroup per tile, at most this many tiles per launch (1.07e9 rows;
-// every workgroup reads the counts of all earlier tiles, so the flag reads grow with the square of
-// the tile count: 4,578 tiles (SF100) cost 68.5 µs against 64.7 µs for the run-claimed decode)
-constexpr uint32_t kLookbackMaxTiles = 8192;
+// eval_decode_lookback: one workgroup per tile, at most this many tiles per launch (6.0e8 rows).
+// Every workgroup reads the counts of all earlier tiles, so the flag reads grow with the square
+// of the tile count: at 4,578 tiles (SF100) the kernel takes 68.5 µs against 64.7 µs for the
+// run-claimed decode; larger launches are not measured, so ordered scans past this size keep the
+// run-claimed decode + ordering pass.
+constexpr uint32_t kLookbackMaxTiles = 4608;
 // Zonemaps: one zone = one decode tile (2,048 words = 131,072 rows). Class byte per zone:
 // bit 0 = no row of the zone is set, bit 1 = every row of the zone is set (a zone past the
 // last row has both).

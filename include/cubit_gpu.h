@@ -77,7 +77,7 @@ extern "C" {
  * index (src/function/table/table_scan.cpp:179-189). cubit_ctx_last_tiles() returns the
  * tile directory ({start, length} per tile) that restores row order for free.
  * CUBIT_SCAN_ORDERED lays the runs out ascending: the look-back decode places each tile's run at
- * the sum of the earlier tiles' counts, so no extra pass (partitions up to 8,192 tiles = 1.07e9
+ * the sum of the earlier tiles' counts, so no extra pass (partitions up to 4,608 tiles = 6.0e8
  * rows; larger ones take one extra device pass). The small partitions that AUTO decodes with the
  * look-back kernel are ascending without the flag, too.
  * Capacity: *d_count is always the full number of qualifying rows. When it exceeds
@@ -127,9 +127,9 @@ const char *cubit_last_error(void);
  * look-back kernel — one workgroup per 131,072-row tile, output offsets by look-back over the
  * earlier tiles' counts — when the partition's tiles fit the co-resident grid; else the
  * run-claimed kernel when a workgroup walks three or more tiles, else the pair-claimed one),
- * or one of them always (tests and benchmarks; LOOKBACK up to 8,192 tiles). Results are
+ * or one of them always (tests and benchmarks; LOOKBACK up to 4,608 tiles). Results are
  * identical. Under AUTO a CUBIT_SCAN_ORDERED scan takes the look-back kernel at any size up to
- * 8,192 tiles (its runs land in tile order). */
+ * 4,608 tiles (its runs land in tile order). */
 #define CUBIT_DECODE_AUTO 0
 #define CUBIT_DECODE_PAIRS 1
 #define CUBIT_DECODE_RUNS 2

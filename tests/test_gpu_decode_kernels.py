@@ -4,7 +4,7 @@ the earlier tiles' published counts) — against the oracle's CPU bitmap evaluat
 a time through cubit_ctx_set_decode_kernel and under the automatic policy. At 140 M rows the
 look-back grid (1,069 workgroups) exceeds what is co-resident, so its waits span workgroups
 that start only after others finish. The look-back runs land in tile order, so its default
-output is already the ascending array, and ordered scans take it up to 8,192 tiles.
+output is already the ascending array, and ordered scans take it up to 4,608 tiles.
 
 The run-claimed kernel keeps decoding a workgroup's tiles into one LDS stage until the next
 tile does not fit, so its interesting cases need workgroups that walk many tiles: tables of
