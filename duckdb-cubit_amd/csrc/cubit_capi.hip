@@ -965,7 +965,9 @@ struct Column {
     std::unique_ptr<DevBuf> bp_bytes, bp_groups;
     std::unique_ptr<DevBuf> bp_vgroup;  // per 2,048-row vector: the group holding its first row
     uint64_t bp_n_groups = 0;
-    bool bp_simple = false;  // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA
+    // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA: the widest FOR group's bits (≥ 1);
+    // else 0 (launch_bitpacked_compare)
+    int bp_simple_width = 0;
     void drop_packed() {
         bp_bytes.reset();
         bp_groups.reset();
@@ -1440,9 +1442,15 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     c.bp_vgroup = std::make_unique<DevBuf>();
     std::swap(c.bp_vgroup->p, d_vgroup.p);
     c.bp_n_groups = groups.size();
-    c.bp_simple = std::all_of(groups.begin(), groups.end(), [](const BpGroup& g) {
-        return g.mode == 2 || g.mode == 3 || (g.mode == 5 && g.width <= 32);
-    });
+    c.bp_simple_width = 0;
+    if (std::all_of(groups.begin(), groups.end(), [](const BpGroup& g) {
+            return g.mode == 2 || g.mode == 3 || (g.mode == 5 && g.width <= 32);
+        })) {
+        int wmax = 1;
+        for (const BpGroup& g : groups)
+            if (g.mode == 5) wmax = std::max<int>(wmax, g.width);
+        c.bp_simple_width = wmax;
+    }
     if (validity) {
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
         HIP_CHECK(hipStreamSynchronize(s));
@@ -2216,7 +2224,7 @@ int compute_k0(cubit_table* t, const PendingK0& k) {
         if (e == hipSuccess)
             e = launch_bitpacked_compare(static_cast<const uint8_t*>(cl.bp_bytes->p),
                                          static_cast<const BpGroup*>(cl.bp_groups->p), cl.bp_n_groups, cl.type,
-                                         cl.validity, k.cmp, k.c, 0, k.bv, t->ctx->stream, cl.bp_simple);
+                                         cl.validity, k.cmp, k.c, 0, k.bv, t->ctx->stream, cl.bp_simple_width);
         t->last_packed++;
     } else {
         e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, k.cmp, k.c, k.bv, t->ctx->stream);

@@ -166,10 +166,11 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
                             hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // K5 + K0 fused: {valid rows whose value cmp constant} straight from the BITPACKING groups
 // (cmp = CUBIT_CMP_* or kCmpBetween); out must be zero (words shared by two groups are OR-ed)
-// simple: every group is FOR of ≤ 32 bits, CONSTANT or CONSTANT_DELTA (bitpacked_compare_waves)
+// simple_width > 0: every group is FOR of ≤ 32 bits, CONSTANT or CONSTANT_DELTA, and the widest
+// FOR group has ≤ simple_width bits (bitpacked_compare_waves); 0: the LDS kernel
 hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
-                                    uint64_t* out, hipStream_t stream, bool simple = false);
+                                    uint64_t* out, hipStream_t stream, int simple_width = 0);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,

@@ -2220,76 +2220,99 @@ __global__ __launch_bounds__(256) void bitpacked_compare_kernel(const uint8_t* _
     }
 }
 
-// The same filter for columns whose groups are all FOR of ≤ 32 bits, CONSTANT or CONSTANT_DELTA
-// (the modes DuckDB's AUTO picks for unsorted integer columns): one wave per group, no LDS, so a
-// CU holds up to eight waves per SIMD instead of three, and each lane fetches the two words its
-// value's bits span straight from global memory — a 64-value chunk spans 2·w words, so a wave's
-// loads coalesce into one or two lines. UNR chunks' loads are in flight before the first is
-// tested. One ballot per chunk = one 64-row output word, stored (or OR-ed where a group's rows
-// share the word with a neighbour) by lane 0, as in bitpacked_compare_kernel.
-// UNR = 8 chunks in flight (44 VGPRs, eight waves per SIMD): 650 µs for a 600 M-row 12-bit FOR
-// column; UNR = 32 (98 VGPRs, one batch per group, four waves per SIMD) 814 µs; the LDS kernel
-// above 930 µs (profiles/r03w_*).
-template <typename T, typename U, int UNR = 8>
+// The same filter for columns whose groups are all FOR of ≤ MAXW bits (MAXW ≤ 32), CONSTANT or
+// CONSTANT_DELTA (the modes DuckDB's AUTO picks for unsorted integer columns): one wave per group.
+// The wave lands its group's packed words in its own LDS slice with coalesced 256-byte loads — all
+// of them in flight at once (≤ MAXW per lane), one round trip per group — then tests 64 values per
+// step, each lane taking its value's bits from the staged words with one funnel shift. One ballot
+// per step = one 64-row output word, stored (or OR-ed where a group's rows share the word with a
+// neighbour) by lane 0, as in bitpacked_compare_kernel. Measured before (profiles/r03w_*): the
+// same wave layout loading each value's two words from global memory, eight 64-value steps in
+// flight: 0.650 ms for a 600 M-row 12-bit column (the LDS kernel above 0.93 ms, K0 0.43 ms).
+template <typename T, typename U, int MAXW>
 __global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __restrict__ bytes,
                                                                const BpGroup* __restrict__ groups, uint32_t n_groups,
                                                                const uint64_t* __restrict__ validity, T lo, T hi,
                                                                int neg, uint64_t* __restrict__ out) {
+    static_assert(MAXW >= 1 && MAXW <= 32, "FOR groups of at most 32 bits");
+    constexpr uint32_t SLICE = 64u * MAXW + 4u;  // a group's words (2,048·w/32) + the read window
+    __shared__ uint32_t s_w[4][SLICE];
     const int lane = threadIdx.x & 63;
-    const uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
-    if (g >= n_groups) return;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t g = blockIdx.x * 4u + wave;
+    if (g >= n_groups) return;  // no workgroup barrier below: each wave works alone
+    uint32_t* L = s_w[wave];
     const BpGroup cur = groups[g];
     const uint64_t end = cur.row_start + cur.count;
-    const bool packed = cur.mode == 5;
+    const bool packed = cur.mode == 5 && cur.width;
     const uint32_t w = packed ? cur.width : 0u;
     const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1u;
-    const uint32_t nwords = packed ? (cur.count + 31u) / 32u * w : 0u;
-    const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + cur.words_off);
+    const uint32_t nwords = packed ? (cur.count + 31u) / 32u * w : 0u;  // ≤ 64·MAXW (host-checked)
+    if (packed) {
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + cur.words_off);
+        uint32_t x[MAXW];
+#pragma unroll
+        for (int m = 0; m < MAXW; ++m) {
+            const uint32_t k = 64u * (uint32_t)m + (uint32_t)lane;
+            x[m] = k < nwords ? __builtin_nontemporal_load(W + k) : 0u;
+        }
+#pragma unroll
+        for (int m = 0; m < MAXW; ++m) L[64u * (uint32_t)m + (uint32_t)lane] = x[m];
+        if (lane < 4) L[64u * MAXW + (uint32_t)lane] = 0u;
+        // the wave's own LDS writes, read back by other lanes of the same wave: LDS operations of a
+        // wave complete in order, so only the compiler must not move the reads above the writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
     const U base = (U)cur.base, d = cur.mode == 3 ? (U)cur.aux : (U)0;
-    const uint32_t nchunks = (cur.count + 63u) / 64u;
-#pragma unroll 1
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += UNR) {
-        uint32_t x0[UNR], x1[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            x0[u] = x1[u] = 0;
-            const uint32_t i = (c0 + (uint32_t)u) * 64u + (uint32_t)lane;
-            if (packed && w && i < cur.count) {  // width 0: every value is the frame
-                const uint32_t bit = i * w, wi = bit >> 5;  // i·w < 2^16, wi < nwords
-                x0[u] = __builtin_nontemporal_load(W + wi);
-                if (wi + 1 < nwords) x1[u] = __builtin_nontemporal_load(W + wi + 1);
+    const uint32_t nchunks = (cur.count + 63u) / 64u;  // ≤ 32
+    // a group starting on a 64-row boundary keeps step c's word in lane c and stores the words
+    // together at the end (one coalesced store; 8-byte stores from lane 0, one per step, cost
+    // more than the whole read); other groups store or OR each word as it is made
+    const bool aligned = (cur.row_start & 63) == 0;
+    uint64_t myword = 0;
+#pragma unroll 2
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        const uint32_t i = c * 64u + (uint32_t)lane;
+        bool p = false;
+        if (i < cur.count) {
+            T v;
+            if (packed) {
+                const uint32_t bit = i * w, wi = bit >> 5;  // i·w < 2^16
+                v = (T)((U)(__builtin_amdgcn_alignbit(L[wi + 1], L[wi], bit & 31) & mask) + base);
+            } else {
+                v = (T)(d * (U)i + base);
+            }
+            p = ((v >= lo) & (v <= hi)) != (neg != 0);
+            if (validity) {
+                const uint64_t r = cur.row_start + i;
+                p = p && ((validity[r >> 6] >> (r & 63)) & 1ull);
             }
         }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t c = c0 + (uint32_t)u;
-            if (c >= nchunks) break;  // uniform
-            const uint32_t i = c * 64u + (uint32_t)lane;
-            bool p = false;
-            if (i < cur.count) {
-                const T v = packed ? (T)((U)(__builtin_amdgcn_alignbit(x1[u], x0[u], (i * w) & 31) & mask) + base)
-                                   : (T)(d * (U)i + base);
-                p = ((v >= lo) & (v <= hi)) != (neg != 0);
-                if (validity) {
-                    const uint64_t r = cur.row_start + i;
-                    p = p && ((validity[r >> 6] >> (r & 63)) & 1ull);
-                }
-            }
-            const uint64_t bits = __ballot(p);
-            const uint64_t r0 = cur.row_start + 64ull * c;  // row of bit 0 (uniform)
-            const uint32_t sh = (uint32_t)(r0 & 63);
-            const uint64_t w0 = r0 >> 6;
-            if (lane == 0) {
-                if (sh == 0) {
-                    if (r0 + 64 <= end) out[w0] = bits;  // only this group's rows
-                    else atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)bits);
-                } else {
-                    atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)(bits << sh));
-                    const uint64_t hi2 = bits >> (64 - sh);
-                    if (hi2) atomicOr(reinterpret_cast<unsigned long long*>(&out[w0 + 1]), (unsigned long long)hi2);
-                }
+        const uint64_t bits = __ballot(p);
+        if (aligned) {
+            if ((uint32_t)lane == c) myword = bits;
+            continue;
+        }
+        const uint64_t r0 = cur.row_start + 64ull * c;  // row of bit 0 (uniform)
+        const uint32_t sh = (uint32_t)(r0 & 63);
+        const uint64_t w0 = r0 >> 6;
+        if (lane == 0) {
+            if (sh == 0) {
+                if (r0 + 64 <= end) out[w0] = bits;  // only this group's rows
+                else atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)bits);
+            } else {
+                atomicOr(reinterpret_cast<unsigned long long*>(&out[w0]), (unsigned long long)(bits << sh));
+                const uint64_t hi2 = bits >> (64 - sh);
+                if (hi2) atomicOr(reinterpret_cast<unsigned long long*>(&out[w0 + 1]), (unsigned long long)hi2);
             }
         }
+    }
+    if (aligned && (uint32_t)lane < nchunks) {
+        const uint64_t r0 = cur.row_start + 64ull * (uint32_t)lane;
+        if (r0 + 64 <= end) out[r0 >> 6] = myword;  // only this group's rows
+        else atomicOr(reinterpret_cast<unsigned long long*>(&out[r0 >> 6]), (unsigned long long)myword);
     }
 }
 
@@ -2974,23 +2997,31 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
 
 hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
-                                    uint64_t* out, hipStream_t stream, bool simple) {
+                                    uint64_t* out, hipStream_t stream, int simple_width) {
     if (n_groups == 0) return hipSuccess;
     if (n_groups > 0x7fffffffull) return hipErrorInvalidValue;
     const CmpRange rg = cmp_range(cmp, constant, constant2);
     const int64_t lo = rg.lo, hi = rg.hi;
     const int neg = rg.neg;
     const uint32_t ng = (uint32_t)n_groups;
-    if (simple) {  // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA: one wave per group
+    if (simple_width > 0) {  // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA: one wave per group
         const dim3 grid((ng + 3) / 4);
         if (type == 0) {
             int32_t lo32, hi32;
             rg.clamp32(lo32, hi32);
-            hipLaunchKernelGGL((bitpacked_compare_waves<int32_t, uint32_t>), grid, dim3(256), 0, stream, bytes, groups,
-                               ng, validity, lo32, hi32, neg, out);
+            if (simple_width <= 16)
+                hipLaunchKernelGGL((bitpacked_compare_waves<int32_t, uint32_t, 16>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo32, hi32, neg, out);
+            else
+                hipLaunchKernelGGL((bitpacked_compare_waves<int32_t, uint32_t, 32>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo32, hi32, neg, out);
         } else {
-            hipLaunchKernelGGL((bitpacked_compare_waves<int64_t, uint64_t>), grid, dim3(256), 0, stream, bytes, groups,
-                               ng, validity, lo, hi, neg, out);
+            if (simple_width <= 16)
+                hipLaunchKernelGGL((bitpacked_compare_waves<int64_t, uint64_t, 16>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo, hi, neg, out);
+            else
+                hipLaunchKernelGGL((bitpacked_compare_waves<int64_t, uint64_t, 32>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo, hi, neg, out);
         }
         return hipGetLastError();
     }
