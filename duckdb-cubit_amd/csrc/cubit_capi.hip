@@ -77,6 +77,7 @@ struct cubit_ctx {
     uint64_t* ticket = nullptr;  // claim ticket of the evaluate kernels (EvalArgs::ticket)
     uint64_t* flags = nullptr;   // look-back flag words of eval_decode_lookback (EvalArgs::flags)
     uint64_t epoch = 0;          // the last look-back launch's epoch (EvalArgs::epoch)
+    uint32_t lookback_spins = 0; // EvalArgs::spin_limit (cubit_ctx_set_lookback_spins; 0 = default)
     int decode_kernel = CUBIT_DECODE_AUTO;  // cubit_ctx_set_decode_kernel
     int last_decode = 0;                    // kernel of the last decode (CUBIT_DECODE_PAIRS / _RUNS)
     // zonemap skip: the live-tile list of a launch, staged in page-locked memory and copied to
@@ -240,6 +241,7 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     a.num_tiles = (uint32_t)tiles;
     a.flags = ctx->flags;
     a.epoch = ++ctx->epoch;
+    a.spin_limit = ctx->lookback_spins;
     a.rowids = order_pass ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
     if (live_zones) {
@@ -297,7 +299,6 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         uint64_t n = 0;
         HIP_CHECK(hipMemcpyAsync(&n, d_count, sizeof(n), hipMemcpyDeviceToHost, ctx->stream));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        if (n == ~0ull) return fail(CUBIT_ERR_DEVICE, "decode look-back did not complete (bounded wait expired)");
         if (n > capacity)
             return fail(CUBIT_ERR_CAPACITY, "%llu qualifying rows exceed the capacity of %llu row ids",
                         (unsigned long long)n, (unsigned long long)capacity);
@@ -390,6 +391,13 @@ int cubit_ctx_set_decode_kernel(cubit_ctx* ctx, int kernel) {
     if (kernel < CUBIT_DECODE_AUTO || kernel > CUBIT_DECODE_LOOKBACK) return fail(CUBIT_ERR_INVALID, "decode kernel %d", kernel);
     CUBIT_LOCK(ctx);
     ctx->decode_kernel = kernel;
+    return CUBIT_OK;
+}
+
+int cubit_ctx_set_lookback_spins(cubit_ctx* ctx, uint32_t spins) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "null context");
+    CUBIT_LOCK(ctx);
+    ctx->lookback_spins = spins;
     return CUBIT_OK;
 }
 

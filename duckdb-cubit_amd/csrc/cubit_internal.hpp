@@ -74,6 +74,9 @@ struct EvalArgs {
     // launch's epoch (> 0, one per launch on the context), which tags every flag it publishes
     uint64_t* flags;
     uint64_t epoch;
+    // polls of one flag before the polling thread counts that tile itself (0 = the kernel's
+    // default; cubit_ctx_set_lookback_spins forces the recount path in tests)
+    uint32_t spin_limit;
 };
 // eval_decode_lookback: one workgroup per tile, at most this many tiles per launch (6.0e8 rows).
 // Every workgroup reads the counts of all earlier tiles, so the flag reads grow with the square

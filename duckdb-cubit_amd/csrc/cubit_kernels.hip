@@ -1092,12 +1092,67 @@ __global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void eval_decode_runs(E
 //   workgroup writes the count: no arrival ticket either. A workgroup waits only on lower block
 //   indices, which are dispatched before it, so the walk completes whatever the residency.
 // A tile with more rows than the stage leaves through it in rounds after the offset is known.
-// A poll that exceeds kLookbackSpins marks the count ~0 (the host reports CUBIT_ERR_DEVICE).
+// A poll that exceeds the spin limit (EvalArgs::spin_limit, kLookbackSpins by default) does not
+// fail the scan: the thread stops waiting and flags the workgroup, which then walks the earlier
+// flags once more without waiting and counts every tile still unpublished from its bitvectors
+// itself (lookback_recount — the same program over the same words, so the same count). No
+// workgroup ever waits on another without bound, every workgroup writes its run, and the last
+// one's count is the true count whatever the dispatch order: the kernel has no failure exit for
+// the host to miss.
 // Runs land in tile order, so the output is one ascending array: ordered scans take this kernel
 // at any size up to kLookbackMaxTiles (SF100, 4,578 tiles: 68.5 µs against 95 µs for the
 // run-claimed decode plus the ordering pass; scripts/smallbench.hip).
 constexpr int kFlagCntBits = 20;  // a tile holds ≤ 131,072 rows
 constexpr uint32_t kLookbackSpins = 1u << 22;
+
+// The expiry path of the look-back (workgroup-uniform call): the rows of tiles 0 … b-1 of the
+// launch, each taken from its published flag when it is there now, else counted by the whole
+// workgroup from the tile's bitvectors (load_tile / eval_words / tail_mask, as the tile's own
+// workgroup does). s_list holds THREADS entries, s_n and s_sum are scratch.
+template <int K, int FORM, int THREADS, int PAIRS>
+__device__ uint64_t lookback_recount(const EvalArgs& a, uint32_t b, int t, uint32_t* s_list, uint32_t* s_n,
+                                     uint64_t* s_sum) {
+    constexpr int NWAVES = THREADS / 64;
+    constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * 2 * PAIRS;
+    constexpr uint64_t kCntMask = (1ull << kFlagCntBits) - 1;
+    uint64_t acc = 0;
+    for (uint32_t j0 = 0; j0 < b; j0 += THREADS) {
+        const uint32_t j = j0 + (uint32_t)t;
+        __syncthreads();  // the previous round's list is consumed
+        if (t == 0) *s_n = 0;
+        __syncthreads();
+        if (j < b) {
+            const uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((f >> kFlagCntBits) == a.epoch) acc += f & kCntMask;
+            else s_list[atomicAdd(s_n, 1u)] = j;
+        }
+        __syncthreads();
+        const uint32_t n_miss = *s_n;
+#pragma unroll 1
+        for (uint32_t i = 0; i < n_miss; ++i) {
+            // one word pair per thread at a time (half the registers of the tile's own pass:
+            // this runs while that pass's words are still live)
+#pragma unroll 1
+            for (int h = 0; h < PAIRS; ++h) {
+                const uint64_t w0 = (uint64_t)tile_at(a, s_list[i]) * TILE_WORDS + (uint64_t)h * 2 * THREADS;
+                u64x2 v[K][1];
+                load_tile<K, 1, THREADS>(a, w0, t, v);
+                uint64_t r[2];
+                eval_words<K, 2, FORM>(a.prog, v, r);
+                tail_mask<2, THREADS>(a, w0, t, r);
+                acc += (uint64_t)(__popcll(r[0]) + __popcll(r[1]));
+            }
+        }
+    }
+    acc = wave_sum_flags(acc);
+    __syncthreads();
+    if ((t & 63) == 0) s_sum[t >> 6] = acc;
+    __syncthreads();
+    uint64_t total = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) total += s_sum[w];
+    return total;
+}
 // DBG (diagnostic builds, scripts/smallbench.hip; 0 in the library): 1 no spin, 2 no ids, 4 no
 // sleep, 8 no flag loads, 16 no LDS decode.
 // Measured and not kept (scripts/smallbench.hip; profiles/r03e_*, r03g_*, r03h_*): eight copies of
@@ -1112,14 +1167,17 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     constexpr uint64_t kCntMask = (1ull << kFlagCntBits) - 1;
     __shared__ uint32_t s_wave_tot[NWAVES];
     __shared__ uint64_t s_pre[NWAVES];
-    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_expired;
+    __shared__ uint32_t s_list_n;
+    __shared__ uint32_t s_list_scratch[THREADS];
     __shared__ uint32_t s_stage[STAGE];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t tile = tile_at(a, b);
     const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
     const bool write_ids = a.rowids != nullptr;
-    if (t == 0) s_bad = 0;
+    const uint32_t spin_limit = a.spin_limit ? a.spin_limit : kLookbackSpins;
+    if (t == 0) s_expired = 0;
     u64x2 v[K][PAIRS];
     load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
     uint64_t r[NW];
@@ -1178,8 +1236,9 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t spins = 0;
         while (!(DBG & 1) && (f >> kFlagCntBits) != a.epoch) {
-            if (++spins == kLookbackSpins) {
-                s_bad = 1;
+            if (++spins >= spin_limit) {
+                s_expired = 1;  // stop waiting: the workgroup recounts below
+                f = 0;
                 break;
             }
             if (!(DBG & 4)) __builtin_amdgcn_s_sleep(2);
@@ -1193,9 +1252,10 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     uint64_t base = 0;
 #pragma unroll
     for (int w = 0; w < NWAVES; ++w) base += s_pre[w];
-    if (s_bad) {
-        if (t == 0) *a.count = ~0ull;
-        return;
+    if (s_expired) {
+        // some earlier tile was not published within the limit: every flag once more, the
+        // missing tiles counted here (s_pre and s_wave_tot are free again; s_stage is not)
+        base = lookback_recount<K, FORM, THREADS, PAIRS>(a, b, t, s_list_scratch, &s_list_n, s_pre);
     }
     const int64_t row0 = a.row_base + (int64_t)(tile_word0 * 64);
     if (t == 0) {
@@ -1210,7 +1270,12 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, tile_count, base, row0, t);
         return;
     }
-    // dense tile: rounds of STAGE ids through the stage
+    // dense tile: rounds of STAGE ids through the stage. Its words are read and evaluated once
+    // more here (more than STAGE ids: the id writes outweigh the re-read ≥ 4:1 for K ≤ 4), so
+    // no result word is held in registers across the look-back walk and its expiry recount.
+    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
+    eval_words<K, NW, FORM>(a.prog, v, r);
+    tail_mask<NW, THREADS>(a, tile_word0, t, r);
     for (uint32_t r0 = 0; r0 < tile_count; r0 += (uint32_t)STAGE) {
         const uint32_t r1 = min(tile_count, r0 + (uint32_t)STAGE);
         if (r0) __syncthreads();  // the previous round's copy-out is done

@@ -130,6 +130,7 @@ GPU_SIGNATURES = {
     "cubit_table_set_inserts": (C.c_int, [_P, _P, _P, _P, _U64]),
     "cubit_table_append": (C.c_int, [_P, _U64, _P, _P, _P, C.c_uint32, _U64]),
     "cubit_ctx_set_decode_kernel": (C.c_int, [_P, C.c_int]),
+    "cubit_ctx_set_lookback_spins": (C.c_int, [_P, C.c_uint32]),
     "cubit_host_alloc": (C.c_int, [_P, _U64, C.POINTER(_P)]),
     "cubit_host_free": (C.c_int, [_P, _P]),
     "cubit_ctx_last_decode_kernel": (C.c_int, [_P, _P]),

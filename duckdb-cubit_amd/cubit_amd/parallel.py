@@ -64,7 +64,9 @@ class RowIdExchange:
         self._nccl = dist.get_backend(group) == "nccl"
         self.recv = None
         if self.rank == dst:
-            self.recv = torch.empty((self.world, max(self.slot, 1)), dtype=dtype, device=device)
+            # exactly `slot` per rank: a recv larger than the matching send never completes on
+            # RCCL (and is a size mismatch on gloo)
+            self.recv = torch.empty((self.world, self.slot), dtype=dtype, device=device)
         self._local = None
         self._works = []
 
@@ -82,8 +84,8 @@ class RowIdExchange:
             dist.all_gather_into_tensor(self.counts, mine, group=self.group)  # one collective, no copies
         else:
             dist.all_gather(self._count_views, mine, group=self.group)
-        if self.world == 1:
-            return
+        if self.world == 1 or self.slot == 0:
+            return  # every rank has the same slot, so all of them skip the payload together
         if self.rank == self.dst:
             ops = [dist.P2POp(dist.irecv, self.recv[r], r, group=self.group)
                    for r in range(self.world) if r != self.dst]

@@ -34,6 +34,11 @@ class Context:
         """L.DECODE_AUTO (measured policy), L.DECODE_PAIRS or L.DECODE_RUNS."""
         L.check(self.lib.cubit_ctx_set_decode_kernel(self.handle, kernel))
 
+    def set_lookback_spins(self, spins: int) -> None:
+        """Polls of an earlier tile's flag before the look-back decode counts that tile itself
+        (0 = library default); a small value forces the expiry path."""
+        L.check(self.lib.cubit_ctx_set_lookback_spins(self.handle, spins))
+
     def last_decode_kernel(self) -> int:
         k = C.c_int()
         L.check(self.lib.cubit_ctx_last_decode_kernel(self.handle, C.byref(k)))

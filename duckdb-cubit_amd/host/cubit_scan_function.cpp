@@ -39,8 +39,10 @@ class BufferPool {
     void* take(cubit_ctx* ctx, size_t bytes, size_t* got) {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            auto it = free_.lower_bound(Key{ctx, bytes});
-            if (it != free_.end() && it->first.ctx == ctx && it->first.bytes <= 2 * bytes) {
+            // page-locked buffers are filed under no context (give), device buffers under theirs
+            cubit_ctx* owner = pinned_ ? nullptr : ctx;
+            auto it = free_.lower_bound(Key{owner, bytes});
+            if (it != free_.end() && it->first.ctx == owner && it->first.bytes <= 2 * bytes) {
                 void* p = it->second;
                 *got = it->first.bytes;
                 cached_ -= it->first.bytes;
@@ -218,7 +220,6 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
                                device_ptr(g->d_ids), cap, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_ORDERED),
               "cubit_table_scan");
         check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
-        if (g->count == ~0ull) throw ScanError(CUBIT_ERR_DEVICE, "cubit_table_scan: device failure");
         if (g->count <= cap) break;
         if (pass == 1) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
         cap = g->count;

@@ -4,20 +4,18 @@
 // This file is the DuckDB-side binding a maintainer adds. It compiles
 // against the DuckDB headers only: `make -C duckdb-cubit_amd shim-check DUCKDB_INCLUDE=…`
 // runs a full semantic check (g++ -fsyntax-only) against a DuckDB v1.1.2 source tree.
-// Linking it needs libduckdb, which this repository does not build.
+// Linking it needs libduckdb, which this repository does not build (DESIGN.md §4).
 //
-//   PRAGMA cubit_attach('lineitem', 'l_shipdate,l_discount,l_quantity,l_extendedprice');
-//     copies those columns to the GPU (one partition per call), builds an exact range index on
-//     each, and adds a CUBIT index (CubitIndex, a BoundIndex) to the table so DuckDB hands it
-//     every committed append and every index removal from then on;
+//   PRAGMA cubit_attach('lineitem', 'l_shipdate,l_discount,l_quantity,l_extendedprice'
+//                       [, 'l_shipdate=range:1994-01-01,1995-01-01;l_discount=range;…']);
+//     copies those columns to the GPU (one partition per table, every column from one
+//     snapshot) and builds the named bitmap indexes;
 //   PRAGMA cubit_sync('lineitem');
-//     brings the partition to the table's committed state (uploads the appends the index
-//     buffered, records committed deletes) and stamps it with the last commit.
+//     brings the partition to the table's committed state (appended rows, committed deletes;
+//     every column again after an UPDATE of an attached one).
 //   The optimizer swaps seq_scan for cubit_scan when every pushed filter of the scan is
 //   supported, every scanned column is attached, and the partition is exactly the state the
-//   scanning transaction sees: no transaction-local rows or deletes on the table (those stay
-//   on seq_scan, which scans them after the persistent rows: DataTable::Scan,
-//   data_table.cpp:277-287), no commit since the stamp, and a snapshot that includes it.
+//   scanning transaction sees (CubitPartitionIsCurrent); otherwise seq_scan runs as before.
 //
 // Reference interfaces used (src/include/duckdb/…):
 //   OptimizerExtension::optimize_function          optimizer/optimizer_extension.hpp:31-41
@@ -31,26 +29,25 @@
 #include "duckdb.hpp"
 #include "duckdb/catalog/catalog_entry/duck_table_entry.hpp"
 #include "duckdb/catalog/catalog_entry/table_catalog_entry.hpp"
+#include "duckdb/common/unordered_set.hpp"
+#include "duckdb/function/function_set.hpp"
 #include "duckdb/function/pragma_function.hpp"
 #include "duckdb/function/table_function.hpp"
 #include "duckdb/main/extension_util.hpp"
 #include "duckdb/optimizer/optimizer_extension.hpp"
+#include "duckdb/parser/statement/insert_statement.hpp"
 #include "duckdb/planner/filter/conjunction_filter.hpp"
 #include "duckdb/planner/filter/constant_filter.hpp"
 #include "duckdb/planner/filter/null_filter.hpp"
+#include "duckdb/planner/operator/logical_delete.hpp"
 #include "duckdb/planner/operator/logical_get.hpp"
+#include "duckdb/planner/operator/logical_insert.hpp"
+#include "duckdb/planner/operator/logical_update.hpp"
 #include "duckdb/planner/table_filter.hpp"
+#include "duckdb/storage/data_table.hpp"
 #include "duckdb/transaction/duck_transaction.hpp"
 #include "duckdb/transaction/duck_transaction_manager.hpp"
 #include "duckdb/transaction/local_storage.hpp"
-#include "duckdb/execution/index/bound_index.hpp"
-#include "duckdb/execution/index/index_type.hpp"
-#include "duckdb/execution/index/index_type_set.hpp"
-#include "duckdb/planner/expression/bound_reference_expression.hpp"
-#include "duckdb/storage/data_table.hpp"
-#include "duckdb/storage/table_io_manager.hpp"
-#include "duckdb/storage/table/append_state.hpp"
-#include "duckdb/storage/table_storage_info.hpp"
 
 #include "cubit_gpu.h"
 #include "cubit_scan.h"
@@ -61,29 +58,41 @@ namespace duckdb {
 
 // ------------------------------------------------------------------ registry
 
-// One GPU partition per attached table: the device context, the cubit_table and which
-// storage columns it holds (with their physical width).
+// A bitmap index the attach builds on one column (cubit_table_build_index): its encoding and
+// keys (empty = every distinct value of the column).
+struct CubitIndexSpec {
+    column_t column;
+    int encoding;  // CUBIT_INDEX_RANGE / _EQUALITY / _BINS
+    vector<int64_t> keys;
+};
+
+// One GPU partition per attached table: the device context, the cubit_table, which storage
+// columns it holds (with their physical width) and how current it is.
+//
+// Staleness is tracked per table, never through the database-wide last commit (every commit,
+// read-only ones included, advances DuckTransactionManager::last_commit: GetCommitTimestamp,
+// duck_transaction_manager.cpp:201-205, 248):
+//  * appends: the table's row count (DataTable::GetTotalRows) against the partition's;
+//  * deletes and updates: every DELETE, UPDATE and INSERT … ON CONFLICT DO UPDATE planned on
+//    the table (CubitOptimize sees each plan) records its transaction id in `writers`. A sync
+//    forgets a writer only once that transaction has finished before the sync's snapshot began
+//    (transaction ids grow, so id < LowestActiveId() means finished), so whatever it committed
+//    is in the snapshot the sync reads;
+//  * the snapshot: `sync_start` is the start time of the transaction the last sync read the
+//    table in (one transaction for every column). A scan may use the partition only if its own
+//    snapshot includes that one (start_time >= sync_start).
 struct CubitAttached {
     cubit_ctx *ctx = nullptr;
     cubit_table *table = nullptr;
     unordered_map<column_t, PhysicalType> columns;
-    vector<column_t> column_order;  // attached storage columns, in the CubitIndex's key order
+    vector<column_t> column_order;  // attached storage columns, in upload order
+    vector<CubitIndexSpec> indexes; // the attach's index specification
     uint64_t gpu_rows = 0;          // rows of the GPU partition (row ids 0 … gpu_rows-1)
-    // the last commit the partition reflects (DuckTransactionManager::GetLastCommit at the
-    // attach / sync that produced it); the swap needs GetLastCommit() == stamp
-    transaction_t stamp = 0;
-    // committed appends handed to the CubitIndex since the last sync: first row id + one
-    // buffer per attached column (int64 values, DuckDB validity), uploaded by cubit_sync
-    struct Pending {
-        row_t first = 0;
-        idx_t count = 0;
-        vector<vector<int64_t>> values;
-        vector<vector<uint64_t>> validity;
-    };
-    vector<Pending> pending;
-    vector<int64_t> deleted;  // row ids removed through the index (cleanup of committed deletes)
-    bool index_added = false; // the table's index list holds this partition's CubitIndex
-    mutex lock;               // the hooks run on DuckDB's commit / cleanup threads
+    transaction_t sync_start = 0;   // start time of the last sync's snapshot
+    // planned writers not yet folded in by a sync: transaction id → whether it may change the
+    // values of an attached column (then the sync re-reads every column)
+    unordered_map<transaction_t, bool> writers;
+    mutex lock;  // scans, writers and syncs of different connections meet here
 };
 
 class CubitRegistry {
@@ -91,16 +100,20 @@ public:
     static CubitAttached *Find(const TableCatalogEntry &t) {
         lock_guard<mutex> g(lock);
         auto it = map().find(&t);
-        return it == map().end() ? nullptr : &it->second;
+        return it == map().end() ? nullptr : it->second.get();
     }
     static CubitAttached &Insert(const TableCatalogEntry &t) {
         lock_guard<mutex> g(lock);
-        return map()[&t];
+        auto &slot = map()[&t];
+        if (!slot) {
+            slot = make_uniq<CubitAttached>();
+        }
+        return *slot;
     }
 
 private:
-    static unordered_map<const TableCatalogEntry *, CubitAttached> &map() {
-        static unordered_map<const TableCatalogEntry *, CubitAttached> m;
+    static unordered_map<const TableCatalogEntry *, unique_ptr<CubitAttached>> &map() {
+        static unordered_map<const TableCatalogEntry *, unique_ptr<CubitAttached>> m;
         return m;
     }
     static mutex lock;
@@ -500,28 +513,79 @@ TableFunction GetCubitScanFunction() {
 // ------------------------------------------------------------------ optimizer swap
 
 // The GPU partition holds exactly what the scanning transaction's seq_scan would read:
-//  * no transaction-local storage on the table: DataTable::Scan reads the persistent row groups
-//    and then the transaction's LocalStorage (data_table.cpp:277-287, local_storage.cpp:326-341),
-//    and local deletes hide persistent rows; none of that is on the GPU;
-//  * no commit since the partition's stamp (a DELETE reaches no index hook until cleanup, so
-//    any later commit may have changed rows the partition shows) and every appended row synced;
-//  * the transaction's snapshot includes the stamp (start_time > stamp: an older snapshot
-//    must not see commits the partition already shows).
+//  * the transaction has changed nothing (DuckTransaction::ChangesMade, duck_transaction.hpp:59):
+//    its own deletes of persistent rows go to the row groups' version info
+//    (DataTable::Delete → RowGroupCollection::Delete, data_table.cpp:1181-1189) and its appends
+//    to its LocalStorage, which DataTable::Scan reads after the persistent rows
+//    (data_table.cpp:277-287, local_storage.cpp:326-341) — none of that is on the GPU;
+//  * no planned writer of the table is outstanding and every committed append is synced;
+//  * the transaction's snapshot includes the one the partition was read in.
 static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
     auto &tx = DuckTransaction::Get(context, table.catalog);
     auto &storage = table.GetStorage();
-    if (LocalStorage::Get(tx).Find(storage)) {
+    if (tx.ChangesMade() || LocalStorage::Get(tx).Find(storage)) {
         return false;
     }
-    auto &tm = DuckTransactionManager::Get(table.catalog.GetAttached());
     lock_guard<mutex> g(attached.lock);
-    return attached.pending.empty() && tm.GetLastCommit() == attached.stamp && tx.start_time > attached.stamp &&
-           storage.GetTotalRows() == attached.gpu_rows;
+    return attached.table && attached.writers.empty() && storage.GetTotalRows() == attached.gpu_rows &&
+           tx.start_time >= attached.sync_start;
 }
 
-static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOperator> &plan) {
+// DELETE / UPDATE / INSERT … ON CONFLICT DO UPDATE planned on an attached table: remember the
+// writing transaction (see CubitAttached). Returns whether the plan writes any table.
+static bool NoteWriters(ClientContext &context, LogicalOperator &op) {
+    bool writes = false;
+    for (auto &child : op.children) {
+        writes |= NoteWriters(context, *child);
+    }
+    optional_ptr<TableCatalogEntry> table;
+    bool changes_values = false;
+    switch (op.type) {
+    case LogicalOperatorType::LOGICAL_DELETE:
+        table = &op.Cast<LogicalDelete>().table;
+        break;
+    case LogicalOperatorType::LOGICAL_UPDATE: {
+        auto &u = op.Cast<LogicalUpdate>();
+        table = &u.table;
+        changes_values = true;  // refined below against the attached columns
+        break;
+    }
+    case LogicalOperatorType::LOGICAL_INSERT: {
+        auto &ins = op.Cast<LogicalInsert>();
+        writes = true;  // appends reach the partition through the row count
+        if (ins.action_type == OnConflictAction::UPDATE || ins.action_type == OnConflictAction::REPLACE) {
+            table = &ins.table;
+            changes_values = true;
+        }
+        break;
+    }
+    default:
+        return writes;
+    }
+    writes = true;
+    if (!table) {
+        return writes;
+    }
+    auto attached = CubitRegistry::Find(*table);
+    if (!attached) {
+        return writes;
+    }
+    auto &tx = DuckTransaction::Get(context, table->catalog);
+    lock_guard<mutex> g(attached->lock);
+    if (changes_values && op.type == LogicalOperatorType::LOGICAL_UPDATE) {
+        changes_values = false;
+        for (auto &c : op.Cast<LogicalUpdate>().columns) {
+            changes_values |= attached->columns.count(c.index) > 0;
+        }
+    }
+    auto &w = attached->writers[tx.transaction_id];
+    w = w || changes_values;
+    return writes;
+}
+
+static void SwapScans(ClientContext &context, unique_ptr<LogicalOperator> &plan) {
     for (auto &child : plan->children) {
-        CubitOptimize(input, child);
+        SwapScans(context, child);
     }
     if (plan->type != LogicalOperatorType::LOGICAL_GET) {
         return;
@@ -538,7 +602,7 @@ static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOper
     if (!attached) {
         return;
     }
-    if (!CubitPartitionIsCurrent(input.context, table->Cast<DuckTableEntry>(), *attached)) {
+    if (!CubitPartitionIsCurrent(context, table->Cast<DuckTableEntry>(), *attached)) {
         return;  // seq_scan reads what the GPU partition does not hold
     }
     for (auto c : get.column_ids) {
@@ -555,155 +619,183 @@ static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOper
     get.bind_data = make_uniq<CubitBindData>(table->Cast<DuckTableEntry>(), *attached);
 }
 
-// ------------------------------------------------------------------ index maintenance
+// OptimizerExtension::optimize_function (optimizer_extension.hpp:31-41), run after the built-in
+// optimizers (optimizer.cpp:222-227). Scans inside a plan that writes keep seq_scan: the rows a
+// DELETE / UPDATE reads are the rows it changes.
+static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOperator> &plan) {
+    if (NoteWriters(input.context, *plan)) {
+        return;
+    }
+    SwapScans(input.context, plan);
+}
 
-// CUBIT's bitmap index as a DuckDB index type ("CUBIT"; DBConfig::GetIndexTypes, registered as
-// IndexTypeSet registers ART, index_type_set.cpp:7-13). cubit_attach adds one instance to the
-// table (DataTable::AddIndex), and from then on DuckDB calls it like any BoundIndex
-// (bound_index.hpp:67-126):
-//   Append  ← DataTable::AppendToIndexes (data_table.cpp:1000-1040), once per committed chunk
-//             (LocalStorage::Flush at commit), and for the insert half of an UPDATE of an
-//             attached column (an UPDATE of an indexed column runs as delete + insert,
-//             table_catalog_entry.cpp:288-308). The chunk's attached columns are buffered; the
-//             next cubit_sync uploads them with cubit_table_append (every bitmap index on the
-//             GPU maintained in place) — until then the swap is refused.
-//   Delete  ← DataTable::RemoveFromIndexes: the revert of a failed append (data_table.cpp:
-//             1032-1037) and the cleanup of committed deletes (cleanup_state.cpp:93); the rows
-//             become deletes of the partition (cubit_table_set_deletes at the next sync).
-//   Insert  ← an index build over existing rows (not used: cubit_attach uploads them itself).
-// Constraint checks pass (CUBIT is not a constraint index), and the index holds no DuckDB-side
-// storage (GetStorageInfo: nothing to persist; the GPU index is rebuilt by cubit_attach).
-class CubitIndex : public BoundIndex {
-public:
-    static constexpr const char *TYPE_NAME = "CUBIT";
+// ------------------------------------------------------------------ attach / sync
 
-    CubitIndex(const string &name, const vector<column_t> &column_ids, TableIOManager &io,
-               const vector<unique_ptr<Expression>> &exprs, AttachedDatabase &db, CubitAttached *attached_p)
-        : BoundIndex(name, TYPE_NAME, IndexConstraintType::NONE, column_ids, io, exprs, db), attached(attached_p) {
-    }
-
-    // IndexType::create_instance: a CUBIT index bound to the table's attached partition
-    static unique_ptr<BoundIndex> Create(CreateIndexInput &input) {
-        return make_uniq<CubitIndex>(input.name, input.column_ids, input.table_io_manager, input.unbound_expressions,
-                                     input.db, nullptr);
-    }
-
-    ErrorData Append(IndexLock &, DataChunk &entries, Vector &row_identifiers) override {
-        if (!attached || entries.size() == 0) {
-            return ErrorData();
-        }
-        DataChunk keys;
-        keys.Initialize(Allocator::DefaultAllocator(), logical_types);
-        ExecuteExpressions(entries, keys);  // the attached columns, in key order
-        keys.Flatten();
-        row_identifiers.Flatten(entries.size());
-        auto rows = FlatVector::GetData<row_t>(row_identifiers);
-        CubitAttached::Pending p;
-        p.first = rows[0];
-        p.count = entries.size();
-        for (idx_t c = 0; c < keys.ColumnCount(); c++) {
-            vector<int64_t> v(p.count, 0);
-            vector<uint64_t> valid((p.count + 63) / 64, 0);
-            auto &vec = keys.data[c];
-            auto &mask = FlatVector::Validity(vec);
-            for (idx_t i = 0; i < p.count; i++) {
-                if (!mask.RowIsValid(i)) {
-                    continue;
-                }
-                valid[i >> 6] |= 1ull << (i & 63);
-                v[i] = PhysicalAsInt64(vec, i);
-            }
-            p.values.push_back(std::move(v));
-            p.validity.push_back(std::move(valid));
-        }
-        lock_guard<mutex> g(attached->lock);
-        attached->pending.push_back(std::move(p));
-        return ErrorData();
-    }
-
-    void Delete(IndexLock &, DataChunk &entries, Vector &row_identifiers) override {
-        if (!attached) {
-            return;
-        }
-        row_identifiers.Flatten(entries.size());
-        auto rows = FlatVector::GetData<row_t>(row_identifiers);
-        lock_guard<mutex> g(attached->lock);
-        for (idx_t i = 0; i < entries.size(); i++) {
-            attached->deleted.push_back(rows[i]);
-        }
-    }
-
-    ErrorData Insert(IndexLock &state, DataChunk &input, Vector &row_identifiers) override {
-        return Append(state, input, row_identifiers);
-    }
-    void VerifyAppend(DataChunk &) override {
-    }
-    void VerifyAppend(DataChunk &, ConflictManager &) override {
-    }
-    void CheckConstraintsForChunk(DataChunk &, ConflictManager &) override {
-    }
-    void CommitDrop(IndexLock &) override {
-        attached = nullptr;
-    }
-    bool MergeIndexes(IndexLock &, BoundIndex &) override {
-        return true;  // local (transaction) indexes are never CUBIT: nothing to merge
-    }
-    void Vacuum(IndexLock &) override {
-    }
-    idx_t GetInMemorySize(IndexLock &) override {
-        return 0;  // the bitvectors live in GPU memory (cubit_table_index_info)
-    }
-    string VerifyAndToString(IndexLock &, const bool) override {
-        return "CUBIT index (GPU partition)";
-    }
-    string GetConstraintViolationMessage(VerifyExistenceType, idx_t, DataChunk &) override {
-        return "CUBIT indexes enforce no constraint";
-    }
-    IndexStorageInfo GetStorageInfo(const bool) override {
-        IndexStorageInfo info(name);
-        return info;
-    }
-
-    CubitAttached *attached;
+// The attached columns of one snapshot, in row-id order: values widened to int64 and DuckDB
+// validity words per column, plus which row ids the snapshot holds (absent = deleted).
+struct CubitSnapshot {
+    uint64_t first = 0;  // row id of element 0
+    uint64_t rows = 0;   // first … first+rows-1
+    vector<vector<int64_t>> values;
+    vector<vector<uint64_t>> validity;
+    vector<bool> present;
 };
 
-// Upload what the CubitIndex buffered and record the committed deletes, under a snapshot that
-// no commit overtakes (stamp taken before the row-id scan, checked unchanged after it).
-static void SyncPartition(ClientContext &context, TableCatalogEntry &entry, CubitAttached &attached,
-                          const string &table_name) {
+// One query over the table's row ids ≥ first in the connection's open transaction.
+static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &entry, const vector<column_t> &cols,
+                     uint64_t first, CubitSnapshot &snap) {
+    string sql = "SELECT rowid";
+    for (auto c : cols) {
+        sql += ", " + KeywordHelper::WriteOptionallyQuoted(entry.GetColumn(LogicalIndex(c)).Name());
+    }
+    sql += " FROM " + KeywordHelper::WriteOptionallyQuoted(table_name);
+    if (first) {
+        sql += " WHERE rowid >= " + to_string(first);
+    }
+    sql += " ORDER BY rowid";
+    auto res = con.Query(sql);
+    if (res->HasError()) {
+        res->ThrowError();
+    }
+    snap.first = first;
+    snap.rows = 0;
+    snap.values.assign(cols.size(), {});
+    snap.validity.assign(cols.size(), {});
+    snap.present.clear();
+    while (auto chunk = res->Fetch()) {
+        chunk->Flatten();
+        auto ids = FlatVector::GetData<int64_t>(chunk->data[0]);
+        for (idx_t i = 0; i < chunk->size(); i++) {
+            const uint64_t r = (uint64_t)ids[i] - first;
+            if (r >= snap.rows) {
+                snap.rows = r + 1;
+                snap.present.resize(snap.rows, false);
+                for (idx_t c = 0; c < cols.size(); c++) {
+                    snap.values[c].resize(snap.rows, 0);
+                    snap.validity[c].resize((snap.rows + 63) / 64, 0);
+                }
+            }
+            snap.present[r] = true;
+            for (idx_t c = 0; c < cols.size(); c++) {
+                auto &vec = chunk->data[c + 1];
+                if (!FlatVector::Validity(vec).RowIsValid(i)) {
+                    continue;
+                }
+                snap.validity[c][r >> 6] |= 1ull << (r & 63);
+                snap.values[c][r] = PhysicalAsInt64(vec, i);
+            }
+        }
+    }
+}
+
+// Every distinct value when the column has at most this many (l_discount 11, l_quantity 50);
+// a column with more gets no index unless the attach names one (l_shipdate's 2,526 distinct
+// dates would take 2,526 bitvectors, 190 GB at SF100): its comparisons are built from the raw
+// column at scan time (K0).
+static constexpr idx_t kDefaultDistinctIndexMax = 256;
+
+static bool FewDistinct(const vector<int64_t> &v, const vector<uint64_t> &valid) {
+    unordered_set<int64_t> seen;
+    for (idx_t r = 0; r < v.size(); r++) {
+        if ((valid[r >> 6] >> (r & 63)) & 1) {
+            seen.insert(v[r]);
+            if (seen.size() > kDefaultDistinctIndexMax) {
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// Upload a whole snapshot as a new partition and build its indexes.
+static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap) {
+    if (attached.table) {
+        cubit_table_destroy(attached.table);
+        attached.table = nullptr;
+    }
+    Check(cubit_table_create(attached.ctx, snap.rows, 0, &attached.table));
+    for (idx_t c = 0; c < attached.column_order.size(); c++) {
+        const column_t col = attached.column_order[c];
+        const bool wide = WidePhysical(attached.columns[col]);
+        vector<int32_t> narrow;
+        if (!wide) {
+            narrow.assign(snap.values[c].begin(), snap.values[c].end());
+        }
+        Check(cubit_table_add_column(attached.table, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
+                                     wide ? (const void *)snap.values[c].data() : (const void *)narrow.data(),
+                                     snap.validity[c].data(), 0));
+        bool named = false;
+        for (auto &ix : attached.indexes) {
+            if (ix.column == col) {
+                Check(cubit_table_build_index(attached.table, (int)col, ix.encoding, ix.keys.data(),
+                                              (uint32_t)ix.keys.size()));
+                named = true;
+            }
+        }
+        if (!named && FewDistinct(snap.values[c], snap.validity[c])) {
+            Check(cubit_table_build_index(attached.table, (int)col, CUBIT_INDEX_RANGE, nullptr, 0));
+        }
+    }
+    attached.gpu_rows = snap.rows;
+}
+
+// Bring the partition to the table's committed state, reading every attached column in one
+// transaction (so no commit lands between two columns). Appends only: the new row ids are
+// read and appended (cubit_table_append, every index maintained in place); after an UPDATE of
+// an attached column, or when row ids shrank (a checkpoint's vacuum renumbers them), every
+// column is read again. Row ids the snapshot lacks are deletes, committed before it began.
+static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAttached &attached,
+                          const string &table_name, bool rebuild) {
     auto &tm = DuckTransactionManager::Get(entry.catalog.GetAttached());
-    for (int attempt = 0; attempt < 3; attempt++) {
-        const transaction_t t0 = tm.GetLastCommit();
-        Connection con(*context.db);
-        auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name));
+    // writers that finished before the snapshot below begins are in it
+    const transaction_t lowest_active = tm.LowestActiveId();
+    Connection con(*context.db);
+    con.BeginTransaction();
+    auto &snap_tx = DuckTransaction::Get(*con.context, entry.catalog);
+    const transaction_t start = snap_tx.start_time;
+    vector<transaction_t> folded;
+    {
+        lock_guard<mutex> g(attached.lock);
+        for (auto &w : attached.writers) {
+            if (w.first < lowest_active) {
+                folded.push_back(w.first);
+                rebuild |= w.second;
+            }
+        }
+    }
+    CubitSnapshot snap;
+    vector<bool> present;  // presence of every row id of the table in this snapshot
+    if (!rebuild && attached.table) {
+        // rows appended since the partition was read, then which older rows remain
+        ReadRows(con, table_name, entry, attached.column_order, attached.gpu_rows, snap);
+        auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name) +
+                             " WHERE rowid < " + to_string(attached.gpu_rows));
         if (res->HasError()) {
             res->ThrowError();
         }
-        vector<bool> present;
+        present.assign(attached.gpu_rows, false);
         while (auto chunk = res->Fetch()) {
             chunk->Flatten();
-            auto rows = FlatVector::GetData<int64_t>(chunk->data[0]);
+            auto ids = FlatVector::GetData<int64_t>(chunk->data[0]);
             for (idx_t i = 0; i < chunk->size(); i++) {
-                const uint64_t r = (uint64_t)rows[i];
-                if (r >= present.size()) {
-                    present.resize(r + 1, false);
-                }
-                present[r] = true;
+                present[(uint64_t)ids[i]] = true;
             }
         }
-        if (tm.GetLastCommit() != t0) {
-            continue;  // a commit landed during the scan: take a new snapshot
+        if (snap.rows == 0 && entry.GetStorage().GetTotalRows() < attached.gpu_rows) {
+            rebuild = true;  // fewer rows than the partition: renumbered by a vacuum
         }
-        lock_guard<mutex> g(attached.lock);
-        // appends in row order, each continuing the partition
-        std::sort(attached.pending.begin(), attached.pending.end(),
-                  [](const CubitAttached::Pending &a, const CubitAttached::Pending &b) { return a.first < b.first; });
-        for (auto &p : attached.pending) {
-            if ((uint64_t)p.first != attached.gpu_rows) {
-                throw InvalidInputException("cubit_sync: appended rows start at %lld, the partition holds %llu rows; "
-                                            "run cubit_attach again",
-                                            (long long)p.first, (unsigned long long)attached.gpu_rows);
-            }
+    }
+    if (rebuild || !attached.table) {
+        ReadRows(con, table_name, entry, attached.column_order, 0, snap);
+        con.Commit();
+        if (snap.rows == 0) {
+            throw InvalidInputException("cubit: %s has no rows to attach", table_name);
+        }
+        BuildPartition(attached, snap);
+        present = snap.present;
+    } else {
+        con.Commit();
+        if (snap.rows) {
             vector<int> cols;
             vector<const void *> data;
             vector<const uint64_t *> valid;
@@ -713,33 +805,33 @@ static void SyncPartition(ClientContext &context, TableCatalogEntry &entry, Cubi
                 const column_t col = attached.column_order[c];
                 cols.push_back((int)col);
                 if (WidePhysical(attached.columns[col])) {
-                    data.push_back(p.values[c].data());
+                    data.push_back(snap.values[c].data());
                 } else {
-                    narrow.emplace_back(p.values[c].begin(), p.values[c].end());
+                    narrow.emplace_back(snap.values[c].begin(), snap.values[c].end());
                     data.push_back(narrow.back().data());
                 }
-                valid.push_back(p.validity[c].data());
+                valid.push_back(snap.validity[c].data());
             }
-            Check(cubit_table_append(attached.table, p.count, cols.data(), data.data(), valid.data(),
+            Check(cubit_table_append(attached.table, snap.rows, cols.data(), data.data(), valid.data(),
                                      (uint32_t)cols.size(), 0));
-            attached.gpu_rows += p.count;
+            attached.gpu_rows += snap.rows;
+            present.insert(present.end(), snap.present.begin(), snap.present.end());
         }
-        attached.pending.clear();
-        // committed deletes: rows of the partition the snapshot does not see (and the rows the
-        // index was told to remove), committed before every later snapshot
-        vector<int64_t> gone;
-        for (uint64_t r = 0; r < attached.gpu_rows; r++) {
-            if (r >= present.size() || !present[r]) {
-                gone.push_back((int64_t)r);
-            }
-        }
-        attached.deleted.clear();
-        vector<uint64_t> ids(gone.size(), 0);
-        Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
-        attached.stamp = t0;
-        return;
     }
-    throw InvalidInputException("cubit_sync: commits kept landing during the sync of %s; retry", table_name);
+    // committed deletes: visible to every snapshot the swap admits (start_time >= start)
+    vector<int64_t> gone;
+    for (uint64_t r = 0; r < attached.gpu_rows; r++) {
+        if (r >= present.size() || !present[r]) {
+            gone.push_back((int64_t)r);
+        }
+    }
+    vector<uint64_t> ids(gone.size(), 0);
+    Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
+    lock_guard<mutex> g(attached.lock);
+    for (auto w : folded) {
+        attached.writers.erase(w);
+    }
+    attached.sync_start = start;
 }
 
 // PRAGMA cubit_sync(table)
@@ -750,100 +842,103 @@ static void CubitSync(ClientContext &context, const FunctionParameters &paramete
     if (!attached || !attached->table) {
         throw InvalidInputException("cubit_sync: %s is not attached", table_name);
     }
-    SyncPartition(context, entry, *attached, table_name);
+    SyncPartition(context, entry.Cast<DuckTableEntry>(), *attached, table_name, false);
 }
 
-// ------------------------------------------------------------------ attach
+// Index specification of cubit_attach's third argument: `column=encoding[:v1,v2,…]` items
+// separated by ';' — encoding range | equality | bins, values as SQL literals of the column's
+// type (dates, decimals), e.g.
+//   'l_shipdate=range:1994-01-01,1995-01-01;l_shipdate=bins:1992-01-01,1993-01-01,…;l_discount=range'
+static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string &spec) {
+    vector<CubitIndexSpec> out;
+    for (auto item : StringUtil::Split(spec, ';')) {
+        StringUtil::Trim(item);
+        if (item.empty()) {
+            continue;
+        }
+        const auto eq = item.find('=');
+        if (eq == string::npos) {
+            throw InvalidInputException("cubit_attach: index item '%s' is not column=encoding[:values]", item);
+        }
+        auto name = item.substr(0, eq);
+        auto rest = item.substr(eq + 1);
+        StringUtil::Trim(name);
+        const auto colon = rest.find(':');
+        auto enc = StringUtil::Lower(rest.substr(0, colon));
+        StringUtil::Trim(enc);
+        const auto &def = entry.GetColumn(name);
+        CubitIndexSpec ix;
+        ix.column = def.StorageOid();
+        if (enc == "range") {
+            ix.encoding = CUBIT_INDEX_RANGE;
+        } else if (enc == "equality") {
+            ix.encoding = CUBIT_INDEX_EQUALITY;
+        } else if (enc == "bins") {
+            ix.encoding = CUBIT_INDEX_BINS;
+        } else {
+            throw InvalidInputException("cubit_attach: unknown index encoding '%s'", enc);
+        }
+        if (colon != string::npos) {
+            for (auto lit : StringUtil::Split(rest.substr(colon + 1), ',')) {
+                StringUtil::Trim(lit);
+                ix.keys.push_back(ConstantAsInt64(Value(lit).DefaultCastAs(def.GetType())));
+            }
+            std::sort(ix.keys.begin(), ix.keys.end());
+            ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end()), ix.keys.end());
+        }
+        if (ix.encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) {
+            throw InvalidInputException("cubit_attach: bins on %s need at least two edges", name);
+        }
+        out.push_back(std::move(ix));
+    }
+    return out;
+}
 
-// PRAGMA cubit_attach(table, 'col,col,…'): read the columns in row-id order through a second
-// connection (its own transaction), upload them and build an exact range index per column.
-// Row ids missing from the scan (deleted rows) become committed deletes of the partition.
-static void CubitAttach(ClientContext &context, const FunctionParameters &parameters) {
-    const auto table_name = parameters.values[0].ToString();
-    const auto column_list = StringUtil::Split(parameters.values[1].ToString(), ',');
+// PRAGMA cubit_attach(table, 'col,col,…' [, index_spec]): read the columns in row-id order in
+// one transaction, upload them and build the named indexes (by default an every-distinct-value
+// range index on the columns with few distinct values). Attaching again replaces the partition.
+static void CubitAttachImpl(ClientContext &context, const string &table_name, const string &column_list,
+                            const string &spec) {
     auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
-    Connection con(*context.db);
-    auto max_row = con.Query("SELECT max(rowid) FROM " + KeywordHelper::WriteOptionallyQuoted(table_name));
-    if (max_row->HasError()) {
-        max_row->ThrowError();
+    if (!entry.IsDuckTable()) {
+        throw InvalidInputException("cubit_attach: %s is not a DuckDB table", table_name);
     }
-    const auto top = max_row->GetValue(0, 0);
-    const uint64_t n_rows = top.IsNull() ? 0 : (uint64_t)top.GetValue<int64_t>() + 1;
-    if (n_rows == 0) {
-        throw InvalidInputException("cubit_attach: %s is empty", table_name);
-    }
+    auto &duck = entry.Cast<DuckTableEntry>();
     auto &attached = CubitRegistry::Insert(entry);
     if (!attached.ctx) {
         Check(cubit_ctx_create(0, &attached.ctx));
     }
-    if (attached.table) {
-        cubit_table_destroy(attached.table);
+    {
+        lock_guard<mutex> g(attached.lock);
         attached.columns.clear();
         attached.column_order.clear();
-    }
-    Check(cubit_table_create(attached.ctx, n_rows, 0, &attached.table));
-    vector<bool> present(n_rows, false);
-    for (auto name : column_list) {
-        StringUtil::Trim(name);
-        const auto &def = entry.GetColumn(name);
-        const auto phys = def.GetType().InternalType();
-        if (!IntegerPhysical(phys)) {
-            throw InvalidInputException("cubit_attach: column %s is not integer-backed", name);
+        for (auto name : StringUtil::Split(column_list, ',')) {
+            StringUtil::Trim(name);
+            const auto &def = duck.GetColumn(name);
+            const auto phys = def.GetType().InternalType();
+            if (!IntegerPhysical(phys)) {
+                throw InvalidInputException("cubit_attach: column %s is not integer-backed", name);
+            }
+            attached.columns[def.StorageOid()] = phys;
+            attached.column_order.push_back(def.StorageOid());
         }
-        const bool wide = WidePhysical(phys);
-        vector<int32_t> v32(wide ? 0 : n_rows, 0);
-        vector<int64_t> v64(wide ? n_rows : 0, 0);
-        vector<uint64_t> valid((n_rows + 63) / 64, 0);
-        auto res = con.Query("SELECT rowid, " + KeywordHelper::WriteOptionallyQuoted(name) + " FROM " +
-                             KeywordHelper::WriteOptionallyQuoted(table_name) + " ORDER BY rowid");
-        if (res->HasError()) {
-            res->ThrowError();
-        }
-        while (auto chunk = res->Fetch()) {
-            chunk->Flatten();
-            auto rows = FlatVector::GetData<int64_t>(chunk->data[0]);
-            auto &vals = chunk->data[1];
-            auto &mask = FlatVector::Validity(vals);
-            for (idx_t i = 0; i < chunk->size(); i++) {
-                const uint64_t r = (uint64_t)rows[i];
-                present[r] = true;
-                if (!mask.RowIsValid(i)) {
-                    continue;
-                }
-                valid[r >> 6] |= 1ull << (r & 63);
-                if (wide) {
-                    v64[r] = PhysicalAsInt64(vals, i);
-                } else {
-                    v32[r] = (int32_t)PhysicalAsInt64(vals, i);
-                }
+        attached.indexes = ParseIndexSpec(duck, spec);
+        for (auto &ix : attached.indexes) {
+            if (!attached.columns.count(ix.column)) {
+                throw InvalidInputException("cubit_attach: an index names a column that is not attached");
             }
         }
-        const column_t storage = def.StorageOid();
-        Check(cubit_table_add_column(attached.table, (int)storage, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
-                                     wide ? (const void *)v64.data() : (const void *)v32.data(), valid.data(), 0));
-        Check(cubit_table_build_index(attached.table, (int)storage, CUBIT_INDEX_RANGE, nullptr, 0));
-        attached.columns[storage] = phys;
-        attached.column_order.push_back(storage);
     }
-    attached.gpu_rows = n_rows;
-    attached.pending.clear();
-    attached.deleted.clear();
-    // from here DuckDB reports every committed append and index removal to the CubitIndex; the
-    // deletes and the stamp come from a snapshot no commit overtook (SyncPartition)
-    auto &duck = entry.Cast<DuckTableEntry>();
-    auto &storage = duck.GetStorage();
-    if (!attached.index_added) {
-        vector<unique_ptr<Expression>> exprs;
-        vector<column_t> ids;
-        for (auto c : attached.column_order) {
-            exprs.push_back(make_uniq<BoundReferenceExpression>(duck.GetColumn(LogicalIndex(c)).GetType(), c));
-            ids.push_back(c);
-        }
-        storage.AddIndex(make_uniq<CubitIndex>("cubit_" + table_name, ids, TableIOManager::Get(storage), exprs,
-                                               entry.catalog.GetAttached(), &attached));
-        attached.index_added = true;
-    }
-    SyncPartition(context, entry, attached, table_name);
+    SyncPartition(context, duck, attached, table_name, true);
+}
+
+static void CubitAttach(ClientContext &context, const FunctionParameters &parameters) {
+    CubitAttachImpl(context, parameters.values[0].ToString(), parameters.values[1].ToString(), "");
+}
+
+static void CubitAttachIndexed(ClientContext &context, const FunctionParameters &parameters) {
+    CubitAttachImpl(context, parameters.values[0].ToString(), parameters.values[1].ToString(),
+                    parameters.values[2].ToString());
 }
 
 } // namespace duckdb
@@ -851,20 +946,17 @@ static void CubitAttach(ClientContext &context, const FunctionParameters &parame
 extern "C" {
 
 DUCKDB_EXTENSION_API void cubit_init(duckdb::DatabaseInstance &db) {
-    auto &config = duckdb::DBConfig::GetConfig(db);
-    duckdb::OptimizerExtension ext;
-    ext.optimize_function = duckdb::CubitOptimize;
+    using namespace duckdb;
+    auto &config = DBConfig::GetConfig(db);
+    OptimizerExtension ext;
+    ext.optimize_function = CubitOptimize;
     config.optimizer_extensions.push_back(std::move(ext));
-    duckdb::ExtensionUtil::RegisterFunction(
-        db, duckdb::PragmaFunction::PragmaCall("cubit_attach", duckdb::CubitAttach,
-                                               {duckdb::LogicalType::VARCHAR, duckdb::LogicalType::VARCHAR}));
-    duckdb::ExtensionUtil::RegisterFunction(
-        db, duckdb::PragmaFunction::PragmaCall("cubit_sync", duckdb::CubitSync, {duckdb::LogicalType::VARCHAR}));
-    // the index type (index_type_set.cpp:7-13 registers ART the same way)
-    duckdb::IndexType cubit_index;
-    cubit_index.name = duckdb::CubitIndex::TYPE_NAME;
-    cubit_index.create_instance = duckdb::CubitIndex::Create;
-    config.GetIndexTypes().RegisterIndexType(cubit_index);
+    PragmaFunctionSet attach("cubit_attach");
+    attach.AddFunction(PragmaFunction::PragmaCall("cubit_attach", CubitAttach, {LogicalType::VARCHAR, LogicalType::VARCHAR}));
+    attach.AddFunction(PragmaFunction::PragmaCall("cubit_attach", CubitAttachIndexed,
+                                                  {LogicalType::VARCHAR, LogicalType::VARCHAR, LogicalType::VARCHAR}));
+    ExtensionUtil::RegisterFunction(db, attach);
+    ExtensionUtil::RegisterFunction(db, PragmaFunction::PragmaCall("cubit_sync", CubitSync, {LogicalType::VARCHAR}));
 }
 
 DUCKDB_EXTENSION_API const char *cubit_version() {

@@ -35,7 +35,7 @@ extern "C" {
 #define CUBIT_ERR_OOM 3          /* device allocation failed */
 #define CUBIT_ERR_UNSUPPORTED 4  /* predicate shape / type not supported */
 #define CUBIT_ERR_CAPACITY 5     /* output buffer too small (count still reported) */
-#define CUBIT_ERR_DEVICE 6       /* in-kernel failure (bounded spin expired) */
+#define CUBIT_ERR_DEVICE 6       /* device-side failure (stream event creation, …) */
 
 /* ---- physical types (DuckDB PhysicalType subset on the path: DATE = INT32,
  *      DECIMAL(15,2) = INT64, BIGINT = INT64, INTEGER = INT32) */
@@ -135,6 +135,11 @@ const char *cubit_last_error(void);
 #define CUBIT_DECODE_RUNS 2
 #define CUBIT_DECODE_LOOKBACK 3
 int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
+/* Look-back decode: polls of an earlier tile's flag before the polling thread counts that tile
+ * from its bitvectors itself (0 = the library default, 2^22). The expiry path is part of every
+ * launch — no workgroup waits without bound and the count is always exact — and a small limit
+ * forces it (tests). */
+int cubit_ctx_set_lookback_spins(cubit_ctx *ctx, uint32_t spins);
 /* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS, or _LOOKBACK; 0 when
  * the partition had no row and nothing was launched). */
 int cubit_ctx_last_decode_kernel(cubit_ctx *ctx, int *kernel);

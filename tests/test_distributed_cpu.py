@@ -95,3 +95,44 @@ def test_partition_range_alignment_and_cover():
         assert b1 % parallel.ROW_GROUP == 0 and b1 % 64 == 0
     sizes = [e - b for b, e in parts]
     assert max(sizes) - min(sizes) <= 2 * parallel.ROW_GROUP
+
+
+def _empty_worker(rank, world, port, result_path):
+    import sys
+
+    from conftest import ROOT
+
+    for p in (str(ROOT / "duckdb-cubit_amd"), str(ROOT)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from cubit_amd import parallel as P
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # every rank's filter keeps nothing: slot 0, no point-to-point op may be posted
+        none = P.gather_rowids(torch.empty(0, dtype=torch.int64), dst=0)
+        ex = P.RowIdExchange(0)
+        ex.post(torch.empty(0, dtype=torch.int64), torch.zeros(1, dtype=torch.int64))
+        none_slots = ex.result()
+        # only the last rank keeps rows (ragged: the others send padding)
+        mine = torch.arange(5, dtype=torch.int64) + 100 * rank if rank == world - 1 else torch.empty(0, dtype=torch.int64)
+        some = P.gather_rowids(mine, dst=0)
+        if rank == 0:
+            np.save(result_path, np.array([none.numel(), none_slots.numel()]))
+            np.save(str(result_path) + ".some.npy", some.numpy())
+        else:
+            assert none is None and none_slots is None and some is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_of_empty_results(tmp_path, world):
+    """when every rank's result is empty the slot is 0; the root must not post a
+    1-element receive against 0-element sends (a hang on RCCL, a size mismatch on gloo)."""
+    res = tmp_path / "empty.npy"
+    mp.spawn(_empty_worker, args=(world, _free_port(), str(res)), nprocs=world, join=True)
+    assert np.load(res).tolist() == [0, 0]
+    assert np.load(str(res) + ".some.npy").tolist() == [100 * (world - 1) + i for i in range(5)]

@@ -202,3 +202,60 @@ def test_ordered_scan_past_the_old_lookback_limit(ctx):
     got = run_program(ctx, dleaves, 2, 0, prog, n, 3, out, cnt, False)
     assert ctx.last_decode_kernel() == L.DECODE_RUNS
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("n", [1_000_003, 100_000_000, 140_000_001])
+def test_lookback_expiry_recounts_and_stays_exact(ctx, n):
+    """The look-back's bounded wait: with a spin limit of 1 poll almost every workgroup finds some
+    earlier flag unpublished and counts that tile from its bitvectors itself. Row ids and count
+    must still equal the oracle's, in row order, for plain, negated and OR programs — the kernel
+    has no failure exit (it used to write count = ~0 and drop its run)."""
+    rng = np.random.default_rng(n % 997)
+    pw, nw = padded_words(n), (n + 63) // 64
+    host = [shaped_leaf(rng, n), rand_words(rng, nw, 1), rand_words(rng, nw, 8)]
+    for w in host[1:]:
+        if n & 63:
+            w[-1] &= np.uint64((1 << (n & 63)) - 1)
+    dleaves = [ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])) for w in host]
+    out = ctx.alloc(max(n // 2, 1024) * 8)
+    cnt = ctx.alloc(16)
+    ctx.set_decode_kernel(L.DECODE_LOOKBACK)
+    try:
+        for spins in (1, 3):
+            ctx.set_lookback_spins(spins)
+            for k, neg, prog in [(1, 0, [0]), (2, 0b10, [0, 1, L.OP_AND]),
+                                 (3, 0, [0, 1, L.OP_AND, 2, L.OP_OR])]:
+                ol = [(~host[j] if (neg >> j) & 1 else host[j]) for j in range(k)]
+                if neg and n & 63:
+                    for j in range(k):
+                        if (neg >> j) & 1:
+                            ol[j] = ol[j].copy()
+                            ol[j][-1] &= np.uint64((1 << (n & 63)) - 1)
+                ref, _ = O.bitmap_eval(ol, prog, n, 11)
+                got = run_program(ctx, dleaves, k, neg, prog, n, 11, out, cnt, True)
+                assert ctx.last_decode_kernel() == L.DECODE_LOOKBACK
+                assert np.array_equal(got, ref), (spins, k, neg, prog)
+    finally:
+        ctx.set_lookback_spins(0)
+        ctx.set_decode_kernel(L.DECODE_AUTO)
+
+
+def test_lookback_expiry_with_zonemap_skip(ctx):
+    """The expiry recount follows the live-tile list (zonemap skip): a clustered column whose
+    filter keeps a few zones, scanned ordered with a spin limit of 1, equals numpy."""
+    n = 50_000_000
+    a = (np.arange(n, dtype=np.int64) // 1000).astype(np.int32)  # ascending: zones skip
+    t = CubitTable(ctx, n, row_base=5)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE, [1000, 20000, 30000, 45000])
+    fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 20000), F.ConstantFilter("<", 30000)])})
+    ref = np.flatnonzero((a >= 20000) & (a < 30000)).astype(np.int64) + 5
+    ctx.set_lookback_spins(1)
+    try:
+        got = t.scan(fs, ordered=True)
+        assert np.array_equal(got, ref)
+        ev, zones = t.last_zones()
+        assert ev < zones
+    finally:
+        ctx.set_lookback_spins(0)
+        t.close()

@@ -229,3 +229,36 @@ def C_release():
     p, d = C.c_uint64(), C.c_uint64()
     L.check_scan(L.scan_lib().cubit_scan_release_cached(C.byref(p), C.byref(d)))
     return int(p.value), int(d.value)
+
+
+def test_pinned_windows_are_reused_across_scans(ctx):
+    """page-locked windows are filed under no context, and a later scan must find
+    them there — two identical scans in a row leave as many pinned bytes cached as one scan
+    (a pool that never hits pins fresh memory for the second scan and caches both)."""
+    n = 2_000_003
+    a = np.random.default_rng(5).integers(0, 1000, n).astype(np.int64)
+    t = CubitTable(ctx, n)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE)
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 300)})
+
+    def drain():
+        fn = CubitScanFunction(t, [0, ROW_ID], [], fs)
+        local = fn.init_local()
+        rows = 0
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                break
+            rows += len(cols[0])
+        fn.close()
+        assert rows == int((a < 300).sum())
+
+    C_release()
+    drain()
+    one, _ = C_release()
+    drain()
+    drain()
+    two, _ = C_release()
+    assert two == one > 0
+    t.close()
