@@ -21,6 +21,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "cubit_internal.hpp"
 
 namespace cubit {
@@ -2285,51 +2288,15 @@ __global__ __launch_bounds__(256) void bitpacked_compare_kernel(const uint8_t* _
     }
 }
 
-// The same filter for columns whose groups are all FOR of ≤ MAXW bits (MAXW ≤ 32), CONSTANT or
-// CONSTANT_DELTA (the modes DuckDB's AUTO picks for unsorted integer columns): one wave per group.
-// The wave lands its group's packed words in its own LDS slice with coalesced 256-byte loads — all
-// of them in flight at once (≤ MAXW per lane), one round trip per group — then tests 64 values per
-// step, each lane taking its value's bits from the staged words with one funnel shift. One ballot
-// per step = one 64-row output word, stored (or OR-ed where a group's rows share the word with a
-// neighbour) by lane 0, as in bitpacked_compare_kernel. Measured before (profiles/r03w_*): the
-// same wave layout loading each value's two words from global memory, eight 64-value steps in
-// flight: 0.650 ms for a 600 M-row 12-bit column (the LDS kernel above 0.93 ms, K0 0.43 ms).
-template <typename T, typename U, int MAXW>
-__global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __restrict__ bytes,
-                                                               const BpGroup* __restrict__ groups, uint32_t n_groups,
-                                                               const uint64_t* __restrict__ validity, T lo, T hi,
-                                                               int neg, uint64_t* __restrict__ out) {
-    static_assert(MAXW >= 1 && MAXW <= 32, "FOR groups of at most 32 bits");
-    constexpr uint32_t SLICE = 64u * MAXW + 4u;  // a group's words (2,048·w/32) + the read window
-    __shared__ uint32_t s_w[4][SLICE];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t g = blockIdx.x * 4u + wave;
-    if (g >= n_groups) return;  // no workgroup barrier below: each wave works alone
-    uint32_t* L = s_w[wave];
-    const BpGroup cur = groups[g];
+// One group's 64-row output words from its values (a FOR group's packed words staged in L,
+// CONSTANT / CONSTANT_DELTA from its record): 64 values per step, each lane taking its value's
+// bits from the staged words with one funnel shift, one ballot per step = one output word
+// (shared by bitpacked_compare_waves and bitpacked_compare_stream).
+template <typename T, typename U>
+__device__ __forceinline__ void compare_group_words(const BpGroup& cur, const uint32_t* L, bool packed, uint32_t w,
+                                                    uint32_t mask, int lane, const uint64_t* __restrict__ validity,
+                                                    T lo, T hi, int neg, uint64_t* __restrict__ out) {
     const uint64_t end = cur.row_start + cur.count;
-    const bool packed = cur.mode == 5 && cur.width;
-    const uint32_t w = packed ? cur.width : 0u;
-    const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1u;
-    const uint32_t nwords = packed ? (cur.count + 31u) / 32u * w : 0u;  // ≤ 64·MAXW (host-checked)
-    if (packed) {
-        const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + cur.words_off);
-        uint32_t x[MAXW];
-#pragma unroll
-        for (int m = 0; m < MAXW; ++m) {
-            const uint32_t k = 64u * (uint32_t)m + (uint32_t)lane;
-            x[m] = k < nwords ? __builtin_nontemporal_load(W + k) : 0u;
-        }
-#pragma unroll
-        for (int m = 0; m < MAXW; ++m) L[64u * (uint32_t)m + (uint32_t)lane] = x[m];
-        if (lane < 4) L[64u * MAXW + (uint32_t)lane] = 0u;
-        // the wave's own LDS writes, read back by other lanes of the same wave: LDS operations of a
-        // wave complete in order, so only the compiler must not move the reads above the writes
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    }
     const U base = (U)cur.base, d = cur.mode == 3 ? (U)cur.aux : (U)0;
     const uint32_t nchunks = (cur.count + 63u) / 64u;  // ≤ 32
     // a group starting on a 64-row boundary keeps step c's word in lane c and stores the words
@@ -2378,6 +2345,117 @@ __global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __
         const uint64_t r0 = cur.row_start + 64ull * (uint32_t)lane;
         if (r0 + 64 <= end) out[r0 >> 6] = myword;  // only this group's rows
         else atomicOr(reinterpret_cast<unsigned long long*>(&out[r0 >> 6]), (unsigned long long)myword);
+    }
+}
+
+// The same filter for columns whose groups are all FOR of ≤ MAXW bits (MAXW ≤ 32), CONSTANT or
+// CONSTANT_DELTA (the modes DuckDB's AUTO picks for unsorted integer columns): one wave per group.
+// The wave lands its group's packed words in its own LDS slice with coalesced 256-byte loads — all
+// of them in flight at once (≤ MAXW per lane), one round trip per group — then tests 64 values per
+// step, each lane taking its value's bits from the staged words with one funnel shift. One ballot
+// per step = one 64-row output word, stored (or OR-ed where a group's rows share the word with a
+// neighbour) by lane 0, as in bitpacked_compare_kernel. Measured before (profiles/r03w_*): the
+// same wave layout loading each value's two words from global memory, eight 64-value steps in
+// flight: 0.650 ms for a 600 M-row 12-bit column (the LDS kernel above 0.93 ms, K0 0.43 ms).
+template <typename T, typename U, int MAXW>
+__global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __restrict__ bytes,
+                                                               const BpGroup* __restrict__ groups, uint32_t n_groups,
+                                                               const uint64_t* __restrict__ validity, T lo, T hi,
+                                                               int neg, uint64_t* __restrict__ out) {
+    static_assert(MAXW >= 1 && MAXW <= 32, "FOR groups of at most 32 bits");
+    constexpr uint32_t SLICE = 64u * MAXW + 4u;  // a group's words (2,048·w/32) + the read window
+    __shared__ uint32_t s_w[4][SLICE];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t g = blockIdx.x * 4u + wave;
+    if (g >= n_groups) return;  // no workgroup barrier below: each wave works alone
+    uint32_t* L = s_w[wave];
+    const BpGroup cur = groups[g];
+    const bool packed = cur.mode == 5 && cur.width;
+    const uint32_t w = packed ? cur.width : 0u;
+    const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1u;
+    const uint32_t nwords = packed ? (cur.count + 31u) / 32u * w : 0u;  // ≤ 64·MAXW (host-checked)
+    if (packed) {
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + cur.words_off);
+        uint32_t x[MAXW];
+#pragma unroll
+        for (int m = 0; m < MAXW; ++m) {
+            const uint32_t k = 64u * (uint32_t)m + (uint32_t)lane;
+            x[m] = k < nwords ? __builtin_nontemporal_load(W + k) : 0u;
+        }
+#pragma unroll
+        for (int m = 0; m < MAXW; ++m) L[64u * (uint32_t)m + (uint32_t)lane] = x[m];
+        if (lane < 4) L[64u * MAXW + (uint32_t)lane] = 0u;
+        // the wave's own LDS writes, read back by other lanes of the same wave: LDS operations of a
+        // wave complete in order, so only the compiler must not move the reads above the writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+    compare_group_words<T, U>(cur, L, packed, w, mask, lane, validity, lo, hi, neg, out);
+}
+
+// bitpacked_compare_waves as a persistent grid: wave v of G takes groups v, v + G, v + 2G, …
+// and issues the packed-word loads of its next group before it tests the current one from LDS,
+// so each wave always has one group's loads in flight behind its compare steps — the LDS ring
+// of DESIGN.md §3, one stage deep per wave, in registers — and the launch is a few thousand
+// workgroups instead of one per four groups.
+template <typename T, typename U, int MAXW>
+__global__ __launch_bounds__(256) void bitpacked_compare_stream(const uint8_t* __restrict__ bytes,
+                                                                const BpGroup* __restrict__ groups, uint32_t n_groups,
+                                                                const uint64_t* __restrict__ validity, T lo, T hi,
+                                                                int neg, uint64_t* __restrict__ out) {
+    static_assert(MAXW >= 1 && MAXW <= 32, "FOR groups of at most 32 bits");
+    constexpr uint32_t SLICE = 64u * MAXW + 4u;
+    __shared__ uint32_t s_w[4][SLICE];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t stride = gridDim.x * 4u;
+    uint32_t g = blockIdx.x * 4u + wave;
+    if (g >= n_groups) return;  // no workgroup barrier below: each wave works alone
+    uint32_t* L = s_w[wave];
+    auto load_words = [&](const BpGroup& gr, uint32_t (&x)[MAXW]) {
+        const bool pk = gr.mode == 5 && gr.width;
+        const uint32_t nw = pk ? (gr.count + 31u) / 32u * gr.width : 0u;  // ≤ 64·MAXW (host-checked)
+        const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + gr.words_off);
+#pragma unroll
+        for (int m = 0; m < MAXW; ++m) {
+            const uint32_t kk = 64u * (uint32_t)m + (uint32_t)lane;
+            x[m] = kk < nw ? __builtin_nontemporal_load(W + kk) : 0u;
+        }
+    };
+    BpGroup cur = groups[g];
+    uint32_t x[MAXW];
+    load_words(cur, x);
+    for (;;) {
+        const uint32_t gn = g + stride;
+        const bool more = gn < n_groups;
+        const bool packed = cur.mode == 5 && cur.width;
+        // the current group's words into this wave's LDS slice (waits for their loads)
+        if (packed) {
+#pragma unroll
+            for (int m = 0; m < MAXW; ++m) L[64u * (uint32_t)m + (uint32_t)lane] = x[m];
+            if (lane < 4) L[64u * MAXW + (uint32_t)lane] = 0u;
+        }
+        // the next group's loads, in flight while this one is tested
+        BpGroup nxt = cur;
+        if (more) {
+            nxt = groups[gn];
+            load_words(nxt, x);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        const uint32_t w = packed ? cur.width : 0u;
+        const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1u;
+        compare_group_words<T, U>(cur, L, packed, w, mask, lane, validity, lo, hi, neg, out);
+        if (!more) break;
+        // every lane has read the slice before the next group's words overwrite it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        cur = nxt;
+        g = gn;
     }
 }
 
@@ -3060,6 +3138,17 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
     return hipGetLastError();
 }
 
+// Which wave kernel the packed filter takes: 1 = bitpacked_compare_stream (persistent, default),
+// 0 = bitpacked_compare_waves (one wave per group); CUBIT_PACKED_FILTER_KERNEL overrides (A/B).
+int packed_filter_kernel() {
+    static const int k = [] {
+        const char* e = std::getenv("CUBIT_PACKED_FILTER_KERNEL");
+        return e && *e ? std::atoi(e) : 1;
+    }();
+    return k;
+}
+constexpr uint32_t kPackedStreamBlocks = 2048;  // 8 workgroups of 4 waves per CU
+
 hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
                                     uint64_t* out, hipStream_t stream, int simple_width) {
@@ -3069,6 +3158,28 @@ hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups,
     const int64_t lo = rg.lo, hi = rg.hi;
     const int neg = rg.neg;
     const uint32_t ng = (uint32_t)n_groups;
+    if (simple_width > 0 && packed_filter_kernel() == 1) {
+        // persistent waves, next group's loads in flight (bitpacked_compare_stream)
+        const dim3 grid(std::min<uint32_t>((ng + 3) / 4, kPackedStreamBlocks));
+        if (type == 0) {
+            int32_t lo32, hi32;
+            rg.clamp32(lo32, hi32);
+            if (simple_width <= 16)
+                hipLaunchKernelGGL((bitpacked_compare_stream<int32_t, uint32_t, 16>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo32, hi32, neg, out);
+            else
+                hipLaunchKernelGGL((bitpacked_compare_stream<int32_t, uint32_t, 32>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo32, hi32, neg, out);
+        } else {
+            if (simple_width <= 16)
+                hipLaunchKernelGGL((bitpacked_compare_stream<int64_t, uint64_t, 16>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo, hi, neg, out);
+            else
+                hipLaunchKernelGGL((bitpacked_compare_stream<int64_t, uint64_t, 32>), grid, dim3(256), 0, stream, bytes,
+                                   groups, ng, validity, lo, hi, neg, out);
+        }
+        return hipGetLastError();
+    }
     if (simple_width > 0) {  // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA: one wave per group
         const dim3 grid((ng + 3) / 4);
         if (type == 0) {

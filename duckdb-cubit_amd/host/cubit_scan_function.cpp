@@ -143,12 +143,20 @@ struct PooledBuffer {
 // laid out in tile order, so consecutive tiles are one contiguous range of ids) and the probe
 // of every emitted column, all on the device — and copies only the count and the tile
 // directory to the host. The ids and values then reach the host per *window* (consecutive
-// non-empty tiles of about kWindowRows rows): the local state that claims a window copies its
+// non-empty tiles of about window_rows() rows): the local state that claims a window copies its
 // range of every emitted column into its own page-locked buffer and hands the window's tiles
 // out as DataChunks. The reference hands out one row group per NextParallelScan and produces
 // its chunks on demand (table_scan.cpp:119-156); a window is the unit a GPU→host copy is worth.
-constexpr idx_t kWindowRows = 1u << 18;
-constexpr idx_t kWindowTiles = 64;
+// Window size: at most window_rows() rows and window_rows() / 4,096 tiles (2^18 rows and 64
+// tiles by default; CUBIT_SCAN_WINDOW_ROWS sets the row bound, a power of two ≥ 2^14).
+idx_t window_rows() {
+    static const idx_t rows = [] {
+        const char* e = std::getenv("CUBIT_SCAN_WINDOW_ROWS");
+        idx_t r = e && *e ? (idx_t)std::strtoull(e, nullptr, 10) : (idx_t)1 << 18;
+        return std::max<idx_t>(r, (idx_t)1 << 14);
+    }();
+    return rows;
+}
 
 struct Window {
     uint32_t first, last;  // index range [first, last) into the non-empty tiles
@@ -247,8 +255,9 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
                                                std::to_string(g->count) + " row ids");
     for (uint32_t i = 0; i < g->tiles.size();) {
         Window w{i, i, g->tile_off[i], 0};
-        while (w.last < g->tiles.size() && (w.last == w.first || (w.len + g->tile_len[w.last] <= kWindowRows &&
-                                                                   w.last - w.first < kWindowTiles))) {
+        const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
+        while (w.last < g->tiles.size() && (w.last == w.first || (w.len + g->tile_len[w.last] <= max_rows &&
+                                                                   w.last - w.first < max_tiles))) {
             w.len += g->tile_len[w.last];
             ++w.last;
         }

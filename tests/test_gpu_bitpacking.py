@@ -197,3 +197,44 @@ def test_fused_sum_reads_packed_column(ctx, mode):
         assert s_plain == want and s_packed == want, (mode, f.comparison)
         assert n_plain == n_packed
     t.close()
+
+
+# ---------------------------------------------------------------- segments DuckDB itself wrote
+
+from test_oracle_bitpacking import REF_SEGMENTS, reference_segment  # noqa: E402
+
+
+@pytest.mark.parametrize("s", REF_SEGMENTS, ids=[s["name"] for s in REF_SEGMENTS])
+def test_gpu_reads_duckdb_written_segment(ctx, s):
+    """BITPACKING bytes exactly as DuckDB v1.1.2 stored them (tests/golden/
+    bitpacking_reference_segments.json: FOR, DELTA_FOR and CONSTANT_DELTA groups, INT32 and
+    INT64, NULL rows, a 49-group segment with a partial last group) through K5: the unpacked
+    column, the packed-segment filter and the fused sum that reads the column at the
+    qualifying rows from the segments must give the reference's values."""
+    col, values, valid = reference_segment(s)
+    n = s["count"]
+    t = CubitTable(ctx, n, row_base=3)
+    vw = validity_from_mask(valid)
+    t.add_bitpacked_column(0, col.data, col.seg_off, col.seg_count, values.dtype, validity=vw)
+    got = t.download_column(0)
+    assert np.array_equal(got[valid], values[valid])
+    assert np.array_equal(got, O.bp_decode(col))  # NULL slots: the stored filler, as the oracle reads it
+    oc = O.Column(values, vw)
+    lo, hi = int(values[valid].min()), int(values[valid].max())
+    mid = int(np.median(values[valid]))
+    for cmp, k in (("=", mid), ("!=", mid), ("<", mid), (">=", mid), ("<=", lo), (">", hi - 1), ("<", lo)):
+        fs = F.TableFilterSet({0: F.ConstantFilter(cmp, k)})
+        ref = O.table_scan([oc], F.serialize(fs), n, row_base=3)
+        t.use_packed_filter(True)
+        assert np.array_equal(t.scan(fs), ref), (s["name"], cmp, k)
+        t.use_packed_filter(False)
+        assert np.array_equal(t.scan(fs), ref), (s["name"], cmp, k)
+    if values.dtype == np.int64:
+        # SELECT sum(v * 1) WHERE v < mid, v read from the segments at the qualifying rows
+        t.add_column(1, np.ones(n, dtype=np.int64))
+        keep = valid & (values < mid)
+        fs = F.TableFilterSet({0: F.ConstantFilter("<", mid)})
+        total, cnt = t.sum_product(0, 1, fs, gather_b=True)
+        assert t.last_sum_packed()
+        assert total == int(values[keep].sum()) and cnt == int(keep.sum())
+    t.close()
