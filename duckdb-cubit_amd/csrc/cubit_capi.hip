@@ -198,7 +198,8 @@ enum class RunMode { kDecode, kCount };
 // other tiles hold no qualifying row. Not with result_words (the skipped words stay unwritten).
 int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t row_base, int64_t* rowids,
              uint64_t capacity, uint64_t* d_count, uint64_t* result_words, RunMode mode, bool timed = false,
-             bool ordered = false, bool check_capacity = false, const std::vector<uint32_t>* live_zones = nullptr) {
+             bool ordered = false, bool check_capacity = false, const std::vector<uint32_t>* live_zones = nullptr,
+             const uint64_t* tile_prefix = nullptr) {
     // the directory describes only the decode launched here: a count, a failed launch or a
     // folded-away filter leaves no tiles behind for cubit_ctx_last_tiles to hand out
     ctx->last_tiles = 0;
@@ -233,15 +234,21 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     // directory is sized for every padded tile, as a live-tile list may name any of them
     const uint64_t tiles = (a.n_words + decode_tile_words() - 1) / decode_tile_words();
     if (int rc = ensure_dir(ctx, pw / decode_tile_words())) return rc;
-    // an ordered scan takes the look-back decode (runs in tile order) unless a kernel is forced
-    const int kernel = ordered && rowids && ctx->decode_kernel == 0 && tiles <= kLookbackMaxTiles ? 3 : ctx->decode_kernel;
-    const bool order_pass = ordered && rowids && !(kernel == 3 && tiles <= kLookbackMaxTiles);
+    // per-tile offsets known up front (tile_prefix): the look-back kernel without its walk, at any
+    // size, unless another kernel is forced; an ordered scan takes the look-back decode (runs in
+    // tile order) unless a kernel is forced
+    const bool prefixed = tile_prefix && rowids && (ctx->decode_kernel == 0 || ctx->decode_kernel == 3);
+    const int kernel = prefixed || (ordered && rowids && ctx->decode_kernel == 0 && tiles <= kLookbackMaxTiles)
+                           ? 3
+                           : ctx->decode_kernel;
+    const bool order_pass = ordered && rowids && !(kernel == 3 && (prefixed || tiles <= kLookbackMaxTiles));
     if (order_pass)
         if (int rc = ensure_tmp(ctx, capacity)) return rc;
     a.num_tiles = (uint32_t)tiles;
     a.flags = ctx->flags;
     a.epoch = ++ctx->epoch;
     a.spin_limit = ctx->lookback_spins;
+    a.tile_prefix = prefixed ? tile_prefix : nullptr;
     a.rowids = order_pass ? ctx->tmp_ids : rowids;
     a.capacity = rowids ? capacity : 0;
     if (live_zones) {
@@ -289,7 +296,8 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         ctx->rep_launches = ctx->repeat;
         ctx->repeat = 0;
     }
-    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, ctx->n_cus);
+    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, ctx->n_cus,
+                                         prefixed);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (order_pass)
@@ -549,6 +557,20 @@ int cubit_memcpy_d2h_stream(cubit_ctx* ctx, void* stream, void* dst, const void*
     const hipStream_t s = static_cast<hipStream_t>(stream);
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    return CUBIT_OK;
+}
+
+int cubit_memcpy_d2h_stream_async(cubit_ctx* ctx, void* stream, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+    return CUBIT_OK;
+}
+
+int cubit_copy_stream_sync(cubit_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return CUBIT_OK;
 }
 
@@ -1078,6 +1100,9 @@ struct cubit_table {
     size_t scratch_used = 0;
     std::unique_ptr<DevBuf> ones;  // all valid rows
     uint32_t last_leaves = 0, last_passes = 0;
+    // the last planned program, when it is one table-owned index bitvector as it stands (no
+    // complement, no patch): its per-zone counts give the decode its offsets up front
+    const uint64_t* single_leaf = nullptr;
     uint32_t last_decoded = 0;  // sum_product: values of b decoded from its index (0 = gathered)
     uint64_t* dummy_count = nullptr;
     std::unique_ptr<DevBuf> dummy;
@@ -1089,6 +1114,11 @@ struct cubit_table {
     struct ZoneMap {
         std::vector<uint64_t> z, o;
         bool informative = false;  // some zone is all-zero or all-one
+        std::vector<uint32_t> cnt;  // set rows per zone
+        // exclusive prefix of cnt on the device (nz + 1 entries), built the first time a scan of
+        // this bitvector alone decodes (EvalArgs::tile_prefix); dropped with the zone map
+        std::shared_ptr<DevBuf> prefix;
+        std::vector<uint64_t> prefix_host;
     };
     std::unordered_map<const uint64_t*, ZoneMap> zones;
     std::unique_ptr<DevBuf> zone_dev;  // class bytes of the bitvectors being summarised
@@ -2892,12 +2922,17 @@ int ensure_zones(cubit_table* t, const std::vector<const uint64_t*>& bvs, const 
     const uint32_t nz = real_zones(t);
     // min, max (int64) + flags per zone, each column's block 8-byte aligned
     const uint64_t per_col = ((uint64_t)nz * 17 + 7) / 8 * 8;
-    const uint64_t bytes = (uint64_t)todo.size() * nz + (uint64_t)todo_c.size() * per_col + 16;
+    // class bytes of the bitvectors, then their per-zone counts (4-byte aligned), then the
+    // columns' statistics (8-byte aligned)
+    const uint64_t cnt_base = ((uint64_t)todo.size() * nz + 3) / 4 * 4;
+    const uint64_t cbase = (cnt_base + (uint64_t)todo.size() * nz * 4 + 7) / 8 * 8;
+    const uint64_t bytes = cbase + (uint64_t)todo_c.size() * per_col + 16;
     uint8_t* dev = zone_scratch(t, bytes);
     if (!dev) return fail(CUBIT_ERR_OOM, "zone classes allocation failed");
     hipStream_t s = t->ctx->stream;
-    for (size_t i = 0; i < todo.size(); ++i) HIP_CHECK(launch_zone_classes(todo[i], t->n_rows, 0, nz, dev + i * nz, s));
-    const uint64_t cbase = ((uint64_t)todo.size() * nz + 7) / 8 * 8;
+    for (size_t i = 0; i < todo.size(); ++i)
+        HIP_CHECK(launch_zone_classes(todo[i], t->n_rows, 0, nz, dev + i * nz, s,
+                                      reinterpret_cast<uint32_t*>(dev + cnt_base) + i * nz));
     for (size_t i = 0; i < todo_c.size(); ++i) {
         const Column& c = t->cols.at(todo_c[i]);
         uint8_t* p = dev + cbase + i * per_col;
@@ -2918,6 +2953,8 @@ int ensure_zones(cubit_table* t, const std::vector<const uint64_t*>& bvs, const 
             if (c & 2) m.o[z >> 6] |= 1ull << (z & 63);
             m.informative |= c != 0;
         }
+        m.cnt.resize(nz);
+        std::memcpy(m.cnt.data(), host.data() + cnt_base + 4ull * i * nz, 4ull * nz);
         t->zones.emplace(todo[i], std::move(m));
     }
     for (size_t i = 0; i < todo_c.size(); ++i) {
@@ -3189,6 +3226,7 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     *empty = false;
     if (live) live->clear();
     cubit_ctx* ctx = t->ctx;
+    t->single_leaf = nullptr;
     t->scratch_used = 0;
     t->last_passes = 0;
     t->last_packed = 0;
@@ -3315,7 +3353,36 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     if (!em.ok) return fail(CUBIT_ERR_UNSUPPORTED, "program does not fit one pass");
     t->last_leaves = em.prog.n_leaves;
     t->last_passes++;
+    t->single_leaf = e->kind == Expr::LEAF && !e->neg && e->leaf.zsrc == kZoneBits && !e->leaf.zbv &&
+                             e->leaf.zdirty < 0 && em.prog.n_leaves == 1 && em.prog.negate == 0
+                         ? e->leaf.bv
+                         : nullptr;
     return CUBIT_OK;
+}
+
+// The device prefix of the per-zone counts of a table-owned bitvector whose zone map is built
+// (null when it is not): the offsets of a decode of that bitvector alone.
+const uint64_t* tile_prefix_of(cubit_table* t, const uint64_t* bv, int* rc) {
+    *rc = CUBIT_OK;
+    auto it = t->zones.find(bv);
+    if (it == t->zones.end() || it->second.cnt.empty()) return nullptr;
+    ZoneMap& m = it->second;
+    if (!m.prefix) {
+        m.prefix_host.assign(m.cnt.size() + 1, 0);
+        for (size_t z = 0; z < m.cnt.size(); ++z) m.prefix_host[z + 1] = m.prefix_host[z] + m.cnt[z];
+        auto b = std::make_shared<DevBuf>();
+        if (hipMalloc(&b->p, m.prefix_host.size() * sizeof(uint64_t)) != hipSuccess) {
+            *rc = fail(CUBIT_ERR_OOM, "tile prefix allocation failed");
+            return nullptr;
+        }
+        if (hipMemcpyAsync(b->p, m.prefix_host.data(), m.prefix_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice,
+                           t->ctx->stream) != hipSuccess) {
+            *rc = fail(CUBIT_ERR_HIP, "tile prefix upload failed");
+            return nullptr;
+        }
+        m.prefix = std::move(b);
+    }
+    return static_cast<const uint64_t*>(m.prefix->p);
 }
 
 // The values `col` can take among the rows the filter keeps, when its constant filters in the
@@ -3399,10 +3466,16 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
         return CUBIT_OK;
     }
     t->last_live = live.empty() ? t->last_zones : (uint32_t)live.size();
+    const uint64_t* prefix = nullptr;
+    if (!count_only && t->single_leaf) {
+        int rc = CUBIT_OK;
+        prefix = tile_prefix_of(t, t->single_leaf, &rc);
+        if (rc) return rc;
+    }
     return run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
                     nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
                     (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0,
-                    live.empty() ? nullptr : &live);
+                    live.empty() ? nullptr : &live, prefix);
 }
 
 extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,

@@ -77,6 +77,10 @@ struct EvalArgs {
     // polls of one flag before the polling thread counts that tile itself (0 = the kernel's
     // default; cubit_ctx_set_lookback_spins forces the recount path in tests)
     uint32_t spin_limit;
+    // eval_decode_lookback: exclusive prefix of every tile's qualifying rows, known before the
+    // launch (a program of one index bitvector: its per-zone counts, a zone being one decode
+    // tile), or null. With it no workgroup publishes or waits, at any tile count.
+    const uint64_t* tile_prefix;
 };
 // eval_decode_lookback: one workgroup per tile, at most this many tiles per launch (6.0e8 rows).
 // Every workgroup reads the counts of all earlier tiles, so the flag reads grow with the square
@@ -105,14 +109,15 @@ int decode_block_threads();
 // lookback_max_tiles — and ordered scans up to kLookbackMaxTiles); decode_kernel_for resolves
 // it for a launch
 int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live = false,
-                      int n_cus = 256);
+                      int n_cus = 256, bool prefixed = false);
 // the largest tile count the measured policy decodes with the look-back kernel (grid = tiles)
 uint32_t lookback_max_tiles(uint32_t n_leaves, int n_cus);
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t stream,
                               hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int kernel = 0, int n_cus = 256);
-// zone classes of a bitvector (class byte per zone, see kZoneWords) for zones [z0, z0 + nz)
+// zone classes of a bitvector (class byte per zone, see kZoneWords) for zones [z0, z0 + nz),
+// and (cnt non-null) each zone's set rows
 hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0, uint32_t nz, uint8_t* out,
-                               hipStream_t stream);
+                               hipStream_t stream, uint32_t* cnt = nullptr);
 // per-zone min / max of a raw column's valid rows; fl bit 0 = some row valid, bit 1 = every row
 hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* validity, uint64_t n_rows, uint32_t nz,
                                     int64_t* mn, int64_t* mx, uint8_t* fl, hipStream_t stream);

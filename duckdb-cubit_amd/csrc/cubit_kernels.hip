@@ -1214,7 +1214,10 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
         tile_count += block_tot[p];
     }
-    if (t == 0)
+    // with per-tile counts known up front (a single index leaf: EvalArgs::tile_prefix) the
+    // offset is one load and no workgroup publishes or waits
+    const bool prefixed = a.tile_prefix != nullptr;
+    if (t == 0 && !prefixed)
         __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBits) | (uint64_t)tile_count, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     const bool staged = tile_count <= (uint32_t)STAGE;
@@ -1235,7 +1238,7 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     }
     // look-back over every earlier workgroup's flag
     uint64_t pre = 0;
-    for (uint32_t j = t; j < b && !(DBG & 8); j += THREADS) {
+    for (uint32_t j = t; !prefixed && j < b && !(DBG & 8); j += THREADS) {
         uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t spins = 0;
         while (!(DBG & 1) && (f >> kFlagCntBits) != a.epoch) {
@@ -1255,7 +1258,9 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     uint64_t base = 0;
 #pragma unroll
     for (int w = 0; w < NWAVES; ++w) base += s_pre[w];
-    if (s_expired) {
+    if (prefixed) {
+        base = a.tile_prefix[tile];
+    } else if (s_expired) {
         // some earlier tile was not published within the limit: every flag once more, the
         // missing tiles counted here (s_pre and s_wave_tot are free again; s_stage is not)
         base = lookback_recount<K, FORM, THREADS, PAIRS>(a, b, t, s_list_scratch, &s_list_n, s_pre);
@@ -2291,7 +2296,7 @@ __global__ __launch_bounds__(256) void bitpacked_compare_kernel(const uint8_t* _
 // One group's 64-row output words from its values (a FOR group's packed words staged in L,
 // CONSTANT / CONSTANT_DELTA from its record): 64 values per step, each lane taking its value's
 // bits from the staged words with one funnel shift, one ballot per step = one output word
-// (shared by bitpacked_compare_waves and bitpacked_compare_stream).
+// (bitpacked_compare_waves).
 template <typename T, typename U>
 __device__ __forceinline__ void compare_group_words(const BpGroup& cur, const uint32_t* L, bool packed, uint32_t w,
                                                     uint32_t mask, int lane, const uint64_t* __restrict__ validity,
@@ -2304,7 +2309,6 @@ __device__ __forceinline__ void compare_group_words(const BpGroup& cur, const ui
     // more than the whole read); other groups store or OR each word as it is made
     const bool aligned = (cur.row_start & 63) == 0;
     uint64_t myword = 0;
-#pragma unroll 2
     for (uint32_t c = 0; c < nchunks; ++c) {
         const uint32_t i = c * 64u + (uint32_t)lane;
         bool p = false;
@@ -2395,70 +2399,6 @@ __global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __
     compare_group_words<T, U>(cur, L, packed, w, mask, lane, validity, lo, hi, neg, out);
 }
 
-// bitpacked_compare_waves as a persistent grid: wave v of G takes groups v, v + G, v + 2G, …
-// and issues the packed-word loads of its next group before it tests the current one from LDS,
-// so each wave always has one group's loads in flight behind its compare steps — the LDS ring
-// of DESIGN.md §3, one stage deep per wave, in registers — and the launch is a few thousand
-// workgroups instead of one per four groups.
-template <typename T, typename U, int MAXW>
-__global__ __launch_bounds__(256) void bitpacked_compare_stream(const uint8_t* __restrict__ bytes,
-                                                                const BpGroup* __restrict__ groups, uint32_t n_groups,
-                                                                const uint64_t* __restrict__ validity, T lo, T hi,
-                                                                int neg, uint64_t* __restrict__ out) {
-    static_assert(MAXW >= 1 && MAXW <= 32, "FOR groups of at most 32 bits");
-    constexpr uint32_t SLICE = 64u * MAXW + 4u;
-    __shared__ uint32_t s_w[4][SLICE];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t stride = gridDim.x * 4u;
-    uint32_t g = blockIdx.x * 4u + wave;
-    if (g >= n_groups) return;  // no workgroup barrier below: each wave works alone
-    uint32_t* L = s_w[wave];
-    auto load_words = [&](const BpGroup& gr, uint32_t (&x)[MAXW]) {
-        const bool pk = gr.mode == 5 && gr.width;
-        const uint32_t nw = pk ? (gr.count + 31u) / 32u * gr.width : 0u;  // ≤ 64·MAXW (host-checked)
-        const uint32_t* W = reinterpret_cast<const uint32_t*>(bytes + gr.words_off);
-#pragma unroll
-        for (int m = 0; m < MAXW; ++m) {
-            const uint32_t kk = 64u * (uint32_t)m + (uint32_t)lane;
-            x[m] = kk < nw ? __builtin_nontemporal_load(W + kk) : 0u;
-        }
-    };
-    BpGroup cur = groups[g];
-    uint32_t x[MAXW];
-    load_words(cur, x);
-    for (;;) {
-        const uint32_t gn = g + stride;
-        const bool more = gn < n_groups;
-        const bool packed = cur.mode == 5 && cur.width;
-        // the current group's words into this wave's LDS slice (waits for their loads)
-        if (packed) {
-#pragma unroll
-            for (int m = 0; m < MAXW; ++m) L[64u * (uint32_t)m + (uint32_t)lane] = x[m];
-            if (lane < 4) L[64u * MAXW + (uint32_t)lane] = 0u;
-        }
-        // the next group's loads, in flight while this one is tested
-        BpGroup nxt = cur;
-        if (more) {
-            nxt = groups[gn];
-            load_words(nxt, x);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        const uint32_t w = packed ? cur.width : 0u;
-        const uint32_t mask = w >= 32 ? ~0u : (1u << w) - 1u;
-        compare_group_words<T, U>(cur, L, packed, w, mask, lane, validity, lo, hi, neg, out);
-        if (!more) break;
-        // every lane has read the slice before the next group's words overwrite it
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        cur = nxt;
-        g = gn;
-    }
-}
-
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -2536,13 +2476,19 @@ __global__ __launch_bounds__(64) void sum_partials_kernel(const int64_t* __restr
 // words, each thread ANDs and ORs 8 words (4 coalesced 16-byte loads). Only rows < n_rows count:
 // words past the last row are skipped, the last word is masked. out[z - z0] bit 0 = no row set,
 // bit 1 = every row set (both for a zone past the last row).
+// Zone class of one bitvector per zone (bit 0: no row set, bit 1: every row set) and, with
+// cnt, the zone's set rows — the per-tile counts a single-leaf decode takes its output offsets
+// from (eval_decode_lookback with EvalArgs::tile_prefix).
 __global__ __launch_bounds__(256) void zone_class_kernel(const uint64_t* __restrict__ bv, uint64_t n_rows,
-                                                         uint32_t z0, uint8_t* __restrict__ out) {
+                                                         uint32_t z0, uint8_t* __restrict__ out,
+                                                         uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t s_cnt[4];
     const uint32_t z = z0 + blockIdx.x;
     const int t = threadIdx.x;
     const uint64_t n_words = (n_rows + 63) / 64;
     const uint64_t last_mask = (n_rows & 63) ? (1ull << (n_rows & 63)) - 1 : ~0ull;
     uint64_t all = ~0ull, any = 0;
+    uint32_t ones = 0;
     const uint64_t w0 = (uint64_t)z * kZoneWords;
 #pragma unroll
     for (int p = 0; p < (int)(kZoneWords / 512); ++p) {
@@ -2554,15 +2500,22 @@ __global__ __launch_bounds__(256) void zone_class_kernel(const uint64_t* __restr
         if (gw + 1 >= n_words) {  // b is past the last row (or a is the last word)
             all &= a | ~ma;
             any |= a & ma;
+            ones += (uint32_t)__popcll(a & ma);
             continue;
         }
         const uint64_t mb = gw + 1 == n_words - 1 ? last_mask : ~0ull;
         all &= (a | ~ma) & (b | ~mb);
         any |= (a & ma) | (b & mb);
+        ones += (uint32_t)(__popcll(a & ma) + __popcll(b & mb));
     }
+    const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(ones), 63);
+    if ((t & 63) == 0) s_cnt[t >> 6] = wsum;
     const int none_set = __syncthreads_and(any == 0);
     const int all_set = __syncthreads_and(all == ~0ull);
-    if (t == 0) out[blockIdx.x] = (uint8_t)((none_set ? 1 : 0) | (all_set ? 2 : 0));
+    if (t == 0) {
+        out[blockIdx.x] = (uint8_t)((none_set ? 1 : 0) | (all_set ? 2 : 0));
+        if (cnt) cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    }
 }
 
 // Per-zone statistics of a raw column (the segment statistics CheckZonemap consults,
@@ -2841,7 +2794,10 @@ uint32_t lookback_max_tiles(uint32_t n_leaves, int n_cus) {
     return std::min<uint32_t>(kLookbackMaxTiles, (uint32_t)lookback_wpc(n_leaves) * (uint32_t)n_cus);
 }
 
-int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live, int n_cus) {
+int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int kernel, bool live, int n_cus,
+                      bool prefixed) {
+    // known per-tile offsets: one tile per workgroup with no inter-workgroup wait, at any size
+    if (prefixed && (kernel == 0 || kernel == 3)) return 3;
     if (kernel == 3 && num_tiles <= kLookbackMaxTiles) return 3;
     if (kernel == 0 && num_tiles <= lookback_max_tiles(n_leaves, n_cus)) return 3;
     // a live-tile list (zonemap skip) needs the run kernel: its stage offsets are taken from the
@@ -2854,7 +2810,7 @@ int decode_kernel_for(uint32_t n_leaves, uint32_t num_tiles, unsigned grid, int 
 template <int K, int FORM>
 void launch_decode_kf(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                       int kernel, int n_cus) {
-    const int which = decode_kernel_for(K, a.num_tiles, grid, kernel, a.live != nullptr, n_cus);
+    const int which = decode_kernel_for(K, a.num_tiles, grid, kernel, a.live != nullptr, n_cus, a.tile_prefix != nullptr);
     if (which == 3)
         hipExtLaunchKernelGGL((eval_decode_lookback<K, FORM, kLookbackStage, lookback_wpc(K)>), dim3(a.num_tiles),
                               dim3(512), 0, s, e0, e1, 0, a, dir);
@@ -2900,8 +2856,9 @@ hipError_t launch_count_k(const EvalArgs& a, hipStream_t s, hipEvent_t e0, hipEv
 
 hipError_t launch_eval_decode(const EvalArgs& a, uint64_t* dir, unsigned grid, hipStream_t s, hipEvent_t e0,
                               hipEvent_t e1, int kernel, int n_cus) {
-    if (decode_kernel_for(a.prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, n_cus) == 3 &&
-        (a.flags == nullptr || a.epoch == 0 || a.num_tiles == 0))
+    if (decode_kernel_for(a.prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, n_cus,
+                          a.tile_prefix != nullptr) == 3 &&
+        (a.num_tiles == 0 || (!a.tile_prefix && (a.flags == nullptr || a.epoch == 0))))
         return hipErrorInvalidValue;  // the look-back kernel needs the context's flags and an epoch
     switch (a.prog.n_leaves) {
     case 1: return launch_decode_k<1>(a, dir, grid, s, e0, e1, kernel, n_cus);
@@ -3138,17 +3095,6 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
     return hipGetLastError();
 }
 
-// Which wave kernel the packed filter takes: 1 = bitpacked_compare_stream (persistent, default),
-// 0 = bitpacked_compare_waves (one wave per group); CUBIT_PACKED_FILTER_KERNEL overrides (A/B).
-int packed_filter_kernel() {
-    static const int k = [] {
-        const char* e = std::getenv("CUBIT_PACKED_FILTER_KERNEL");
-        return e && *e ? std::atoi(e) : 1;
-    }();
-    return k;
-}
-constexpr uint32_t kPackedStreamBlocks = 2048;  // 8 workgroups of 4 waves per CU
-
 hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
                                     uint64_t* out, hipStream_t stream, int simple_width) {
@@ -3158,28 +3104,6 @@ hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups,
     const int64_t lo = rg.lo, hi = rg.hi;
     const int neg = rg.neg;
     const uint32_t ng = (uint32_t)n_groups;
-    if (simple_width > 0 && packed_filter_kernel() == 1) {
-        // persistent waves, next group's loads in flight (bitpacked_compare_stream)
-        const dim3 grid(std::min<uint32_t>((ng + 3) / 4, kPackedStreamBlocks));
-        if (type == 0) {
-            int32_t lo32, hi32;
-            rg.clamp32(lo32, hi32);
-            if (simple_width <= 16)
-                hipLaunchKernelGGL((bitpacked_compare_stream<int32_t, uint32_t, 16>), grid, dim3(256), 0, stream, bytes,
-                                   groups, ng, validity, lo32, hi32, neg, out);
-            else
-                hipLaunchKernelGGL((bitpacked_compare_stream<int32_t, uint32_t, 32>), grid, dim3(256), 0, stream, bytes,
-                                   groups, ng, validity, lo32, hi32, neg, out);
-        } else {
-            if (simple_width <= 16)
-                hipLaunchKernelGGL((bitpacked_compare_stream<int64_t, uint64_t, 16>), grid, dim3(256), 0, stream, bytes,
-                                   groups, ng, validity, lo, hi, neg, out);
-            else
-                hipLaunchKernelGGL((bitpacked_compare_stream<int64_t, uint64_t, 32>), grid, dim3(256), 0, stream, bytes,
-                                   groups, ng, validity, lo, hi, neg, out);
-        }
-        return hipGetLastError();
-    }
     if (simple_width > 0) {  // every group FOR ≤ 32 bits / CONSTANT / CONSTANT_DELTA: one wave per group
         const dim3 grid((ng + 3) / 4);
         if (type == 0) {
@@ -3222,9 +3146,9 @@ hipError_t launch_fill_valid(uint64_t* words, uint64_t n_rows, hipStream_t strea
 }
 
 hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0, uint32_t nz, uint8_t* out,
-                               hipStream_t stream) {
+                               hipStream_t stream, uint32_t* cnt) {
     if (nz == 0) return hipSuccess;
-    hipLaunchKernelGGL(zone_class_kernel, dim3(nz), dim3(256), 0, stream, bv, n_rows, z0, out);
+    hipLaunchKernelGGL(zone_class_kernel, dim3(nz), dim3(256), 0, stream, bv, n_rows, z0, out, cnt);
     return hipGetLastError();
 }
 

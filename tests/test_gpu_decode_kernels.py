@@ -259,3 +259,42 @@ def test_lookback_expiry_with_zonemap_skip(ctx):
     finally:
         ctx.set_lookback_spins(0)
         t.close()
+
+
+def test_single_index_leaf_decodes_from_tile_counts(ctx):
+    """A filter answered by one index bitvector as it stands (v < c on an edge of a range index)
+    decodes with its per-tile offsets known up front — the bitvector's per-zone counts, kept
+    with its zone map — so the look-back kernel runs without its walk at any size (here 1,526
+    tiles, twice the co-resident grid, where the walk would not be used). Rows equal numpy in
+    tile-run and ordered output, with zones skipped, and stay equal after an append changes the
+    bitvector (its counts are dropped with the zone map)."""
+    rng = np.random.default_rng(17)
+    n = 200_000_003
+    a = rng.integers(0, 1_000_000, n).astype(np.int32)
+    a[50_000_000:90_000_000] = 999_999  # zones where the leaf is empty: a live-tile list
+    t = CubitTable(ctx, n, row_base=9)
+    t.add_column(0, a)
+    t.build_index(0, L.INDEX_RANGE, [10_000, 500_000])
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 10_000)})
+    ctx.set_decode_kernel(L.DECODE_AUTO)
+
+    def check(vals):
+        ref = np.flatnonzero(vals < 10_000).astype(np.int64) + 9
+        for ordered in (False, True):
+            got = t.scan(fs, ordered=ordered)
+            assert ctx.last_decode_kernel() == L.DECODE_LOOKBACK, ordered
+            if not ordered:
+                d, _ = ctx.last_tiles()
+                got = runs_in_row_order(got, d)
+            assert np.array_equal(got, ref), ordered
+        assert t.last_zones()[0] < t.last_zones()[1]  # the zonemap skipped zones
+        # a complemented leaf (v >= c: NOT L(c) within the valid rows) is not one bitvector as
+        # it stands: the decode takes the usual kernels and still equals numpy
+        ge = F.TableFilterSet({0: F.ConstantFilter(">=", 10_000)})
+        assert t.count(ge) == int((vals >= 10_000).sum())
+
+    check(a)
+    extra = rng.integers(0, 20_000, 3_000_000).astype(np.int32)
+    t.append({0: extra})
+    check(np.concatenate([a, extra]))  # dense tiles at the end: the stage rounds
+    t.close()
