@@ -560,20 +560,6 @@ int cubit_memcpy_d2h_stream(cubit_ctx* ctx, void* stream, void* dst, const void*
     return CUBIT_OK;
 }
 
-int cubit_memcpy_d2h_stream_async(cubit_ctx* ctx, void* stream, void* dst, const void* src, uint64_t bytes) {
-    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
-    if (int rc = set_device(ctx)) return rc;
-    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
-    return CUBIT_OK;
-}
-
-int cubit_copy_stream_sync(cubit_ctx* ctx, void* stream) {
-    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
-    if (int rc = set_device(ctx)) return rc;
-    HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    return CUBIT_OK;
-}
-
 int cubit_memset_d(cubit_ctx* ctx, void* dst, int value, uint64_t bytes) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
     HIP_CHECK(hipMemsetAsync(dst, value, bytes, ctx->stream));

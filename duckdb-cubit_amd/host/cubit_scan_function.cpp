@@ -192,10 +192,6 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     uint32_t tile_slot = 0;        // current tile (index into tiles)
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
-    // the next window this state claimed, its copy in flight into next_host while the current
-    // one is handed out (-1 = none)
-    int64_t next_window = -1;
-    std::vector<PooledBuffer> next_host;
     // this task's copy stream (ordered after init_global's device work): the tasks' window
     // copies run side by side instead of queueing on the context stream
     cubit_ctx* ctx = nullptr;
@@ -290,48 +286,30 @@ std::unique_ptr<LocalTableFunctionState> CubitScanInitLocal(TableFunctionInitInp
 }
 
 // TableScanParallelStateNext analogue: take the next window (row_group_collection.cpp hands
-// out row groups under a mutex; one atomic suffices here). Its rows of every emitted column
-// reach this state's page-locked buffers on the state's copy stream; the window after it is
-// claimed at once and copied while this one is handed out (claims stay in order, so the state's
-// batch indexes still ascend). Measured before the pinned pool found its buffers again, that
-// prefetch lost at 8 and 16 tasks (profiles/r03mn_*): it pinned fresh memory per window.
+// out row groups under a mutex; one atomic suffices here) and copy its rows of every emitted
+// column to this state's page-locked buffers. A state copies one window at a time: claiming
+// the next window and copying it while the current one is handed out measured slower at 8 and
+// 16 tasks, before and after the pinned pool reused its buffers (12.4 vs 5.09 ms at 8 tasks,
+// profiles/r04c_pipeline_prefetch_not_kept.txt; round 3: profiles/r03mn_*).
 bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
+    const uint32_t w = g.next.fetch_add(1);
+    if (w >= g.windows.size()) {
+        l.window = (int64_t)g.windows.size();
+        return false;
+    }
+    const Window& win = g.windows[w];
     if (!l.copy_stream) {
         check(cubit_copy_stream_create(g.ctx, &l.copy_stream), "copy stream");
         l.ctx = g.ctx;
     }
-    auto start_copy = [&](uint32_t w, std::vector<PooledBuffer>& bufs) {
-        const Window& win = g.windows[w];
-        if (bufs.size() != g.emit.size()) bufs.resize(g.emit.size());
-        for (size_t e = 0; e < g.emit.size(); ++e) {
-            if (!bufs[e].p) bufs[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
-            const column_t col = g.column_ids[g.emit[e]];
-            PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
-            check(cubit_memcpy_d2h_stream_async(g.ctx, l.copy_stream, bufs[e].p, device_ptr(src) + win.off,
-                                                win.len * 8),
-                  "window copy");
-        }
-    };
-    uint32_t w;
-    if (l.next_window >= 0) {
-        w = (uint32_t)l.next_window;
-        l.next_window = -1;
-        std::swap(l.host, l.next_host);
-    } else {
-        w = g.next.fetch_add(1);
-        if (w >= g.windows.size()) {
-            l.window = (int64_t)g.windows.size();
-            return false;
-        }
-        start_copy(w, l.host);
+    if (l.host.size() != g.emit.size()) l.host.resize(g.emit.size());
+    for (size_t e = 0; e < g.emit.size(); ++e) {
+        if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
+        const column_t col = g.column_ids[g.emit[e]];
+        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
+        check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
+              "window copy");
     }
-    check(cubit_copy_stream_sync(g.ctx, l.copy_stream), "window copy");
-    const uint32_t w2 = g.next.fetch_add(1);
-    if (w2 < g.windows.size()) {
-        start_copy(w2, l.next_host);
-        l.next_window = w2;
-    }
-    const Window& win = g.windows[w];
     l.window = w;
     l.tile_slot = win.first;
     l.pos = 0;

@@ -183,10 +183,6 @@ int cubit_sync(cubit_ctx *ctx);
 int cubit_copy_stream_create(cubit_ctx *ctx, void **stream);
 int cubit_copy_stream_destroy(cubit_ctx *ctx, void *stream);
 int cubit_memcpy_d2h_stream(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
-/* The same copy, enqueued only (dst must stay valid until cubit_copy_stream_sync returns): a
- * pipeline task copies its next window while it hands out the current one. */
-int cubit_memcpy_d2h_stream_async(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
-int cubit_copy_stream_sync(cubit_ctx *ctx, void *stream);
 /* Synchronise the context stream and report any pending HIP error. */
 int cubit_ctx_check(cubit_ctx *ctx);
 /* Tile directory of the last row-id materialisation on this context (device pointer, valid

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold gpurun_out/prof/<workload>/ (scripts/profile.sh) into profiles/: copy the kernel
+"""Fold a profile tree (scripts/gpu.sh profile:<workload> steps) into profiles/: copy the kernel
 stats and the eval_decode_tiles PMC rows as profiles/<round>_<workload>_*.csv and write
 profiles/pmc_summary.json (per-launch HBM bytes of the dominant kernel, with the gfx950
 FETCH_SIZE x2 correction of MI355X_MICROARCH.md §HBM), which bench.py reports as
@@ -13,6 +13,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 ROUND = sys.argv[1] if len(sys.argv) > 1 else "r01"
+# the profile tree of one run: gpurun_out/prof (old per-round scripts) or gpurun_out/<out>/prof
+# (scripts/gpu.sh profile:<workload> steps)
+PROF = Path(sys.argv[2]) if len(sys.argv) > 2 else ROOT / "gpurun_out" / "prof"
 KERNELS = ("eval_decode_pairs", "eval_decode_runs", "eval_decode_lookback")  # the bench line names the one it launched
 
 
@@ -75,7 +78,7 @@ def probe_summary(wdir, line, summary):
 def smallbench_summary(summary):
     """eval_decode_lookback at SF100/8 (75,004,738 rows, 573 tiles) and 1e8 rows (763 tiles)
     from scripts/smallbench under rocprofv3: per-launch FETCH / WRITE and kernel-trace time."""
-    wdir = ROOT / "gpurun_out" / "prof" / "smallbench"
+    wdir = PROF / "smallbench"
     if not wdir.exists():
         return
     fetch = rows(f"{wdir}/fetch/**/*counter_collection.csv")
@@ -107,7 +110,7 @@ def smallbench_summary(summary):
 def main():
     summary_p = ROOT / "profiles" / "pmc_summary.json"
     summary = json.loads(summary_p.read_text()) if summary_p.exists() else {}
-    for wdir in sorted(glob.glob(str(ROOT / "gpurun_out" / "prof" / "*"))):
+    for wdir in sorted(glob.glob(str(PROF / "*"))):
         w = Path(wdir).name
         log = Path(wdir) / "bench_kt.log"
         try:
