@@ -296,8 +296,10 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
         ctx->rep_launches = ctx->repeat;
         ctx->repeat = 0;
     }
-    ctx->last_decode = decode_kernel_for(prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, ctx->n_cus,
-                                         prefixed);
+    ctx->last_decode = prefixed && prog.n_leaves == 1
+                           ? CUBIT_DECODE_PREFIXED
+                           : decode_kernel_for(prog.n_leaves, a.num_tiles, grid, kernel, a.live != nullptr, ctx->n_cus,
+                                               prefixed);
     ctx->last_tiles = (uint32_t)tiles;
     ctx->last_tile_rows = decode_tile_words() * 64;
     if (order_pass)

@@ -1180,6 +1180,11 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     const uint64_t tile_word0 = (uint64_t)tile * TILE_WORDS;
     const bool write_ids = a.rowids != nullptr;
     const uint32_t spin_limit = a.spin_limit ? a.spin_limit : kLookbackSpins;
+    // with per-tile counts known up front (a single index leaf: EvalArgs::tile_prefix) the
+    // offset is one load, issued here so that it lands while the tile is read and decoded, and
+    // no workgroup publishes or waits
+    const bool prefixed = a.tile_prefix != nullptr;
+    const uint64_t known_base = prefixed ? a.tile_prefix[tile] : 0;
     if (t == 0) s_expired = 0;
     u64x2 v[K][PAIRS];
     load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
@@ -1214,9 +1219,6 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
         pair_off[p] = tile_count + wave_pre[p] + ((excl >> (16 * p)) & 0xffffu);
         tile_count += block_tot[p];
     }
-    // with per-tile counts known up front (a single index leaf: EvalArgs::tile_prefix) the
-    // offset is one load and no workgroup publishes or waits
-    const bool prefixed = a.tile_prefix != nullptr;
     if (t == 0 && !prefixed)
         __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBits) | (uint64_t)tile_count, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -1259,7 +1261,7 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
 #pragma unroll
     for (int w = 0; w < NWAVES; ++w) base += s_pre[w];
     if (prefixed) {
-        base = a.tile_prefix[tile];
+        base = known_base;
     } else if (s_expired) {
         // some earlier tile was not published within the limit: every flag once more, the
         // missing tiles counted here (s_pre and s_wave_tot are free again; s_stage is not)

@@ -33,6 +33,7 @@ SCAN_ORDERED = 2
 SCAN_CHECK_CAPACITY = 4  # synchronise; ERR_CAPACITY when the count exceeds the buffer
 SCAN_NO_ZONEMAP = 8  # evaluate every zone (the zonemap skip off; results are identical)
 DECODE_AUTO, DECODE_PAIRS, DECODE_RUNS, DECODE_LOOKBACK = 0, 1, 2, 3
+DECODE_PREFIXED = 4  # reported only (cubit_ctx_last_decode_kernel): one index bitvector, offsets from its zone counts
 
 
 class FilterNode(C.Structure):

@@ -134,13 +134,17 @@ const char *cubit_last_error(void);
 #define CUBIT_DECODE_PAIRS 1
 #define CUBIT_DECODE_RUNS 2
 #define CUBIT_DECODE_LOOKBACK 3
+/* reported by cubit_ctx_last_decode_kernel only: a program of one index bitvector as it stands
+ * decodes with its offsets known up front (the bitvector's per-zone counts, kept with its zone
+ * map): the look-back kernel without its walk, at any tile count; taken under AUTO and LOOKBACK */
+#define CUBIT_DECODE_PREFIXED 4
 int cubit_ctx_set_decode_kernel(cubit_ctx *ctx, int kernel);
 /* Look-back decode: polls of an earlier tile's flag before the polling thread counts that tile
  * from its bitvectors itself (0 = the library default, 2^22). The expiry path is part of every
  * launch — no workgroup waits without bound and the count is always exact — and a small limit
  * forces it (tests). */
 int cubit_ctx_set_lookback_spins(cubit_ctx *ctx, uint32_t spins);
-/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS, or _LOOKBACK; 0 when
+/* The kernel the context's last decode launched (CUBIT_DECODE_PAIRS, _RUNS, _LOOKBACK or _PREFIXED; 0 when
  * the partition had no row and nothing was launched). */
 int cubit_ctx_last_decode_kernel(cubit_ctx *ctx, int *kernel);
 /* Filter-kernel durations measured with HIP events recorded around each launch on the

@@ -264,8 +264,8 @@ def test_lookback_expiry_with_zonemap_skip(ctx):
 def test_single_index_leaf_decodes_from_tile_counts(ctx):
     """A filter answered by one index bitvector as it stands (v < c on an edge of a range index)
     decodes with its per-tile offsets known up front — the bitvector's per-zone counts, kept
-    with its zone map — so the look-back kernel runs without its walk at any size (here 1,526
-    tiles, twice the co-resident grid, where the walk would not be used). Rows equal numpy in
+    with its zone map — by the look-back kernel without its walk, at any size (here 1,526 tiles,
+    twice the co-resident grid the walk needs). Rows equal numpy in
     tile-run and ordered output, with zones skipped, and stay equal after an append changes the
     bitvector (its counts are dropped with the zone map)."""
     rng = np.random.default_rng(17)
@@ -282,7 +282,7 @@ def test_single_index_leaf_decodes_from_tile_counts(ctx):
         ref = np.flatnonzero(vals < 10_000).astype(np.int64) + 9
         for ordered in (False, True):
             got = t.scan(fs, ordered=ordered)
-            assert ctx.last_decode_kernel() == L.DECODE_LOOKBACK, ordered
+            assert ctx.last_decode_kernel() == L.DECODE_PREFIXED, ordered
             if not ordered:
                 d, _ = ctx.last_tiles()
                 got = runs_in_row_order(got, d)
