@@ -946,6 +946,14 @@ extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const i
     return CUBIT_OK;
 }
 
+extern "C" int cubit_narrow_i32(cubit_ctx* ctx, const int64_t* d_in, const uint64_t* d_count, uint64_t max_n,
+                                int64_t offset, int32_t* d_out) {
+    if (!ctx || !d_in || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    HIP_CHECK(launch_narrow_i32(d_in, d_count, max_n, offset, d_out, ctx->stream));
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_gather_sum_product(cubit_ctx* ctx, const int64_t* d_a, const int64_t* d_b,
                                         const int64_t* d_rowids, const uint64_t* d_count, uint64_t max_n,
                                         int64_t row_base, int64_t* d_out) {

@@ -2401,6 +2401,28 @@ __global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __
     compare_group_words<T, U>(cur, L, packed, w, mask, lane, validity, lo, hi, neg, out);
 }
 
+// ------------------------------------------------------------------ transfer compaction
+
+// out[i] = (int32)(in[i] - offset) for i < min(*d_count, max_n): the DataChunk column of a
+// window crosses PCIe at 4 bytes per row when every value of the column lies within 2^31 of the
+// offset (the host mirror widens while it fills the chunk). 16-byte loads, 8-byte stores.
+__global__ __launch_bounds__(256) void narrow_i32_kernel(const int64_t* __restrict__ in, const uint64_t* __restrict__ d_count,
+                                                          uint64_t max_n, int64_t offset, int32_t* __restrict__ out) {
+    const uint64_t n = min(*d_count, max_n);
+    for (uint64_t i = 2 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 2ull * gridDim.x * blockDim.x) {
+        if (i + 1 < n) {
+            const u64x2 v = *reinterpret_cast<const u64x2*>(in + i);
+            typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
+            i32x2 o;
+            o.x = (int32_t)((int64_t)v.x - offset);
+            o.y = (int32_t)((int64_t)v.y - offset);
+            *reinterpret_cast<i32x2*>(out + i) = o;
+        } else {
+            out[i] = (int32_t)(in[i] - offset);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -2966,6 +2988,14 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
         else CUBIT_PRESENCE(int64_t, false);
     }
 #undef CUBIT_PRESENCE
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,
+                             hipStream_t stream) {
+    if (max_n == 0) return hipSuccess;
+    hipLaunchKernelGGL(narrow_i32_kernel, dim3(grid_for((max_n + 1) / 2)), dim3(256), 0, stream, in, d_count, max_n,
+                       offset, out);
     return hipGetLastError();
 }
 

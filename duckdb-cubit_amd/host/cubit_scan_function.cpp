@@ -171,6 +171,11 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     idx_t rows_per_tile = 0;
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
+    // transfer compaction per emitted position: the window copies move int32 (value - offset)
+    // from d_narrow when every value fits, and the chunk fill widens them back
+    std::vector<bool> narrow;
+    std::vector<int64_t> offset;
+    std::vector<PooledBuffer> d_narrow;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
     std::vector<Window> windows;
@@ -276,6 +281,36 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
                                 g->count, device_ptr(g->d_cols[e])),
               "cubit_table_probe");
     }
+    // transfer compaction: a column whose values all lie within 2^31 of an offset crosses PCIe
+    // as int32 (row ids: the partition's rows below 2^31, offset row_base; probed columns: their
+    // statistics' range, widened by any update records)
+    g->narrow.assign(g->emit.size(), false);
+    g->offset.assign(g->emit.size(), 0);
+    g->d_narrow.resize(g->emit.size());
+    for (size_t e = 0; e < g->emit.size() && g->count; ++e) {
+        const column_t col = g->column_ids[g->emit[e]];
+        bool fits = false;
+        int64_t off = 0;
+        if (col == COLUMN_IDENTIFIER_ROW_ID) {
+            fits = bind.n_rows <= (uint64_t)INT32_MAX;
+            off = bind.row_base;
+        } else {
+            int64_t mn = 0, mx = 0;
+            int hn = 0, hv = 0;
+            // the statistics bound the valid values only: a column with NULL rows (whose slots
+            // hold whatever was stored) keeps the 8-byte transfer
+            if (cubit_table_column_statistics(bind.table, (int)col, &mn, &mx, &hn, &hv) == CUBIT_OK)
+                fits = !hn && mn >= INT32_MIN && mx <= INT32_MAX;
+        }
+        if (!fits) continue;
+        g->narrow[e] = true;
+        g->offset[e] = off;
+        g->d_narrow[e].allocate(device_pool(), ctx, g->count * 4);
+        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g->d_ids : g->d_cols[e];
+        check(cubit_narrow_i32(ctx, device_ptr(src), static_cast<uint64_t*>(d_cnt.p), g->count, off,
+                               static_cast<int32_t*>(g->d_narrow[e].p)),
+              "cubit_narrow_i32");
+    }
     // d_cnt goes back to the pool while the probes may still read it: stream order on this
     // context keeps a later user of the buffer behind them; other contexts never get it
     return g;
@@ -306,6 +341,11 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     for (size_t e = 0; e < g.emit.size(); ++e) {
         if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
         const column_t col = g.column_ids[g.emit[e]];
+        if (g.narrow[e]) {
+            const int32_t* src = static_cast<const int32_t*>(g.d_narrow[e].p) + win.off;
+            check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, src, win.len * 4), "window copy");
+            continue;
+        }
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
         check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
               "window copy");
@@ -332,8 +372,16 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
         if (l.pos < len) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
             const idx_t at = g.tile_off[l.tile_slot] - win.off + l.pos;
-            for (size_t e = 0; e < g.emit.size(); ++e)
-                std::memcpy(output.data[e].data(), l.host[e].i64() + at, n * sizeof(int64_t));
+            for (size_t e = 0; e < g.emit.size(); ++e) {
+                if (g.narrow[e]) {  // widen the compacted transfer
+                    const int32_t* src = static_cast<const int32_t*>(l.host[e].p) + at;
+                    int64_t* dst = output.data[e].data();
+                    const int64_t off = g.offset[e];
+                    for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
+                } else {
+                    std::memcpy(output.data[e].data(), l.host[e].i64() + at, n * sizeof(int64_t));
+                }
+            }
             l.pos += n;
             output.SetCardinality(n);
             g.emitted.fetch_add(n);

@@ -220,6 +220,13 @@ int cubit_bitvector_eval(cubit_ctx *ctx, const uint64_t *const *d_leaves, uint32
  * of ids is read from *d_count (device), at most max_n. */
 int cubit_gather(cubit_ctx *ctx, const void *d_col, int type, const int64_t *d_rowids, const uint64_t *d_count,
                  uint64_t max_n, int64_t row_base, int64_t *d_out);
+/* Transfer compaction of a DataChunk column: d_out[i] = (int32)(d_in[i] - offset) for
+ * i < min(*d_count, max_n). A caller whose column values all lie within [offset - 2^31,
+ * offset + 2^31) (row ids of a partition below 2^31 rows with offset = row_base; DATE, or
+ * DECIMAL / BIGINT whose statistics fit) moves 4 instead of 8 bytes per row to the host and
+ * widens while it fills the vector (the table-function mirror's windows). */
+int cubit_narrow_i32(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n, int64_t offset,
+                     int32_t *d_out);
 /* Fused probe + reduce: sum over ids of a[r]*b[r] as a 128-bit integer (lo, hi int64 at
  * d_out[0..1]) — Q6's sum(l_extendedprice*l_discount) (DECIMAL(38,4) storage). */
 int cubit_gather_sum_product(cubit_ctx *ctx, const int64_t *d_a, const int64_t *d_b, const int64_t *d_rowids,

@@ -262,3 +262,41 @@ def test_pinned_windows_are_reused_across_scans(ctx):
     two, _ = C_release()
     assert two == one > 0
     t.close()
+
+
+def test_window_transfer_compaction_round_trips(ctx):
+    """Windows cross PCIe as int32 (value - offset) where a column's statistics allow it
+    (cubit_narrow_i32) and as int64 otherwise; either way the chunks carry the exact values:
+    row ids of a partition based at 2^40, a DATE-like int32 column, a DECIMAL-like int64 column
+    inside int32 range with negatives, one far outside it, and a column with NULL rows (kept
+    at 8 bytes: its stored slots are not bounded by the statistics)."""
+    from cubit_amd.datagen import validity_from_mask
+
+    n = 1_500_007
+    base = 1 << 40
+    rng = np.random.default_rng(31)
+    key = rng.integers(0, 100, n).astype(np.int32)
+    small = rng.integers(-2_000_000, 2_000_000, n).astype(np.int64)
+    big = rng.integers(-(1 << 50), 1 << 50, n).astype(np.int64)
+    date = (8035 + rng.integers(0, 2526, n)).astype(np.int32)
+    nulls = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    valid = rng.random(n) > 0.05
+    t = CubitTable(ctx, n, row_base=base)
+    t.add_column(0, key)
+    t.add_column(1, small)
+    t.add_column(2, big)
+    t.add_column(3, date)
+    t.add_column(4, nulls, validity_from_mask(valid))
+    t.build_index(0, L.INDEX_RANGE)
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 30)})
+    fn = CubitScanFunction(t, [ROW_ID, 1, 2, 3, 4, 0], [0, 1, 2, 3, 4], fs)
+    chunks = drain(fn, 3)
+    fn.close()
+    keep = np.flatnonzero(key < 30)
+    assert np.array_equal(ordered(chunks, 0), keep.astype(np.int64) + base)
+    assert np.array_equal(ordered(chunks, 1), small[keep])
+    assert np.array_equal(ordered(chunks, 2), big[keep])
+    assert np.array_equal(ordered(chunks, 3), date[keep].astype(np.int64))
+    got = ordered(chunks, 4)
+    assert np.array_equal(got[valid[keep]], nulls[keep][valid[keep]])
+    t.close()
