@@ -1365,21 +1365,46 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     return CUBIT_OK;
 }
 
+// The segments' T (a CUBIT_TYPE_* code): its byte size and signedness, the column type its
+// values widen to and the BpGroup::tnorm that carries T's arithmetic there.
+struct SegType {
+    uint32_t tsz;
+    bool sgn;
+    int col_type;
+    uint8_t tnorm;
+};
+bool seg_type_of(int type, SegType& st) {
+    switch (type) {
+    case CUBIT_TYPE_INT32: st = {4, true, CUBIT_TYPE_INT32, 0}; return true;
+    case CUBIT_TYPE_INT64: st = {8, true, CUBIT_TYPE_INT64, 0}; return true;
+    case CUBIT_TYPE_INT8: st = {1, true, CUBIT_TYPE_INT32, 8 | 0x80}; return true;
+    case CUBIT_TYPE_INT16: st = {2, true, CUBIT_TYPE_INT32, 16 | 0x80}; return true;
+    case CUBIT_TYPE_UINT8: st = {1, false, CUBIT_TYPE_INT32, 8}; return true;
+    case CUBIT_TYPE_UINT16: st = {2, false, CUBIT_TYPE_INT32, 16}; return true;
+    case CUBIT_TYPE_UINT32: st = {4, false, CUBIT_TYPE_INT64, 32}; return true;
+    case CUBIT_TYPE_UINT64: st = {8, false, CUBIT_TYPE_INT64, 0}; return true;
+    default: return false;
+    }
+}
+
 // DuckDB BITPACKING segments → device column (K5). The host walks each segment's metadata
 // (header = end of the metadata words, one word per 2,048-row group, highest address first:
 // BitpackingScanState / LoadNextGroup, bitpacking.cpp:620-690), checks every group's bounds,
-// and the GPU unpacks all groups in parallel.
+// and the GPU unpacks all groups in parallel. A T of 1 or 2 bytes leaves its groups' packed
+// runs off the 4-byte alignment the kernels' word loads need (the header fields are T-sized,
+// WriteData, :448-451): those runs are copied behind the segment bytes, 16-aligned.
 extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int type, const uint8_t* bytes,
                                                 uint64_t n_bytes, const uint64_t* seg_offsets,
                                                 const uint64_t* seg_rows, uint32_t n_segments,
                                                 const uint64_t* validity) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(t->ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    SegType st;
+    if (!seg_type_of(type, st)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (t->n_rows == 0 && n_segments == 0) {  // empty partition, no segments
         Column c;
-        c.type = type;
+        c.type = st.col_type;
         t->cols[col] = std::move(c);
         drop_patches(t, col);
         t->idx.erase(col);
@@ -1388,8 +1413,11 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     }
     if (!bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
     if (int rc = set_device(t->ctx)) return rc;
-    const uint64_t tsz = type == CUBIT_TYPE_INT32 ? 4 : 8;
+    const uint64_t tsz = st.tsz;
+    const uint64_t esz = st.col_type == CUBIT_TYPE_INT32 ? 4 : 8;
+    const uint64_t bytes_padded = (n_bytes + 15) / 16 * 16;
     std::vector<BpGroup> groups;
+    std::vector<uint8_t> moved;  // packed runs copied to 16-aligned offsets behind the bytes
     uint64_t row = 0;
     for (uint32_t sg = 0; sg < n_segments; ++sg) {
         const uint64_t base = seg_offsets[sg];
@@ -1405,7 +1433,8 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
             BpGroup bg{};
             const uint32_t mode = enc >> 24;
             const uint64_t data_off = base + (enc & 0x00ffffffu);
-            bg.mode = (uint16_t)mode;
+            bg.mode = (uint8_t)mode;
+            bg.tnorm = st.tnorm;
             bg.row_start = row + g * 2048;
             bg.count = (uint32_t)std::min<uint64_t>(2048, seg_rows[sg] - g * 2048);
             // header fields (BitpackingScanState::LoadNextGroup, bitpacking.cpp:620-690)
@@ -1415,7 +1444,7 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
             if (data_off < base + 8 || data_off + n_fields * tsz > n_bytes)
                 return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
             auto field = [&](uint64_t i) {
-                uint64_t v = 0;  // the T's bits, zero-extended (the kernel truncates to T)
+                uint64_t v = 0;  // T's bits, zero-extended (the kernels work mod 2^bits: bp_norm)
                 std::memcpy(&v, bytes + data_off + i * tsz, tsz);
                 return v;
             };
@@ -1433,6 +1462,12 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
             bg.words_off = data_off + n_fields * tsz;
             if (bg.words_off + packed > n_bytes)
                 return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
+            if (packed && bg.words_off % 4) {
+                const uint64_t at = moved.size();
+                moved.resize(at + (packed + 15) / 16 * 16, 0);
+                std::memcpy(moved.data() + at, bytes + bg.words_off, packed);
+                bg.words_off = bytes_padded + at;
+            }
             groups.push_back(bg);
         }
         row += seg_rows[sg];
@@ -1450,22 +1485,25 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     hipStream_t s = t->ctx->stream;
     DevBuf d_bytes, d_groups, d_vgroup;
     auto out = std::make_unique<DevBuf>();
-    // +16: the kernel stages packed words with 16-byte-aligned loads that may run past the end
-    if (hipMalloc(&d_bytes.p, (n_bytes + 15) / 16 * 16 + 16) != hipSuccess ||
+    // +16: the kernels stage packed words with 16-byte-aligned loads that may run past the end
+    if (hipMalloc(&d_bytes.p, bytes_padded + moved.size() + 16) != hipSuccess ||
         hipMalloc(&d_groups.p, groups.size() * sizeof(BpGroup)) != hipSuccess ||
-        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * tsz, 16)) != hipSuccess ||
+        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess ||
         hipMalloc(&d_vgroup.p, vgroup.size() * 4) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "bitpacked column allocation failed");
     HIP_CHECK(hipMemcpyAsync(d_bytes.p, bytes, n_bytes, hipMemcpyHostToDevice, s));
+    if (!moved.empty())
+        HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(d_bytes.p) + bytes_padded, moved.data(), moved.size(),
+                                 hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_vgroup.p, vgroup.data(), vgroup.size() * 4, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_groups.p, groups.data(), groups.size() * sizeof(BpGroup), hipMemcpyHostToDevice, s));
     hipEvent_t e0, e1;
     if (int rc = timing_events(t->ctx, e0, e1)) return rc;
     HIP_CHECK(launch_bitunpack(static_cast<const uint8_t*>(d_bytes.p), static_cast<const BpGroup*>(d_groups.p),
-                               groups.size(), type, out->p, s, e0, e1));
+                               groups.size(), st.col_type, out->p, s, e0, e1));
     HIP_CHECK(hipStreamSynchronize(s));
     Column c;
-    c.type = type;
+    c.type = st.col_type;
     c.data = out->p;
     c.cap_rows = t->n_rows;
     c.owned.push_back(std::move(out));
@@ -1488,6 +1526,17 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     if (validity) {
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
         HIP_CHECK(hipStreamSynchronize(s));
+    }
+    if (type == CUBIT_TYPE_UINT64) {
+        // held as INT64: every valid value must stay below 2^63, i.e. read as a non-negative INT64
+        std::vector<int64_t> unused;
+        int64_t vmin = 0, vmax = 0;
+        bool any = false;
+        if (int rc = value_stats(t, c.data, CUBIT_TYPE_INT64, c.validity, t->n_rows, unused, false, vmin, vmax, any))
+            return rc;
+        if (any && vmin < 0)
+            return fail(CUBIT_ERR_UNSUPPORTED, "UINT64 column %d holds a value of 2^63 or more (an INT64 column cannot hold it)",
+                        col);
     }
     t->cols[col] = std::move(c);
     drop_patches(t, col);

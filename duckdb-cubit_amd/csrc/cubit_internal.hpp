@@ -167,7 +167,12 @@ struct BpGroup {
     uint64_t base;       // CONSTANT value | CONSTANT_DELTA first | FOR minimum | DELTA_FOR min_delta (T bits)
     uint64_t aux;        // CONSTANT_DELTA delta | DELTA_FOR delta_offset (T bits)
     uint32_t count;      // rows in the group (≤ 2,048)
-    uint16_t mode;
+    uint8_t mode;
+    // the segments' T when narrower than the column's values (an 8- / 16-bit T in an INT32
+    // column, UINT32 in an INT64 column): its bits | 0x80 when signed; 0 = T is the column's
+    // type. Decoded values are taken mod 2^bits and sign- or zero-extended (bp_norm), which is
+    // T's own wrap-around arithmetic
+    uint8_t tnorm;
     uint16_t width;      // bit width of the packed values (FOR / DELTA_FOR)
 };
 hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "cubit_internal.hpp"
 
@@ -1313,6 +1314,18 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a,
     }
 }
 
+// A decoded value in the segments' own T when T is narrower than the column's values
+// (BpGroup::tnorm, uniform per group): mod 2^bits, then sign- or zero-extended — T's
+// wrap-around arithmetic (a UINT32 DELTA_FOR run that wraps, an INT16 CONSTANT_DELTA that
+// steps by -3) carried out in the wider U
+template <typename U>
+__device__ __forceinline__ U bp_norm(U v, uint32_t tn) {
+    if (!tn) return v;
+    typedef typename std::conditional<sizeof(U) == 8, int64_t, int32_t>::type S;
+    const uint32_t sh = (uint32_t)(sizeof(U) * 8) - (tn & 0x7fu);
+    return (tn & 0x80u) ? (U)((S)(v << sh) >> sh) : (U)((U)(v << sh) >> sh);
+}
+
 // ------------------------------------------------------------------ K1+K3: fused filter + probe-sum
 
 __device__ __forceinline__ void add128(uint64_t& lo, int64_t& hi, __int128 x) {
@@ -1367,7 +1380,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
     __shared__ int32_t s_gst[NREC];   // group's first row - the tile's first row
     __shared__ uint32_t s_gcnt[NREC];
     __shared__ uint64_t s_gbase[NREC], s_gaux[NREC], s_goff[NREC];
-    __shared__ uint8_t s_gmode[NREC], s_gw[NREC];
+    __shared__ uint8_t s_gmode[NREC], s_gw[NREC], s_gtn[NREC];
     uint32_t tile_g0 = 0, tile_ng = 0;  // staged records: groups tile_g0 … tile_g0 + tile_ng - 1
     uint64_t tile_row0 = 0;
     auto stage_groups = [&](uint64_t row0) {
@@ -1383,7 +1396,8 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
             s_gbase[t] = gr.base;
             s_gaux[t] = gr.aux;
             s_goff[t] = gr.words_off;
-            s_gmode[t] = (uint8_t)gr.mode;
+            s_gmode[t] = gr.mode;
+            s_gtn[t] = gr.tnorm;
             s_gw[t] = (uint8_t)gr.width;
         }
     };
@@ -1398,13 +1412,13 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
         if (rl < (int64_t)s_gst[g] || rl >= (int64_t)s_gst[g] + (int64_t)s_gcnt[g])
             return __builtin_nontemporal_load(s.a_plain + r);  // past the staged groups
         const uint64_t i = (uint64_t)(rl - (int64_t)s_gst[g]);
-        const uint32_t mode = s_gmode[g];
+        const uint32_t mode = s_gmode[g], tn = s_gtn[g];
         const uint64_t base = s_gbase[g];
-        if (mode == 2) return (int64_t)base;
-        if (mode == 3) return (int64_t)(base + s_gaux[g] * i);
+        if (mode == 2) return (int64_t)bp_norm<uint64_t>(base, tn);
+        if (mode == 3) return (int64_t)bp_norm<uint64_t>(base + s_gaux[g] * i, tn);
         if (mode != 5) return __builtin_nontemporal_load(s.a_plain + r);  // DELTA_FOR: needs its prefix
         const uint32_t w = s_gw[g];
-        if (w == 0) return (int64_t)base;
+        if (w == 0) return (int64_t)bp_norm<uint64_t>(base, tn);
         const uint32_t* words = reinterpret_cast<const uint32_t*>(s.a_bytes + s_goff[g]);
         const uint64_t bit = i * w;
         const uint32_t wi = (uint32_t)(bit >> 5), off = (uint32_t)(bit & 31);
@@ -1412,7 +1426,7 @@ __global__ __launch_bounds__(512, 4) void eval_sum_product(EvalArgs a, SumArgs s
                       (off + w > 32 ? (uint64_t)__builtin_nontemporal_load(words + wi + 1) << 32 : 0ull)) >> off;
         if (off + w > 64) x |= (uint64_t)__builtin_nontemporal_load(words + wi + 2) << (64 - off);
         if (w < 64) x &= (1ull << w) - 1;
-        return (int64_t)(x + base);
+        return (int64_t)bp_norm<uint64_t>(x + base, tn);
     };
     auto accumulate = [&](int64_t row, int64_t bval_decoded) {
         const uint64_t r = (uint64_t)(row - a.row_base);
@@ -2003,7 +2017,7 @@ __device__ __forceinline__ void unpack_group(const uint8_t* __restrict__ bytes, 
         for (int c = 0; c < QUADS; ++c) {
             U v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (U)(d * (U)(4u * (uint32_t)(t + THREADS * c) + j) + base);
+            for (int j = 0; j < 4; ++j) v[j] = bp_norm<U>((U)(d * (U)(4u * (uint32_t)(t + THREADS * c) + j) + base), g.tnorm);
             store_quad(c, v);
         }
         return;
@@ -2037,7 +2051,7 @@ __device__ __forceinline__ void unpack_group(const uint8_t* __restrict__ bytes, 
                 if (off + w > 64) x |= (uint64_t)s_words[sh + wi + 2] << (64 - off);
                 if (w < 64) x &= (1ull << w) - 1;
             }
-            v[c][j] = (U)x + fr;
+            v[c][j] = bp_norm<U>((U)x + fr, g.tnorm);
         }
     if (!delta) {
 #pragma unroll
@@ -2074,7 +2088,7 @@ __device__ __forceinline__ void unpack_group(const uint8_t* __restrict__ bytes, 
         __syncthreads();  // s_tot is rewritten by the next half
         carry += tot;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[c][j] += pre;
+        for (int j = 0; j < 4; ++j) v[c][j] = bp_norm<U>(v[c][j] + pre, g.tnorm);
         store_quad(c, v[c]);
     }
 }
@@ -2268,11 +2282,11 @@ __global__ __launch_bounds__(256) void bitpacked_compare_kernel(const uint8_t* _
             test_and_store([&](uint32_t i) -> T {
                 const uint32_t bit = i * w, wi = sh + (bit >> 5);  // i·w < 2^16
                 const uint32_t x = __builtin_amdgcn_alignbit(W[wi + 1], W[wi], bit & 31) & mask;
-                return (T)((U)x + fr);
+                return (T)bp_norm<U>((U)x + fr, cur.tnorm);
             });
         } else if (cur.mode == 2 || cur.mode == 3) {  // CONSTANT, CONSTANT_DELTA: no packed words
             const U base = (U)cur.base, d = cur.mode == 3 ? (U)cur.aux : (U)0;
-            test_and_store([&](uint32_t i) -> T { return (T)(d * (U)i + base); });
+            test_and_store([&](uint32_t i) -> T { return (T)bp_norm<U>(d * (U)i + base, cur.tnorm); });
         } else {
             // DELTA_FOR (a running sum) or FOR wider than 32 bits: unpack into LDS values first
             unpack_group<T, U, true>(bytes, cur, const_cast<uint32_t*>(W), s_tot, [&](int qq, const U (&v)[4]) {
@@ -2318,9 +2332,9 @@ __device__ __forceinline__ void compare_group_words(const BpGroup& cur, const ui
             T v;
             if (packed) {
                 const uint32_t bit = i * w, wi = bit >> 5;  // i·w < 2^16
-                v = (T)((U)(__builtin_amdgcn_alignbit(L[wi + 1], L[wi], bit & 31) & mask) + base);
+                v = (T)bp_norm<U>((U)(__builtin_amdgcn_alignbit(L[wi + 1], L[wi], bit & 31) & mask) + base, cur.tnorm);
             } else {
-                v = (T)(d * (U)i + base);
+                v = (T)bp_norm<U>(d * (U)i + base, cur.tnorm);
             }
             p = ((v >= lo) & (v <= hi)) != (neg != 0);
             if (validity) {

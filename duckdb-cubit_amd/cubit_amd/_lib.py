@@ -20,6 +20,11 @@ SCAN_LIB = LIB_DIR / "libcubit_scan.so"
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_OOM, ERR_UNSUPPORTED, ERR_CAPACITY, ERR_DEVICE = 1, 2, 3, 4, 5, 6
 TYPE_INT32, TYPE_INT64 = 0, 1
+# the T of BITPACKING segments (cubit_table_add_bitpacked_column): numpy dtype → CUBIT_TYPE_*
+TYPE_INT8, TYPE_INT16, TYPE_UINT8, TYPE_UINT16, TYPE_UINT32, TYPE_UINT64 = 2, 3, 4, 5, 6, 7
+SEGMENT_TYPES = {"int8": TYPE_INT8, "int16": TYPE_INT16, "int32": TYPE_INT32, "int64": TYPE_INT64,
+                 "uint8": TYPE_UINT8, "uint16": TYPE_UINT16, "uint32": TYPE_UINT32, "uint64": TYPE_UINT64,
+                 "bool": TYPE_INT8}
 CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
 FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = range(5)
 INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2

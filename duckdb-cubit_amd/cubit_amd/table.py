@@ -193,16 +193,19 @@ class CubitTable:
     def add_bitpacked_column(self, col: int, data: np.ndarray, seg_offsets: np.ndarray, seg_rows: np.ndarray,
                              dtype, validity: Optional[np.ndarray] = None) -> None:
         """A column given as DuckDB BITPACKING segment images (uint8 bytes, per-segment byte
-        offsets and row counts); unpacked on the GPU (K5)."""
+        offsets and row counts); unpacked on the GPU (K5). `dtype` is the segments' T (any
+        integral type DuckDB bit-packs); the column holds the values as INT32 (8-, 16- and
+        32-bit signed T, 8- and 16-bit unsigned) or INT64 (UINT32, INT64, UINT64 below 2^63)."""
         data = np.ascontiguousarray(data, dtype=np.uint8)
         so = np.ascontiguousarray(seg_offsets, dtype=np.uint64)
         sr = np.ascontiguousarray(seg_rows, dtype=np.uint64)
         vw = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
-        typ = L.TYPE_INT32 if np.dtype(dtype) == np.int32 else L.TYPE_INT64
+        typ = L.SEGMENT_TYPES[np.dtype(dtype).name]
         L.check(self.lib.cubit_table_add_bitpacked_column(self.handle, col, typ, data.ctypes.data, data.nbytes,
                                                           so.ctypes.data, sr.ctypes.data, len(so),
                                                           vw.ctypes.data if vw is not None else None))
-        self.types[col] = typ
+        self.types[col] = L.TYPE_INT32 if typ in (L.TYPE_INT8, L.TYPE_INT16, L.TYPE_UINT8, L.TYPE_UINT16,
+                                                  L.TYPE_INT32) else L.TYPE_INT64
 
     def column_data(self, col: int):
         """(device pointer, CUBIT type) of a registered column's values."""

@@ -38,9 +38,20 @@ extern "C" {
 #define CUBIT_ERR_DEVICE 6       /* device-side failure (stream event creation, …) */
 
 /* ---- physical types (DuckDB PhysicalType subset on the path: DATE = INT32,
- *      DECIMAL(15,2) = INT64, BIGINT = INT64, INTEGER = INT32) */
+ *      DECIMAL(15,2) = INT64, BIGINT = INT64, INTEGER = INT32). A column holds INT32 or INT64
+ *      values; the narrower and unsigned codes name the T of BITPACKING segments
+ *      (cubit_table_add_bitpacked_column; bitpacking.cpp:953-977 GetFunction: BOOL and INT8
+ *      as int8_t, …, UINT64 and LIST offsets as uint64_t), unpacked into an INT32 column
+ *      (INT8, INT16, UINT8, UINT16) or an INT64 column (UINT32, and UINT64 whose every valid
+ *      value is below 2^63). */
 #define CUBIT_TYPE_INT32 0
 #define CUBIT_TYPE_INT64 1
+#define CUBIT_TYPE_INT8 2
+#define CUBIT_TYPE_INT16 3
+#define CUBIT_TYPE_UINT8 4
+#define CUBIT_TYPE_UINT16 5
+#define CUBIT_TYPE_UINT32 6
+#define CUBIT_TYPE_UINT64 7
 
 /* ---- comparison (ExpressionType COMPARE_* used by ConstantFilter,
  *      src/planner/filter/constant_filter.cpp) */
@@ -259,7 +270,10 @@ int cubit_table_column_changed(cubit_table *t, int col);
  * 2,048-row groups growing down), segment i at seg_offsets[i] (8-aligned) with seg_rows[i]
  * rows; the segments cover the partition in row order. The GPU unpacks every group
  * (CONSTANT, CONSTANT_DELTA, FOR, DELTA_FOR) into the column; NULLs come from `validity`
- * (host words; DuckDB keeps them in a separate validity segment). Malformed segments are
+ * (host words; DuckDB keeps them in a separate validity segment). `type` is the segments' T,
+ * any CUBIT_TYPE_* (header fields of T's size, T's wrap-around arithmetic); the column holds
+ * the values widened to INT32 or INT64 (see the type codes). A UINT64 column with a valid value
+ * of 2^63 or more is refused (CUBIT_ERR_UNSUPPORTED) after the unpack. Malformed segments are
  * refused before anything is launched. With timing on, the unpack kernel is a timed launch
  * (cubit_last_kernel_ms). */
 int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,

@@ -20,7 +20,8 @@
  * and from src/include/duckdb/common/bitpacking.hpp: 32-value algorithm groups packed
  * horizontally (value i of a group at bits [i·w, (i+1)·w) of little-endian 32-bit words,
  * fastpforlib fastpack), MinimumBitWidth / GetEffectiveWidth (:84-210).
- * Values are INT32 (DATE, INTEGER, DECIMAL ≤ 9) or INT64 (BIGINT, DECIMAL 10..18).
+ * Values are any of the integral physical types the reference bit-packs: INT8 … INT64 and
+ * UINT8 … UINT64 (TINYINT … BIGINT, UTINYINT … UBIGINT, DATE, DECIMAL ≤ 18).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -34,54 +35,103 @@
 /* BitpackingMode (src/include/duckdb/storage/compression/bitpacking.hpp:15) */
 enum { BP_INVALID = 0, BP_AUTO = 1, BP_CONSTANT = 2, BP_CONSTANT_DELTA = 3, BP_DELTA_FOR = 4, BP_FOR = 5 };
 
+/* ---------------------------------------------------------------- the value type T */
+
+/* T is one of DuckDB's bitpacked physical types: 1, 2, 4 or 8 bytes, signed or unsigned
+ * (bitpacking.cpp:951-977 GetBitpackingFunction: INT8..INT64, UINT8..UINT64). The caller's
+ * ttype = byte size | 0x100 when unsigned. Values travel as T's bits, zero-extended to 64;
+ * T_S is the signed type of T's size (the deltas, MakeSigned<T>). */
+typedef struct {
+    int tsize, bits, sgn;
+    uint64_t mask;
+} bp_t;
+
+static int bp_ttype_ok(int ttype) {
+    const int sz = ttype & 0xff;
+    return (ttype & ~0x1ff) == 0 && (sz == 1 || sz == 2 || sz == 4 || sz == 8);
+}
+static bp_t bp_type(int ttype) {
+    bp_t t;
+    t.tsize = ttype & 0xff;
+    t.bits = 8 * t.tsize;
+    t.sgn = !(ttype & 0x100);
+    t.mask = t.bits == 64 ? ~0ull : ((1ull << t.bits) - 1);
+    return t;
+}
+/* the signed value of T_S bits x */
+static int64_t sx(uint64_t x, int bits) { return bits == 64 ? (int64_t)x : (int64_t)(x << (64 - bits)) >> (64 - bits); }
+/* a < b in T's order */
+static int t_lt(bp_t t, uint64_t a, uint64_t b) { return t.sgn ? sx(a, t.bits) < sx(b, t.bits) : a < b; }
+static uint64_t t_max(bp_t t) { return t.sgn ? t.mask >> 1 : t.mask; }
+static uint64_t t_min(bp_t t) { return t.sgn ? (t.mask >> 1) + 1 : 0; }
+/* TrySubtractOperator in T_S: a - b of T_S bits, 0 when it overflows T_S */
+static int sub_s(bp_t t, uint64_t a, uint64_t b, uint64_t *out) {
+    const int64_t x = sx(a, t.bits), y = sx(b, t.bits);
+    int64_t r;
+    if (__builtin_sub_overflow(x, y, &r)) return 0;
+    if (t.bits < 64 && (r < -(1ll << (t.bits - 1)) || r > (1ll << (t.bits - 1)) - 1)) return 0;
+    *out = (uint64_t)r & t.mask;
+    return 1;
+}
+/* TrySubtractOperator in T */
+static int sub_t(bp_t t, uint64_t a, uint64_t b, uint64_t *out) {
+    if (t.sgn) return sub_s(t, a, b, out);
+    if (a < b) return 0;
+    *out = a - b;
+    return 1;
+}
+
 /* ---------------------------------------------------------------- width helpers */
 
-/* unsigned bits of v (v ≥ 0), through GetEffectiveWidth */
-static int eff_width(int w, int tsize) {
-    const int bits = tsize * 8;
-    return (w + tsize > bits) ? bits : w;
-}
-static int width_unsigned(uint64_t v, int tsize) {
+/* GetEffectiveWidth (bitpacking.hpp:202-210) */
+static int eff_width(int w, bp_t t) { return (w + t.tsize > t.bits) ? t.bits : w; }
+/* MinimumBitWidth<T, false>(v) (bitpacking.hpp:139-188, is_signed = false) */
+static int width_u(bp_t t, uint64_t v) {
+    v &= t.mask;
     int w = 0;
     while (v) {
         w++;
         v >>= 1;
     }
-    return w == 0 ? 0 : eff_width(w, tsize);
+    return w == 0 ? 0 : eff_width(w, t);
 }
-/* MinimumBitWidth<T signed>(value, value) for value ≥ 0: one sign bit more */
-static int width_signed_nonneg(int64_t v, int tsize) {
-    if (v == 0) return 0;
+/* MinimumBitWidth<T>(v) with T's own signedness: signed T takes |v| plus a sign bit, and the
+ * full width for T's minimum */
+static int width_t(bp_t t, uint64_t v) {
+    if (!t.sgn) return width_u(t, v);
+    const int64_t x = sx(v & t.mask, t.bits);
+    if ((v & t.mask) == t_min(t)) return t.bits;
+    uint64_t a = (uint64_t)(x < 0 ? -x : x);
+    if (a == 0) return 0;
     int w = 1;
-    uint64_t x = (uint64_t)v;
-    while (x) {
+    while (a) {
         w++;
-        x >>= 1;
+        a >>= 1;
     }
-    return eff_width(w, tsize);
+    return eff_width(w, t);
 }
-
-static int64_t tmin(int tsize) { return tsize == 4 ? INT32_MIN : INT64_MIN; }
-static int64_t tmax(int tsize) { return tsize == 4 ? INT32_MAX : INT64_MAX; }
-static int sub_ok(int64_t a, int64_t b, int tsize, int64_t *out) {
-    if (tsize == 4) {
-        const int64_t r = a - b;
-        if (r < INT32_MIN || r > INT32_MAX) return 0;
-        *out = r;
-        return 1;
-    }
-    return !__builtin_sub_overflow(a, b, out);
-}
-static uint64_t umask(int tsize) { return tsize == 4 ? 0xffffffffull : ~0ull; }
 
 /* ---------------------------------------------------------------- packing */
+
+/* 32-bit little-endian word i of a packed run (any byte alignment: narrow T's headers leave
+ * the run unaligned) */
+static uint32_t get_word(const uint8_t *p, uint64_t i) {
+    uint32_t x;
+    memcpy(&x, p + 4 * i, 4);
+    return x;
+}
+static void or_word(uint8_t *p, uint64_t i, uint32_t v) {
+    uint32_t x;
+    memcpy(&x, p + 4 * i, 4);
+    x |= v;
+    memcpy(p + 4 * i, &x, 4);
+}
 
 static void pack_values(uint8_t *dst, const uint64_t *v, uint64_t count, int w) {
     const uint64_t n = (count + BP_ALG - 1) / BP_ALG * BP_ALG;
     const uint64_t bytes = n * (uint64_t)w / 8;
     memset(dst, 0, bytes);
     if (w == 0) return;
-    uint32_t *words = (uint32_t *)dst;
     const uint64_t mask = w == 64 ? ~0ull : ((1ull << w) - 1);
     for (uint64_t i = 0; i < n; i++) {
         uint64_t x = (i < count ? v[i] : 0) & mask;
@@ -91,7 +141,7 @@ static void pack_values(uint8_t *dst, const uint64_t *v, uint64_t count, int w) 
             const uint64_t wi = bit >> 5;
             const int off = (int)(bit & 31);
             const int take = (32 - off) < left ? (32 - off) : left;
-            words[wi] |= (uint32_t)((x & ((take == 64) ? ~0ull : ((1ull << take) - 1))) << off);
+            or_word(dst, wi, (uint32_t)((x & ((1ull << take) - 1)) << off));
             x >>= take;
             bit += (uint64_t)take;
             left -= take;
@@ -101,14 +151,13 @@ static void pack_values(uint8_t *dst, const uint64_t *v, uint64_t count, int w) 
 
 static uint64_t unpack_value(const uint8_t *src, uint64_t i, int w) {
     if (w == 0) return 0;
-    const uint32_t *words = (const uint32_t *)src;
     uint64_t bit = i * (uint64_t)w, x = 0;
     int got = 0;
     while (got < w) {
         const uint64_t wi = bit >> 5;
         const int off = (int)(bit & 31);
         const int take = (32 - off) < (w - got) ? (32 - off) : (w - got);
-        const uint64_t part = ((uint64_t)words[wi] >> off) & ((1ull << take) - 1);
+        const uint64_t part = ((uint64_t)get_word(src, wi) >> off) & ((1ull << take) - 1);
         x |= part << got;
         got += take;
         bit += (uint64_t)take;
@@ -129,18 +178,9 @@ typedef struct {
     uint64_t seg_rows;
     uint64_t *seg_off, *seg_size, *seg_count;
     uint32_t n_segs, max_segs;
-    int tsize;
+    bp_t t;
     int failed;
 } bp_writer;
-
-static void store_t(uint8_t *p, int64_t v, int tsize) {
-    if (tsize == 4) {
-        int32_t x = (int32_t)v;
-        memcpy(p, &x, 4);
-    } else {
-        memcpy(p, &v, 8);
-    }
-}
 
 static void seg_begin(bp_writer *w) {
     memset(w->blk, 0, w->block_size);
@@ -157,7 +197,7 @@ static void seg_flush(bp_writer *w) {
     const uint64_t header = meta_at + meta_size;
     memcpy(w->blk, &header, 8);
     /* segments start 8-aligned in the concatenated image (each is a block of its own in the
-     * reference, so every field stays aligned to its width) */
+     * reference) */
     w->out_used = (w->out_used + 7) / 8 * 8;
     if (w->n_segs >= w->max_segs || w->out_used + total > w->out_cap) {
         w->failed = 1;
@@ -190,26 +230,28 @@ static void write_meta(bp_writer *w, int mode) {
     memcpy(w->blk + w->meta_off, &enc, 4);
 }
 
-static void put_t(bp_writer *w, int64_t v) {
-    store_t(w->blk + w->data_off, v, w->tsize);
-    w->data_off += (uint64_t)w->tsize;
+/* WriteData<T>: T's bytes, unaligned (little-endian: the low tsize bytes of the bits) */
+static void put_t(bp_writer *w, uint64_t v) {
+    memcpy(w->blk + w->data_off, &v, (size_t)w->t.tsize);
+    w->data_off += (uint64_t)w->t.tsize;
 }
 
 typedef struct {
-    int64_t buf[BP_GROUP + 1]; /* buf[0] = the "previous value" slot (stays 0) */
-    int64_t delta[BP_GROUP];
+    uint64_t buf[BP_GROUP + 1]; /* T bits; buf[0] = the "previous value" slot (stays 0) */
+    uint64_t delta[BP_GROUP];   /* T_S bits */
     int valid[BP_GROUP];
     uint64_t idx;
-    int64_t minimum, maximum, min_delta, max_delta, min_max_diff, min_max_delta_diff, delta_offset;
+    uint64_t minimum, maximum, min_max_diff;                          /* T */
+    uint64_t min_delta, max_delta, min_max_delta_diff, delta_offset;  /* T_S */
     int all_valid, all_invalid, can_delta, can_for;
     int mode;
 } bp_state;
 
-static void st_reset(bp_state *s, int tsize) {
-    s->minimum = tmax(tsize);
-    s->maximum = tmin(tsize);
-    s->min_delta = tmax(tsize);
-    s->max_delta = tmin(tsize);
+static void st_reset(bp_state *s, bp_t t) {
+    s->minimum = t_max(t);
+    s->maximum = t_min(t);
+    s->min_delta = t.mask >> 1;    /* T_S maximum */
+    s->max_delta = (t.mask >> 1) + 1;  /* T_S minimum */
     s->delta_offset = 0;
     s->all_valid = 1;
     s->all_invalid = 1;
@@ -220,29 +262,29 @@ static void st_reset(bp_state *s, int tsize) {
     s->min_max_delta_diff = 0;
 }
 
-/* Flush one group (BitpackingState::Flush); 0 = the column cannot be bitpacked */
+/* Flush one group (BitpackingState::Flush, bitpacking.cpp:231-296); 0 = the column cannot be
+ * bitpacked */
 static int st_flush(bp_state *s, bp_writer *w) {
-    const int ts = w->tsize;
-    int64_t *cb = s->buf + 1;
+    const bp_t t = w->t;
+    const uint64_t ts = (uint64_t)t.tsize;
+    uint64_t *cb = s->buf + 1;
     if (s->idx == 0) return 1;
     if ((s->all_invalid || s->maximum == s->minimum) && (s->mode == BP_AUTO || s->mode == BP_CONSTANT)) {
-        reserve(w, (uint64_t)ts);
+        reserve(w, ts);
         write_meta(w, BP_CONSTANT);
         put_t(w, s->maximum);
         w->seg_rows += s->idx;
         return 1;
     }
-    s->can_for = sub_ok(s->maximum, s->minimum, ts, &s->min_max_diff);
-    /* CalculateDeltaStats (T signed: the T_S maximum check never fires) */
-    if (s->idx >= 2 && s->all_valid) {
-        int64_t bogus;
-        const int can_all = sub_ok(s->minimum, s->maximum, ts, &bogus) && sub_ok(s->maximum, s->minimum, ts, &bogus);
+    s->can_for = sub_t(t, s->maximum, s->minimum, &s->min_max_diff); /* CalculateFORStats */
+    /* CalculateDeltaStats (:155-214): unsigned T above T_S's maximum never delta-encodes; a
+     * NULL or a single value neither. Every delta is a T_S subtraction (for signed T whose
+     * max - min fits T_S the reference skips the overflow check: none can occur). */
+    const int above_ts = !t.sgn && s->maximum > (t.mask >> 1);
+    if (!above_ts && s->idx >= 2 && s->all_valid) {
         int ok = 1;
         for (uint64_t i = 0; i < s->idx; i++) {
-            if (can_all) {
-                s->delta[i] = ts == 4 ? (int64_t)(int32_t)((uint32_t)cb[i] - (uint32_t)cb[(int64_t)i - 1])
-                                      : (int64_t)((uint64_t)cb[i] - (uint64_t)cb[(int64_t)i - 1]);
-            } else if (!sub_ok(cb[i], cb[(int64_t)i - 1], ts, &s->delta[i])) {
+            if (!sub_s(t, cb[i], cb[(int64_t)i - 1], &s->delta[i])) {
                 ok = 0;
                 break;
             }
@@ -250,33 +292,33 @@ static int st_flush(bp_state *s, bp_writer *w) {
         if (ok) {
             s->can_delta = 1;
             for (uint64_t i = 1; i < s->idx; i++) {
-                if (s->delta[i] > s->max_delta) s->max_delta = s->delta[i];
-                if (s->delta[i] < s->min_delta) s->min_delta = s->delta[i];
+                if (sx(s->delta[i], t.bits) > sx(s->max_delta, t.bits)) s->max_delta = s->delta[i];
+                if (sx(s->delta[i], t.bits) < sx(s->min_delta, t.bits)) s->min_delta = s->delta[i];
             }
             s->delta[0] = s->min_delta;
-            s->can_delta = s->can_delta && sub_ok(s->max_delta, s->min_delta, ts, &s->min_max_delta_diff);
-            s->can_delta = s->can_delta && sub_ok(cb[0], s->min_delta, ts, &s->delta_offset);
+            s->can_delta = s->can_delta && sub_s(t, s->max_delta, s->min_delta, &s->min_max_delta_diff);
+            s->can_delta = s->can_delta && sub_s(t, cb[0], s->min_delta, &s->delta_offset);
         }
     }
     if (s->can_delta) {
         if (s->max_delta == s->min_delta && s->mode != BP_FOR && s->mode != BP_DELTA_FOR) {
-            reserve(w, 2 * (uint64_t)ts);
+            reserve(w, 2 * ts);
             write_meta(w, BP_CONSTANT_DELTA);
             put_t(w, cb[0]);
             put_t(w, s->max_delta);
             w->seg_rows += s->idx;
             return 1;
         }
-        const int dw = width_unsigned((uint64_t)s->min_max_delta_diff & umask(ts), ts);
-        const int rw = width_signed_nonneg(s->min_max_diff, ts);
+        const int dw = width_u(t, s->min_max_delta_diff);
+        const int rw = width_t(t, s->min_max_diff);
         if (dw < rw && s->mode != BP_FOR) {
             uint64_t u[BP_GROUP];
-            for (uint64_t i = 0; i < s->idx; i++) u[i] = ((uint64_t)s->delta[i] - (uint64_t)s->min_delta) & umask(ts);
+            for (uint64_t i = 0; i < s->idx; i++) u[i] = (s->delta[i] - s->min_delta) & t.mask;
             const uint64_t bp = (s->idx + BP_ALG - 1) / BP_ALG * BP_ALG * (uint64_t)dw / 8;
-            reserve(w, bp + 3 * (uint64_t)ts);
+            reserve(w, bp + 3 * ts);
             write_meta(w, BP_DELTA_FOR);
             put_t(w, s->min_delta);
-            put_t(w, dw);
+            put_t(w, (uint64_t)dw);
             put_t(w, s->delta_offset);
             pack_values(w->blk + w->data_off, u, s->idx, dw);
             w->data_off += bp;
@@ -285,14 +327,14 @@ static int st_flush(bp_state *s, bp_writer *w) {
         }
     }
     if (s->can_for) {
-        const int fw = width_unsigned((uint64_t)s->min_max_diff, ts);
+        const int fw = width_u(t, s->min_max_diff);
         uint64_t u[BP_GROUP];
-        for (uint64_t i = 0; i < s->idx; i++) u[i] = ((uint64_t)cb[i] - (uint64_t)s->minimum) & umask(ts);
+        for (uint64_t i = 0; i < s->idx; i++) u[i] = (cb[i] - s->minimum) & t.mask;
         const uint64_t bp = (s->idx + BP_ALG - 1) / BP_ALG * BP_ALG * (uint64_t)fw / 8;
-        reserve(w, bp + 2 * (uint64_t)ts);
+        reserve(w, bp + 2 * ts);
         write_meta(w, BP_FOR);
         put_t(w, s->minimum);
-        put_t(w, fw);
+        put_t(w, (uint64_t)fw);
         pack_values(w->blk + w->data_off, u, s->idx, fw);
         w->data_off += bp;
         w->seg_rows += s->idx;
@@ -301,10 +343,11 @@ static int st_flush(bp_state *s, bp_writer *w) {
     return 0;
 }
 
-int oracle_bp_compress(const void *values, int tsize, const uint8_t *valid, uint64_t n, int mode, uint64_t block_size,
+int oracle_bp_compress(const void *values, int ttype, const uint8_t *valid, uint64_t n, int mode, uint64_t block_size,
                        uint8_t *out, uint64_t out_cap, uint64_t *seg_off, uint64_t *seg_size, uint64_t *seg_count,
                        uint32_t max_segs, uint32_t *n_segs) {
-    if ((tsize != 4 && tsize != 8) || !values || !out || !n_segs) return -1;
+    if (!bp_ttype_ok(ttype) || !values || !out || !n_segs) return -1;
+    const bp_t t = bp_type(ttype);
     bp_writer w;
     memset(&w, 0, sizeof(w));
     w.out = out;
@@ -315,7 +358,7 @@ int oracle_bp_compress(const void *values, int tsize, const uint8_t *valid, uint
     w.seg_size = seg_size;
     w.seg_count = seg_count;
     w.max_segs = max_segs;
-    w.tsize = tsize;
+    w.t = t;
     bp_state *s = (bp_state *)calloc(1, sizeof(bp_state));
     if (!w.blk || !s) {
         free(w.blk);
@@ -323,24 +366,25 @@ int oracle_bp_compress(const void *values, int tsize, const uint8_t *valid, uint
         return -1;
     }
     s->mode = mode;
-    st_reset(s, tsize);
+    st_reset(s, t);
     seg_begin(&w);
     int ok = 1;
-    for (uint64_t r = 0; r < n && ok; r++) {
+    for (uint64_t r = 0; r < n && ok; r++) { /* BitpackingState::Update (:298-318) */
         const int v_ok = valid ? valid[r] != 0 : 1;
-        const int64_t v = tsize == 4 ? (int64_t)((const int32_t *)values)[r] : ((const int64_t *)values)[r];
+        uint64_t v = 0;
+        memcpy(&v, (const uint8_t *)values + r * (uint64_t)t.tsize, (size_t)t.tsize);
         s->valid[s->idx] = v_ok;
         s->all_valid = s->all_valid && v_ok;
         s->all_invalid = s->all_invalid && !v_ok;
         if (v_ok) {
             s->buf[1 + s->idx] = v;
-            if (v < s->minimum) s->minimum = v;
-            if (v > s->maximum) s->maximum = v;
+            if (t_lt(t, v, s->minimum)) s->minimum = v;
+            if (t_lt(t, s->maximum, v)) s->maximum = v;
         }
         s->idx++;
         if (s->idx == BP_GROUP) {
             ok = st_flush(s, &w);
-            st_reset(s, tsize);
+            st_reset(s, t);
         }
     }
     if (ok) ok = st_flush(s, &w);
@@ -355,20 +399,20 @@ int oracle_bp_compress(const void *values, int tsize, const uint8_t *valid, uint
 
 /* ---------------------------------------------------------------- CPU decode */
 
-static int64_t load_t(const uint8_t *p, int tsize) {
-    if (tsize == 4) {
-        int32_t x;
-        memcpy(&x, p, 4);
-        return x;
-    }
-    int64_t x;
-    memcpy(&x, p, 8);
+static uint64_t load_t(const uint8_t *p, bp_t t) {
+    uint64_t x = 0;
+    memcpy(&x, p, (size_t)t.tsize);
     return x;
 }
 
-/* Sequential scan of the segments (LoadNextGroup + BitpackingScanPartial). */
+/* Sequential scan of the segments (LoadNextGroup + BitpackingScanPartial, :585-868): every
+ * value in T's arithmetic (mod 2^bits), written as T. */
 int oracle_bp_decode(const uint8_t *bytes, const uint64_t *seg_off, const uint64_t *seg_count, uint32_t n_segs,
-                     int tsize, void *out_values) {
+                     int ttype, void *out_values) {
+    if (!bp_ttype_ok(ttype)) return -1;
+    const bp_t t = bp_type(ttype);
+    const uint64_t ts = (uint64_t)t.tsize;
+    uint8_t *outb = (uint8_t *)out_values;
     uint64_t row = 0;
     for (uint32_t sg = 0; sg < n_segs; sg++) {
         const uint8_t *base = bytes + seg_off[sg];
@@ -381,37 +425,38 @@ int oracle_bp_decode(const uint8_t *bytes, const uint64_t *seg_off, const uint64
             const int mode = (int)(enc >> 24);
             const uint8_t *g = base + (enc & 0x00ffffff);
             const uint64_t cnt = seg_count[sg] - done < BP_GROUP ? seg_count[sg] - done : BP_GROUP;
-            int64_t for_v = 0, c = 0, doff = 0;
+            uint64_t for_v = 0, c = 0, doff = 0;
             int w = 0;
             const uint8_t *packed = g;
             if (mode == BP_CONSTANT) {
-                c = load_t(g, tsize);
+                c = load_t(g, t);
             } else if (mode == BP_CONSTANT_DELTA) {
-                for_v = load_t(g, tsize);
-                c = load_t(g + tsize, tsize);
+                for_v = load_t(g, t);
+                c = load_t(g + ts, t);
             } else if (mode == BP_FOR || mode == BP_DELTA_FOR) {
-                for_v = load_t(g, tsize);
-                w = (int)(uint8_t)load_t(g + tsize, tsize);
-                packed = g + 2 * tsize;
+                for_v = load_t(g, t);
+                w = (int)(uint8_t)load_t(g + ts, t); /* the width is stored as a T */
+                packed = g + 2 * ts;
                 if (mode == BP_DELTA_FOR) {
-                    doff = load_t(packed, tsize);
-                    packed += tsize;
+                    doff = load_t(packed, t);
+                    packed += ts;
                 }
+                if (w > t.bits) return -1;
             } else {
                 return -1;
             }
-            uint64_t run = (uint64_t)doff;
+            uint64_t run = doff;
             for (uint64_t i = 0; i < cnt; i++) {
                 uint64_t v;
-                if (mode == BP_CONSTANT) v = (uint64_t)c;
-                else if (mode == BP_CONSTANT_DELTA) v = (uint64_t)c * i + (uint64_t)for_v;
-                else if (mode == BP_FOR) v = unpack_value(packed, i, w) + (uint64_t)for_v;
+                if (mode == BP_CONSTANT) v = c;
+                else if (mode == BP_CONSTANT_DELTA) v = c * i + for_v;
+                else if (mode == BP_FOR) v = unpack_value(packed, i, w) + for_v;
                 else {
-                    run += unpack_value(packed, i, w) + (uint64_t)for_v;
+                    run += unpack_value(packed, i, w) + for_v;
                     v = run;
                 }
-                if (tsize == 4) ((int32_t *)out_values)[row + i] = (int32_t)(uint32_t)v;
-                else ((int64_t *)out_values)[row + i] = (int64_t)v;
+                v &= t.mask;
+                memcpy(outb + (row + i) * ts, &v, (size_t)ts);
             }
             row += cnt;
         }

@@ -73,12 +73,13 @@ void oracle_build_bitvector(const ocol *c, uint64_t n_rows, int cmp, int64_t con
 uint64_t oracle_xor_hash(const int64_t *rowids, uint64_t n);
 
 /* DuckDB BITPACKING restatement (bitpacking_ref.c). mode: 1 AUTO, 2 CONSTANT, 3 CONSTANT_DELTA,
- * 4 DELTA_FOR, 5 FOR (BitpackingMode). compress: 0 ok, 1 not bitpackable, < 0 error. */
-int oracle_bp_compress(const void *values, int tsize, const uint8_t *valid, uint64_t n, int mode, uint64_t block_size,
+ * 4 DELTA_FOR, 5 FOR (BitpackingMode). ttype: the value's byte size (1, 2, 4, 8) | 0x100 when
+ * unsigned. compress: 0 ok, 1 not bitpackable, < 0 error. */
+int oracle_bp_compress(const void *values, int ttype, const uint8_t *valid, uint64_t n, int mode, uint64_t block_size,
                        uint8_t *out, uint64_t out_cap, uint64_t *seg_off, uint64_t *seg_size, uint64_t *seg_count,
                        uint32_t max_segs, uint32_t *n_segs);
 int oracle_bp_decode(const uint8_t *bytes, const uint64_t *seg_off, const uint64_t *seg_count, uint32_t n_segs,
-                     int tsize, void *out_values);
+                     int ttype, void *out_values);
 int oracle_bp_group_modes(const uint8_t *bytes, const uint64_t *seg_off, const uint64_t *seg_count, uint32_t n_segs,
                           uint8_t *modes, uint64_t cap);
 

@@ -229,12 +229,24 @@ class BitpackedColumn:
         return int(self.seg_count.sum())
 
 
+BP_DTYPES = tuple(np.dtype(d) for d in (np.int8, np.int16, np.int32, np.int64,
+                                           np.uint8, np.uint16, np.uint32, np.uint64))
+
+
+def bp_ttype(dtype) -> int:
+    """The restatement's value type code: byte size | 0x100 when unsigned."""
+    dt = np.dtype(dtype)
+    assert dt in BP_DTYPES, dt
+    return dt.itemsize | (0x100 if dt.kind == "u" else 0)
+
+
 def bp_compress(values: np.ndarray, valid: Optional[np.ndarray] = None, mode: str = "auto",
                 block_size: int = DUCKDB_BLOCK_SIZE) -> Optional[BitpackedColumn]:
     """Compress like DuckDB's checkpoint would with force_bitpacking_mode=`mode` (None when
-    the column is not bitpackable, e.g. a group whose max - min overflows)."""
+    the column is not bitpackable, e.g. a group whose max - min overflows). `values` may be
+    any integral type DuckDB bit-packs (TINYINT … BIGINT, UTINYINT … UBIGINT)."""
     values = np.ascontiguousarray(values)
-    assert values.dtype in (np.int32, np.int64)
+    ttype = bp_ttype(values.dtype)
     n = len(values)
     vb = None if valid is None else np.ascontiguousarray(valid, dtype=np.uint8)
     cap = n * values.itemsize * 2 + (n // 2048 + 8) * 64 + 4 * block_size
@@ -244,7 +256,7 @@ def bp_compress(values: np.ndarray, valid: Optional[np.ndarray] = None, mode: st
     ss = np.zeros(max_segs, dtype=np.uint64)
     sc = np.zeros(max_segs, dtype=np.uint64)
     ns = C.c_uint32()
-    rc = lib().oracle_bp_compress(values.ctypes.data, values.itemsize, vb.ctypes.data if vb is not None else None, n,
+    rc = lib().oracle_bp_compress(values.ctypes.data, ttype, vb.ctypes.data if vb is not None else None, n,
                                   BP_MODES[mode], block_size, out.ctypes.data, cap, so.ctypes.data, ss.ctypes.data,
                                   sc.ctypes.data, max_segs, C.byref(ns))
     if rc == 1:
@@ -258,7 +270,7 @@ def bp_compress(values: np.ndarray, valid: Optional[np.ndarray] = None, mode: st
 def bp_decode(col: BitpackedColumn) -> np.ndarray:
     out = np.zeros(max(col.n_rows, 1), dtype=col.dtype)
     rc = lib().oracle_bp_decode(col.data.ctypes.data, col.seg_off.ctypes.data, col.seg_count.ctypes.data,
-                                len(col.seg_off), np.dtype(col.dtype).itemsize, out.ctypes.data)
+                                len(col.seg_off), bp_ttype(col.dtype), out.ctypes.data)
     assert rc == 0
     return out[:col.n_rows]
 

@@ -17,7 +17,7 @@ BITPACKING segments belong to:
       struct_of_fixed_array.a  INTEGER[3]    as fixed_int_array
       list_of_fixed_int_array  INTEGER[3][]  rows [min,max,min], [max,min,max], NULL  (its list child)
       fixed_array_of_int_list  INTEGER[][3]  rows [[],L,[]], [L,[],L], NULL with L = [42,999,NULL,NULL,-42]
-                                             (the list offsets column: UBIGINT running ends)
+                                             (the list offsets column: running ends, packed as uint64_t)
     A NULL array keeps its child slots; they are NULL (their stored bytes are whatever the
     compressor put there and are not compared).
 
@@ -102,7 +102,8 @@ EXPECTED = {
                                                  "test_all_types.cpp:228-235"),
     "all_types.list_of_fixed_int_array (list child)": ("int32", [N, 2, 3, 4, 5, 6, N, 2, 3, 4, 5, 6, N, 2, 3, 4, 5, 6],
                                                        "test_all_types.cpp:270-276"),
-    "all_types.fixed_array_of_int_list (list offsets)": ("int64", L_ENDS, "test_all_types.cpp:263-268, 99-104"),
+    # LIST offsets are bit-packed as uint64_t (bitpacking.cpp:976-977)
+    "all_types.fixed_array_of_int_list (list offsets)": ("uint64", L_ENDS, "test_all_types.cpp:263-268, 99-104"),
 }
 
 

@@ -219,7 +219,7 @@ def test_gpu_reads_duckdb_written_segment(ctx, s):
     got = t.download_column(0)
     assert np.array_equal(got[valid], values[valid])
     assert np.array_equal(got, O.bp_decode(col))  # NULL slots: the stored filler, as the oracle reads it
-    oc = O.Column(values, vw)
+    oc = O.Column(values.astype(np.int64) if values.dtype.kind == "u" else values, vw)  # UBIGINT offsets < 2^63
     lo, hi = int(values[valid].min()), int(values[valid].max())
     mid = int(np.median(values[valid]))
     for cmp, k in (("=", mid), ("!=", mid), ("<", mid), (">=", mid), ("<=", lo), (">", hi - 1), ("<", lo)):
@@ -237,4 +237,146 @@ def test_gpu_reads_duckdb_written_segment(ctx, s):
         total, cnt = t.sum_product(0, 1, fs, gather_b=True)
         assert t.last_sum_packed()
         assert total == int(values[keep].sum()) and cnt == int(keep.sum())
+    t.close()
+
+
+# ---------------------------------------------------------------- every integral type
+
+from test_oracle_bitpacking import (FORCED, INT_DTYPES, bitwidth_tables, filter_pushdown_column,  # noqa: E402
+                                    typed_case)
+
+
+def packed_table(ctx, c, dtype, n, valid=None, row_base=0):
+    t = CubitTable(ctx, n, row_base=row_base)
+    vw = None if valid is None else validity_from_mask(valid)
+    t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, dtype, validity=vw)
+    return t, vw
+
+
+@pytest.mark.parametrize("mode", ["auto"] + FORCED)
+@pytest.mark.parametrize("dtype", INT_DTYPES)
+def test_every_type_unpacks_and_filters(ctx, dtype, mode):
+    """Segments of every integral T (INT8 … UBIGINT; header fields of T's size, packed runs off
+    the 4-byte alignment for 1- and 2-byte T, T's wrap-around arithmetic in descending
+    DELTA_FOR / CONSTANT_DELTA groups) unpack into the INT32 / INT64 column to the oracle's
+    values, and the filter straight from the segments equals the oracle's scan of them, for
+    every comparison. UBIGINT values of 2^63 and more are refused loudly."""
+    below = np.dtype(dtype) == np.uint64
+    v, valid, c = typed_case(dtype, mode, below_2_63=below)
+    n = len(v)
+    t, vw = packed_table(ctx, c, dtype, n, valid, row_base=7)
+    got = t.download_column(0)
+    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else np.int64)
+    assert np.array_equal(got[valid], v[valid].astype(np.int64)), (np.dtype(dtype).name, mode)
+    wide = v.astype(np.int64)
+    oc = O.Column(wide, vw)
+    rng = np.random.default_rng(11)
+    picks = [int(x) for x in rng.choice(wide[valid], 4)] + [int(wide[valid].min()), int(wide[valid].max())]
+    for i, k in enumerate(picks):
+        cmp = ["=", "!=", "<", "<=", ">", ">="][i % 6]
+        fs = F.TableFilterSet({0: F.ConstantFilter(cmp, k)})
+        ref = O.table_scan([oc], F.serialize(fs), n, row_base=7)
+        t.use_packed_filter(True)
+        assert np.array_equal(t.scan(fs), ref), (np.dtype(dtype).name, mode, cmp, k)
+        assert t.last_packed() in (0, 1)
+        t.use_packed_filter(False)
+        assert np.array_equal(t.scan(fs), ref), (np.dtype(dtype).name, mode, cmp, k)
+    t.close()
+    if below:
+        v2, valid2, c2 = typed_case(dtype, mode)  # the full UBIGINT range
+        if (v2[valid2] >= np.uint64(2 ** 63)).any():
+            t2 = CubitTable(ctx, len(v2))
+            with pytest.raises(Exception, match="2\\^63"):
+                t2.add_bitpacked_column(0, c2.data, c2.seg_off, c2.seg_count, dtype,
+                                        validity=validity_from_mask(valid2))
+            t2.close()
+
+
+@pytest.mark.parametrize("mode", FORCED)
+@pytest.mark.parametrize("bits", [8, 16, 32, 64])
+def test_bitwidths_reference_case_on_gpu(ctx, bits, mode):
+    """bitpacking_bitwidths.test_slow through K5: each table's unpacked column has the
+    reference's distinct-value counts (bits or bits - 1 values, 2,048 rows each), and an
+    equality scan straight from the segments finds each value's 2,048 rows. UBIGINT's 2^63 is
+    beyond an INT64 column: that table is refused."""
+    for name, v in bitwidth_tables(bits).items():
+        c = O.bp_compress(v, None, mode)
+        t = CubitTable(ctx, len(v))
+        if v.dtype == np.uint64 and int(v.max()) >= 2 ** 63:
+            with pytest.raises(Exception, match="2\\^63"):
+                t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, v.dtype)
+            t.close()
+            continue
+        t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, v.dtype)
+        got = t.download_column(0)
+        assert np.array_equal(got, v.astype(np.int64)), (name, mode)
+        vals, counts = np.unique(got, return_counts=True)
+        assert len(vals) == (bits - 1 if name == "test_signed_pos" else bits) and set(counts.tolist()) == {2048}
+        t.use_packed_filter(True)
+        for k in (int(vals[0]), int(vals[-1])):
+            rows = t.scan(F.TableFilterSet({0: F.ConstantFilter("=", k)}))
+            assert len(rows) == 2048 and np.all(got[rows] == k), (name, mode, k)
+        t.close()
+
+
+@pytest.mark.parametrize("mode", FORCED)
+@pytest.mark.parametrize("dtype", INT_DTYPES + [np.bool_])
+def test_nullpack_reference_case_on_gpu(ctx, dtype, mode):
+    """bitpacking_bitwidths.test_slow:101-117 through K5: AVG of the unpacked column = 0.5."""
+    dt = np.int8 if dtype is np.bool_ else dtype
+    v = ((np.arange(12000) // 3000) % 2).astype(dt)
+    c = O.bp_compress(v, None, mode)
+    t = CubitTable(ctx, len(v))
+    t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, dt)
+    assert t.download_column(0).mean() == 0.5
+    t.close()
+
+
+@pytest.mark.parametrize("mode", FORCED)
+def test_nulls_reference_case_on_gpu(ctx, mode):
+    """bitpacking_nulls.test through K5: sum 70,694,000, min 0, max 9,999 over the valid rows —
+    the sum from the fused sum-product reading the column straight from its segments."""
+    i = np.arange(10000, dtype=np.int64)
+    v = np.concatenate([np.full(10000, 1337, np.int64), i, i // 2])
+    valid = np.tile(i % 5 != 0, 3)
+    c = O.bp_compress(v, valid.astype(np.uint8), mode)
+    n = len(v)
+    t, _ = packed_table(ctx, c, np.int64, n, valid)
+    got = t.download_column(0)[valid]
+    assert (int(got.min()), int(got.max())) == (0, 9999)
+    t.add_column(1, np.ones(n, np.int64))
+    t.add_column(2, np.zeros(n, np.int32))
+    t.build_index(2, L.INDEX_RANGE)
+    total, cnt = t.sum_product(0, 1, F.TableFilterSet({2: F.ConstantFilter("=", 0)}), gather_b=True)
+    assert (total, cnt) == (70694000, n)  # cnt: the rows the filter passes (NULL a adds nothing)
+    t.close()
+
+
+def test_delta_full_range_reference_case_on_gpu(ctx):
+    """bitpacking_delta.test_slow's UBIGINT column (0 and 2^64 - 1) is refused by K5 with a
+    message naming the bound, not read back wrong."""
+    v = np.where(np.arange(100_000) % 2 == 0, np.uint64(0), np.uint64(2 ** 64 - 1)).astype(np.uint64)
+    c = O.bp_compress(v, None, "for")
+    t = CubitTable(ctx, len(v))
+    with pytest.raises(Exception, match="2\\^63"):
+        t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, np.uint64)
+    t.close()
+
+
+@pytest.mark.parametrize("mode", ["auto"] + FORCED)
+def test_filter_pushdown_reference_case_on_gpu(ctx, mode):
+    """bitpacking_filter_pushdown.test through K5: WHERE col = 1337 straight from the segments →
+    SUM 13371337, MIN = MAX = 1337, COUNT 10001 (col read back by the probe); WHERE id = 5000 on
+    the other column → col 5000."""
+    col, ids = filter_pushdown_column()
+    c = O.bp_compress(col, None, mode)
+    n = len(col)
+    t, _ = packed_table(ctx, c, np.int32, n)
+    t.add_column(1, ids)
+    t.use_packed_filter(True)
+    rows = t.scan(F.TableFilterSet({0: F.ConstantFilter("=", 1337)}))
+    vals = probe_all(ctx, t, 0, n)[rows]
+    assert (int(vals.sum()), int(vals.min()), int(vals.max()), len(vals)) == (13371337, 1337, 1337, 10001)
+    rows = t.scan(F.TableFilterSet({1: F.ConstantFilter("=", 5000)}))
+    assert probe_all(ctx, t, 0, n)[rows].tolist() == [5000]
     t.close()

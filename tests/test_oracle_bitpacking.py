@@ -135,7 +135,7 @@ def test_reference_segments_cover_three_modes():
         col, _, _ = reference_segment(s)
         modes |= set(O.bp_group_modes(col))
     assert modes == {"for", "delta_for", "constant_delta"}
-    assert {s["dtype"] for s in REF_SEGMENTS} == {"int32", "int64"}
+    assert {s["dtype"] for s in REF_SEGMENTS} == {"int32", "int64", "uint64"}
 
 
 @pytest.mark.parametrize("s", REF_SEGMENTS, ids=[s["name"] for s in REF_SEGMENTS])
@@ -161,3 +161,168 @@ def test_compressor_writes_duckdbs_bytes(s):
     tsize = np.dtype(s["dtype"]).itemsize
     assert len(mine) == len(ref)
     assert packed_tail_masked(mine, tsize, s["count"]) == packed_tail_masked(ref, tsize, s["count"])
+
+
+# ---------------------------------------------------------------- every integral type
+
+INT_DTYPES = [np.int8, np.int16, np.int32, np.int64, np.uint8, np.uint16, np.uint32, np.uint64]
+FORCED = ["delta_for", "for", "constant_delta", "constant"]
+
+
+def bitwidth_tables(bits):
+    """The three tables of test/sql/storage/compression/bitpacking/bitpacking_bitwidths.test_slow
+    (:19, :43, :67) for one type size: 2**(i//2048) as UINT<bits> and -(2**(i//2048)) as
+    INT<bits> over bits·2048 rows, 2**(i//2048) as INT<bits> over (bits-1)·2048 rows."""
+    k = np.arange(bits * 2048) // 2048
+    unsigned = np.array([1 << int(x) for x in k], dtype=object).astype(f"uint{bits}")
+    neg = np.array([-(1 << int(x)) for x in k], dtype=object).astype(f"int{bits}")
+    pos = np.array([1 << int(x) for x in k[: (bits - 1) * 2048]], dtype=object).astype(f"int{bits}")
+    return {"test_unsigned": unsigned, "test_signed_neg": neg, "test_signed_pos": pos}
+
+
+@pytest.mark.parametrize("mode", FORCED)
+@pytest.mark.parametrize("bits", [8, 16, 32, 64])
+def test_bitwidths_reference_case(bits, mode):
+    """bitpacking_bitwidths.test_slow under each forced mode: every table reads back bits (or
+    bits - 1) distinct values, 2,048 rows each, each distinct value twice the one before
+    (`i // lag(i)` = 2). The groups line up with the 2,048-row runs, so each is one value: a
+    forced CONSTANT / CONSTANT_DELTA writes it as such, FOR and DELTA_FOR as FOR of width 0
+    (DELTA_FOR's delta width 0 is not below the value width 0, bitpacking.cpp:258-261)."""
+    for name, v in bitwidth_tables(bits).items():
+        c = O.bp_compress(v, None, mode)
+        assert c is not None, (name, mode)
+        d = O.bp_decode(c)
+        assert d.dtype == v.dtype and np.array_equal(d, v), (name, mode)
+        vals, counts = np.unique(d, return_counts=True)
+        assert len(vals) == (bits - 1 if name == "test_signed_pos" else bits)
+        assert set(counts.tolist()) == {2048}
+        if name != "test_signed_neg":
+            assert all(int(b) // int(a) == 2 for a, b in zip(vals[:-1], vals[1:]))
+        # per group: a forced CONSTANT / CONSTANT_DELTA as such — but an unsigned value above T_S's
+        # maximum never delta-encodes (bitpacking.cpp:155-160), so that group falls to FOR
+        firsts = v[::2048]
+        above = (firsts.astype(np.uint64) > np.uint64(2 ** (bits - 1) - 1)) if v.dtype.kind == "u" else \
+            np.zeros(len(firsts), bool)
+        want = [{"constant": "constant", "constant_delta": "for" if a else "constant_delta"}.get(mode, "for")
+                for a in above]
+        assert O.bp_group_modes(c) == want, (name, mode)
+
+
+@pytest.mark.parametrize("mode", FORCED)
+@pytest.mark.parametrize("dtype", INT_DTYPES + [np.bool_])
+def test_nullpack_reference_case(dtype, mode):
+    """bitpacking_bitwidths.test_slow:101-117: CAST((i//3000)%2 AS <integral type> | BOOL) over
+    12,000 rows → AVG 0.5 (BOOL is packed as int8_t, bitpacking.cpp:955-957)."""
+    v = ((np.arange(12000) // 3000) % 2).astype(np.int8 if dtype is np.bool_ else dtype)
+    c = O.bp_compress(v, None, mode)
+    assert c is not None
+    assert O.bp_decode(c).astype(np.int64).mean() == 0.5
+
+
+@pytest.mark.parametrize("mode", FORCED)
+def test_nulls_reference_case(mode):
+    """bitpacking_nulls.test: a BIGINT column of three 10,000-row inserts (1337, i, i//2) with
+    every fifth row NULL → sum 70,694,000, min 0, max 9,999, under each forced mode."""
+    i = np.arange(10000, dtype=np.int64)
+    v = np.concatenate([np.full(10000, 1337, np.int64), i, i // 2])
+    valid = np.tile(i % 5 != 0, 3)
+    c = O.bp_compress(v, valid.astype(np.uint8), mode)
+    assert c is not None
+    d = O.bp_decode(c)[valid]
+    assert (int(d.sum()), int(d.min()), int(d.max())) == (70694000, 0, 9999)
+
+
+@pytest.mark.parametrize("mode", FORCED)
+def test_delta_full_range_reference_case(mode):
+    """bitpacking_delta.test_slow: UBIGINT alternating 0 and 18446744073709551615 over 1 M rows
+    stays BITPACKING under every forced mode (no delta above T_S's maximum: FOR of width 64,
+    bitpacking.cpp:155-160) and reads back 500,000 of each."""
+    v = np.where(np.arange(1_000_000) % 2 == 0, np.uint64(0), np.uint64(2 ** 64 - 1)).astype(np.uint64)
+    c = O.bp_compress(v, None, mode)
+    assert c is not None
+    d = O.bp_decode(c)
+    vals, counts = np.unique(d, return_counts=True)
+    assert vals.tolist() == [0, 2 ** 64 - 1] and counts.tolist() == [500000, 500000]
+    assert set(O.bp_group_modes(c)) == {"for"}
+
+
+def filter_pushdown_column():
+    """bitpacking_filter_pushdown.test:24-30: INTEGER col = range(10000), 1337 × 10,000,
+    range(30000, 40000); id = the row's source integer."""
+    col = np.concatenate([np.arange(10000), np.full(10000, 1337), np.arange(30000, 40000)]).astype(np.int32)
+    ids = np.concatenate([np.arange(10000), np.arange(20000, 30000), np.arange(30000, 40000)]).astype(np.int64)
+    return col, ids
+
+
+@pytest.mark.parametrize("mode", ["auto"] + FORCED)
+def test_filter_pushdown_reference_case(mode):
+    """bitpacking_filter_pushdown.test: WHERE col = 1337 → SUM 13371337, MIN = MAX = 1337,
+    COUNT 10001; WHERE id = 5000 → col 5000, one row; under AUTO and each forced mode."""
+    from cubit_amd import filters as F
+
+    col, ids = filter_pushdown_column()
+    c = O.bp_compress(col, None, mode)
+    assert c is not None
+    d = O.bp_decode(c)
+    assert np.array_equal(d, col)
+    fs = F.TableFilterSet({0: F.ConstantFilter("=", 1337)})
+    rows = O.table_scan([O.Column(d)], F.serialize(fs), len(d))
+    got = d[rows]
+    assert (int(got.sum()), int(got.min()), int(got.max()), len(got)) == (13371337, 1337, 1337, 10001)
+    fs = F.TableFilterSet({1: F.ConstantFilter("=", 5000)})
+    rows = O.table_scan([O.Column(d), O.Column(ids)], F.serialize(fs), len(d))
+    assert d[rows].tolist() == [5000]
+
+
+def typed_case(dtype, mode, n=2048 * 7 + 1001, below_2_63=False):
+    """Values of one integral type — the type's extremes, a run of one value, a constant step, a
+    descending sorted stretch (negative deltas: a DELTA_FOR frame below zero, T's wrap-around in
+    the unsigned types), values next to the minimum, NULLs, an all-NULL group where the mode
+    allows one, a partial last group — and their segments under force_bitpacking_mode `mode`.
+    below_2_63: UBIGINT values stay below 2^63 (an INT64 column can hold them)."""
+    rng = np.random.default_rng(abs(hash((np.dtype(dtype).name, mode, below_2_63))) % 2 ** 32)
+    info = np.iinfo(dtype)
+    # random groups over half the type's span (a signed group whose max - min overflows T is
+    # not bitpackable at all: the reference picks another compression), the unsigned ones over
+    # all of it (width 64 for UBIGINT)
+    lo, hi = (info.min // 2, info.max // 2) if info.min < 0 else (info.min, info.max)
+    if below_2_63:
+        hi = 2 ** 63 - 1
+    v = rng.integers(lo, hi, n, dtype=dtype, endpoint=True)
+    v[:2048] = hi                                                             # one value
+    step = 3 if info.bits >= 16 else 0  # 2,048 distinct 8-bit values do not exist
+    v[2048:4096] = (np.arange(2048) * step + 1).astype(dtype)                 # constant delta
+    v[4096:6144] = np.sort(rng.integers(lo, min(hi, info.max // 2), 2048, dtype=dtype))[::-1]  # descending
+    v[6144:8192] = info.min + rng.integers(0, 7, 2048).astype(dtype)         # next to the minimum
+    valid = rng.random(n) > 0.05
+    valid[:6144] = True                                                       # the delta groups need all-valid
+    if mode in ("auto", "constant"):
+        # an all-NULL group is CONSTANT; under the other forced modes it is not bitpackable at
+        # all (max - min of an empty group overflows T, bitpacking.cpp:149-151, 231-234)
+        valid[10240:12288] = False
+    c = O.bp_compress(v, valid.astype(np.uint8), mode)
+    assert c is not None, (np.dtype(dtype).name, mode)
+    return v, valid, c
+
+
+@pytest.mark.parametrize("mode", ["auto"] + FORCED)
+@pytest.mark.parametrize("dtype", INT_DTYPES)
+def test_every_type_round_trips(dtype, mode):
+    """Every integral type DuckDB bit-packs through the writer and back (typed_case)."""
+    v, valid, c = typed_case(dtype, mode)
+    d = O.bp_decode(c)
+    assert d.dtype == np.dtype(dtype)
+    assert np.array_equal(d[valid], v[valid])
+    if mode == "auto":
+        assert {"constant", "for"} <= set(O.bp_group_modes(c))
+
+
+@pytest.mark.parametrize("mode", ["for", "delta_for", "constant_delta"])
+def test_all_null_group_is_not_bitpackable_under_forced_modes(mode):
+    """A forced FOR / DELTA_FOR / CONSTANT_DELTA cannot write an all-NULL group (its max - min
+    overflows T and it has no deltas): Flush fails and the reference picks another compression."""
+    v = np.zeros(4096, np.int32)
+    valid = np.ones(4096, np.uint8)
+    valid[2048:] = 0
+    assert O.bp_compress(v, valid, mode) is None
+    assert O.bp_compress(v, valid, "auto") is not None
