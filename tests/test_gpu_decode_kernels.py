@@ -298,3 +298,33 @@ def test_single_index_leaf_decodes_from_tile_counts(ctx):
     t.append({0: extra})
     check(np.concatenate([a, extra]))  # dense tiles at the end: the stage rounds
     t.close()
+
+
+def test_row_ids_past_2_32(ctx):
+    """A partition of 2^32 + 4,097 rows (32,769 tiles, two 537 MB leaves): row ids and tile
+    offsets past 32 bits, under every decode kernel (the look-back only where the policy lets
+    it run), in tile-run and ordered output, bit-exact against the oracle — the largest
+    partition one SF300 GPU holds is 1.8 G rows; this is 2.4× that."""
+    n = (1 << 32) + 4097
+    rng = np.random.default_rng(32)
+    nw = (n + 63) // 64
+    pw = padded_words(n)
+    host = [rand_words(rng, nw, 8), rand_words(rng, nw, 1)]
+    for w in host:
+        w[-1] &= np.uint64((1 << (n & 63)) - 1)
+    host[0][-TILE_WORDS:] |= rand_words(rng, TILE_WORDS, 2)  # a denser last tile, ending mid-word
+    host[0][-1] &= np.uint64((1 << (n & 63)) - 1)
+    dleaves = [ctx.upload(np.concatenate([w, np.zeros(pw - nw, dtype=np.uint64)])) for w in host]
+    base = 3
+    ref, _ = O.bitmap_eval(host, [0, 1, L.OP_AND], n, base)
+    assert ref[-1] >= 1 << 32
+    out = ctx.alloc(len(ref) * 8 + 1024)
+    cnt = ctx.alloc(16)
+    for kernel in (L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_LOOKBACK, L.DECODE_AUTO):
+        ctx.set_decode_kernel(kernel)
+        for ordered in (False, True):
+            got = run_program(ctx, dleaves, 2, 0, [0, 1, L.OP_AND], n, base, out, cnt, ordered)
+            assert np.array_equal(got, ref), (kernel, ordered)
+    ctx.set_decode_kernel(L.DECODE_AUTO)
+    for d in dleaves + [out, cnt]:
+        d.free()
