@@ -1164,9 +1164,10 @@ __device__ uint64_t lookback_recount(const EvalArgs& a, uint32_t b, int t, uint3
 // loads issued before the LDS decode; a decoupled look-back (aggregate, then inclusive-prefix flags,
 // walks that stop at the nearest prefix) — slower at every size measured, 573 to 4,578 tiles (at
 // 4,578 the sum over every earlier flag costs 68.5 µs, the decoupled walk 91 µs).
-template <int K, int FORM, int STAGE, int WPC, int SAUX = 16, int DBG = 0>
-__global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback(EvalArgs a, uint64_t* __restrict__ dir) {
-    constexpr int THREADS = 512, PAIRS = 2, NW = 2 * PAIRS, NWAVES = THREADS / 64;
+template <int K, int FORM, int STAGE, int WPC, int SAUX = 16, int DBG = 0, int THREADS = 512>
+__global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_lookback(EvalArgs a,
+                                                                                    uint64_t* __restrict__ dir) {
+    constexpr int PAIRS = 2, NW = 2 * PAIRS, NWAVES = THREADS / 64;
     constexpr uint64_t TILE_WORDS = (uint64_t)THREADS * NW;
     constexpr uint64_t kCntMask = (1ull << kFlagCntBits) - 1;
     __shared__ uint32_t s_wave_tot[NWAVES];

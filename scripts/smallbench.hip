@@ -226,7 +226,17 @@ struct Variant {
     std::string name;
     std::function<void(EvalArgs&, hipStream_t)> launch;
     bool check;
+    uint32_t tmul = 1;  // directory entries per 131,072-row tile (2: 65,536-row tiles)
 };
+
+// the look-back decode over 65,536-row tiles: 256-thread workgroups, twice the grid, a 4,096-id
+// stage, up to 6 workgroups per CU
+template <int K>
+void lookback_t256(EvalArgs& a, uint64_t* dir, hipStream_t st) {
+    a.num_tiles = (uint32_t)((a.n_words + 1023) / 1024);
+    hipLaunchKernelGGL((eval_decode_lookback<K, FORM_CONJ, 4096, 6, 16, 0, 256>), dim3(a.num_tiles), dim3(256), 0, st,
+                       a, dir);
+}
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 50;
@@ -280,7 +290,7 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&ids_ord, cap * 8));
         CK(hipMalloc(&dst_off, (uint64_t)tiles * 8 + 64));
         CK(hipMalloc(&cnt, 16));
-        CK(hipMalloc(&dir, 2 * (uint64_t)tiles * 8 + 64));
+        CK(hipMalloc(&dir, 4 * (uint64_t)tiles * 8 + 64));
         CK(hipMalloc(&dir_ref, 2 * (uint64_t)tiles * 8 + 64));
         EvalArgs base{};
         for (int k = 0; k < c.k; ++k) base.prog.leaf[k] = leaf[k];
@@ -339,6 +349,12 @@ int main(int argc, char** argv) {
             add("DBG no flag loads, no ids", lookback_variant<1, 16, 10>, lookback_variant<4, 16, 10>, false);
             add("DBG no wait, no ids", lookback_variant<1, 16, 3>, lookback_variant<4, 16, 3>, false);
         }
+        if (2 * tiles <= kLookbackMaxTiles)
+            vs.push_back({"lookback 65,536-row tiles (grid " + std::to_string((W + 1023) / 1024) + ")",
+                          [&](EvalArgs& a, hipStream_t st) {
+                              a.epoch = ++epoch;
+                              (c.k == 4 ? lookback_t256<4> : lookback_t256<1>)(a, dir, st);
+                          }, true, 2});
         vs.push_back({"AUTO (library policy)", [&](EvalArgs& a, hipStream_t st) {
                           a.epoch = ++epoch;
                           CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 0, cus));
@@ -365,7 +381,8 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < vs.size(); ++i) {
             if (!vs[i].check) continue;
             EvalArgs a = base;
-            CK(hipMemsetAsync(dir, 0, 2 * (uint64_t)tiles * 8, s));
+            const uint32_t vt = tiles * vs[i].tmul;
+            CK(hipMemsetAsync(dir, 0, 2 * (uint64_t)vt * 8, s));
             CK(hipMemsetAsync(cnt, 0xff, 8, s));
             vs[i].launch(a, s);
             CK(hipStreamSynchronize(s));
@@ -373,12 +390,12 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(&got, cnt, 8, hipMemcpyDeviceToHost));
             std::vector<int64_t> h(std::min<uint64_t>(got, cap));
             CK(hipMemcpy(h.data(), ids, h.size() * 8, hipMemcpyDeviceToHost));
-            std::vector<uint64_t> d(2 * (uint64_t)tiles);
+            std::vector<uint64_t> d(2 * (uint64_t)vt);
             CK(hipMemcpy(d.data(), dir, d.size() * 8, hipMemcpyDeviceToHost));
             std::vector<int64_t> o;
             o.reserve(h.size());
             bool ok_dir = true;
-            for (uint32_t tt = 0; tt < tiles; ++tt) {
+            for (uint32_t tt = 0; tt < vt; ++tt) {
                 if (d[2 * tt] + d[2 * tt + 1] > h.size()) {
                     ok_dir = false;
                     break;
