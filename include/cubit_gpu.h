@@ -283,9 +283,9 @@ int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const ui
  * a constant comparison the index cannot answer (K0) then unpacks and compares in one pass over
  * the packed bytes (w/8 bytes per row — the reference's ColumnSegment::Scan →
  * BitpackingScanPartial → FilterSelection, column_segment.cpp:378-522) instead of reading the
- * plain column. Off by default: on MI355X it measured 0.93 ms vs K0's 0.46 ms for a 600 M-row
- * 12-bit date column (2.6x fewer bytes, but the unpack is instruction-bound at this occupancy;
- * DESIGN.md §3). Results are identical either way. Appends and merges drop the segments (the
+ * plain column. Off by default: on MI355X it measured 0.41–0.45 ms against K0's 0.43–0.44 ms
+ * for a 600 M-row 12-bit date column (2.6x fewer bytes, but the unpack is instruction-bound, so
+ * it does not win). Results are identical either way. Appends and merges drop the segments (the
  * plain column stays). cubit_table_last_packed: leaves the last scan built so. */
 int cubit_table_use_packed_filter(cubit_table *t, int on);
 int cubit_table_last_packed(cubit_table *t, uint32_t *n_leaves);
