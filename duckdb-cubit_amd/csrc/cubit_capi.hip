@@ -1221,7 +1221,65 @@ int copy_validity(cubit_table* t, Column& c, const uint64_t* validity, int on_de
     return CUBIT_OK;
 }
 
+int value_stats(cubit_table* t, const void* data, int type, const uint64_t* validity, uint64_t n,
+                std::vector<int64_t>& distinct, bool want_distinct, int64_t& vmin, int64_t& vmax, bool& any);
+
+// The INT32 / INT64 column type a type code's values are held as (INT8, INT16, UINT8, UINT16 →
+// INT32; UINT32, UINT64 → INT64), and the code's value size; false for an unknown code.
+bool storage_of(int type, int& col_type, uint64_t& src_size) {
+    switch (type) {
+    case CUBIT_TYPE_INT32: col_type = CUBIT_TYPE_INT32, src_size = 4; return true;
+    case CUBIT_TYPE_INT64: col_type = CUBIT_TYPE_INT64, src_size = 8; return true;
+    case CUBIT_TYPE_INT8: case CUBIT_TYPE_UINT8: col_type = CUBIT_TYPE_INT32, src_size = 1; return true;
+    case CUBIT_TYPE_INT16: case CUBIT_TYPE_UINT16: col_type = CUBIT_TYPE_INT32, src_size = 2; return true;
+    case CUBIT_TYPE_UINT32: col_type = CUBIT_TYPE_INT64, src_size = 4; return true;
+    case CUBIT_TYPE_UINT64: col_type = CUBIT_TYPE_INT64, src_size = 8; return true;
+    default: return false;
+    }
+}
+
+// A column of a narrower or unsigned type code: its values (host or device) widened on the
+// device into an owned INT32 / INT64 column; UINT64 values must stay below 2^63.
+int widen_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
+    int col_type = 0;
+    uint64_t ssz = 0;
+    storage_of(type, col_type, ssz);
+    const uint64_t esz = col_type == CUBIT_TYPE_INT32 ? 4 : 8;
+    c.type = col_type;
+    if (t->n_rows == 0) return CUBIT_OK;
+    hipStream_t s = t->ctx->stream;
+    DevBuf staged;
+    const void* src = data;
+    if (!on_device) {
+        if (hipMalloc(&staged.p, t->n_rows * ssz) != hipSuccess) return fail(CUBIT_ERR_OOM, "column staging failed");
+        HIP_CHECK(hipMemcpyAsync(staged.p, data, t->n_rows * ssz, hipMemcpyHostToDevice, s));
+        src = staged.p;
+    }
+    auto b = std::make_unique<DevBuf>();
+    if (hipMalloc(&b->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "column allocation failed");
+    HIP_CHECK(launch_widen(src, type, t->n_rows, b->p, s));
+    c.data = b->p;
+    c.cap_rows = t->n_rows;
+    c.owned.push_back(std::move(b));
+    if (validity) {
+        if (int rc = copy_validity(t, c, validity, on_device)) return rc;
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (type == CUBIT_TYPE_UINT64) {
+        std::vector<int64_t> unused;
+        int64_t vmin = 0, vmax = 0;
+        bool any = false;
+        if (int rc = value_stats(t, c.data, CUBIT_TYPE_INT64, c.validity, t->n_rows, unused, false, vmin, vmax, any))
+            return rc;
+        if (any && vmin < 0)
+            return fail(CUBIT_ERR_UNSUPPORTED, "UINT64 column holds a value of 2^63 or more (an INT64 column cannot hold it)");
+    }
+    return CUBIT_OK;
+}
+
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return widen_column(t, c, type, data, validity, on_device);
     const uint64_t esz = type == CUBIT_TYPE_INT32 ? 4 : 8;
     if (t->n_rows == 0) {  // empty partition: nothing to copy
         c.type = type;
@@ -1353,7 +1411,9 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
                                       int on_device) {
     if (!t || !data) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(t->ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    int col_type = 0;
+    uint64_t src_size = 0;
+    if (!storage_of(type, col_type, src_size)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (int rc = set_device(t->ctx)) return rc;
     Column c;

@@ -185,6 +185,8 @@ hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
                                     uint64_t* out, hipStream_t stream, int simple_width = 0);
 // out[i] = (int32)(in[i] - offset), i < min(*d_count, max_n) (transfer compaction of a column)
+// a narrower / unsigned column (CUBIT_TYPE_INT8 … UINT64) widened to its INT32 / INT64 storage
+hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hipStream_t stream);
 hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,
                              hipStream_t stream);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "../../include/cubit_gpu.h"
 #include "cubit_internal.hpp"
 
 namespace cubit {
@@ -2438,6 +2439,18 @@ __global__ __launch_bounds__(256) void narrow_i32_kernel(const int64_t* __restri
     }
 }
 
+// out[i] = in[i] widened: a column registered with a narrower or unsigned type code
+// (cubit_table_add_column) is held as INT32 / INT64 values. 4 values per thread per step.
+template <typename S, typename D>
+__global__ __launch_bounds__(256) void widen_kernel(const S* __restrict__ in, uint64_t n, D* __restrict__ out) {
+    const uint64_t stride = 4ull * gridDim.x * blockDim.x;
+    for (uint64_t i = 4ull * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += stride) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i + j < n) out[i + j] = (D)in[i + j];
+    }
+}
+
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -3011,6 +3024,40 @@ hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_
     if (max_n == 0) return hipSuccess;
     hipLaunchKernelGGL(narrow_i32_kernel, dim3(grid_for((max_n + 1) / 2)), dim3(256), 0, stream, in, d_count, max_n,
                        offset, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid(grid_for((n + 3) / 4)), block(256);
+    switch (src_type) {
+    case CUBIT_TYPE_INT8:
+        hipLaunchKernelGGL((widen_kernel<int8_t, int32_t>), grid, block, 0, stream, static_cast<const int8_t*>(in), n,
+                           static_cast<int32_t*>(out));
+        break;
+    case CUBIT_TYPE_INT16:
+        hipLaunchKernelGGL((widen_kernel<int16_t, int32_t>), grid, block, 0, stream, static_cast<const int16_t*>(in), n,
+                           static_cast<int32_t*>(out));
+        break;
+    case CUBIT_TYPE_UINT8:
+        hipLaunchKernelGGL((widen_kernel<uint8_t, int32_t>), grid, block, 0, stream, static_cast<const uint8_t*>(in), n,
+                           static_cast<int32_t*>(out));
+        break;
+    case CUBIT_TYPE_UINT16:
+        hipLaunchKernelGGL((widen_kernel<uint16_t, int32_t>), grid, block, 0, stream, static_cast<const uint16_t*>(in), n,
+                           static_cast<int32_t*>(out));
+        break;
+    case CUBIT_TYPE_UINT32:
+        hipLaunchKernelGGL((widen_kernel<uint32_t, int64_t>), grid, block, 0, stream, static_cast<const uint32_t*>(in), n,
+                           static_cast<int64_t*>(out));
+        break;
+    case CUBIT_TYPE_UINT64:  // the bits as they are; the caller checks every valid value is below 2^63
+        hipLaunchKernelGGL((widen_kernel<uint64_t, int64_t>), grid, block, 0, stream, static_cast<const uint64_t*>(in), n,
+                           static_cast<int64_t*>(out));
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

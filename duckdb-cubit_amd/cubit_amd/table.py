@@ -175,20 +175,19 @@ class CubitTable:
         self._keep = []
 
     def add_column(self, col: int, data: np.ndarray, validity: Optional[np.ndarray] = None) -> None:
+        """Register a column of any integral dtype: int32 / int64 as they are, the narrower and
+        unsigned ones widened by the library into an INT32 / INT64 column (uint64 below 2^63)."""
         data = np.ascontiguousarray(data)
-        if data.dtype == np.int32:
-            t = L.TYPE_INT32
-        elif data.dtype == np.int64:
-            t = L.TYPE_INT64
-        else:
+        if data.dtype.name not in L.SEGMENT_TYPES:
             raise TypeError(f"unsupported dtype {data.dtype}")
+        t = L.SEGMENT_TYPES[data.dtype.name]
         assert data.shape[0] == self.n_rows
         vptr = None
         if validity is not None:
             validity = np.ascontiguousarray(validity, dtype=np.uint64)
             vptr = validity.ctypes.data
         L.check(self.lib.cubit_table_add_column(self.handle, col, t, data.ctypes.data, vptr, 0))
-        self.types[col] = t
+        self.types[col] = self.column_data(col)[1]
 
     def add_bitpacked_column(self, col: int, data: np.ndarray, seg_offsets: np.ndarray, seg_rows: np.ndarray,
                              dtype, validity: Optional[np.ndarray] = None) -> None:

@@ -259,7 +259,12 @@ int cubit_table_column_data(cubit_table *t, int col, const void **data, int *typ
  * buffer must not change while registered unless the caller says so with
  * cubit_table_column_changed: the table caches per-zone statistics of the values (zonemaps,
  * column statistics, selectivity estimates) and would otherwise skip zones by stale bounds.
- * Index bitvectors are not rebuilt by it (rebuild with cubit_table_build_index). */
+ * Index bitvectors are not rebuilt by it (rebuild with cubit_table_build_index). `type` may be
+ * any CUBIT_TYPE_* code: an 8- / 16-bit or unsigned column is widened on the device into an
+ * owned INT32 / INT64 column (even from on_device data) — TINYINT … UINTEGER vectors as DuckDB
+ * holds them — and a UINT64 column with a valid value of 2^63 or
+ * more is refused (CUBIT_ERR_UNSUPPORTED). Appends, updates and probes then use the INT32 /
+ * INT64 values (cubit_table_column_data reports the type held). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
 /* The values of a caller-owned column changed: drop what the table derived from them. */

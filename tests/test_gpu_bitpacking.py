@@ -380,3 +380,46 @@ def test_filter_pushdown_reference_case_on_gpu(ctx, mode):
     rows = t.scan(F.TableFilterSet({1: F.ConstantFilter("=", 5000)}))
     assert probe_all(ctx, t, 0, n)[rows].tolist() == [5000]
     t.close()
+
+
+@pytest.mark.parametrize("dtype", INT_DTYPES + [np.bool_])
+def test_plain_columns_of_every_type(ctx, dtype):
+    """cubit_table_add_column with a narrower or unsigned type code (TINYINT … UBIGINT vectors
+    as DuckDB holds them) widens the values on the device into an INT32 / INT64 column; index
+    scans, unindexed comparisons and the probe then equal numpy on the widened values. UBIGINT
+    values of 2^63 and more are refused."""
+    rng = np.random.default_rng(abs(hash(np.dtype(dtype).name)) % 2 ** 32)
+    n = 300_007
+    if dtype is np.bool_:
+        v = rng.random(n) < 0.3
+    else:
+        info = np.iinfo(dtype)
+        hi = min(int(info.max), 2 ** 63 - 1)
+        v = rng.integers(info.min, hi, n, dtype=dtype, endpoint=True)
+        v[:1000] = info.min
+    wide = v.astype(np.int64)
+    valid = rng.random(n) > 0.1
+    t = CubitTable(ctx, n, row_base=9)
+    t.add_column(0, v, validity=validity_from_mask(valid))
+    got = t.download_column(0)
+    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else np.int64)
+    assert np.array_equal(got[valid], wide[valid])
+    assert np.array_equal(probe_all(ctx, t, 0, n, row_base=9)[valid], wide[valid])
+    k = int(np.median(wide[valid]))
+    for cmp, mask in (("<", wide < k), (">=", wide >= k), ("=", wide == int(wide[valid][0]))):
+        kk = int(wide[valid][0]) if cmp == "=" else k
+        fs = F.TableFilterSet({0: F.ConstantFilter(cmp, kk)})
+        ref = np.flatnonzero(mask & valid).astype(np.int64) + 9
+        assert np.array_equal(t.scan(fs), ref), (np.dtype(dtype).name, cmp)
+    if np.dtype(dtype).itemsize <= 2:
+        t.build_index(0, L.INDEX_EQUALITY)
+        fs = F.TableFilterSet({0: F.ConstantFilter("=", int(wide[valid][1]))})
+        ref = np.flatnonzero((wide == int(wide[valid][1])) & valid).astype(np.int64) + 9
+        assert np.array_equal(t.scan(fs), ref)
+    t.close()
+    if np.dtype(dtype) == np.uint64:
+        big = np.full(1000, 2 ** 63, np.uint64)
+        t2 = CubitTable(ctx, len(big))
+        with pytest.raises(Exception, match="2\\^63"):
+            t2.add_column(0, big)
+        t2.close()
