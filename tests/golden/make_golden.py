@@ -3,6 +3,7 @@ container, where /root/reference exists). The JSON it writes is data only: expec
 outputs quoted from the reference's answer files and tests, plus the fingerprints the
 survey measured by running the reference."""
 import json
+import re
 from pathlib import Path
 
 REF = Path("/root/reference")
@@ -117,9 +118,44 @@ def main():
         # TIMESTAMP rows NOW() and NOW() - 10 years; ts >= NOW() - 1 year -> COUNT(*) = 1
         "timestamp": {"count": 1},
     }
+    # test/sql/transactions/test_multi_version.test: rows 1, 2, 3; con1 updates, updates again,
+    # deletes and inserts inside one transaction, then commits; SUM(i) as each connection sees
+    # it after each statement. The sums are read from the file (the `query R conX` blocks, in
+    # order) and must equal the steps below.
+    mv_src = REF / "test/sql/transactions/test_multi_version.test"
+    mv_sums = [(c, float(v)) for c, v in re.findall(r"query R (con\d)\nSELECT SUM\(i\) FROM integers\n----\n([0-9.]+)",
+                                                    mv_src.read_text())]
+    mv = {
+        "source": "test/sql/transactions/test_multi_version.test:9-99",
+        "rows": [1, 2, 3],
+        "steps": [
+            {"do": "start", "expect": {"con1": 6, "con2": 6}},
+            {"do": "con1 BEGIN; UPDATE integers SET i=5 WHERE i=1", "expect": {"con1": 10, "con2": 6}},
+            {"do": "con1 UPDATE integers SET i=10 WHERE i=5", "expect": {"con1": 15, "con2": 6}},
+            {"do": "con1 DELETE FROM integers WHERE i>5", "expect": {"con1": 5, "con2": 6}},
+            {"do": "con1 INSERT INTO integers VALUES (1), (2)", "expect": {"con1": 8, "con2": 6}},
+            {"do": "con1 COMMIT", "expect": {"con2": 8}},
+        ],
+    }
+    assert mv_sums == [(c, float(v)) for st in mv["steps"] for c, v in st["expect"].items()], mv_sums
+    # test/sql/parallelism/interquery/concurrent_reads_while_updating.test_slow: integers =
+    # range(10000); thread 0 runs UPDATE integers SET i=i+1 20 times while 19 threads run
+    # SELECT COUNT(*)==10000, SUM(i) BETWEEN 49995000 AND 50195000 200 times each; afterwards
+    # COUNT(*), SUM(i) = 10000, 50195000.
+    cr_src = (REF / "test/sql/parallelism/interquery/concurrent_reads_while_updating.test_slow").read_text()
+    for needle in ("range(10000)", "concurrentloop threadid 0 20", "loop i 0 20", "UPDATE integers SET i=i+1",
+                   "loop i 0 200", "SUM(i)>= 49995000 AND SUM(i) <= 50195000", "10000\t50195000"):
+        assert needle in cr_src, needle
+    cr = {
+        "source": "test/sql/parallelism/interquery/concurrent_reads_while_updating.test_slow",
+        "rows": 10000, "threads": 20, "updates": 20, "reads_per_thread": 200,
+        "reader_count": 10000, "reader_sum_range": [49995000, 50195000],
+        "final": {"count": 10000, "sum": 50195000},
+    }
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
-                                                          "table_filter_pushdown": tfp},
+                                                          "table_filter_pushdown": tfp, "multi_version": mv,
+                                                          "concurrent_reads_while_updating": cr},
                                                          indent=1, sort_keys=True) + "\n")
 
 

@@ -8,7 +8,7 @@ from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import filter_pushdown_tables, residual_from_json, update_case_views
+from test_oracle_tpch import filter_pushdown_tables, multi_version_views, residual_from_json, update_case_views
 
 pytestmark = pytest.mark.gpu
 
@@ -100,6 +100,96 @@ def test_update(ctx, golden, encoding):
             for con, eq, expect in step["checks"]:
                 fs = F.TableFilterSet({0: F.ConstantFilter("=", eq)}) if eq is not None else F.TableFilterSet()
                 assert select_all(t, fs, L.Txn(*conns[con])) == expect, (step["do"], con, eq, merged)
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE])
+def test_multi_version(ctx, golden, encoding):
+    """test/sql/transactions/test_multi_version.test through the table function: con1's
+    update, second update, delete and insert (rows appended with its transaction id) are seen
+    by con1 alone until COMMIT re-stamps them with commit id 6; con2's later snapshot sees all."""
+    t = CubitTable(ctx, 3)
+    t.add_column(0, np.array([1, 2, 3], dtype=np.int32))
+    if encoding is not None:
+        t.build_index(0, encoding)
+    appended = False
+    for step, upd, deleted, (ins, ins_id), conns in multi_version_views(golden):
+        t.set_updates(0, *upd)
+        drows = [r for r, d in enumerate(deleted) if d != 2 ** 64 - 2]
+        t.set_deletes(np.array(drows, np.int64), np.array([deleted[r] for r in drows], np.uint64))
+        if ins and not appended:
+            t.append({0: np.array(ins, dtype=np.int32)}, insert_id=ins_id)
+            appended = True
+        elif ins:
+            t.set_inserts(np.array([3]), np.array([3 + len(ins)]), np.array([ins_id], np.uint64))
+        for con, want in step["expect"].items():
+            got = select_all(t, F.TableFilterSet(), L.Txn(*conns[con]))
+            assert sum(got) == want, (step["do"], con, got)
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE])
+def test_concurrent_reads_while_updating(ctx, golden, encoding):
+    """concurrent_reads_while_updating.test_slow on one context: one thread commits the 20
+    UPDATE i=i+1 (each adds 10,000 update records stamped with its commit id) while 19 threads
+    take snapshots and read — SELECT i through the table function, and count(*) WHERE i < 5000
+    through the (patched) index. Every snapshot is whole: after k commits it sees 10,000 rows
+    summing to 49,995,000 + 10,000·k and 5,000 - k rows below 5,000 — never a torn state. Then
+    the update chains are merged and the final 10,000 / 50,195,000 read back."""
+    import threading
+
+    c = golden["cases"]["concurrent_reads_while_updating"]
+    n, n_upd, lo, hi = c["rows"], c["updates"], c["reader_sum_range"][0], c["reader_sum_range"][1]
+    t = CubitTable(ctx, n)
+    t.add_column(0, np.arange(n, dtype=np.int32))
+    if encoding is not None:
+        t.build_index(0, encoding)
+    lock = threading.Lock()
+    state = {"k": 0}
+    errors, seen = [], set()
+    lt5000 = F.TableFilterSet({0: F.ConstantFilter("<", 5000)})
+
+    def updater():
+        try:
+            for k in range(1, n_upd + 1):
+                rows = np.tile(np.arange(n, dtype=np.int64), k)
+                vals = np.concatenate([np.arange(n, dtype=np.int64) + j for j in range(1, k + 1)])
+                vers = np.repeat(np.arange(1, k + 1, dtype=np.uint64) * 10, n)
+                o = np.argsort(rows, kind="stable")  # each row's records in commit order
+                t.set_updates(0, rows[o], vals[o], vers[o])
+                with lock:
+                    state["k"] = k  # committed: snapshots from now on start after 10·k
+        except Exception as e:
+            errors.append(repr(e))
+
+    def reader(tid):
+        try:
+            for _ in range(10):
+                with lock:
+                    k = state["k"]
+                txn = L.Txn(10 * k + 1, 4611686018427388000 + 1000 + tid)
+                got = select_all(t, F.TableFilterSet(), txn)
+                total = sum(got)
+                if len(got) != c["reader_count"] or not lo <= total <= hi or total != lo + n * k:
+                    errors.append(f"reader {tid}: k={k} rows={len(got)} sum={total}")
+                cnt = t.count(lt5000, txn=txn)
+                if cnt != 5000 - k:
+                    errors.append(f"reader {tid}: k={k} count(i<5000)={cnt}")
+                seen.add(k)
+        except Exception as e:
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=updater)] + [threading.Thread(target=reader, args=(i,))
+                                               for i in range(1, c["threads"])]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:3]
+    assert t.merge_updates(0, 10 * n_upd + 1) == n
+    final = select_all(t, F.TableFilterSet(), L.Txn(10 * n_upd + 2, 4611686018427388000 + 5000))
+    assert (len(final), sum(final)) == (c["final"]["count"], c["final"]["sum"])
+    assert t.count(lt5000) == 5000 - n_upd
     t.close()
 
 

@@ -224,6 +224,65 @@ def test_update_reference_case(golden):
             assert list(seen) == expect, (step["do"], con, eq)
 
 
+NOT_DELETED = 2 ** 64 - 2  # NOT_DELETED_ID, src/common/constants.cpp:16
+
+
+def multi_version_views(golden):
+    """test/sql/transactions/test_multi_version.test as version state per step: yields (step,
+    update list of column 0, per-row delete ids, rows inserted by con1 (appended after the three
+    base rows) with their insert id, {connection: (start, transaction id)}). con1's statements
+    carry its transaction id until COMMIT gives them commit id 6; con2's snapshot starts at 5,
+    and after the commit a new one at 7."""
+    t1, t2 = TXN_START + 1, TXN_START + 2
+    u = lambda vals, vers: (np.zeros(len(vals), np.int64), np.array(vals, np.int64), np.array(vers, np.uint64))
+    none = u([], [])
+    steps = golden["cases"]["multi_version"]["steps"]
+    conns = {"con1": (5, t1), "con2": (5, t2)}
+    yield steps[0], none, [NOT_DELETED] * 3, ([], 0), conns
+    yield steps[1], u([5], [t1]), [NOT_DELETED] * 3, ([], 0), conns
+    yield steps[2], u([5, 10], [t1, t1]), [NOT_DELETED] * 3, ([], 0), conns
+    yield steps[3], u([5, 10], [t1, t1]), [t1, NOT_DELETED, NOT_DELETED], ([], 0), conns
+    yield steps[4], u([5, 10], [t1, t1]), [t1, NOT_DELETED, NOT_DELETED], ([1, 2], t1), conns
+    yield steps[5], u([5, 10], [6, 6]), [6, NOT_DELETED, NOT_DELETED], ([1, 2], 6), {"con2": (7, TXN_START + 3)}
+
+
+def test_multi_version_reference_case(golden):
+    """test/sql/transactions/test_multi_version.test:9-99: a writer's update, second update,
+    delete and insert seen by the writer only; by every later snapshot after COMMIT."""
+    base = [1, 2, 3]
+    for step, upd, deleted, (ins, ins_id), conns in multi_version_views(golden):
+        data = np.array(base + ins, dtype=np.int32)
+        n = len(data)
+        inserted = np.array([0] * 3 + [ins_id] * len(ins), dtype=np.uint64)
+        dele = np.array(deleted + [NOT_DELETED] * len(ins), dtype=np.uint64)
+        col = O.Column(data, updates=upd)
+        for con, want in step["expect"].items():
+            tx = O.Mvcc(*conns[con], inserted=inserted, deleted=dele)
+            rows = O.table_scan([col], F.serialize(F.TableFilterSet()), n, tx=tx)
+            assert int(O.fetch(col, rows, tx=tx).sum()) == want, (step["do"], con)
+
+
+def test_concurrent_reads_while_updating_reference_case(golden):
+    """concurrent_reads_while_updating.test_slow, serially: after k of the 20 committed
+    UPDATE i=i+1, a snapshot sees 10,000 rows summing to 49,995,000 + 10,000·k — inside the
+    reader's bounds — and the last one the final 10,000 / 50,195,000."""
+    c = golden["cases"]["concurrent_reads_while_updating"]
+    n = c["rows"]
+    data = np.arange(n, dtype=np.int32)
+    rows = np.tile(np.arange(n, dtype=np.int64), c["updates"])
+    vals = np.concatenate([np.arange(n, dtype=np.int64) + k for k in range(1, c["updates"] + 1)])
+    vers = np.repeat(np.arange(1, c["updates"] + 1, dtype=np.uint64) * 10, n)
+    order = np.argsort(rows, kind="stable")  # chronological per row
+    col = O.Column(data, updates=(rows[order], vals[order], vers[order]))
+    lo, hi = c["reader_sum_range"]
+    for k in (0, 1, 7, c["updates"]):
+        tx = O.Mvcc(10 * k + 1, TXN_START + 100 + k)
+        r = O.table_scan([col], F.serialize(F.TableFilterSet()), n, tx=tx)
+        total = int(O.fetch(col, r, tx=tx).sum())
+        assert len(r) == c["reader_count"] and lo <= total <= hi and total == lo + n * k
+    assert (len(r), total) == (c["final"]["count"], c["final"]["sum"])
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
