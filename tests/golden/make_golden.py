@@ -152,10 +152,20 @@ def main():
         "reader_count": 10000, "reader_sum_range": [49995000, 50195000],
         "final": {"count": 10000, "sum": 50195000},
     }
+    # test/sql/update/test_update_many_updaters.test: rows 1, 2, 3; an updater commits one
+    # update per row between four readers' BEGINs (immediate_transaction_mode), reverts, and
+    # again; then three readers update and commit in phases. Every `query I <con>` view, in
+    # file order (the conflicting statements fail and change nothing).
+    mu_src = (REF / "test/sql/update/test_update_many_updaters.test").read_text()
+    assert "SET immediate_transaction_mode=true" in mu_src
+    mu_views = [[c, [int(x) for x in v.split()]]
+                for c, v in re.findall(r"query I (\w+)\nSELECT \* FROM test ORDER BY a\n----\n((?:-?\d+\n?)+)", mu_src)]
+    mu = {"source": "test/sql/update/test_update_many_updaters.test", "rows": [1, 2, 3], "views": mu_views}
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
-                                                          "concurrent_reads_while_updating": cr},
+                                                          "concurrent_reads_while_updating": cr,
+                                                          "many_updaters": mu},
                                                          indent=1, sort_keys=True) + "\n")
 
 

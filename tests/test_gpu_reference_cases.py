@@ -8,7 +8,8 @@ from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import filter_pushdown_tables, multi_version_views, residual_from_json, update_case_views
+from test_oracle_tpch import (filter_pushdown_tables, many_updaters_reads, multi_version_views, residual_from_json,
+                              update_case_views)
 
 pytestmark = pytest.mark.gpu
 
@@ -125,6 +126,27 @@ def test_multi_version(ctx, golden, encoding):
         for con, want in step["expect"].items():
             got = select_all(t, F.TableFilterSet(), L.Txn(*conns[con]))
             assert sum(got) == want, (step["do"], con, got)
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_many_updaters(ctx, golden, encoding):
+    """test/sql/update/test_update_many_updaters.test through the table function: all 26
+    views (SELECT * ORDER BY a) of four snapshots, the writer and the committed state, and the
+    same views under a pushed filter a >= 4 (the patched index leaves when indexed)."""
+    c = golden["cases"]["many_updaters"]
+    t = CubitTable(ctx, 3)
+    t.add_column(0, np.array(c["rows"], dtype=np.int32))
+    if encoding is not None:
+        t.build_index(0, encoding)
+    ge4 = F.TableFilterSet({0: F.ConstantFilter(">=", 4)})
+    reads = list(many_updaters_reads(golden))
+    assert [r[0] for r in reads] == [v[0] for v in c["views"]]
+    for (con, snap, upd), (_, want) in zip(reads, c["views"]):
+        t.set_updates(0, *upd)
+        txn = L.Txn(*snap)
+        assert sorted(select_all(t, F.TableFilterSet(), txn)) == want, (con, snap)
+        assert sorted(select_all(t, ge4, txn)) == [v for v in want if v >= 4], (con, snap)
     t.close()
 
 

@@ -283,6 +283,71 @@ def test_concurrent_reads_while_updating_reference_case(golden):
     assert (len(r), total) == (c["final"]["count"], c["final"]["sum"])
 
 
+def many_updaters_reads(golden):
+    """test/sql/update/test_update_many_updaters.test as the version state at each read: yields
+    (connection, (start, transaction id), update list of column a) in file order, to pair with
+    the golden views. Start times and commit ids share one increasing counter; BEGIN takes the
+    snapshot (immediate_transaction_mode); a statement outside BEGIN is its own transaction; an
+    uncommitted record carries its writer's transaction id until COMMIT re-stamps it."""
+    tid = {c: TXN_START + i for i, c in enumerate(("con1", "con2", "con3", "con4", "updater"), 1)}
+    recs = []  # [row, value, version or writer connection]
+    committed = {}  # connection -> commit id of its records
+    snap = {}
+
+    def ulist():
+        order = sorted(range(len(recs)), key=lambda i: (recs[i][0], i))  # per row, chronological
+        vers = [committed.get(recs[i][2], tid.get(recs[i][2])) if isinstance(recs[i][2], str) else recs[i][2]
+                for i in order]
+        return (np.array([recs[i][0] for i in order], np.int64), np.array([recs[i][1] for i in order], np.int64),
+                np.array(vers, np.uint64))
+
+    def reads(*cons):
+        for c in cons:
+            yield c, snap[c], ulist()
+
+    for phase_start in (1, 9):  # the process runs twice; phase 1 ends with the revert at 8
+        c = phase_start
+        snap["con1"] = (c, tid["con1"])
+        recs.append([0, 4, c + 1])
+        snap["con2"] = (c + 2, tid["con2"])
+        recs.append([1, 5, c + 3])
+        snap["con3"] = (c + 4, tid["con3"])
+        recs.append([2, 6, c + 5])
+        snap["con4"] = (c + 6, tid["con4"])
+        yield from reads("con1", "con2", "con3", "con4")
+        if phase_start == 1:
+            recs.extend([[0, 1, 8], [1, 2, 8], [2, 3, 8]])  # updater: a=a-3, committed at 8
+    recs.extend([[0, 7, "con2"], [1, 8, "con3"], [2, 9, "con4"]])
+    yield from reads("con1", "con2", "con3", "con4")
+    snap["updater"] = (16, tid["updater"])
+    yield from reads("updater")
+    committed["con4"] = 17
+    snap["con4"] = (18, TXN_START + 10)
+    yield from reads("con1", "con2", "con3", "con4")
+    committed["con2"] = 19
+    snap["con2"] = snap["con4"] = (20, TXN_START + 11)
+    yield from reads("con1", "con2", "con3", "con4")
+    committed["con3"] = 21
+    snap["con2"] = snap["con3"] = snap["con4"] = (22, TXN_START + 12)
+    yield from reads("con1", "con2", "con3", "con4")
+    snap["con1"] = (23, TXN_START + 13)
+    yield from reads("con1")
+
+
+def test_many_updaters_reference_case(golden):
+    """test/sql/update/test_update_many_updaters.test: the 26 views four snapshots, a writer
+    and the committed state take of one 3-row table while updates commit between them."""
+    c = golden["cases"]["many_updaters"]
+    data = np.array(c["rows"], dtype=np.int32)
+    got = list(many_updaters_reads(golden))
+    assert [g[0] for g in got] == [v[0] for v in c["views"]]
+    for (con, (start, tx_id), upd), (_, want) in zip(got, c["views"]):
+        col = O.Column(data, updates=upd)
+        tx = O.Mvcc(start, tx_id)
+        rows = O.table_scan([col], F.serialize(F.TableFilterSet()), 3, tx=tx)
+        assert sorted(O.fetch(col, rows, tx=tx).tolist()) == want, (con, start)
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
