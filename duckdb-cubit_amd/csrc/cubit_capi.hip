@@ -3583,6 +3583,31 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
                     live.empty() ? nullptr : &live, prefix);
 }
 
+// cubit_table_scan and its tile directory under one hold of the context lock: the directory is
+// copied on the context's stream before any other thread's scan can reuse the context's buffer
+// (cubit_ctx_last_tiles read after a separate cubit_table_scan may describe another thread's
+// scan when several DuckDB pipeline tasks share the context).
+extern "C" int cubit_table_scan_tiles(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
+                                      const cubit_txn* txn, int64_t* d_rowids, uint64_t capacity, uint64_t* d_count,
+                                      uint32_t flags, uint64_t* d_dir, uint32_t dir_cap, uint32_t* n_tiles,
+                                      uint64_t* rows_per_tile) {
+    if (!t || !n_tiles) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (flags & CUBIT_SCAN_COUNT_ONLY) return fail(CUBIT_ERR_INVALID, "a count-only scan has no tile directory");
+    CUBIT_LOCK(t->ctx);
+    if (int rc = cubit_table_scan(t, nodes, n_nodes, txn, d_rowids, capacity, d_count, flags)) return rc;
+    cubit_ctx* ctx = t->ctx;
+    *n_tiles = ctx->last_tiles;
+    if (rows_per_tile) *rows_per_tile = ctx->last_tile_rows;
+    if (ctx->last_tiles > dir_cap)
+        return fail(CUBIT_ERR_CAPACITY, "tile directory of %u tiles, room for %u", ctx->last_tiles, dir_cap);
+    if (ctx->last_tiles) {
+        if (!d_dir) return fail(CUBIT_ERR_INVALID, "d_dir is null");
+        HIP_CHECK(hipMemcpyAsync(d_dir, ctx->dir, 2ull * ctx->last_tiles * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                                 ctx->stream));
+    }
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
                                        const cubit_txn* txn, int col_a, int col_b, int64_t* d_out,
                                        uint64_t* d_count, uint32_t flags) {

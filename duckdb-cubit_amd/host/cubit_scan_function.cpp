@@ -226,23 +226,27 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     // one decode into a buffer sized by a guess (an eighth of the rows); only a filter that
     // keeps more rows than that runs a second time, with the exact count
     uint64_t cap = std::max<uint64_t>(bind.n_rows / 8 + 4096, 1);
+    // this scan's tile directory, copied out within the scan call: other pipeline tasks or
+    // queries may scan on the same context right after it (cubit_table_scan_tiles)
+    const uint32_t dir_cap = (uint32_t)((bind.n_rows + 131071) / 131072 + 1);
+    PooledBuffer d_dir;
+    d_dir.allocate(device_pool(), ctx, 2ull * dir_cap * 8);
+    uint32_t n_tiles = 0;
     for (int pass = 0; pass < 2; ++pass) {
         g->d_ids.allocate(device_pool(), ctx, cap * 8);
         cap = g->d_ids.bytes / 8;
-        check(cubit_table_scan(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
-                               device_ptr(g->d_ids), cap, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_ORDERED),
-              "cubit_table_scan");
+        check(cubit_table_scan_tiles(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
+                                     device_ptr(g->d_ids), cap, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_ORDERED,
+                                     static_cast<uint64_t*>(d_dir.p), dir_cap, &n_tiles, &g->rows_per_tile),
+              "cubit_table_scan_tiles");
         check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
         if (g->count <= cap) break;
         if (pass == 1) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
         cap = g->count;
     }
-    const uint64_t* d_dir = nullptr;
-    uint32_t n_tiles = 0;
-    check(cubit_ctx_last_tiles(ctx, &d_dir, &n_tiles, &g->rows_per_tile), "tiles");
     if (g->count == 0) n_tiles = 0;  // nothing qualified: no run to hand out, whatever the directory holds
     std::vector<uint64_t> dir(2 * (size_t)n_tiles);
-    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), d_dir, dir.size() * 8), "directory");
+    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), d_dir.p, dir.size() * 8), "directory");
     // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
     idx_t off = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {

@@ -370,6 +370,15 @@ int cubit_table_merge_updates(cubit_table *t, int col, uint64_t horizon, uint64_
  * RowGroup::TemplatedScan's filter + row-id materialisation (table_scan.cpp:119-146). */
 int cubit_table_scan(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
                      int64_t *d_rowids, uint64_t capacity, uint64_t *d_count, uint32_t flags);
+/* cubit_table_scan plus this scan's tile directory (as cubit_ctx_last_tiles describes it),
+ * copied into d_dir (room for dir_cap tiles, 2 words each) on the context's stream within the
+ * same call: safe when several threads scan on one context, where a cubit_ctx_last_tiles read
+ * after the scan may already describe another thread's scan. *n_tiles = 0: no run (the filter
+ * folded away or nothing to decode). Not with CUBIT_SCAN_COUNT_ONLY; CUBIT_ERR_CAPACITY when
+ * dir_cap is too small (a partition has ⌈n_rows / 131,072⌉ tiles). */
+int cubit_table_scan_tiles(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
+                           int64_t *d_rowids, uint64_t capacity, uint64_t *d_count, uint32_t flags, uint64_t *d_dir,
+                           uint32_t dir_cap, uint32_t *n_tiles, uint64_t *rows_per_tile);
 /* Probe column `col` at the scan's row ids (visible values for txn). */
 int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64_t *d_rowids, const uint64_t *d_count,
                       uint64_t max_n, int64_t *d_out);
