@@ -442,19 +442,50 @@ int64_t oracle_table_scan_mt(const oscan *s, int nthreads, uint64_t *sum_rowid) 
 int oracle_fetch(const ocol *c, const omvcc *tx, const int64_t *rowids, uint64_t n, int64_t row_base,
                  int64_t *out_vals, uint8_t *out_valid) {
     uint64_t st = tx ? tx->start_time : UINT64_MAX - 2, tid = tx ? tx->transaction_id : UINT64_MAX - 2;
+    /* each row's update records, in list (= chronological) order: a stable bucketing by row, so
+     * a fetch costs O(rows + records) instead of rows × records (test-speed only; same result) */
+    uint64_t max_row = 0;
+    for (uint64_t u = 0; u < c->n_updates; u++)
+        if ((uint64_t)c->upd_rows[u] > max_row) max_row = (uint64_t)c->upd_rows[u];
+    uint64_t *first = NULL, *order = NULL;
+    if (c->n_updates) {
+        first = (uint64_t *)calloc(max_row + 2, sizeof(uint64_t));
+        order = (uint64_t *)malloc(c->n_updates * sizeof(uint64_t));
+        if (!first || !order) {
+            free(first);
+            free(order);
+            return -1;
+        }
+        for (uint64_t u = 0; u < c->n_updates; u++) first[(uint64_t)c->upd_rows[u] + 1]++;
+        for (uint64_t r = 0; r <= max_row; r++) first[r + 1] += first[r];
+        uint64_t *fill = (uint64_t *)malloc((max_row + 1) * sizeof(uint64_t));
+        if (!fill) {
+            free(first);
+            free(order);
+            return -1;
+        }
+        memcpy(fill, first, (max_row + 1) * sizeof(uint64_t));
+        for (uint64_t u = 0; u < c->n_updates; u++) order[fill[(uint64_t)c->upd_rows[u]]++] = u;
+        free(fill);
+    }
     for (uint64_t i = 0; i < n; i++) {
         uint64_t r = (uint64_t)(rowids[i] - row_base);
         int64_t v = c->type == OTYPE_INT32 ? (int64_t)((const int32_t *)c->data)[r] : ((const int64_t *)c->data)[r];
         int valid = row_valid(c, r);
-        for (uint64_t u = 0; u < c->n_updates; u++) {
-            if ((uint64_t)c->upd_rows[u] == r && use_inserted(st, tid, c->upd_version[u])) {
-                v = c->upd_values[u];
-                valid = 1;
+        if (c->n_updates && r <= max_row) {
+            for (uint64_t k = first[r]; k < first[r + 1]; k++) {
+                const uint64_t u = order[k];
+                if (use_inserted(st, tid, c->upd_version[u])) { /* the newest visible record wins */
+                    v = c->upd_values[u];
+                    valid = 1;
+                }
             }
         }
         out_vals[i] = valid ? v : 0;
         if (out_valid) out_valid[i] = (uint8_t)valid;
     }
+    free(first);
+    free(order);
     return 0;
 }
 

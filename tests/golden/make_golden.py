@@ -161,11 +161,22 @@ def main():
     mu_views = [[c, [int(x) for x in v.split()]]
                 for c, v in re.findall(r"query I (\w+)\nSELECT \* FROM test ORDER BY a\n----\n((?:-?\d+\n?)+)", mu_src)]
     mu = {"source": "test/sql/update/test_update_many_updaters.test", "rows": [1, 2, 3], "views": mu_views}
+    # test/sql/update/block_boundary_update.test_slow: BIGINT range(0, 50000); UPDATE i=i+1
+    # twice, INSERT INTO test SELECT * FROM test, UPDATE i=i+1 twice; COUNT(i), SUM(i) after
+    # the CREATE and after each statement (read from the file, in order)
+    bb_src = (REF / "test/sql/update/block_boundary_update.test_slow").read_text()
+    assert "CREATE TABLE test AS SELECT * FROM range (0, 50000, 1) t1(i);" in bb_src
+    stmts = re.findall(r"statement ok\n(UPDATE test SET i=i\+1|INSERT INTO test SELECT \* FROM test;)", bb_src)
+    counts = [[int(a), int(b)] for a, b in re.findall(r"SELECT COUNT\(i\), SUM\(i\) FROM test\n----\n(\d+)\t(\d+)", bb_src)]
+    bb = {"source": "test/sql/update/block_boundary_update.test_slow", "rows": 50000,
+          "statements": ["update" if x.startswith("UPDATE") else "insert_select" for x in stmts],
+          "count_sum": counts}
+    assert len(counts) == len(stmts) + 1
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
-                                                          "many_updaters": mu},
+                                                          "many_updaters": mu, "block_boundary_update": bb},
                                                          indent=1, sort_keys=True) + "\n")
 
 

@@ -8,8 +8,8 @@ from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import (filter_pushdown_tables, many_updaters_reads, multi_version_views, residual_from_json,
-                              update_case_views)
+from test_oracle_tpch import (block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
+                              residual_from_json, update_case_views)
 
 pytestmark = pytest.mark.gpu
 
@@ -147,6 +147,38 @@ def test_many_updaters(ctx, golden, encoding):
         txn = L.Txn(*snap)
         assert sorted(select_all(t, F.TableFilterSet(), txn)) == want, (con, snap)
         assert sorted(select_all(t, ge4, txn)) == [v for v in want if v >= 4], (con, snap)
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE])
+def test_block_boundary_update(ctx, golden, encoding):
+    """block_boundary_update.test_slow through the table function: COUNT(i), SUM(i) after
+    whole-table updates (every vector and row-group boundary of 50,000 / 100,000 rows) and an
+    INSERT … SELECT of the table into itself (appended with its commit id), then the same after
+    the update chains are merged into the base and the index; a filter i < 1000 on the
+    (patched) index counts the rows the reference's values give."""
+    c = golden["cases"]["block_boundary_update"]
+    t = CubitTable(ctx, c["rows"])
+    t.add_column(0, np.arange(c["rows"], dtype=np.int64))
+    if encoding is not None:
+        t.build_index(0, encoding)
+    lt = F.TableFilterSet({0: F.ConstantFilter("<", 1000)})
+    cur = np.arange(c["rows"], dtype=np.int64)
+    for st, appended, upd, ins, start, want in block_boundary_states(golden):
+        if appended is not None:
+            t.append({0: appended}, insert_id=start - 1)
+            cur = np.concatenate([cur, cur])
+        elif st == "update":
+            cur = cur + 1
+        t.set_updates(0, *upd)
+        txn = L.Txn(start, 4611686018427388000 + 60)
+        got = select_all(t, F.TableFilterSet(), txn)
+        assert (len(got), sum(got)) == want, st
+        assert t.count(lt, txn=txn) == int((cur < 1000).sum()), st
+    assert t.merge_updates(0, 2 ** 62) == len(cur)
+    got = select_all(t, F.TableFilterSet(), L.Txn(100, 4611686018427388000 + 61))
+    assert (len(got), sum(got)) == tuple(c["count_sum"][-1])
+    assert t.count(lt) == int((cur < 1000).sum())
     t.close()
 
 

@@ -348,6 +348,52 @@ def test_many_updaters_reference_case(golden):
         assert sorted(O.fetch(col, rows, tx=tx).tolist()) == want, (con, start)
 
 
+def block_boundary_states(golden):
+    """test/sql/update/block_boundary_update.test_slow as version state: yields, after the
+    CREATE and after each statement, (statement, rows appended by it or None, update list of
+    column i, per-row insert ids, snapshot start, expected (count, sum)). Statement k commits at
+    2k; each read starts at 2k + 1. UPDATE i=i+1 adds one record per row (value = the row's
+    current value + 1); INSERT INTO test SELECT * FROM test appends a copy of the current values."""
+    c = golden["cases"]["block_boundary_update"]
+    cur = np.arange(c["rows"], dtype=np.int64)
+    ins = np.zeros(c["rows"], np.uint64)
+    rows, vals, vers = [], [], []
+
+    def ulist():
+        if not rows:
+            return (np.zeros(0, np.int64),) * 2 + (np.zeros(0, np.uint64),)
+        r, v, w = np.concatenate(rows), np.concatenate(vals), np.concatenate(vers)
+        o = np.argsort(r, kind="stable")  # per row, in commit order
+        return r[o], v[o], w[o]
+
+    yield "create", None, ulist(), ins, 1, tuple(c["count_sum"][0])
+    for k, st in enumerate(c["statements"], 1):
+        appended = None
+        if st == "update":
+            cur = cur + 1
+            rows.append(np.arange(len(cur), dtype=np.int64))
+            vals.append(cur.copy())
+            vers.append(np.full(len(cur), 2 * k, np.uint64))
+        else:
+            appended = cur.copy()
+            ins = np.concatenate([ins, np.full(len(cur), 2 * k, np.uint64)])
+            cur = np.concatenate([cur, cur])
+        yield st, appended, ulist(), ins, 2 * k + 1, tuple(c["count_sum"][k])
+
+
+def test_block_boundary_update_reference_case(golden):
+    """block_boundary_update.test_slow: COUNT(i), SUM(i) after whole-table updates across
+    vector and row-group boundaries and an INSERT … SELECT of the table into itself."""
+    base = np.arange(golden["cases"]["block_boundary_update"]["rows"], dtype=np.int64)
+    for st, appended, upd, ins, start, (cnt, total) in block_boundary_states(golden):
+        if appended is not None:
+            base = np.concatenate([base, appended])
+        col = O.Column(base, updates=upd)
+        tx = O.Mvcc(start, TXN_START + 50, inserted=ins)
+        r = O.table_scan([col], F.serialize(F.TableFilterSet()), len(base), tx=tx)
+        assert (len(r), int(O.fetch(col, r, tx=tx).sum())) == (cnt, total), st
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
