@@ -44,7 +44,12 @@
 #include "duckdb/planner/operator/logical_insert.hpp"
 #include "duckdb/planner/operator/logical_update.hpp"
 #include "duckdb/planner/table_filter.hpp"
+#include "duckdb/common/enums/compression_type.hpp"
+#include "duckdb/storage/block_manager.hpp"
+#include "duckdb/storage/buffer_manager.hpp"
 #include "duckdb/storage/data_table.hpp"
+#include "duckdb/storage/table_io_manager.hpp"
+#include "duckdb/storage/table_storage_info.hpp"
 #include "duckdb/transaction/duck_transaction.hpp"
 #include "duckdb/transaction/duck_transaction_manager.hpp"
 #include "duckdb/transaction/local_storage.hpp"
@@ -707,8 +712,138 @@ static bool FewDistinct(const vector<int64_t> &v, const vector<uint64_t> &valid)
     return true;
 }
 
-// Upload a whole snapshot as a new partition and build its indexes.
-static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap) {
+// The CUBIT_TYPE_* of a column's BITPACKING segments: the T DuckDB packs its physical type
+// with (bitpacking.cpp:953-977, BOOL as int8_t); -1 for a type the partition does not hold.
+static int SegmentType(PhysicalType t) {
+    switch (t) {
+    case PhysicalType::BOOL:
+    case PhysicalType::INT8:
+        return CUBIT_TYPE_INT8;
+    case PhysicalType::INT16:
+        return CUBIT_TYPE_INT16;
+    case PhysicalType::INT32:
+        return CUBIT_TYPE_INT32;
+    case PhysicalType::INT64:
+        return CUBIT_TYPE_INT64;
+    case PhysicalType::UINT8:
+        return CUBIT_TYPE_UINT8;
+    case PhysicalType::UINT16:
+        return CUBIT_TYPE_UINT16;
+    case PhysicalType::UINT32:
+        return CUBIT_TYPE_UINT32;
+    default:
+        return -1;
+    }
+}
+
+// K5 from the database file: when every segment of column `col` is a persistent BITPACKING
+// segment without in-memory updates and together they hold rows [0, n_rows) in order, the
+// column is registered from those segment images as DuckDB wrote them
+// (cubit_table_add_bitpacked_column: unpacked on the GPU, the packed filter and the packed
+// probe reachable) and true is returned; otherwise false, and the caller uploads decoded values.
+// The segments come from DataTable::GetColumnSegmentInfo (data_table.hpp:198 — the rows behind
+// pragma_storage_info; ColumnData::GetColumnSegmentInfo, column_data.cpp:597-645: column_path
+// "[c]" is the values, "[c, 0]" the validity, segment_start an absolute row) and are read from
+// the row-data block manager (TableIOManager::GetBlockManagerForRowData, table_io_manager.hpp:30;
+// BlockManager::RegisterBlock, block_manager.hpp:83; BufferManager::Pin, buffer_manager.hpp:41)
+// at their block offset. A segment's first 8 bytes are the end of its metadata, i.e. its size
+// (BitpackingCompressState::FlushSegment). Deleted rows stay in the segments (visibility is the
+// partition's delete list); updates make has_updates true and keep this path off.
+static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalType ptype, uint64_t n_rows,
+                                  cubit_table *t, const uint64_t *validity) {
+    const int seg_type = SegmentType(ptype);
+    if (seg_type < 0 || n_rows == 0) {
+        return false;
+    }
+    auto &storage = entry.GetStorage();
+    const string path = "[" + to_string(col) + "]";
+    const string bitpacking = CompressionTypeToString(CompressionType::COMPRESSION_BITPACKING);
+    vector<ColumnSegmentInfo> segs;
+    for (auto &info : storage.GetColumnSegmentInfo()) {
+        if (info.column_id == col && info.column_path == path) {
+            segs.push_back(info);
+        }
+    }
+    std::sort(segs.begin(), segs.end(), [](const ColumnSegmentInfo &a, const ColumnSegmentInfo &b) {
+        return a.segment_start < b.segment_start;
+    });
+    uint64_t next = 0;
+    for (auto &sg : segs) {
+        if (!sg.persistent || sg.has_updates || sg.compression_type != bitpacking || sg.segment_start != next) {
+            return false;
+        }
+        next += sg.segment_count;
+    }
+    if (next != n_rows) {
+        return false;
+    }
+    auto &block_manager = TableIOManager::Get(storage).GetBlockManagerForRowData();
+    vector<uint8_t> bytes;
+    vector<uint64_t> offsets, rows;
+    for (auto &sg : segs) {
+        auto handle = block_manager.RegisterBlock(sg.block_id);
+        auto pin = block_manager.buffer_manager.Pin(handle);
+        const_data_ptr_t p = pin.Ptr() + sg.block_offset;
+        uint64_t size = 0;
+        memcpy(&size, p, sizeof(size));
+        if (size < 8 || sg.block_offset + size > block_manager.GetBlockSize()) {
+            return false;  // not a BITPACKING segment header
+        }
+        const uint64_t at = (bytes.size() + 7) / 8 * 8;
+        bytes.resize(at + size, 0);
+        memcpy(bytes.data() + at, p, size);
+        offsets.push_back(at);
+        rows.push_back(sg.segment_count);
+    }
+    return cubit_table_add_bitpacked_column(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(),
+                                            rows.data(), (uint32_t)segs.size(), validity) == CUBIT_OK;
+}
+
+// The column as registered against the snapshot's values on a sample (the valid rows of a
+// stride over the partition, at most 4,096, read back with cubit_table_probe): a column taken
+// from the segments stays so only when they agree, so a segment that no longer matches the
+// snapshot (the file moved on under it) falls back to the decoded values.
+static bool SampleMatches(cubit_ctx *ctx, cubit_table *t, column_t col, const vector<int64_t> &values,
+                          const vector<uint64_t> &validity, uint64_t n) {
+    vector<int64_t> ids;
+    const uint64_t stride = std::max<uint64_t>(1, n / 4096);
+    for (uint64_t r = 0; r < n && ids.size() < 4096; r += stride) {
+        if ((validity[r >> 6] >> (r & 63)) & 1) {
+            ids.push_back((int64_t)r);
+        }
+    }
+    if (ids.empty()) {
+        return true;
+    }
+    const uint64_t k = ids.size();
+    void *d_ids = nullptr, *d_cnt = nullptr, *d_out = nullptr;
+    vector<int64_t> got(k);
+    bool ok = cubit_dev_alloc(ctx, k * 8, &d_ids) == CUBIT_OK && cubit_dev_alloc(ctx, 16, &d_cnt) == CUBIT_OK &&
+              cubit_dev_alloc(ctx, k * 8, &d_out) == CUBIT_OK;
+    ok = ok && cubit_memcpy_h2d(ctx, d_ids, ids.data(), k * 8) == CUBIT_OK &&
+         cubit_memcpy_h2d(ctx, d_cnt, &k, 8) == CUBIT_OK &&
+         cubit_table_probe(t, (int)col, nullptr, static_cast<const int64_t *>(d_ids), static_cast<const uint64_t *>(d_cnt),
+                           k, static_cast<int64_t *>(d_out)) == CUBIT_OK &&
+         cubit_memcpy_d2h(ctx, got.data(), d_out, k * 8) == CUBIT_OK;
+    for (void *p : {d_ids, d_cnt, d_out}) {
+        if (p) {
+            cubit_dev_free(ctx, p);
+        }
+    }
+    if (!ok) {
+        return false;
+    }
+    for (uint64_t i = 0; i < k; i++) {
+        if (got[i] != values[(size_t)ids[i]]) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// Upload a whole snapshot as a new partition and build its indexes. With `entry`, a column held
+// in persistent BITPACKING segments is registered from them (AttachBitpackedColumn).
+static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, DuckTableEntry *entry) {
     if (attached.table) {
         cubit_table_destroy(attached.table);
         attached.table = nullptr;
@@ -716,14 +851,20 @@ static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap) {
     Check(cubit_table_create(attached.ctx, snap.rows, 0, &attached.table));
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
         const column_t col = attached.column_order[c];
-        const bool wide = WidePhysical(attached.columns[col]);
-        vector<int32_t> narrow;
-        if (!wide) {
-            narrow.assign(snap.values[c].begin(), snap.values[c].end());
+        const bool from_segments =
+            entry && AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, attached.table,
+                                           snap.validity[c].data()) &&
+            SampleMatches(attached.ctx, attached.table, col, snap.values[c], snap.validity[c], snap.rows);
+        if (!from_segments) {  // (re-)registering replaces a column taken from segments
+            const bool wide = WidePhysical(attached.columns[col]);
+            vector<int32_t> narrow;
+            if (!wide) {
+                narrow.assign(snap.values[c].begin(), snap.values[c].end());
+            }
+            Check(cubit_table_add_column(attached.table, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
+                                         wide ? (const void *)snap.values[c].data() : (const void *)narrow.data(),
+                                         snap.validity[c].data(), 0));
         }
-        Check(cubit_table_add_column(attached.table, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
-                                     wide ? (const void *)snap.values[c].data() : (const void *)narrow.data(),
-                                     snap.validity[c].data(), 0));
         bool named = false;
         for (auto &ix : attached.indexes) {
             if (ix.column == col) {
@@ -787,11 +928,17 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
     }
     if (rebuild || !attached.table) {
         ReadRows(con, table_name, entry, attached.column_order, 0, snap);
-        con.Commit();
         if (snap.rows == 0) {
+            con.Commit();
             throw InvalidInputException("cubit: %s has no rows to attach", table_name);
         }
-        BuildPartition(attached, snap);
+        // before the snapshot's transaction ends: while it runs, a commit's updates cannot be
+        // checkpointed into the segments (CanCheckpoint, duck_transaction_manager.cpp:126-131)
+        // and a concurrent checkpoint does not vacuum deleted rows (:132-135); later appends show
+        // as more rows than the snapshot's. Either keeps that column on decoded values, and the
+        // sample check in BuildPartition backs this up.
+        BuildPartition(attached, snap, &entry);
+        con.Commit();
         present = snap.present;
     } else {
         con.Commit();
