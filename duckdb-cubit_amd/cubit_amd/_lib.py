@@ -119,6 +119,11 @@ GPU_SIGNATURES = {
         C.c_int,
         [_P, C.POINTER(FilterNode), _U32, C.POINTER(Txn), _P, _U64, _P, _U32],
     ),
+    "cubit_table_scan_tiles": (
+        C.c_int,
+        [_P, C.POINTER(FilterNode), _U32, C.POINTER(Txn), _P, _U64, _P, _U32, _P, _U32, C.POINTER(_U32),
+         C.POINTER(_U64)],
+    ),
     "cubit_table_probe": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P]),
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_last_zones": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),

@@ -300,3 +300,45 @@ def test_window_transfer_compaction_round_trips(ctx):
     got = ordered(chunks, 4)
     assert np.array_equal(got[valid[keep]], nulls[keep][valid[keep]])
     t.close()
+
+
+def test_scan_tiles_returns_this_scans_directory(ctx):
+    """cubit_table_scan_tiles: the directory copied within the scan call equals the one
+    cubit_ctx_last_tiles describes right after it, survives a later scan on the context, and a
+    directory buffer too small is refused with CUBIT_ERR_CAPACITY."""
+    import ctypes as C
+
+    from cubit_amd.filters import serialize, to_ctypes
+
+    rng = np.random.default_rng(5)
+    n = 1_000_003
+    v = rng.integers(0, 100, n, dtype=np.int32)
+    t = CubitTable(ctx, n, row_base=4)
+    t.add_column(0, v)
+    t.build_index(0, L.INDEX_RANGE)
+
+    def scan_tiles(lt, dir_cap):
+        nodes = to_ctypes(serialize(F.TableFilterSet({0: F.ConstantFilter("<", lt)})).nodes)
+        ids, cnt = ctx.alloc(n * 8), ctx.alloc(16)
+        d = ctx.alloc(max(dir_cap, 1) * 16)
+        nt, rpt = C.c_uint32(), C.c_uint64()
+        rc = ctx.lib.cubit_table_scan_tiles(t.handle, nodes, len(nodes), None, C.c_void_p(ids.addr), n,
+                                            C.c_void_p(cnt.addr), L.SCAN_ORDERED, C.c_void_p(d.addr), dir_cap,
+                                            C.byref(nt), C.byref(rpt))
+        return rc, ids, cnt, d, nt.value, rpt.value
+
+    tiles = (n + 131071) // 131072
+    rc, ids, cnt, d, nt, rpt = scan_tiles(7, tiles)
+    assert rc == 0 and nt == tiles and rpt == 131072
+    mine = d.download(np.uint64, 2 * nt).reshape(-1, 2)
+    last, _ = ctx.last_tiles()
+    assert np.array_equal(mine, np.asarray(last, dtype=np.uint64).reshape(-1, 2))
+    k = int(cnt.download(np.uint64, 1)[0])
+    ref = np.flatnonzero(v < 7).astype(np.int64) + 4
+    assert np.array_equal(ids.download(np.int64, k), ref)
+    assert int(mine[:, 1].sum()) == k
+    scan_tiles(50, tiles)  # another scan on the context leaves the first copy alone
+    assert np.array_equal(d.download(np.uint64, 2 * nt).reshape(-1, 2), mine)
+    rc, *_ = scan_tiles(7, tiles - 1)
+    assert rc == L.ERR_CAPACITY
+    t.close()
