@@ -172,11 +172,32 @@ def main():
           "statements": ["update" if x.startswith("UPDATE") else "insert_select" for x in stmts],
           "count_sum": counts}
     assert len(counts) == len(stmts) + 1
+    # test/sql/filter/test_zonemap.test_slow (marked `mode skip` in the reference for memory on
+    # 32-bit builds; its expected counts stand): t = range(100000000) as a, length(range) b (the
+    # digit count), cross-column OR trees, count(*). The trees use the residual syntax above,
+    # column 0 = a, 1 = b.
+    zt_src = (REF / "test/sql/filter/test_zonemap.test_slow").read_text()
+    zt_counts = [int(x) for x in re.findall(r"query I\nselect count\(\*\) from t where [^\n]*\n----\n(\d+)", zt_src)]
+    zt_sql = re.findall(r"query I\nselect count\(\*\) from t where ([^\n]*)\n----", zt_src)
+    trees = {
+        "a > 500 or a <= 700": ["or", [0, ">", 500], [0, "<=", 700]],
+        "(a > 500 and b = 3) or (a > 7000 and b = 2)":
+            ["or", ["and", [0, ">", 500], [1, "=", 3]], ["and", [0, ">", 7000], [1, "=", 2]]],
+        "(a > 500 AND b = 3) OR (a > 400) OR (a > 300 AND b=4) OR (a > 600 AND a > 300)":
+            ["or", ["and", [0, ">", 500], [1, "=", 3]], [0, ">", 400], ["and", [0, ">", 300], [1, "=", 4]],
+             ["and", [0, ">", 600], [0, ">", 300]]],
+        "(a > 500 AND b = 1) OR b < 2": ["or", ["and", [0, ">", 500], [1, "=", 1]], [1, "<", 2]],
+    }
+    assert "create temporary table t as select range a, length(range) b" in zt_src and "range(100000000)" in zt_src
+    zt = {"source": "test/sql/filter/test_zonemap.test_slow", "rows": 100000000,
+          "queries": [{"sql": q, "tree": trees[q], "count": c} for q, c in zip(zt_sql, zt_counts)]}
+    assert len(zt["queries"]) == 6
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
-                                                          "many_updaters": mu, "block_boundary_update": bb},
+                                                          "many_updaters": mu, "block_boundary_update": bb,
+                                                          "zonemap_or_trees": zt},
                                                          indent=1, sort_keys=True) + "\n")
 
 

@@ -9,7 +9,7 @@ from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
 from test_oracle_tpch import (block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
-                              residual_from_json, update_case_views)
+                              residual_from_json, update_case_views, zonemap_table)
 
 pytestmark = pytest.mark.gpu
 
@@ -147,6 +147,33 @@ def test_many_updaters(ctx, golden, encoding):
         txn = L.Txn(*snap)
         assert sorted(select_all(t, F.TableFilterSet(), txn)) == want, (con, snap)
         assert sorted(select_all(t, ge4, txn)) == [v for v in want if v >= 4], (con, snap)
+    t.close()
+
+
+@pytest.mark.parametrize("a_index", [False, True])
+def test_zonemap_or_trees(ctx, golden, a_index):
+    """test/sql/filter/test_zonemap.test_slow on the GPU at its full 1e8 rows: count(*) of the
+    cross-column OR trees (residual filters) equals the file's counts — with a unindexed (K0 over
+    the BIGINT column) or range-indexed at the trees' constants, b range-indexed; the row ids of
+    the selective trees equal numpy's."""
+    c = golden["cases"]["zonemap_or_trees"]
+    a, b = zonemap_table(c["rows"])
+    t = CubitTable(ctx, c["rows"])
+    t.add_column(0, a)
+    t.add_column(1, b)
+    t.build_index(1, L.INDEX_RANGE)
+    if a_index:
+        t.build_index(0, L.INDEX_RANGE, [301, 401, 501, 601, 701, 7001])
+    for q in c["queries"]:
+        res = residual_from_json(q["tree"])
+        assert t.count(None, res) == q["count"], (q["sql"], a_index)
+        if q["count"] < 1000:
+            mask = np.zeros(len(a), bool)
+            if q["count"] == 499:
+                mask = ((a > 500) & (b == 3)) | ((a > 7000) & (b == 2))
+            else:
+                mask = ((a > 500) & (b == 1)) | (b < 2)
+            assert np.array_equal(t.scan(None, res, capacity=1024), np.flatnonzero(mask)), q["sql"]
     t.close()
 
 

@@ -394,6 +394,24 @@ def test_block_boundary_update_reference_case(golden):
         assert (len(r), int(O.fetch(col, r, tx=tx).sum())) == (cnt, total), st
 
 
+def zonemap_table(n):
+    """test_zonemap.test_slow's t: a = range(n) (BIGINT), b = length(range) — its digit count."""
+    a = np.arange(n, dtype=np.int64)
+    b = (np.searchsorted(10 ** np.arange(1, 10, dtype=np.int64), a, side="right") + 1).astype(np.int32)
+    return a, b
+
+
+def test_zonemap_or_trees_reference_case(golden):
+    """test/sql/filter/test_zonemap.test_slow: count(*) of cross-column OR trees over 1e8 rows
+    (a = range, b = digit count) equals the file's counts — the oracle's morsel-parallel scan."""
+    c = golden["cases"]["zonemap_or_trees"]
+    a, b = zonemap_table(c["rows"])
+    cols = [O.Column(a), O.Column(b)]
+    for q in c["queries"]:
+        n, _ = O.table_scan_mt(cols, F.serialize(None, residual_from_json(q["tree"])), c["rows"], threads=8)
+        assert n == q["count"], q["sql"]
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
