@@ -192,12 +192,32 @@ def main():
     zt = {"source": "test/sql/filter/test_zonemap.test_slow", "rows": 100000000,
           "queries": [{"sql": q, "tree": trees[q], "count": c} for q, c in zip(zt_sql, zt_counts)]}
     assert len(zt["queries"]) == 6
+    # test/sql/filter/test_obsolete_filters.test: integers(a, b) = (1,10) (2,12) (3,14) (4,16)
+    # (5,NULL) (NULL,NULL); every query whose WHERE is an AND of comparisons of a with integer
+    # constants — redundant, subsumed and contradictory ones, all pushed into the scan as one
+    # column's conjunction — with the rows it returns (the VARCHAR table and the constant-only
+    # WHEREs, which the planner folds before any scan, are not taken)
+    ob_src = (REF / "test/sql/filter/test_obsolete_filters.test").read_text()
+    assert "INSERT INTO integers VALUES (1, 10), (2, 12), (3, 14), (4, 16), (5, NULL), (NULL, NULL)" in ob_src
+    term = re.compile(r"^a(<=|>=|<>|<|>|=)(-?\d+)$")
+    ob_q = []
+    for where, body in re.findall(r"query II\nSELECT \* FROM integers WHERE ([^\n]*?)(?: ORDER BY 1)?\n----\n((?:[^\n]+\n?)*)",
+                                  ob_src):
+        parts = [x.strip() for x in where.split(" AND ")]
+        if not all(term.match(x) for x in parts):
+            continue
+        rows = [[None if v == "NULL" else int(v) for v in line.split("\t")] for line in body.strip().split("\n") if line]
+        ob_q.append({"where": where, "terms": [[term.match(x).group(1), int(term.match(x).group(2))] for x in parts],
+                     "rows": rows})
+    ob = {"source": "test/sql/filter/test_obsolete_filters.test",
+          "a": [1, 2, 3, 4, 5, None], "b": [10, 12, 14, 16, None, None], "queries": ob_q}
+    assert len(ob_q) >= 30, len(ob_q)
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
                                                           "many_updaters": mu, "block_boundary_update": bb,
-                                                          "zonemap_or_trees": zt},
+                                                          "zonemap_or_trees": zt, "obsolete_filters": ob},
                                                          indent=1, sort_keys=True) + "\n")
 
 

@@ -9,7 +9,8 @@ from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
 from test_oracle_tpch import (block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
-                              residual_from_json, update_case_views, zonemap_table)
+                              obsolete_filter_columns, obsolete_filter_sets, residual_from_json, update_case_views,
+                              zonemap_table)
 
 pytestmark = pytest.mark.gpu
 
@@ -147,6 +148,33 @@ def test_many_updaters(ctx, golden, encoding):
         txn = L.Txn(*snap)
         assert sorted(select_all(t, F.TableFilterSet(), txn)) == want, (con, snap)
         assert sorted(select_all(t, ge4, txn)) == [v for v in want if v >= 4], (con, snap)
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_obsolete_filters(ctx, golden, encoding):
+    """test/sql/filter/test_obsolete_filters.test's 33 integer queries through the table
+    function: AND chains on nullable a (redundant, subsumed, contradictory) return the file's
+    (a, b) rows, with a unindexed or indexed."""
+    (a, av), (b, bv) = obsolete_filter_columns(golden)
+    t = CubitTable(ctx, len(a))
+    t.add_column(0, a, validity=validity_from_mask(av))
+    t.add_column(1, b, validity=validity_from_mask(bv))
+    if encoding is not None:
+        t.build_index(0, encoding)
+    for where, fs, want in obsolete_filter_sets(golden):
+        rows = t.scan(fs)
+        got = sorted((int(a[r]) if av[r] else None, int(b[r]) if bv[r] else None) for r in rows)
+        assert got == want, (where, encoding)
+        fn = CubitScanFunction(t, [0, 1], None, fs)
+        local = fn.init_local()
+        seen = []
+        while True:
+            chunk = fn.function(local)
+            if len(chunk[0]) == 0:
+                break
+            seen += list(zip(chunk[0].tolist(), chunk[1].tolist()))
+        assert len(seen) == len(want), (where, encoding)
     t.close()
 
 

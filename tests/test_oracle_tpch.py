@@ -412,6 +412,39 @@ def test_zonemap_or_trees_reference_case(golden):
         assert n == q["count"], q["sql"]
 
 
+def obsolete_filter_sets(golden):
+    """test_obsolete_filters.test's integer queries as (WHERE text, TableFilterSet of the AND
+    chain on column a, expected (a, b) rows sorted)."""
+    c = golden["cases"]["obsolete_filters"]
+    op = {"<>": "!="}
+    for q in c["queries"]:
+        fs = F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(op.get(o, o), k) for o, k in q["terms"]])})
+        yield q["where"], fs, sorted(tuple(r) for r in q["rows"])
+
+
+def obsolete_filter_columns(golden):
+    c = golden["cases"]["obsolete_filters"]
+    out = []
+    for vals in (c["a"], c["b"]):
+        valid = np.array([v is not None for v in vals])
+        data = np.array([0 if v is None else v for v in vals], dtype=np.int32)
+        out.append((data, valid))
+    return out
+
+
+def test_obsolete_filters_reference_case(golden):
+    """test/sql/filter/test_obsolete_filters.test: redundant, subsumed and contradictory AND
+    chains on one nullable column return the file's rows."""
+    from cubit_amd.datagen import validity_from_mask
+
+    (a, av), (b, bv) = obsolete_filter_columns(golden)
+    cols = [O.Column(a, validity_from_mask(av)), O.Column(b, validity_from_mask(bv))]
+    for where, fs, want in obsolete_filter_sets(golden):
+        rows = O.table_scan(cols, F.serialize(fs), len(a))
+        got = sorted((int(a[r]) if av[r] else None, int(b[r]) if bv[r] else None) for r in rows)
+        assert got == want, where
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
