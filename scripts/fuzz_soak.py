@@ -33,7 +33,22 @@ def round_(ctx, seed, n, with_updates):
         d = rng.integers(0, 50, n).astype(np.int32 if c % 2 == 0 else np.int64)
         valid = rng.random(n) > (0.12 if c != 1 else 0.0)
         vw = validity_from_mask(valid) if c != 1 else None
-        t.add_column(c, d, vw)
+        if c == 3:
+            # any integral type DuckDB holds, registered plain (widened on the device) or as
+            # BITPACKING segments under a random forced mode, the packed filter on or off
+            dt = np.dtype(rng.choice(["int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64"]))
+            typed = d.astype(dt)
+            if rng.random() < 0.5:
+                c3 = O.bp_compress(typed, valid.astype(np.uint8), str(rng.choice(["auto", "for", "delta_for"])))
+                if c3 is None:
+                    c3 = O.bp_compress(typed, valid.astype(np.uint8), "auto")
+                t.add_bitpacked_column(c, c3.data, c3.seg_off, c3.seg_count, dt, validity=vw)
+                t.use_packed_filter(bool(rng.random() < 0.5))
+            else:
+                t.add_column(c, typed, vw)
+            d = typed.astype(np.int32 if dt.itemsize <= 2 or dt == np.int32 else np.int64)
+        else:
+            t.add_column(c, d, vw)
         data.append((d, vw))
     t.build_index(0, L.INDEX_RANGE)
     t.build_index(1, L.INDEX_EQUALITY)
