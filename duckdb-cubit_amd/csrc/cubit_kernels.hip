@@ -1159,7 +1159,7 @@ __device__ uint64_t lookback_recount(const EvalArgs& a, uint32_t b, int t, uint3
     return total;
 }
 // DBG (diagnostic builds, scripts/smallbench.hip; 0 in the library): 1 no spin, 2 no ids, 4 no
-// sleep, 8 no flag loads, 16 no LDS decode.
+// sleep, 8 no flag loads, 16 no LDS decode, 64 the staging loop without its LDS stores.
 // Measured and not kept (scripts/smallbench.hip; profiles/r03e_*, r03g_*, r03h_*): eight copies of
 // every flag, each reader on its own; a two-level walk (groups of 64 tiles + group totals); flag
 // loads issued before the LDS decode; a decoupled look-back (aggregate, then inclusive-prefix flags,
@@ -1234,6 +1234,15 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
             for (int e = 0; e < 2; ++e) {
                 uint64_t w = r[2 * p + e];
                 const uint32_t wrow = (uint32_t)((p * 2 * THREADS + 2 * t + e) * 64);
+                if (DBG & 64) {  // diagnostic: the loop without its LDS stores (positions summed)
+                    uint32_t acc = 0;
+                    while (w) {
+                        acc += wrow + (uint32_t)__builtin_ctzll(w) + off++;
+                        w &= w - 1;
+                    }
+                    if (acc == 0xffffffffu) s_stage[0] = acc;
+                    continue;
+                }
                 while (w) {
                     s_stage[off++] = wrow + (uint32_t)__builtin_ctzll(w);
                     w &= w - 1;

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(512, WPC * 2) void eval_decode_lookback_r03(EvalArg
 
 
 // look-back variants: the kernel's diagnostic switches (DBG: 1 no spin, 2 no ids, 4 no sleep,
-// 8 no flag loads, 16 no LDS decode)
+// 8 no flag loads, 16 no LDS decode, 64 the staging loop without its LDS stores)
 template <int K, int SAUX, int DBG>
 void lookback_variant(EvalArgs& a, uint64_t* dir, hipStream_t st) {
     hipLaunchKernelGGL((eval_decode_lookback<K, FORM_CONJ, kLookbackStage, lookback_wpc(K), SAUX, DBG>), dim3(a.num_tiles),
@@ -292,6 +292,7 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&cnt, 16));
         CK(hipMalloc(&dir, 4 * (uint64_t)tiles * 8 + 64));
         CK(hipMalloc(&dir_ref, 2 * (uint64_t)tiles * 8 + 64));
+        uint64_t* d_prefix = nullptr;
         EvalArgs base{};
         for (int k = 0; k < c.k; ++k) base.prog.leaf[k] = leaf[k];
         base.prog.n_leaves = c.k;
@@ -355,6 +356,49 @@ int main(int argc, char** argv) {
                               a.epoch = ++epoch;
                               (c.k == 4 ? lookback_t256<4> : lookback_t256<1>)(a, dir, st);
                           }, true, 2});
+        // K = 1: the decode with its tile offsets known (EvalArgs::tile_prefix, as a single index
+        // leaf decodes from its per-zone counts), and its diagnostic cuts: no ids written (DBG 2),
+        // no LDS staging of the ids (16; the copy-out still runs), the copy-out only (2|16 = 18 is
+        // not a variant: 2 returns first)
+        if (c.k == 1) {
+            if (!d_prefix) {
+                // per-tile counts from one look-back decode, exclusive prefix on the host
+                EvalArgs a = base;
+                a.epoch = ++epoch;
+                CK(launch_eval_decode(a, dir, grid, s, nullptr, nullptr, 3, cus));
+                CK(hipStreamSynchronize(s));
+                std::vector<uint64_t> d(2 * (uint64_t)tiles);
+                CK(hipMemcpy(d.data(), dir, d.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<uint64_t> pre(tiles);
+                uint64_t acc = 0;
+                for (uint32_t tt = 0; tt < tiles; ++tt) {
+                    pre[tt] = acc;
+                    acc += d[2 * tt + 1];
+                }
+                CK(hipMalloc(&d_prefix, tiles * 8ull));
+                CK(hipMemcpy(d_prefix, pre.data(), tiles * 8ull, hipMemcpyHostToDevice));
+            }
+            vs.push_back({"prefixed (offsets known)", [&](EvalArgs& a, hipStream_t st) {
+                              a.tile_prefix = d_prefix;
+                              hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 0>),
+                                                 dim3(a.num_tiles), dim3(512), 0, st, a, dir);
+                          }, true});
+            vs.push_back({"prefixed DBG staging loop without LDS stores", [&](EvalArgs& a, hipStream_t st) {
+                              a.tile_prefix = d_prefix;
+                              hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 64>),
+                                                 dim3(a.num_tiles), dim3(512), 0, st, a, dir);
+                          }, false});
+            vs.push_back({"prefixed DBG no ids", [&](EvalArgs& a, hipStream_t st) {
+                              a.tile_prefix = d_prefix;
+                              hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 2>),
+                                                 dim3(a.num_tiles), dim3(512), 0, st, a, dir);
+                          }, false});
+            vs.push_back({"prefixed DBG no LDS staging", [&](EvalArgs& a, hipStream_t st) {
+                              a.tile_prefix = d_prefix;
+                              hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 16>),
+                                                 dim3(a.num_tiles), dim3(512), 0, st, a, dir);
+                          }, false});
+        }
         vs.push_back({"AUTO (library policy)", [&](EvalArgs& a, hipStream_t st) {
                           a.epoch = ++epoch;
                           CK(launch_eval_decode(a, dir, grid, st, nullptr, nullptr, 0, cus));
@@ -452,6 +496,7 @@ int main(int argc, char** argv) {
         CK(hipFree(cnt));
         CK(hipFree(dir));
         CK(hipFree(dir_ref));
+        if (d_prefix) CK(hipFree(d_prefix));
     }
     return 0;
 }
