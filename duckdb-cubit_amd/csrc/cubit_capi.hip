@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -1099,6 +1100,10 @@ struct cubit_table {
     // the last planned program, when it is one table-owned index bitvector as it stands (no
     // complement, no patch): its per-zone counts give the decode its offsets up front
     const uint64_t* single_leaf = nullptr;
+    // CUBIT_HOST_TIMING: host time of cubit_table_scan split into planning, tile offsets and
+    // launch (ns, summed), printed when the table is destroyed (diagnostic)
+    uint64_t host_ns[3] = {0, 0, 0};
+    uint64_t host_scans = 0;
     uint32_t last_decoded = 0;  // sum_product: values of b decoded from its index (0 = gathered)
     uint64_t* dummy_count = nullptr;
     std::unique_ptr<DevBuf> dummy;
@@ -1398,9 +1403,23 @@ extern "C" int cubit_table_create(cubit_ctx* ctx, uint64_t n_rows, int64_t row_b
     return CUBIT_OK;
 }
 
+bool host_timing() {
+    static const bool on = std::getenv("CUBIT_HOST_TIMING") != nullptr;
+    return on;
+}
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 extern "C" int cubit_table_destroy(cubit_table* t) {
     if (!t) return CUBIT_OK;
     CUBIT_LOCK(t->ctx);
+    if (host_timing() && t->host_scans)
+        std::fprintf(stderr, "cubit host timing: %llu scans; per scan plan %.2f us, tile offsets %.2f us, launch %.2f us\n",
+                     (unsigned long long)t->host_scans, t->host_ns[0] * 1e-3 / t->host_scans,
+                     t->host_ns[1] * 1e-3 / t->host_scans, t->host_ns[2] * 1e-3 / t->host_scans);
     (void)hipSetDevice(t->ctx->device);
     (void)hipStreamSynchronize(t->ctx->stream);
     delete t;
@@ -3564,7 +3583,9 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
     const bool zonemap = (flags & CUBIT_SCAN_NO_ZONEMAP) == 0;
     t->last_zones = real_zones(t);
     t->last_live = 0;
+    const uint64_t h0 = host_timing() ? now_ns() : 0;
     if (int rc = plan_program(t, nodes, n_nodes, txn, em, &empty, zonemap ? &live : nullptr)) return rc;
+    const uint64_t h1 = host_timing() ? now_ns() : 0;
     if (empty) {  // the filter folded to FALSE (or the zonemaps rule out every zone): no launch, no tiles
         t->ctx->last_tiles = 0;
         HIP_CHECK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), t->ctx->stream));
@@ -3577,10 +3598,19 @@ extern "C" int cubit_table_scan(cubit_table* t, const cubit_filter_node* nodes, 
         prefix = tile_prefix_of(t, t->single_leaf, &rc);
         if (rc) return rc;
     }
-    return run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
-                    nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
-                    (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0,
-                    live.empty() ? nullptr : &live, prefix);
+    const uint64_t h2 = host_timing() ? now_ns() : 0;
+    const int rc = run_eval(t->ctx, em.prog, t->n_rows, t->row_base, count_only ? nullptr : d_rowids, capacity, d_count,
+                            nullptr, count_only ? RunMode::kCount : RunMode::kDecode, true,
+                            (flags & CUBIT_SCAN_ORDERED) != 0, (flags & CUBIT_SCAN_CHECK_CAPACITY) != 0,
+                            live.empty() ? nullptr : &live, prefix);
+    if (host_timing()) {
+        const uint64_t h3 = now_ns();
+        t->host_ns[0] += h1 - h0;
+        t->host_ns[1] += h2 - h1;
+        t->host_ns[2] += h3 - h2;
+        t->host_scans++;
+    }
+    return rc;
 }
 
 // cubit_table_scan and its tile directory under one hold of the context lock: the directory is
