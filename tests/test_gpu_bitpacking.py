@@ -423,3 +423,36 @@ def test_plain_columns_of_every_type(ctx, dtype):
         with pytest.raises(Exception, match="2\\^63"):
             t2.add_column(0, big)
         t2.close()
+
+
+@pytest.mark.parametrize("mode", ["auto", "for", "delta_for", "constant_delta"])
+def test_fused_sum_reads_uint32_segments(ctx, mode):
+    """The fused sum reading `a` at the qualifying rows straight from UINTEGER segments (an
+    INT64 column of 32-bit T: CONSTANT / CONSTANT_DELTA / FOR values taken in T's arithmetic,
+    including descending runs whose deltas wrap in uint32): equal to numpy and to the plain
+    column's sum."""
+    rng = np.random.default_rng({"auto": 11, "for": 12, "delta_for": 13, "constant_delta": 14}[mode])
+    n = 300_007
+    a = rng.integers(0, 2 ** 32 - 1, n, dtype=np.uint64).astype(np.uint32)
+    a[:2048] = 7
+    a[2048:4096] = (4_000_000_000 - 3 * np.arange(2048)).astype(np.uint32)   # constant step -3
+    a[4096:6144] = np.sort(rng.integers(0, 2 ** 31, 2048, dtype=np.uint64))[::-1].astype(np.uint32)
+    c = O.bp_compress(a, None, mode)
+    assert c is not None
+    b = rng.integers(0, 11, n).astype(np.int64)
+    key = rng.integers(0, 100, n).astype(np.int32)
+    t = CubitTable(ctx, n, row_base=2)
+    t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, np.uint32)
+    assert np.array_equal(t.download_column(0), a.astype(np.int64))
+    t.add_column(1, b)
+    t.add_column(2, key)
+    t.build_index(2, L.INDEX_RANGE)
+    for f in (F.ConstantFilter("<", 5), F.ConstantFilter(">=", 90)):
+        fs = F.TableFilterSet({2: f})
+        keep = key < 5 if f.comparison == "<" else key >= 90
+        want = int((a[keep].astype(object) * b[keep].astype(object)).sum())
+        s_packed, _ = t.sum_product(0, 1, fs, gather_b=True)
+        assert t.last_sum_packed()
+        s_plain, _ = t.sum_product(0, 1, fs, gather_b=True, packed_a=False)
+        assert s_packed == want and s_plain == want, (mode, f.comparison)
+    t.close()
