@@ -212,12 +212,33 @@ def main():
     ob = {"source": "test/sql/filter/test_obsolete_filters.test",
           "a": [1, 2, 3, 4, 5, None], "b": [10, 12, 14, 16, None, None], "queries": ob_q}
     assert len(ob_q) >= 30, len(ob_q)
+    # the index variant (ART scans, here the bitmap index) on the reference's ART scan
+    # tests: test/sql/index/art/scan/test_art_negative_range_scan.test (range(-500, 500), sums of
+    # closed ranges) and test_art_many_matches.test (0, 1 interleaved n times, counts of every
+    # comparison), read from the files
+    art_dir = REF / "test/sql/index/art/scan"
+    neg_src = (art_dir / "test_art_negative_range_scan.test").read_text()
+    assert "INSERT INTO integers SELECT * FROM range(-500, 500, 1)" in neg_src
+    neg = [{"ge": int(a), "le": int(b), "sum": int(float(v))} for a, b, v in re.findall(
+        r"query R\nSELECT sum\(i\) FROM integers WHERE i >= (-?\d+) AND i <= (-?\d+)\n----\n(-?[0-9.]+)", neg_src)]
+    mm_src = (art_dir / "test_art_many_matches.test").read_text()
+    blocks = []
+    for part in mm_src.split("BEGIN TRANSACTION")[1:]:
+        m = re.search(r"RANGE\(0, (\d+), 1\) t2\(j\), \(VALUES \(0\), \(1\)\) t1\(i\) ORDER BY j, i", part)
+        qs = [[op, int(k), int(v)] for op, k, v in re.findall(
+            r"query I\nSELECT COUNT\(\*\) FROM integers WHERE i(<=|>=|<|>|=)(\d+)\n----\n(\d+)", part)]
+        blocks.append({"pairs": int(m.group(1)), "counts": qs})
+    art = {"negative_range": {"source": "test/sql/index/art/scan/test_art_negative_range_scan.test",
+                              "range": [-500, 500], "queries": neg},
+           "many_matches": {"source": "test/sql/index/art/scan/test_art_many_matches.test", "blocks": blocks}}
+    assert len(neg) == 3 and len(blocks) == 2 and all(len(b["counts"]) == 6 for b in blocks)
     (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
                                                           "many_updaters": mu, "block_boundary_update": bb,
-                                                          "zonemap_or_trees": zt, "obsolete_filters": ob},
+                                                          "zonemap_or_trees": zt, "obsolete_filters": ob,
+                                                          "art_scans": art},
                                                          indent=1, sort_keys=True) + "\n")
 
 

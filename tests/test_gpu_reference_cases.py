@@ -8,7 +8,7 @@ from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import (block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
+from test_oracle_tpch import (art_scan_cases, block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
                               obsolete_filter_columns, obsolete_filter_sets, residual_from_json, update_case_views,
                               zonemap_table)
 
@@ -149,6 +149,24 @@ def test_many_updaters(ctx, golden, encoding):
         assert sorted(select_all(t, F.TableFilterSet(), txn)) == want, (con, snap)
         assert sorted(select_all(t, ge4, txn)) == [v for v in want if v >= 4], (con, snap)
     t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_art_scans(ctx, golden, encoding):
+    """The reference's ART scan tests (test_art_negative_range_scan, test_art_many_matches) on
+    the index variant: the bitmap index in place of the ART (or no index), sums through the
+    table function and counts through the count kernel equal the files'."""
+    for v, queries in art_scan_cases(golden):
+        t = CubitTable(ctx, len(v))
+        t.add_column(0, v)
+        if encoding is not None:
+            t.build_index(0, encoding)
+        for fs, kind, want in queries:
+            if kind == "sum":
+                assert sum(select_all(t, fs, None)) == want, (encoding, want)
+            else:
+                assert t.count(fs) == want and len(t.scan(fs)) == want, (encoding, want)
+        t.close()
 
 
 @pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])

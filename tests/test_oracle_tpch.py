@@ -445,6 +445,29 @@ def test_obsolete_filters_reference_case(golden):
         assert got == want, where
 
 
+def art_scan_cases(golden):
+    """The reference's ART scan tests as (values, [(TableFilterSet, "sum" | "count", expected)]):
+    test_art_negative_range_scan.test (closed ranges over range(-500, 500)) and
+    test_art_many_matches.test (0, 1 interleaved, every comparison)."""
+    c = golden["cases"]["art_scans"]
+    lo, hi = c["negative_range"]["range"]
+    yield np.arange(lo, hi, dtype=np.int32), [
+        (F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", q["ge"]), F.ConstantFilter("<=", q["le"])])}),
+         "sum", q["sum"]) for q in c["negative_range"]["queries"]]
+    for b in c["many_matches"]["blocks"]:
+        v = np.tile(np.array([0, 1], dtype=np.int32), b["pairs"])
+        yield v, [(F.TableFilterSet({0: F.ConstantFilter(op, k)}), "count", want) for op, k, want in b["counts"]]
+
+
+def test_art_scans_reference_case(golden):
+    """test/sql/index/art/scan/test_art_{negative_range_scan,many_matches}.test on the oracle."""
+    for v, queries in art_scan_cases(golden):
+        for fs, kind, want in queries:
+            rows = O.table_scan([O.Column(v)], F.serialize(fs), len(v))
+            got = int(v[rows].sum()) if kind == "sum" else len(rows)
+            assert got == want, (kind, want)
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
