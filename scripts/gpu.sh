@@ -14,6 +14,7 @@
 #                              --pmc pass each for FETCH_SIZE and WRITE_SIZE (never combined)
 #   dist1                      the bench as one torchrun rank over RCCL (the N > 1 code path)
 #   dist2                      two gloo ranks sharing the GPU (strong scaling rehearsal)
+#   distg:<n>                  n gloo ranks sharing the GPU (n <= 4 here: the N = 8 case is the driver's)
 #   run:<cmd,args>             any other command (e.g. run:./scripts/smallbench,10)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -64,6 +65,11 @@ for step in "$@"; do
       CUBIT_BENCH_SHARE_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 2 --steps 10 --warmup 3 --dist-backend gloo \
           --no-cpu-baseline > "$OUT/$n.bench_dist2_gloo.json" 2> "$log" ;;
+    distg)
+      [ "$rest" -ge 2 ] && [ "$rest" -le 4 ] || { echo "distg: 2 to 4 ranks" >&2; exit 2; }
+      CUBIT_BENCH_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$rest" \
+          --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus "$rest" --steps 10 --warmup 3 --dist-backend gloo \
+          --no-cpu-baseline > "$OUT/$n.bench_dist${rest}_gloo.json" 2> "$log" ;;
     run)
       timeout -k 10 600 ${rest//,/ } > "$log" 2>&1 ;;
     *)
