@@ -71,7 +71,7 @@ def _worker(rank, world, port, sf, result_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_partitioned_q6_gathers_to_whole_table_result(tmp_path, world, li01):
     from cubit_amd import filters as F
     from oracle import oracle as O
