@@ -1177,6 +1177,9 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
     __shared__ uint32_t s_list_n;
     __shared__ uint32_t s_list_scratch[THREADS];
     __shared__ uint32_t s_stage[STAGE];
+    // a dense tile's result words, kept here across the look-back walk (16 KiB: three workgroups
+    // per CU still fit the 160 KiB) instead of being read and evaluated a second time
+    __shared__ uint64_t s_words[(uint32_t)THREADS * 2 * PAIRS];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t tile = tile_at(a, b);
@@ -1226,6 +1229,10 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
         __hip_atomic_store(a.flags + b, (a.epoch << kFlagCntBits) | (uint64_t)tile_count, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     const bool staged = tile_count <= (uint32_t)STAGE;
+    if (!staged && write_ids && !(DBG & 2)) {
+#pragma unroll
+        for (int j = 0; j < NW; ++j) s_words[(uint32_t)j * THREADS + t] = r[j];
+    }
     if (!(DBG & 16) && staged && write_ids && tile_count) {
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
@@ -1292,12 +1299,11 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
         emit_ids<THREADS, SAUX>(a.rowids, a.capacity, s_stage, tile_count, base, row0, t);
         return;
     }
-    // dense tile: rounds of STAGE ids through the stage. Its words are read and evaluated once
-    // more here (more than STAGE ids: the id writes outweigh the re-read ≥ 4:1 for K ≤ 4), so
-    // no result word is held in registers across the look-back walk and its expiry recount.
-    load_tile<K, PAIRS, THREADS>(a, tile_word0, t, v);
-    eval_words<K, NW, FORM>(a.prog, v, r);
-    tail_mask<NW, THREADS>(a, tile_word0, t, r);
+    // dense tile: rounds of STAGE ids through the stage, its result words back from s_words (no
+    // word is held in registers across the look-back walk and its expiry recount; reading and
+    // evaluating the tile a second time instead cost 39.2 vs 30.7 µs for 673 dense tiles)
+#pragma unroll
+    for (int j = 0; j < NW; ++j) r[j] = s_words[(uint32_t)j * THREADS + t];
     for (uint32_t r0 = 0; r0 < tile_count; r0 += (uint32_t)STAGE) {
         const uint32_t r1 = min(tile_count, r0 + (uint32_t)STAGE);
         if (r0) __syncthreads();  // the previous round's copy-out is done
