@@ -3,7 +3,8 @@
 a larger size and for a fixed wall-clock budget, with fresh seeds — random pushed
 TableFilterSets and residual AND/OR trees over range / equality / edge-keyed range + bins /
 unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
-updates from a writer. Every result is compared with the oracle; prints one summary line.
+updates from a writer; each scan under a random decode kernel (AUTO, pair-claimed, run-claimed,
+look-back). Every result is compared with the oracle; prints one summary line.
 
   python scripts/fuzz_soak.py [seconds] [rows] [first seed]
 """
@@ -78,6 +79,8 @@ def round_(ctx, seed, n, with_updates):
         plan = F.serialize(fs, residual)
         start, tid = views[i % 3]
         ref = O.table_scan(ocols, plan, n, row_base=row_base, tx=O.Mvcc(start, tid, deleted=deleted))
+        # every decode kernel, not only the one AUTO picks at this size (results are identical)
+        ctx.set_decode_kernel(int(rng.choice([L.DECODE_AUTO, L.DECODE_PAIRS, L.DECODE_RUNS, L.DECODE_LOOKBACK])))
         got = t.scan(fs, residual, txn=L.Txn(start, tid), ordered=bool(i % 2))
         if i % 2 == 0:
             got = np.sort(got)
@@ -88,6 +91,7 @@ def round_(ctx, seed, n, with_updates):
             if c != len(ref):
                 raise AssertionError(f"seed {seed} case {i}: count {c} vs {len(ref)}")
         checks += 1
+    ctx.set_decode_kernel(L.DECODE_AUTO)
     t.close()
     return checks
 
