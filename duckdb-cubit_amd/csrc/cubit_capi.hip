@@ -955,6 +955,14 @@ extern "C" int cubit_narrow_i32(cubit_ctx* ctx, const int64_t* d_in, const uint6
     return CUBIT_OK;
 }
 
+extern "C" int cubit_narrow_i32_checked(cubit_ctx* ctx, const int64_t* d_in, const uint64_t* d_count, uint64_t max_n,
+                                        int64_t offset, int32_t* d_out, uint32_t* d_overflow) {
+    if (!ctx || !d_in || !d_count || !d_out || !d_overflow) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    HIP_CHECK(launch_narrow_i32(d_in, d_count, max_n, offset, d_out, ctx->stream, d_overflow));
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_gather_sum_product(cubit_ctx* ctx, const int64_t* d_a, const int64_t* d_b,
                                         const int64_t* d_rowids, const uint64_t* d_count, uint64_t max_n,
                                         int64_t row_base, int64_t* d_out) {
@@ -1018,6 +1026,14 @@ struct Updates {
     std::unique_ptr<DevBuf> rows, values, versions;
     std::vector<int64_t> h_rows, h_values;
     std::vector<uint64_t> h_versions;
+    // NULL-ness per record (the validity column's update chain, InitializeUpdateValidity,
+    // update_segment.cpp:588-600): 1 = the record's value, 0 = SET NULL. Empty / null when every
+    // record carries a value.
+    std::vector<uint8_t> h_valids;
+    std::unique_ptr<DevBuf> valids;
+    bool any_null = false;
+    const uint8_t* d_valids() const { return valids ? static_cast<const uint8_t*>(valids->p) : nullptr; }
+    bool valid_at(uint64_t i) const { return h_valids.empty() || h_valids[i]; }
     std::vector<uint64_t> distinct_versions;  // sorted
     uint64_t n = 0;
     // distinct updated values, sorted: the update statistics the planner widens the index
@@ -1892,20 +1908,23 @@ std::vector<int64_t> distinct_sorted(const int64_t* v, uint64_t n) {
     return out;
 }
 
-// store an update list (rows, values, versions) for col: records grouped by row, each row's
-// records kept in chronological order (UpdateInfo chains, update_info.hpp)
+// store an update list (rows, values, versions, and NULL-ness when valids is not null) for col:
+// records grouped by row, each row's records kept in chronological order (UpdateInfo chains,
+// update_info.hpp)
 int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* values, const uint64_t* versions,
-                  uint64_t n) {
+                  uint64_t n, const uint8_t* valids = nullptr) {
     std::vector<uint64_t> order(n);
     for (uint64_t i = 0; i < n; ++i) order[i] = i;
     if (!std::is_sorted(rows, rows + n))  // grouping keeps each row's records in list order
         std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
     Updates u;
     u.n = n;
+    for (uint64_t i = 0; valids && i < n; ++i) u.any_null |= valids[i] == 0;
     for (uint64_t i : order) {
         u.h_rows.push_back(rows[i]);
         u.h_values.push_back(values[i]);
         u.h_versions.push_back(versions[i]);
+        if (u.any_null) u.h_valids.push_back(valids[i] ? 1 : 0);
     }
     {
         const auto dv = distinct_sorted(reinterpret_cast<const int64_t*>(u.h_versions.data()), n);
@@ -1913,7 +1932,14 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
         u.distinct_versions.assign(dv.begin(), dv.end());
         std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
     }
-    u.stat_values = distinct_sorted(u.h_values.data(), n);
+    if (u.any_null) {  // the statistics cover the records that carry a value
+        std::vector<int64_t> vv;
+        for (uint64_t i = 0; i < n; ++i)
+            if (u.h_valids[i]) vv.push_back(u.h_values[i]);
+        u.stat_values = distinct_sorted(vv.data(), vv.size());
+    } else {
+        u.stat_values = distinct_sorted(u.h_values.data(), n);
+    }
     u.rows = std::make_unique<DevBuf>();
     u.values = std::make_unique<DevBuf>();
     u.versions = std::make_unique<DevBuf>();
@@ -1925,6 +1951,11 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
         HIP_CHECK(hipMemcpy(u.rows->p, u.h_rows.data(), n * 8, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(u.values->p, u.h_values.data(), n * 8, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(u.versions->p, u.h_versions.data(), n * 8, hipMemcpyHostToDevice));
+    }
+    if (u.any_null) {
+        u.valids = std::make_unique<DevBuf>();
+        if (hipMalloc(&u.valids->p, n) != hipSuccess) return fail(CUBIT_ERR_OOM, "update list allocation failed");
+        HIP_CHECK(hipMemcpy(u.valids->p, u.h_valids.data(), n, hipMemcpyHostToDevice));
     }
     t->upd[col] = std::move(u);
     return CUBIT_OK;
@@ -1941,6 +1972,41 @@ extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* r
     for (uint64_t i = 0; i < n; ++i)
         if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
     return store_updates(t, col, rows, values, versions, n);
+}
+
+namespace {
+
+// A validity bitvector for a column registered without one (every row valid): a SET NULL
+// record, visible or merged, needs the NN leaf to patch or flip (the planner folds IS NOT NULL on
+// a column without validity to TRUE).
+int ensure_validity(cubit_table* t, Column& c) {
+    if (c.validity) return CUBIT_OK;
+    auto b = std::make_unique<DevBuf>();
+    if (int rc = alloc_table_bv(t, *b)) return fail(rc, "validity allocation failed");
+    if (t->n_rows) HIP_CHECK(launch_fill_valid(static_cast<uint64_t*>(b->p), t->n_rows, t->ctx->stream));
+    c.validity = static_cast<const uint64_t*>(b->p);
+    c.owned.push_back(std::move(b));
+    drop_zones(t);
+    return CUBIT_OK;
+}
+
+}  // namespace
+
+extern "C" int cubit_table_set_updates_nullable(cubit_table* t, int col, const int64_t* rows, const int64_t* values,
+                                                const uint8_t* valid, const uint64_t* versions, uint64_t n) {
+    if (!t || (n && (!rows || !values || !versions))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    auto cit = t->cols.find(col);
+    if (cit == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    bool any_null = false;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
+        any_null |= valid && !valid[i];
+    }
+    if (any_null)
+        if (int rc = ensure_validity(t, cit->second)) return rc;
+    return store_updates(t, col, rows, values, versions, n, any_null ? valid : nullptr);
 }
 
 // ------------------------------------------------------------------ index maintenance
@@ -2254,7 +2320,9 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     Column& c = cit->second;
     const Updates& u = uit->second;
     std::vector<int64_t> m_rows, m_vals, k_rows, k_vals;
+    std::vector<uint8_t> m_valid, k_valid;
     std::vector<uint64_t> k_vers;
+    bool m_null = false;
     for (uint64_t i = 0; i < u.n;) {
         uint64_t j = i;
         while (j < u.n && u.h_rows[j] == u.h_rows[i]) ++j;
@@ -2262,16 +2330,20 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         while (p < j && u.h_versions[p] < horizon) ++p;
         if (p > i) {
             const int64_t v = u.h_values[p - 1];
-            if (c.type == CUBIT_TYPE_INT32 && (v < INT32_MIN || v > INT32_MAX))
+            const bool ok = u.valid_at(p - 1);  // the newest merged record decides value and NULL-ness
+            if (ok && c.type == CUBIT_TYPE_INT32 && (v < INT32_MIN || v > INT32_MAX))
                 return fail(CUBIT_ERR_INVALID, "row %lld: value %lld does not fit an INT32 column",
                             (long long)u.h_rows[i], (long long)v);
             m_rows.push_back(u.h_rows[i]);
-            m_vals.push_back(v);
+            m_vals.push_back(ok ? v : 0);
+            m_valid.push_back(ok ? 1 : 0);
+            m_null |= !ok;
         }
         for (uint64_t q = p; q < j; ++q) {
             k_rows.push_back(u.h_rows[q]);
             k_vals.push_back(u.h_values[q]);
             k_vers.push_back(u.h_versions[q]);
+            k_valid.push_back(u.valid_at(q) ? 1 : 0);
         }
         i = j;
     }
@@ -2279,13 +2351,17 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     HIP_CHECK(hipStreamSynchronize(s));
     drop_zones(t);  // the merge flips index bits in place
     if (int rc = own_column(t, c, std::max<uint64_t>(t->n_rows, c.cap_rows))) return rc;
+    if (m_null)
+        if (int rc = ensure_validity(t, c)) return rc;
     c.drop_packed();  // merged values are not in the segments
     const uint64_t m = m_rows.size();
-    DevBuf d_rows, d_vals;
-    if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess)
+    DevBuf d_rows, d_vals, d_valid;
+    if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess ||
+        (m_null && hipMalloc(&d_valid.p, m) != hipSuccess))
         return fail(CUBIT_ERR_OOM, "merge list allocation failed");
     HIP_CHECK(hipMemcpyAsync(d_rows.p, m_rows.data(), m * 8, hipMemcpyHostToDevice, s));
     HIP_CHECK(hipMemcpyAsync(d_vals.p, m_vals.data(), m * 8, hipMemcpyHostToDevice, s));
+    if (m_null) HIP_CHECK(hipMemcpyAsync(d_valid.p, m_valid.data(), m, hipMemcpyHostToDevice, s));
     Index* ixs[2] = {t->idx.count(col) ? &t->idx[col] : nullptr, t->bins.count(col) ? &t->bins[col] : nullptr};
     MergeIndex mi[2] = {};
     DevBuf d_keys[2], d_bvs[2];
@@ -2302,13 +2378,18 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         mi[x].n_keys = (uint32_t)ix->keys.size();
         mi[x].encoding = ix->encoding == CUBIT_INDEX_RANGE ? 0 : ix->encoding == CUBIT_INDEX_EQUALITY ? 1 : 2;
     }
-    HIP_CHECK(launch_merge_rows(static_cast<const int64_t*>(d_rows.p), static_cast<const int64_t*>(d_vals.p), m,
-                                const_cast<void*>(c.data), c.type, const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
+    HIP_CHECK(launch_merge_rows(static_cast<const int64_t*>(d_rows.p), static_cast<const int64_t*>(d_vals.p),
+                                static_cast<const uint8_t*>(d_valid.p), m, const_cast<void*>(c.data), c.type,
+                                const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
     HIP_CHECK(hipStreamSynchronize(s));
-    // statistics and exact keys for the merged values
-    const std::vector<int64_t> added = distinct_sorted(m_vals.data(), m_vals.size());
+    // statistics and exact keys for the merged values (a merged NULL leaves the index bounds:
+    // they only have to contain the valid values)
+    std::vector<int64_t> valid_vals;
+    for (uint64_t i = 0; i < m; ++i)
+        if (m_valid[i]) valid_vals.push_back(m_vals[i]);
+    const std::vector<int64_t> added = distinct_sorted(valid_vals.data(), valid_vals.size());
     for (Index* ix : ixs) {
-        if (!ix) continue;
+        if (!ix || added.empty()) continue;
         const bool was_empty = ix->empty;
         const int64_t old_min = ix->vmin;
         ix->vmin = was_empty ? added.front() : std::min(ix->vmin, added.front());
@@ -2317,7 +2398,8 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         if (int rc = maintain_exact_keys(t, col, *ix, added, old_min, was_empty)) return rc;
     }
     // the records left (each row's suffix at or past horizon), still grouped and chronological
-    if (int rc = store_updates(t, col, k_rows.data(), k_vals.data(), k_vers.data(), k_rows.size())) return rc;
+    if (int rc = store_updates(t, col, k_rows.data(), k_vals.data(), k_vers.data(), k_rows.size(), k_valid.data()))
+        return rc;
     if (k_rows.empty()) t->upd.erase(col);
     drop_derived(t);
     if (n_merged) *n_merged = m;
@@ -2908,8 +2990,9 @@ int fit(cubit_table* t, ExprP& e) {
 // update_info.hpp:44-55). Done on the device: copy the leaf, clear the updated rows, then
 // set the rows whose visible value passes the leaf predicate.
 __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ values,
-                                  const uint64_t* __restrict__ versions, uint64_t n, uint64_t start_time,
-                                  uint64_t tid, int pred, int cmp, int64_t c, int64_t c2, uint64_t* __restrict__ bv) {
+                                  const uint8_t* __restrict__ valids, const uint64_t* __restrict__ versions, uint64_t n,
+                                  uint64_t start_time, uint64_t tid, int pred, int cmp, int64_t c, int64_t c2,
+                                  uint64_t* __restrict__ bv) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t ver = versions[i];
@@ -2927,8 +3010,12 @@ __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_
         }
         if (!newest) continue;
         const int64_t v = values[i];
+        // a SET NULL record: the row leaves the validity leaf and fails every comparison
+        // (UpdateMergeValidity, update_segment.cpp:94-99; NULL never passes a filter)
+        const bool ok = !valids || valids[i];
         bool p;
-        if (pred == 1) p = true;
+        if (pred == 1) p = ok;
+        else if (!ok) p = false;
         else if (pred == 2) p = v >= c && v < c2;
         else if (cmp == 0) p = v == c;
         else if (cmp == 1) p = v != c;
@@ -2978,8 +3065,9 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
             const unsigned grid = (unsigned)std::min<uint64_t>((u.n + 255) / 256, 4096);
             hipLaunchKernelGGL(patch_leaf_kernel, dim3(std::max(grid, 1u)), dim3(256), 0, t->ctx->stream,
                                static_cast<const int64_t*>(u.rows->p), static_cast<const int64_t*>(u.values->p),
-                               static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time, txn->transaction_id,
-                               e->leaf.pred, e->leaf.cmp, e->leaf.constant, e->leaf.constant2, copy);
+                               u.d_valids(), static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time,
+                               txn->transaction_id, e->leaf.pred, e->leaf.cmp, e->leaf.constant, e->leaf.constant2,
+                               copy);
             HIP_CHECK(hipGetLastError());
             patched[e->leaf.bv] = copy;
         }
@@ -3638,6 +3726,11 @@ extern "C" int cubit_table_scan_tiles(cubit_table* t, const cubit_filter_node* n
     return CUBIT_OK;
 }
 
+namespace {
+int probe_impl(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_rowids, const uint64_t* d_count,
+               uint64_t max_n, int64_t* d_out, uint64_t* d_valid);
+}  // namespace
+
 extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
                                        const cubit_txn* txn, int col_a, int col_b, int64_t* d_out,
                                        uint64_t* d_count, uint32_t flags) {
@@ -3662,19 +3755,21 @@ extern "C" int cubit_table_sum_product(cubit_table* t, const cubit_filter_node* 
         return txn && u != t->upd.end() && u->second.any_visible(txn);
     };
     if (visible_updates(col_a) || visible_updates(col_b)) {
-        // MVCC fallback: row ids, then the probe (which applies the visible updates), then
-        // a plain sum over the two value arrays
-        if (ait->second.validity || bit->second.validity)
-            return fail(CUBIT_ERR_UNSUPPORTED, "sum_product with visible updates on nullable columns");
+        // MVCC fallback: row ids, then the probe (which applies the visible updates, NULL-ness
+        // included), then a plain sum over the two value arrays. A nullable column probes with
+        // its validity, which leaves 0 at NULL rows: those rows add nothing, as SUM skips NULLs.
+        const bool nullable = ait->second.validity || bit->second.validity;
         const uint64_t cap = t->n_rows;
-        if (int rc = ensure_tmp(ctx, 3 * cap)) return rc;
+        const uint64_t vwords = nullable ? (cap + 63) / 64 : 0;
+        if (int rc = ensure_tmp(ctx, 3 * cap + vwords)) return rc;
         int64_t* ids = ctx->tmp_ids + 0;
         int64_t* xa = ctx->tmp_ids + cap;
         int64_t* xb = ctx->tmp_ids + 2 * cap;
+        uint64_t* vw = nullable ? reinterpret_cast<uint64_t*>(ctx->tmp_ids + 3 * cap) : nullptr;
         // the scan's own decode must not use tmp_ids (ordered flag off)
         if (int rc = cubit_table_scan(t, nodes, n_nodes, txn, ids, cap, count, 0)) return rc;
-        if (int rc = cubit_table_probe(t, col_a, txn, ids, count, cap, xa)) return rc;
-        if (int rc = cubit_table_probe(t, col_b, txn, ids, count, cap, xb)) return rc;
+        if (int rc = probe_impl(t, col_a, txn, ids, count, cap, xa, vw)) return rc;
+        if (int rc = probe_impl(t, col_b, txn, ids, count, cap, xb, vw)) return rc;
         HIP_CHECK(launch_sum_product_arrays(xa, xb, count, cap, ctx->partials, d_out, ctx->stream));
         ctx->last_tiles = 0;  // the directory described ids in scratch, not a caller's buffer
         return CUBIT_OK;
@@ -3779,6 +3874,9 @@ extern "C" int cubit_table_column_statistics(cubit_table* t, int col, int64_t* v
         lo = std::min(lo, uit->second.stat_values.front());
         hi = std::max(hi, uit->second.stat_values.back());
     }
+    // a SET NULL record makes the column nullable (UpdateValidityStatistics,
+    // update_segment.cpp:907-918: an update vector with an invalid row sets has_null)
+    if (uit != t->upd.end() && uit->second.any_null) any_null = true;
     if (vmin) *vmin = any_valid ? lo : 0;
     if (vmax) *vmax = any_valid ? hi : 0;
     if (has_null) *has_null = any_null ? 1 : 0;
@@ -3855,11 +3953,14 @@ extern "C" int cubit_table_last_sum_decode(cubit_table* t, uint32_t* n_values) {
 
 namespace {
 
-// visible value of updated rows for a probe: patch gathered values in place
+// visible value of updated rows for a probe: patch gathered values in place — and their
+// NULL-ness when out_valid is given (FetchRowValidity, update_segment.cpp:357-370: the newest
+// visible record of the validity chain sets the row's bit)
 __global__ void patch_probe_kernel(const int64_t* __restrict__ rowids, const uint64_t* __restrict__ d_count,
                                    uint64_t max_n, int64_t row_base, const int64_t* __restrict__ urows,
-                                   const int64_t* __restrict__ uvalues, const uint64_t* __restrict__ uversions,
-                                   uint64_t nu, uint64_t start_time, uint64_t tid, int64_t* __restrict__ out) {
+                                   const int64_t* __restrict__ uvalues, const uint8_t* __restrict__ uvalids,
+                                   const uint64_t* __restrict__ uversions, uint64_t nu, uint64_t start_time,
+                                   uint64_t tid, int64_t* __restrict__ out, uint64_t* __restrict__ out_valid) {
     const uint64_t n = min(*d_count, max_n);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -3871,11 +3972,53 @@ __global__ void patch_probe_kernel(const int64_t* __restrict__ rowids, const uin
             if (urows[mid] < r) lo = mid + 1;
             else hi = mid;
         }
+        int vis = -1;  // newest visible record of the row
         for (uint64_t j = lo; j < nu && urows[j] == r; ++j) {
             const uint64_t v = uversions[j];
-            if (v < start_time || v == tid) out[i] = uvalues[j];
+            if (v < start_time || v == tid) vis = (int)(j - lo);
+        }
+        if (vis < 0) continue;
+        const uint64_t j = lo + (uint64_t)vis;
+        const bool ok = !uvalids || uvalids[j];
+        out[i] = ok ? uvalues[j] : 0;
+        if (out_valid) {
+            unsigned long long* w = reinterpret_cast<unsigned long long*>(&out_valid[i >> 6]);
+            if (ok) atomicOr(w, 1ull << (i & 63));
+            else atomicAnd(w, ~(1ull << (i & 63)));
         }
     }
+}
+
+}  // namespace
+
+namespace {
+
+// K3 for cubit_table_probe (d_valid null: values only, a NULL row's slot as stored) and
+// cubit_table_probe_validity (values, 0 at NULL rows, and the validity words), then the visible
+// update records on top
+int probe_impl(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_rowids, const uint64_t* d_count,
+               uint64_t max_n, int64_t* d_out, uint64_t* d_valid) {
+    auto it = t->cols.find(col);
+    if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    const Column& c = it->second;
+    if (d_valid)
+        HIP_CHECK(launch_gather_valid(c.data, c.type, c.validity, d_rowids, d_count, max_n, t->row_base, d_out, d_valid,
+                                      t->ctx->stream));
+    else
+        HIP_CHECK(launch_gather(c.data, c.type, d_rowids, d_count, max_n, t->row_base, d_out, t->ctx->stream));
+    auto uit = t->upd.find(col);
+    if (txn && uit != t->upd.end() && uit->second.any_visible(txn)) {
+        const Updates& u = uit->second;
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((max_n + 255) / 256, 4096));
+        hipLaunchKernelGGL(patch_probe_kernel, dim3(grid), dim3(256), 0, t->ctx->stream, d_rowids, d_count, max_n,
+                           t->row_base, static_cast<const int64_t*>(u.rows->p),
+                           static_cast<const int64_t*>(u.values->p), u.d_valids(),
+                           static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time, txn->transaction_id,
+                           d_out, d_valid);
+        HIP_CHECK(hipGetLastError());
+    }
+    return CUBIT_OK;
 }
 
 }  // namespace
@@ -3884,22 +4027,15 @@ extern "C" int cubit_table_probe(cubit_table* t, int col, const cubit_txn* txn, 
                                  const uint64_t* d_count, uint64_t max_n, int64_t* d_out) {
     if (!t || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(t->ctx);
-    auto it = t->cols.find(col);
-    if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
-    if (int rc = set_device(t->ctx)) return rc;
-    HIP_CHECK(launch_gather(it->second.data, it->second.type, d_rowids, d_count, max_n, t->row_base, d_out,
-                            t->ctx->stream));
-    auto uit = t->upd.find(col);
-    if (txn && uit != t->upd.end() && uit->second.any_visible(txn)) {
-        const Updates& u = uit->second;
-        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((max_n + 255) / 256, 4096));
-        hipLaunchKernelGGL(patch_probe_kernel, dim3(grid), dim3(256), 0, t->ctx->stream, d_rowids, d_count, max_n,
-                           t->row_base, static_cast<const int64_t*>(u.rows->p),
-                           static_cast<const int64_t*>(u.values->p), static_cast<const uint64_t*>(u.versions->p), u.n,
-                           txn->start_time, txn->transaction_id, d_out);
-        HIP_CHECK(hipGetLastError());
-    }
-    return CUBIT_OK;
+    return probe_impl(t, col, txn, d_rowids, d_count, max_n, d_out, nullptr);
+}
+
+extern "C" int cubit_table_probe_validity(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_rowids,
+                                          const uint64_t* d_count, uint64_t max_n, int64_t* d_out,
+                                          uint64_t* d_validity) {
+    if (!t || !d_rowids || !d_count || !d_out || !d_validity) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    return probe_impl(t, col, txn, d_rowids, d_count, max_n, d_out, d_validity);
 }
 
 extern "C" int cubit_table_info(cubit_table* t, uint64_t* n_rows, int64_t* row_base, cubit_ctx** ctx) {

@@ -188,9 +188,14 @@ hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups,
 // a narrower / unsigned column (CUBIT_TYPE_INT8 … UINT64) widened to its INT32 / INT64 storage
 hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hipStream_t stream);
 hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,
-                             hipStream_t stream);
+                             hipStream_t stream, uint32_t* overflow = nullptr);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
+// the probe with NULL-ness: values (0 at NULL rows) and out_valid bit i = row rowids[i] valid
+// (⌈min(*d_count, max_n) / 64⌉ words written; validity nullptr = every row valid)
+hipError_t launch_gather_valid(const void* col, int type, const uint64_t* validity, const int64_t* rowids,
+                               const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* out,
+                               uint64_t* out_valid, hipStream_t stream);
 hipError_t launch_gather_sum_product(const int64_t* a, const int64_t* b, const int64_t* rowids,
                                      const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* partials,
                                      int64_t* out, hipStream_t stream);
@@ -252,7 +257,9 @@ struct MergeIndex {
 };
 hipError_t launch_splice_bits(uint64_t* dst, const uint64_t* src, uint64_t bit_off, uint64_t n_bits,
                               hipStream_t stream);
-hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, uint64_t m, void* col, int type,
-                             uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1, hipStream_t stream);
+// valids: per merged row 1 = the value, 0 = NULL (nullptr: every row valid; a NULL needs `validity`)
+hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, const uint8_t* valids, uint64_t m, void* col,
+                             int type, uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1,
+                             hipStream_t stream);
 
 }  // namespace cubit

@@ -2437,21 +2437,31 @@ __global__ __launch_bounds__(256) void bitpacked_compare_waves(const uint8_t* __
 // out[i] = (int32)(in[i] - offset) for i < min(*d_count, max_n): the DataChunk column of a
 // window crosses PCIe at 4 bytes per row when every value of the column lies within 2^31 of the
 // offset (the host mirror widens while it fills the chunk). 16-byte loads, 8-byte stores.
+// (overflow, optional: set to 1 when some value - offset lies outside int32 — the caller's bound
+// did not hold and the compacted copy must not be used)
 __global__ __launch_bounds__(256) void narrow_i32_kernel(const int64_t* __restrict__ in, const uint64_t* __restrict__ d_count,
-                                                          uint64_t max_n, int64_t offset, int32_t* __restrict__ out) {
+                                                          uint64_t max_n, int64_t offset, int32_t* __restrict__ out,
+                                                          uint32_t* __restrict__ overflow) {
     const uint64_t n = min(*d_count, max_n);
+    auto fits = [](int64_t d) { return d >= INT32_MIN && d <= INT32_MAX; };
+    bool bad = false;
     for (uint64_t i = 2 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 2ull * gridDim.x * blockDim.x) {
         if (i + 1 < n) {
             const u64x2 v = *reinterpret_cast<const u64x2*>(in + i);
+            const int64_t dx = (int64_t)((uint64_t)v.x - (uint64_t)offset), dy = (int64_t)((uint64_t)v.y - (uint64_t)offset);
+            bad |= !fits(dx) || !fits(dy);
             typedef int32_t i32x2 __attribute__((ext_vector_type(2)));
             i32x2 o;
-            o.x = (int32_t)((int64_t)v.x - offset);
-            o.y = (int32_t)((int64_t)v.y - offset);
+            o.x = (int32_t)dx;
+            o.y = (int32_t)dy;
             *reinterpret_cast<i32x2*>(out + i) = o;
         } else {
-            out[i] = (int32_t)(in[i] - offset);
+            const int64_t d = (int64_t)((uint64_t)in[i] - (uint64_t)offset);
+            bad |= !fits(d);
+            out[i] = (int32_t)d;
         }
     }
+    if (overflow && bad) *overflow = 1u;
 }
 
 // out[i] = in[i] widened: a column registered with a narrower or unsigned type code
@@ -2476,6 +2486,35 @@ __global__ __launch_bounds__(256) void gather_kernel(const T* __restrict__ col, 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         out[i] = (int64_t)__builtin_nontemporal_load(col + (__builtin_nontemporal_load(rowids + i) - row_base));
+}
+
+// K3 with NULL-ness (ColumnData::FilterScan + Vector::Slice carry the vector's validity with
+// its values, column_data.cpp:305-309, vector.cpp:223-258): out[i] = col[r] for a valid row and
+// 0 for a NULL one, and bit i of out_valid (LSB-first words over output positions — DuckDB's
+// ValidityMask layout) says whether row r is valid. A wave takes 64 consecutive positions, so
+// one ballot forms each word and lane 0 stores it: 1 bit per row beside the 8-byte value.
+template <typename T>
+__global__ __launch_bounds__(256) void gather_valid_kernel(const T* __restrict__ col,
+                                                           const uint64_t* __restrict__ validity,
+                                                           const int64_t* __restrict__ rowids,
+                                                           const uint64_t* __restrict__ d_count, uint64_t max_n,
+                                                           int64_t row_base, int64_t* __restrict__ out,
+                                                           uint64_t* __restrict__ out_valid) {
+    const uint64_t n = min(*d_count, max_n);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // the loop bound is the wave's first position: every lane of a wave runs the ballot together
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t i = base + lane;
+        bool ok = false;
+        if (i < n) {
+            const int64_t r = __builtin_nontemporal_load(rowids + i) - row_base;
+            ok = !validity || ((validity[r >> 6] >> (r & 63)) & 1ull);
+            out[i] = ok ? (int64_t)__builtin_nontemporal_load(col + r) : 0;
+        }
+        const uint64_t word = __ballot(ok);
+        if (lane == 0) out_valid[base >> 6] = word;
+    }
 }
 
 __global__ __launch_bounds__(256) void gather_sum_product_kernel(const int64_t* __restrict__ x,
@@ -2711,51 +2750,58 @@ __device__ __forceinline__ void flip_bit(uint64_t* bv, int64_t r) {
 }
 
 __global__ __launch_bounds__(256) void merge_rows_kernel(const int64_t* __restrict__ rows,
-                                                         const int64_t* __restrict__ values, uint64_t m, void* col,
+                                                         const int64_t* __restrict__ values,
+                                                         const uint8_t* __restrict__ valids, uint64_t m, void* col,
                                                          int type, uint64_t* validity, MergeIndex ix0, MergeIndex ix1) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
         const int64_t r = rows[i];
         const int64_t nv = values[i];
         const bool old_valid = !validity || ((validity[r >> 6] >> (r & 63)) & 1ull);
+        // a NULL record (UPDATE … SET x = NULL: the validity column's update chain,
+        // update_segment.cpp:588-600) clears the row's validity and leaves every index leaf
+        const bool new_valid = !valids || valids[i];
         int64_t ov;
         if (type == 0) {
             ov = static_cast<int32_t*>(col)[r];
-            static_cast<int32_t*>(col)[r] = (int32_t)nv;
+            static_cast<int32_t*>(col)[r] = new_valid ? (int32_t)nv : 0;
         } else {
             ov = static_cast<int64_t*>(col)[r];
-            static_cast<int64_t*>(col)[r] = nv;
+            static_cast<int64_t*>(col)[r] = new_valid ? nv : 0;
         }
-        if (!old_valid) atomicOr(reinterpret_cast<unsigned long long*>(&validity[r >> 6]), 1ull << (r & 63));
+        if (old_valid != new_valid) flip_bit(validity, r);
         for (int x = 0; x < 2; ++x) {
             const MergeIndex& ix = x ? ix1 : ix0;
             if (!ix.bvs) continue;
             const uint32_t n = ix.n_keys;
-            if (ix.encoding == 0) {  // range: L(k) = {valid, v < k}
-                uint32_t a, b;     // flip keys [a, b)
-                if (!old_valid) {
-                    a = upper_key(ix.keys, n, nv);  // new membership: every key > nv
-                    b = n;
-                } else {
+            if (ix.encoding == 0) {  // range: L(k) = {valid, v < k}; a valid value's keys are [upper(v), n)
+                uint32_t a = n, b = n;  // flip keys [a, b): the two memberships' symmetric difference
+                if (old_valid && new_valid) {
                     const int64_t lo = ov < nv ? ov : nv, hi = ov < nv ? nv : ov;
                     a = upper_key(ix.keys, n, lo);
                     b = upper_key(ix.keys, n, hi);  // keys in (lo, hi]
+                } else if (old_valid) {
+                    a = upper_key(ix.keys, n, ov);
+                } else if (new_valid) {
+                    a = upper_key(ix.keys, n, nv);
                 }
                 for (uint32_t k = a; k < b; ++k) flip_bit(ix.bvs[k], r);
             } else if (ix.encoding == 1) {  // equality: E(k) = {valid, v == k}
-                if (old_valid && ov == nv) continue;
+                if (old_valid && new_valid && ov == nv) continue;
                 if (old_valid) {
                     const uint32_t k = upper_key(ix.keys, n, ov);
                     if (k > 0 && ix.keys[k - 1] == ov) flip_bit(ix.bvs[k - 1], r);
                 }
-                const uint32_t k = upper_key(ix.keys, n, nv);
-                if (k > 0 && ix.keys[k - 1] == nv) flip_bit(ix.bvs[k - 1], r);
+                if (new_valid) {
+                    const uint32_t k = upper_key(ix.keys, n, nv);
+                    if (k > 0 && ix.keys[k - 1] == nv) flip_bit(ix.bvs[k - 1], r);
+                }
             } else {  // bins: B_i = {valid, e_i <= v < e_{i+1}}, n = edges
                 auto bin = [&](int64_t v) -> int64_t {
                     const uint32_t k = upper_key(ix.keys, n, v);  // e_{k-1} <= v < e_k
                     return (k == 0 || k == n) ? -1 : (int64_t)k - 1;
                 };
-                const int64_t ob = old_valid ? bin(ov) : -1, nb = bin(nv);
+                const int64_t ob = old_valid ? bin(ov) : -1, nb = new_valid ? bin(nv) : -1;
                 if (ob == nb) continue;
                 if (ob >= 0) flip_bit(ix.bvs[ob], r);
                 if (nb >= 0) flip_bit(ix.bvs[nb], r);
@@ -3035,10 +3081,10 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
 }
 
 hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,
-                             hipStream_t stream) {
+                             hipStream_t stream, uint32_t* overflow) {
     if (max_n == 0) return hipSuccess;
     hipLaunchKernelGGL(narrow_i32_kernel, dim3(grid_for((max_n + 1) / 2)), dim3(256), 0, stream, in, d_count, max_n,
-                       offset, out);
+                       offset, out, overflow);
     return hipGetLastError();
 }
 
@@ -3085,6 +3131,19 @@ hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const
     else
         hipLaunchKernelGGL(gather_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col), rowids,
                            d_count, max_n, row_base, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_valid(const void* col, int type, const uint64_t* validity, const int64_t* rowids,
+                               const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* out,
+                               uint64_t* out_valid, hipStream_t stream) {
+    const dim3 grid(grid_for(max_n, 8192)), block(256);
+    if (type == 0)
+        hipLaunchKernelGGL(gather_valid_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
+                           validity, rowids, d_count, max_n, row_base, out, out_valid);
+    else
+        hipLaunchKernelGGL(gather_valid_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, rowids, d_count, max_n, row_base, out, out_valid);
     return hipGetLastError();
 }
 
@@ -3298,11 +3357,12 @@ hipError_t launch_splice_bits(uint64_t* dst, const uint64_t* src, uint64_t bit_o
     return hipGetLastError();
 }
 
-hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, uint64_t m, void* col, int type,
-                             uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1, hipStream_t stream) {
+hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, const uint8_t* valids, uint64_t m, void* col,
+                             int type, uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1,
+                             hipStream_t stream) {
     if (m == 0) return hipSuccess;
-    hipLaunchKernelGGL(merge_rows_kernel, dim3(grid_for(m)), dim3(256), 0, stream, rows, values, m, col, type, validity,
-                       ix0, ix1);
+    hipLaunchKernelGGL(merge_rows_kernel, dim3(grid_for(m)), dim3(256), 0, stream, rows, values, valids, m, col, type,
+                       validity, ix0, ix1);
     return hipGetLastError();
 }
 

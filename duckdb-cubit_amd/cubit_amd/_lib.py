@@ -105,6 +105,7 @@ GPU_SIGNATURES = {
     ),
     "cubit_gather": (C.c_int, [_P, _P, C.c_int, _P, _P, _U64, _I64, _P]),
     "cubit_narrow_i32": (C.c_int, [_P, _P, _P, _U64, C.c_int64, _P]),
+    "cubit_narrow_i32_checked": (C.c_int, [_P, _P, _P, _U64, C.c_int64, _P, _P]),
     "cubit_gather_sum_product": (C.c_int, [_P, _P, _P, _P, _P, _U64, _I64, _P]),
     "cubit_table_create": (C.c_int, [_P, _U64, _I64, C.POINTER(_P)]),
     "cubit_table_destroy": (C.c_int, [_P]),
@@ -115,6 +116,7 @@ GPU_SIGNATURES = {
     "cubit_table_index_info": (C.c_int, [_P, C.c_int, C.POINTER(_U32), C.POINTER(_U64)]),
     "cubit_table_set_deletes": (C.c_int, [_P, _P, _P, _U64]),
     "cubit_table_set_updates": (C.c_int, [_P, C.c_int, _P, _P, _P, _U64]),
+    "cubit_table_set_updates_nullable": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _U64]),
     "cubit_table_scan": (
         C.c_int,
         [_P, C.POINTER(FilterNode), _U32, C.POINTER(Txn), _P, _U64, _P, _U32],
@@ -125,6 +127,7 @@ GPU_SIGNATURES = {
          C.POINTER(_U64)],
     ),
     "cubit_table_probe": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P]),
+    "cubit_table_probe_validity": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P, _P]),
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_last_zones": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_use_packed_filter": (C.c_int, [_P, C.c_int]),
@@ -167,6 +170,7 @@ SCAN_SIGNATURES = {
     "cubit_scan_max_threads": (C.c_int, [_P, C.POINTER(_U64)]),
     "cubit_scan_init_local": (C.c_int, [_P, C.POINTER(_P)]),
     "cubit_scan_function": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_U64)]),
+    "cubit_scan_function_validity": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_U64)]),
     "cubit_scan_batch_index": (C.c_int, [_P, _P, C.POINTER(_U64)]),
     "cubit_scan_progress": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "cubit_scan_cardinality": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_U64)]),

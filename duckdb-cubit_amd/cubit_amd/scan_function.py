@@ -47,6 +47,8 @@ class LocalState:
         self.handle = h
         self.bufs = [np.empty(VECTOR_SIZE, dtype=np.int64) for _ in range(scan.n_out)]
         self.ptrs = (C.c_void_p * max(scan.n_out, 1))(*[b.ctypes.data for b in self.bufs])
+        self.vbufs = [np.empty(VECTOR_SIZE // 64, dtype=np.uint64) for _ in range(scan.n_out)]
+        self.vptrs = (C.c_void_p * max(scan.n_out, 1))(*[b.ctypes.data for b in self.vbufs])
 
     def __del__(self):
         try:
@@ -88,6 +90,16 @@ class CubitScanFunction:
         n = C.c_uint64()
         L.check_scan(self.lib.cubit_scan_function(self.handle, local.handle, local.ptrs, C.byref(n)))
         return [b[: n.value].copy() for b in local.bufs]
+
+    def function_validity(self, local: LocalState):
+        """The next chunk with each column's validity (cubit_scan_function_validity):
+        (columns, valid) — int64 values (0 at NULL rows) and bool masks, empty at the end."""
+        n = C.c_uint64()
+        L.check_scan(self.lib.cubit_scan_function_validity(self.handle, local.handle, local.ptrs, local.vptrs,
+                                                           C.byref(n)))
+        k = n.value
+        valid = [np.unpackbits(w.view(np.uint8), bitorder="little")[:k].astype(bool) for w in local.vbufs]
+        return [b[:k].copy() for b in local.bufs], valid
 
     def get_batch_index(self, local: LocalState) -> int:
         v = C.c_uint64()

@@ -255,12 +255,20 @@ class CubitTable:
         i = np.ascontiguousarray(ids, dtype=np.uint64)
         L.check(self.lib.cubit_table_set_inserts(self.handle, b.ctypes.data, e.ctypes.data, i.ctypes.data, len(b)))
 
-    def set_updates(self, col: int, rows: np.ndarray, values: np.ndarray, versions: np.ndarray) -> None:
+    def set_updates(self, col: int, rows: np.ndarray, values: np.ndarray, versions: np.ndarray,
+                    valid: Optional[np.ndarray] = None) -> None:
+        """Update records (row, value, version), chronological. valid (bool per record, optional):
+        False = the record sets the row NULL (cubit_table_set_updates_nullable)."""
         rows = np.ascontiguousarray(rows, dtype=np.int64)
         values = np.ascontiguousarray(values, dtype=np.int64)
         versions = np.ascontiguousarray(versions, dtype=np.uint64)
-        L.check(self.lib.cubit_table_set_updates(self.handle, col, rows.ctypes.data, values.ctypes.data,
-                                                 versions.ctypes.data, len(rows)))
+        if valid is None:
+            L.check(self.lib.cubit_table_set_updates(self.handle, col, rows.ctypes.data, values.ctypes.data,
+                                                     versions.ctypes.data, len(rows)))
+            return
+        v = np.ascontiguousarray(valid, dtype=np.uint8)
+        L.check(self.lib.cubit_table_set_updates_nullable(self.handle, col, rows.ctypes.data, values.ctypes.data,
+                                                          v.ctypes.data, versions.ctypes.data, len(rows)))
 
     # ------------------------------------------------------------------ index maintenance
     def append(self, columns: Dict[int, np.ndarray], validity: Optional[Dict[int, np.ndarray]] = None,
@@ -336,6 +344,26 @@ class CubitTable:
         L.check(self.lib.cubit_table_probe(self.handle, col, C.byref(txn) if txn is not None else None,
                                            C.c_void_p(rowids_dptr), C.c_void_p(count_dptr), max_n,
                                            C.c_void_p(out_dptr)))
+
+    def probe_validity(self, col: int, rowids_dptr: int, count_dptr: int, max_n: int, out_dptr: int,
+                       valid_dptr: int, txn: Optional[L.Txn] = None) -> None:
+        """The probe with NULL-ness: values (0 at NULL rows) and LSB-first validity words."""
+        L.check(self.lib.cubit_table_probe_validity(self.handle, col, C.byref(txn) if txn is not None else None,
+                                                    C.c_void_p(rowids_dptr), C.c_void_p(count_dptr), max_n,
+                                                    C.c_void_p(out_dptr), C.c_void_p(valid_dptr)))
+
+    def fetch(self, col: int, rowids: np.ndarray, txn: Optional[L.Txn] = None):
+        """Synchronous probe of host row ids → (values, valid bool array), as the oracle's fetch."""
+        ids = np.ascontiguousarray(rowids, dtype=np.int64)
+        n = len(ids)
+        d_ids, d_cnt = self.ctx.upload(ids), self.ctx.upload(np.array([n], dtype=np.uint64))
+        d_out, d_val = self.ctx.alloc(max(n, 1) * 8), self.ctx.alloc(((n + 63) // 64 + 1) * 8)
+        self.probe_validity(col, d_ids.addr, d_cnt.addr, n, d_out.addr, d_val.addr, txn)
+        self.ctx.check()
+        vals = d_out.download(np.int64, n)
+        words = d_val.download(np.uint64, (n + 63) // 64)
+        valid = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
+        return vals, valid
 
     def sum_product(self, col_a: int, col_b: int, filter_set: Optional[TableFilterSet] = None,
                     residual: Optional[Residual] = None, txn: Optional[L.Txn] = None,

@@ -176,6 +176,16 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     std::vector<bool> narrow;
     std::vector<int64_t> offset;
     std::vector<PooledBuffer> d_narrow;
+    // the compaction bound is checked on the device (cubit_narrow_i32_checked): one flag word per
+    // emitted position, read once before the first window copy; a column whose flag is set goes
+    // back to the 8-byte copy
+    PooledBuffer d_overflow;
+    std::once_flag overflow_checked;
+    // NULL-ness per emitted position: a column whose statistics admit NULLs (update records
+    // included) is probed with its validity (cubit_table_probe_validity): d_valid holds one bit
+    // per ordered output row, and the windows copy their words beside the values
+    std::vector<bool> nullable;
+    std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
     std::vector<Window> windows;
@@ -197,6 +207,8 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     uint32_t tile_slot = 0;        // current tile (index into tiles)
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
+    std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
+    uint64_t valid_word0 = 0;              // ordered-output word of host_valid[e][0]
     // this task's copy stream (ordered after init_global's device work): the tasks' window
     // copies run side by side instead of queueing on the context stream
     cubit_ctx* ctx = nullptr;
@@ -275,23 +287,47 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         i = w.last;
     }
     // probe every emitted storage column at the ordered row ids (ColumnData::FilterScan
-    // semantics), on the device; the copies of the first window wait for them in stream order
-    g->d_cols.resize(g->emit.size());
-    for (size_t e = 0; e < g->emit.size(); ++e) {
+    // semantics, column_data.cpp:305-309: values with their validity), on the device; the copies
+    // of the first window wait for them in stream order. The statistics (DataTable::GetStatistics,
+    // update records of any version included) say which columns can hold a NULL: those probe with
+    // their validity, which also leaves 0 in a NULL row's value.
+    const size_t n_emit = g->emit.size();
+    g->d_cols.resize(n_emit);
+    g->nullable.assign(n_emit, false);
+    g->d_valid.resize(n_emit);
+    std::vector<int64_t> st_min(n_emit, 0), st_max(n_emit, 0);
+    for (size_t e = 0; e < n_emit; ++e) {
         const column_t col = g->column_ids[g->emit[e]];
         if (col == COLUMN_IDENTIFIER_ROW_ID || g->count == 0) continue;
+        int hn = 0, hv = 0;
+        check(cubit_table_column_statistics(bind.table, (int)col, &st_min[e], &st_max[e], &hn, &hv),
+              "cubit_table_column_statistics");
+        g->nullable[e] = hn != 0;
         g->d_cols[e].allocate(device_pool(), ctx, g->count * 8);
-        check(cubit_table_probe(bind.table, (int)col, txn, device_ptr(g->d_ids), static_cast<uint64_t*>(d_cnt.p),
-                                g->count, device_ptr(g->d_cols[e])),
-              "cubit_table_probe");
+        if (g->nullable[e]) {
+            g->d_valid[e].allocate(device_pool(), ctx, (g->count + 63) / 64 * 8);
+            check(cubit_table_probe_validity(bind.table, (int)col, txn, device_ptr(g->d_ids),
+                                             static_cast<uint64_t*>(d_cnt.p), g->count, device_ptr(g->d_cols[e]),
+                                             static_cast<uint64_t*>(g->d_valid[e].p)),
+                  "cubit_table_probe_validity");
+        } else {
+            check(cubit_table_probe(bind.table, (int)col, txn, device_ptr(g->d_ids), static_cast<uint64_t*>(d_cnt.p),
+                                    g->count, device_ptr(g->d_cols[e])),
+                  "cubit_table_probe");
+        }
     }
     // transfer compaction: a column whose values all lie within 2^31 of an offset crosses PCIe
     // as int32 (row ids: the partition's rows below 2^31, offset row_base; probed columns: their
-    // statistics' range, widened by any update records)
-    g->narrow.assign(g->emit.size(), false);
-    g->offset.assign(g->emit.size(), 0);
-    g->d_narrow.resize(g->emit.size());
-    for (size_t e = 0; e < g->emit.size() && g->count; ++e) {
+    // statistics' range, widened by any update records — a NULL row holds 0 after the validity
+    // probe, inside that window too). The device checks the bound as it narrows.
+    g->narrow.assign(n_emit, false);
+    g->offset.assign(n_emit, 0);
+    g->d_narrow.resize(n_emit);
+    if (g->count) {
+        g->d_overflow.allocate(device_pool(), ctx, n_emit * 4);
+        check(cubit_memset_d(ctx, g->d_overflow.p, 0, n_emit * 4), "overflow flags");
+    }
+    for (size_t e = 0; e < n_emit && g->count; ++e) {
         const column_t col = g->column_ids[g->emit[e]];
         bool fits = false;
         int64_t off = 0;
@@ -299,21 +335,17 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
             fits = bind.n_rows <= (uint64_t)INT32_MAX;
             off = bind.row_base;
         } else {
-            int64_t mn = 0, mx = 0;
-            int hn = 0, hv = 0;
-            // the statistics bound the valid values only: a column with NULL rows (whose slots
-            // hold whatever was stored) keeps the 8-byte transfer
-            if (cubit_table_column_statistics(bind.table, (int)col, &mn, &mx, &hn, &hv) == CUBIT_OK)
-                fits = !hn && mn >= INT32_MIN && mx <= INT32_MAX;
+            fits = st_min[e] >= INT32_MIN && st_max[e] <= INT32_MAX;
         }
         if (!fits) continue;
         g->narrow[e] = true;
         g->offset[e] = off;
         g->d_narrow[e].allocate(device_pool(), ctx, g->count * 4);
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g->d_ids : g->d_cols[e];
-        check(cubit_narrow_i32(ctx, device_ptr(src), static_cast<uint64_t*>(d_cnt.p), g->count, off,
-                               static_cast<int32_t*>(g->d_narrow[e].p)),
-              "cubit_narrow_i32");
+        check(cubit_narrow_i32_checked(ctx, device_ptr(src), static_cast<uint64_t*>(d_cnt.p), g->count, off,
+                                       static_cast<int32_t*>(g->d_narrow[e].p),
+                                       static_cast<uint32_t*>(g->d_overflow.p) + e),
+              "cubit_narrow_i32_checked");
     }
     // d_cnt goes back to the pool while the probes may still read it: stream order on this
     // context keeps a later user of the buffer behind them; other contexts never get it
@@ -341,9 +373,31 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         check(cubit_copy_stream_create(g.ctx, &l.copy_stream), "copy stream");
         l.ctx = g.ctx;
     }
-    if (l.host.size() != g.emit.size()) l.host.resize(g.emit.size());
+    // the device's verdict on the compaction bounds, once per scan before any window copy (the
+    // copy stream starts after init_global's work, the narrowing included)
+    std::call_once(g.overflow_checked, [&] {
+        if (!g.d_overflow.p) return;
+        std::vector<uint32_t> ov(g.emit.size());
+        check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, ov.data(), g.d_overflow.p, ov.size() * 4), "overflow flags");
+        for (size_t e = 0; e < ov.size(); ++e)
+            if (ov[e]) g.narrow[e] = false;
+    });
+    if (l.host.size() != g.emit.size()) {
+        l.host.resize(g.emit.size());
+        l.host_valid.resize(g.emit.size());
+    }
+    // validity words covering the window's rows [off, off + len) of the ordered output
+    const uint64_t w0 = win.off / 64, w1 = (win.off + win.len + 63) / 64;
+    l.valid_word0 = w0;
     for (size_t e = 0; e < g.emit.size(); ++e) {
         if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
+        if (g.nullable[e]) {
+            // + 2 words: a window may start and end inside a word, and the chunk fill reads one ahead
+            if (!l.host_valid[e].p) l.host_valid[e].allocate(pinned_pool(), g.ctx, (g.max_window / 64 + 3) * 8);
+            check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host_valid[e].p,
+                                          static_cast<const uint64_t*>(g.d_valid[e].p) + w0, (w1 - w0) * 8),
+                  "window validity copy");
+        }
         const column_t col = g.column_ids[g.emit[e]];
         if (g.narrow[e]) {
             const int32_t* src = static_cast<const int32_t*>(g.d_narrow[e].p) + win.off;
@@ -358,6 +412,24 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     l.tile_slot = win.first;
     l.pos = 0;
     return true;
+}
+
+// The chunk's mask from the window's validity words: rows [first, first + n) of the window
+// copy (bit positions counted from its first word). Left all-valid when every row is valid, as
+// a vector of a segment without NULLs (validity_mask.hpp: no buffer = all valid).
+void FillValidity(const uint64_t* words, uint64_t first, idx_t n, ValidityMask& mask) {
+    const uint64_t q = first / 64;
+    const unsigned sh = (unsigned)(first % 64);
+    uint64_t all = ~0ull;
+    const idx_t nw = (n + 63) / 64;
+    for (idx_t j = 0; j < nw; ++j) {
+        uint64_t w = words[q + j] >> sh;
+        if (sh) w |= words[q + j + 1] << (64 - sh);
+        if (j == nw - 1 && (n & 63)) w |= ~0ull << (n & 63);  // rows past the chunk read as valid
+        mask.words[j] = w;
+        all &= w;
+    }
+    mask.all_valid = all == ~0ull;
 }
 
 void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
@@ -377,6 +449,8 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
             const idx_t at = g.tile_off[l.tile_slot] - win.off + l.pos;
             for (size_t e = 0; e < g.emit.size(); ++e) {
+                if (g.nullable[e]) FillValidity(static_cast<const uint64_t*>(l.host_valid[e].p), win.off + at - 64 * l.valid_word0,
+                                                n, output.validity[e]);
                 if (g.narrow[e]) {  // widen the compacted transfer
                     const int32_t* src = static_cast<const int32_t*>(l.host[e].p) + at;
                     int64_t* dst = output.data[e].data();
@@ -534,16 +608,29 @@ int cubit_scan_init_local(cubit_scan* s, cubit_scan_local** out) {
     return CUBIT_OK;
 }
 
-int cubit_scan_function(cubit_scan* s, cubit_scan_local* l, int64_t* const* out_columns, uint64_t* out_count) {
+int cubit_scan_function_validity(cubit_scan* s, cubit_scan_local* l, int64_t* const* out_columns,
+                                 uint64_t* const* out_validity, uint64_t* out_count) {
     if (!s || !l || !out_count) return scan_fail(CUBIT_ERR_INVALID, "null argument");
-    TableFunctionInput in{&s->bind, l->lstate.get(), s->gstate.get()};
-    s->fn.function(in, l->chunk);
+    try {
+        TableFunctionInput in{&s->bind, l->lstate.get(), s->gstate.get()};
+        s->fn.function(in, l->chunk);
+    } catch (const ScanError& e) {
+        return scan_fail(e.code, e.what());
+    }
     const idx_t n = l->chunk.size();
-    if (out_columns)
-        for (size_t c = 0; c < l->chunk.data.size(); ++c)
-            if (out_columns[c]) std::memcpy(out_columns[c], l->chunk.data[c].data(), n * sizeof(int64_t));
+    for (size_t c = 0; c < l->chunk.data.size(); ++c) {
+        if (out_columns && out_columns[c]) std::memcpy(out_columns[c], l->chunk.data[c].data(), n * sizeof(int64_t));
+        if (out_validity && out_validity[c]) {
+            const ValidityMask& m = l->chunk.validity[c];
+            for (idx_t j = 0; j < STANDARD_VECTOR_SIZE / 64; ++j) out_validity[c][j] = m.all_valid ? ~0ull : m.words[j];
+        }
+    }
     *out_count = n;
     return CUBIT_OK;
+}
+
+int cubit_scan_function(cubit_scan* s, cubit_scan_local* l, int64_t* const* out_columns, uint64_t* out_count) {
+    return cubit_scan_function_validity(s, l, out_columns, nullptr, out_count);
 }
 
 int cubit_scan_batch_index(cubit_scan* s, cubit_scan_local* l, uint64_t* out) {

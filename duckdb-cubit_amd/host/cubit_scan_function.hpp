@@ -36,16 +36,31 @@ using column_t = uint64_t;
 constexpr column_t COLUMN_IDENTIFIER_ROW_ID = (column_t)-1;  // src/include/duckdb/common/constants.hpp
 constexpr idx_t STANDARD_VECTOR_SIZE = 2048;                  // common/vector_size.hpp:16-20
 
+// ValidityMask of one flat vector (src/include/duckdb/common/types/validity_mask.hpp:22,164-168):
+// LSB-first 64-bit words, bit i = row i valid; no words allocated (all_valid) = every row valid,
+// the state FlatVector::Validity starts in and a scan leaves for a column without NULLs.
+struct ValidityMask {
+    bool all_valid = true;
+    uint64_t words[STANDARD_VECTOR_SIZE / 64];
+    void SetAllValid() { all_valid = true; }
+    bool RowIsValid(idx_t i) const { return all_valid || ((words[i >> 6] >> (i & 63)) & 1ull); }
+};
+
 // DataChunk with flat int64 vectors (ROW_TYPE row ids; DATE / DECIMAL(15,2) physical values
-// widened to int64). size() == 0 signals the end of the scan.
+// widened to int64) and their validity masks. size() == 0 signals the end of the scan.
 struct DataChunk {
     std::vector<std::vector<int64_t>> data;
+    std::vector<ValidityMask> validity;
     idx_t count = 0;
     void Initialize(idx_t n_columns) {
         data.assign(n_columns, std::vector<int64_t>(STANDARD_VECTOR_SIZE));
+        validity.assign(n_columns, ValidityMask{});
         count = 0;
     }
-    void Reset() { count = 0; }
+    void Reset() {
+        count = 0;
+        for (auto& v : validity) v.SetAllValid();
+    }
     idx_t size() const { return count; }
     void SetCardinality(idx_t n) { count = n; }
 };

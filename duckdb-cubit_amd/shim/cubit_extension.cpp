@@ -16,6 +16,10 @@
 //   The optimizer swaps seq_scan for cubit_scan when every pushed filter of the scan is
 //   supported, every scanned column is attached, and the partition is exactly the state the
 //   scanning transaction sees (CubitPartitionIsCurrent); otherwise seq_scan runs as before.
+//   The swapped scan checks again when it runs (CubitInitGlobal, in the executing transaction)
+//   and hands the whole scan to seq_scan's own callbacks when the partition is not current —
+//   a prepared statement keeps its plan across EXECUTEs (prepared_statement_data.cpp:64 re-plans
+//   only on a catalog change), so the plan-time check alone would not do.
 //
 // Reference interfaces used (src/include/duckdb/…):
 //   OptimizerExtension::optimize_function          optimizer/optimizer_extension.hpp:31-41
@@ -33,7 +37,11 @@
 #include "duckdb/function/function_set.hpp"
 #include "duckdb/function/pragma_function.hpp"
 #include "duckdb/function/table_function.hpp"
+#include "duckdb/main/attached_database.hpp"
+#include "duckdb/main/client_context_state.hpp"
 #include "duckdb/main/extension_util.hpp"
+#include "duckdb/planner/extension_callback.hpp"
+#include "duckdb/transaction/meta_transaction.hpp"
 #include "duckdb/optimizer/optimizer_extension.hpp"
 #include "duckdb/parser/statement/insert_statement.hpp"
 #include "duckdb/planner/filter/conjunction_filter.hpp"
@@ -94,8 +102,11 @@ struct CubitAttached {
     vector<CubitIndexSpec> indexes; // the attach's index specification
     uint64_t gpu_rows = 0;          // rows of the GPU partition (row ids 0 … gpu_rows-1)
     transaction_t sync_start = 0;   // start time of the last sync's snapshot
-    // planned writers not yet folded in by a sync: transaction id → whether it may change the
-    // values of an attached column (then the sync re-reads every column)
+    // writers not yet folded in by a sync: transaction id → whether it may change the values of
+    // an attached column (then the sync re-reads every column). Recorded when a statement that
+    // deleted or updated rows ends (CubitContextState::QueryEnd, every connection, prepared and
+    // unoptimized statements included), when a DELETE / UPDATE is planned (NoteWriters), and at
+    // attach for every still-active transaction that had already written (CubitRegistry::Dirty).
     unordered_map<transaction_t, bool> writers;
     mutex lock;  // scans, writers and syncs of different connections meet here
 };
@@ -106,6 +117,34 @@ public:
         lock_guard<mutex> g(lock);
         auto it = map().find(&t);
         return it == map().end() ? nullptr : it->second.get();
+    }
+    // Every attached table of database `db` (a writer's changes cannot be attributed to a table
+    // from the transaction's undo properties, so they count against all of them).
+    static vector<std::pair<const TableCatalogEntry *, CubitAttached *>> InDatabase(const AttachedDatabase &db) {
+        lock_guard<mutex> g(lock);
+        vector<std::pair<const TableCatalogEntry *, CubitAttached *>> out;
+        for (auto &kv : map()) {
+            if (&kv.first->catalog.GetAttached() == &db) {
+                out.emplace_back(kv.first, kv.second.get());
+            }
+        }
+        return out;
+    }
+    // Transactions that deleted or updated rows, per database, whether or not a table was
+    // attached then: an attach must not miss a writer that started before it and commits after
+    // its snapshot. Entries of finished transactions (id < LowestActiveId) are dropped.
+    static void NoteDirty(const AttachedDatabase &db, transaction_t id, bool values) {
+        lock_guard<mutex> g(lock);
+        auto &w = dirty()[&db][id];
+        w = w || values;
+    }
+    static unordered_map<transaction_t, bool> Dirty(const AttachedDatabase &db, transaction_t lowest_active) {
+        lock_guard<mutex> g(lock);
+        auto &m = dirty()[&db];
+        for (auto it = m.begin(); it != m.end();) {
+            it = it->first < lowest_active ? m.erase(it) : std::next(it);
+        }
+        return m;
     }
     static CubitAttached &Insert(const TableCatalogEntry &t) {
         lock_guard<mutex> g(lock);
@@ -119,6 +158,10 @@ public:
 private:
     static unordered_map<const TableCatalogEntry *, unique_ptr<CubitAttached>> &map() {
         static unordered_map<const TableCatalogEntry *, unique_ptr<CubitAttached>> m;
+        return m;
+    }
+    static unordered_map<const AttachedDatabase *, unordered_map<transaction_t, bool>> &dirty() {
+        static unordered_map<const AttachedDatabase *, unordered_map<transaction_t, bool>> m;
         return m;
     }
     static mutex lock;
@@ -302,11 +345,18 @@ static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node>
 
 // ------------------------------------------------------------------ table function
 
+// The swapped scan keeps the seq_scan it replaced — TableScanFunction's callbacks and its
+// TableScanBindData, as the binder made them (table_scan.cpp:405-442) — so that a scan whose
+// partition is not current when it runs is seq_scan's, unchanged.
 struct CubitBindData : public TableFunctionData {
-    CubitBindData(DuckTableEntry &table_p, CubitAttached &attached_p) : table(table_p), attached(attached_p) {
+    CubitBindData(DuckTableEntry &table_p, CubitAttached &attached_p, TableFunction seq_p,
+                  unique_ptr<FunctionData> seq_bind_p)
+        : table(table_p), attached(attached_p), seq(std::move(seq_p)), seq_bind(std::move(seq_bind_p)) {
     }
     DuckTableEntry &table;
     CubitAttached &attached;
+    TableFunction seq;
+    unique_ptr<FunctionData> seq_bind;
 };
 
 struct CubitGlobalState : public GlobalTableFunctionState {
@@ -316,11 +366,13 @@ struct CubitGlobalState : public GlobalTableFunctionState {
         }
     }
     idx_t MaxThreads() const override {
-        return max_threads;
+        return seq_global ? seq_global->MaxThreads() : max_threads;
     }
     cubit_scan *scan = nullptr;
     idx_t max_threads = 1;
     vector<LogicalType> out_types;  // output chunk column types, in output order
+    // set when the scan runs as seq_scan (the partition was not current at init_global)
+    unique_ptr<GlobalTableFunctionState> seq_global;
 };
 
 struct CubitLocalState : public LocalTableFunctionState {
@@ -332,10 +384,34 @@ struct CubitLocalState : public LocalTableFunctionState {
     cubit_scan_local *local = nullptr;
     vector<vector<int64_t>> staging;  // one STANDARD_VECTOR_SIZE int64 buffer per output column
     vector<int64_t *> ptrs;
+    vector<vector<uint64_t>> validity;  // one STANDARD_VECTOR_SIZE / 64-word mask per output column
+    vector<uint64_t *> vptrs;
+    unique_ptr<LocalTableFunctionState> seq_local;
 };
+
+static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached);
+
+// the scan's columns are all on the GPU (a re-attach may have changed the column set)
+static bool ColumnsAttached(CubitAttached &attached, const vector<column_t> &column_ids) {
+    lock_guard<mutex> g(attached.lock);
+    for (auto c : column_ids) {
+        if (c != COLUMN_IDENTIFIER_ROW_ID && !attached.columns.count(c)) {
+            return false;
+        }
+    }
+    return true;
+}
 
 static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &context, TableFunctionInitInput &input) {
     auto &bind = input.bind_data->Cast<CubitBindData>();
+    // the plan may be older than the partition's state (a prepared statement, a write committed
+    // since planning): check again in the executing transaction, and run as seq_scan if stale
+    if (!CubitPartitionIsCurrent(context, bind.table, bind.attached) || !ColumnsAttached(bind.attached, input.column_ids)) {
+        auto g = make_uniq<CubitGlobalState>();
+        TableFunctionInitInput seq_input(bind.seq_bind.get(), input.column_ids, input.projection_ids, input.filters);
+        g->seq_global = bind.seq.init_global(context, seq_input);
+        return std::move(g);
+    }
     vector<cubit_filter_node> nodes;
     if (input.filters && !input.filters->filters.empty()) {
         // the TableFilterSet is an AND over columns; its keys index column_ids
@@ -375,12 +451,22 @@ static unique_ptr<LocalTableFunctionState> CubitInitLocal(ExecutionContext &cont
                                                           GlobalTableFunctionState *global_state) {
     auto &g = global_state->Cast<CubitGlobalState>();
     auto l = make_uniq<CubitLocalState>();
+    if (g.seq_global) {
+        auto &bind = input.bind_data->Cast<CubitBindData>();
+        if (bind.seq.init_local) {
+            TableFunctionInitInput seq_input(bind.seq_bind.get(), input.column_ids, input.projection_ids, input.filters);
+            l->seq_local = bind.seq.init_local(context, seq_input, g.seq_global.get());
+        }
+        return std::move(l);
+    }
     if (cubit_scan_init_local(g.scan, &l->local) != CUBIT_OK) {
         throw InternalException("cubit_scan: %s", cubit_scan_last_error());
     }
     l->staging.resize(g.out_types.size(), vector<int64_t>(STANDARD_VECTOR_SIZE));
-    for (auto &s : l->staging) {
-        l->ptrs.push_back(s.data());
+    l->validity.resize(g.out_types.size(), vector<uint64_t>(STANDARD_VECTOR_SIZE / 64));
+    for (idx_t c = 0; c < g.out_types.size(); c++) {
+        l->ptrs.push_back(l->staging[c].data());
+        l->vptrs.push_back(l->validity[c].data());
     }
     return std::move(l);
 }
@@ -435,15 +521,41 @@ static void CopyOut(const int64_t *src, Vector &dst, idx_t n) {
     }
 }
 
+// the chunk's mask for one column (FlatVector::Validity, validity_mask.hpp:22,164-168): left
+// all-valid unless a row is NULL, as a vector read from a segment without NULLs
+static void CopyValidity(const uint64_t *words, Vector &dst, idx_t n) {
+    const idx_t nw = (n + 63) / 64;
+    bool all = true;
+    for (idx_t j = 0; j < nw; j++) {
+        all = all && words[j] == ~0ull;
+    }
+    if (all) {
+        return;
+    }
+    auto &mask = FlatVector::Validity(dst);
+    mask.Initialize(STANDARD_VECTOR_SIZE);
+    auto data = mask.GetData();
+    for (idx_t j = 0; j < nw; j++) {
+        data[j] = words[j];
+    }
+}
+
 static void CubitScanFunc(ClientContext &context, TableFunctionInput &data, DataChunk &output) {
     auto &g = data.global_state->Cast<CubitGlobalState>();
     auto &l = data.local_state->Cast<CubitLocalState>();
+    if (g.seq_global) {
+        auto &bind = data.bind_data->Cast<CubitBindData>();
+        TableFunctionInput seq_data(bind.seq_bind.get(), l.seq_local.get(), g.seq_global.get());
+        bind.seq.function(context, seq_data, output);
+        return;
+    }
     uint64_t n = 0;
-    if (cubit_scan_function(g.scan, l.local, l.ptrs.data(), &n) != CUBIT_OK) {
+    if (cubit_scan_function_validity(g.scan, l.local, l.ptrs.data(), l.vptrs.data(), &n) != CUBIT_OK) {
         throw InternalException("cubit_scan: %s", cubit_scan_last_error());
     }
     for (idx_t c = 0; c < output.ColumnCount(); c++) {
         CopyOut(l.ptrs[c], output.data[c], n);
+        CopyValidity(l.vptrs[c], output.data[c], n);
     }
     output.SetCardinality(n);  // 0 rows = finished (PhysicalTableScan::GetData)
 }
@@ -452,6 +564,10 @@ static idx_t CubitBatchIndex(ClientContext &context, const FunctionData *bind_da
                              LocalTableFunctionState *local_state, GlobalTableFunctionState *global_state) {
     auto &g = global_state->Cast<CubitGlobalState>();
     auto &l = local_state->Cast<CubitLocalState>();
+    if (g.seq_global) {
+        auto &bind = bind_data->Cast<CubitBindData>();
+        return bind.seq.get_batch_index(context, bind.seq_bind.get(), l.seq_local.get(), g.seq_global.get());
+    }
     uint64_t b = 0;
     cubit_scan_batch_index(g.scan, l.local, &b);
     return b;
@@ -460,6 +576,11 @@ static idx_t CubitBatchIndex(ClientContext &context, const FunctionData *bind_da
 static double CubitProgress(ClientContext &context, const FunctionData *bind_data,
                             const GlobalTableFunctionState *global_state) {
     auto &g = global_state->Cast<CubitGlobalState>();
+    if (g.seq_global) {
+        auto &bind = bind_data->Cast<CubitBindData>();
+        return bind.seq.table_scan_progress ? bind.seq.table_scan_progress(context, bind.seq_bind.get(), g.seq_global.get())
+                                            : -1;
+    }
     double p = 0;
     cubit_scan_progress(g.scan, &p);
     return p;
@@ -523,7 +644,8 @@ TableFunction GetCubitScanFunction() {
 //    (DataTable::Delete → RowGroupCollection::Delete, data_table.cpp:1181-1189) and its appends
 //    to its LocalStorage, which DataTable::Scan reads after the persistent rows
 //    (data_table.cpp:277-287, local_storage.cpp:326-341) — none of that is on the GPU;
-//  * no planned writer of the table is outstanding and every committed append is synced;
+//  * no writer of the table is outstanding (CubitAttached::writers: recorded when its statement
+//    ends or when it is planned) and every committed append is synced;
 //  * the transaction's snapshot includes the one the partition was read in.
 static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
     auto &tx = DuckTransaction::Get(context, table.catalog);
@@ -620,14 +742,71 @@ static void SwapScans(ClientContext &context, unique_ptr<LogicalOperator> &plan)
             return;
         }
     }
+    auto seq = get.function;
+    auto seq_bind = std::move(get.bind_data);
     get.function = GetCubitScanFunction();
-    get.bind_data = make_uniq<CubitBindData>(table->Cast<DuckTableEntry>(), *attached);
+    get.bind_data = make_uniq<CubitBindData>(table->Cast<DuckTableEntry>(), *attached, std::move(seq), std::move(seq_bind));
 }
+
+// A writer recorded when its statement ends, whatever planned it: ClientContextState::QueryEnd
+// (client_context_state.hpp:38-44) runs in ClientContext::EndQueryInternal before an autocommit
+// commits (client_context.cpp:205-228), and for an explicit transaction after each of its
+// statements, so a DELETE or UPDATE is known before any other transaction can see it — prepared
+// statements run again with EXECUTE, statements planned with enable_optimizer off and writes of
+// transactions that began before the attach included. The undo buffer says whether the
+// transaction deleted or updated rows (UndoBufferProperties, undo_buffer.hpp:19-25) but not in
+// which table, so the writer counts against every attached table of the database it modified
+// (MetaTransaction::ModifiedDatabase, meta_transaction.hpp:59-62). Appends need no record: they
+// reach the partition through the row count.
+class CubitContextState : public ClientContextState {
+public:
+    void QueryEnd(ClientContext &context) override {
+        if (!context.transaction.HasActiveTransaction()) {
+            return;
+        }
+        auto &meta = context.ActiveTransaction();
+        auto db = meta.ModifiedDatabase();
+        if (!db || db->IsSystem() || db->IsTemporary()) {
+            return;
+        }
+        auto tr = meta.TryGetTransaction(*db);
+        if (!tr || !tr->IsDuckTransaction()) {
+            return;
+        }
+        auto &tx = tr->Cast<DuckTransaction>();
+        auto props = tx.GetUndoProperties();
+        if (!props.has_deletes && !props.has_updates) {
+            return;
+        }
+        CubitRegistry::NoteDirty(*db, tx.transaction_id, props.has_updates);
+        for (auto &kv : CubitRegistry::InDatabase(*db)) {
+            lock_guard<mutex> g(kv.second->lock);
+            auto &w = kv.second->writers[tx.transaction_id];
+            w = w || props.has_updates;
+        }
+    }
+};
+
+static void RegisterContextState(ClientContext &context) {
+    if (!context.registered_state.count("cubit")) {
+        context.registered_state["cubit"] = make_shared_ptr<CubitContextState>();
+    }
+}
+
+// ExtensionCallback::OnConnectionOpened (extension_callback.hpp:22): every connection opened
+// after the load carries the state (cubit_init registers it on the ones already open)
+class CubitExtensionCallback : public ExtensionCallback {
+public:
+    void OnConnectionOpened(ClientContext &context) override {
+        RegisterContextState(context);
+    }
+};
 
 // OptimizerExtension::optimize_function (optimizer_extension.hpp:31-41), run after the built-in
 // optimizers (optimizer.cpp:222-227). Scans inside a plan that writes keep seq_scan: the rows a
 // DELETE / UPDATE reads are the rows it changes.
 static void CubitOptimize(OptimizerExtensionInput &input, unique_ptr<LogicalOperator> &plan) {
+    RegisterContextState(input.context);
     if (NoteWriters(input.context, *plan)) {
         return;
     }
@@ -646,9 +825,14 @@ struct CubitSnapshot {
     vector<bool> present;
 };
 
-// One query over the table's row ids ≥ first in the connection's open transaction.
+// One query over the table's row ids ≥ first in the connection's open transaction. The
+// snapshot covers at least row ids [first, total_rows): rows the transaction does not see —
+// deleted by a commit before it began — are absent (present = false), the tail included, so the
+// partition's row count stays DataTable::GetTotalRows' (total_rows is read before the
+// transaction begins: every row it counts was committed before the snapshot, since appends reach
+// the row groups inside the commit, under the lock StartTransaction takes).
 static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &entry, const vector<column_t> &cols,
-                     uint64_t first, CubitSnapshot &snap) {
+                     uint64_t first, uint64_t total_rows, CubitSnapshot &snap) {
     string sql = "SELECT rowid";
     for (auto c : cols) {
         sql += ", " + KeywordHelper::WriteOptionallyQuoted(entry.GetColumn(LogicalIndex(c)).Name());
@@ -689,6 +873,14 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
                 snap.validity[c][r >> 6] |= 1ull << (r & 63);
                 snap.values[c][r] = PhysicalAsInt64(vec, i);
             }
+        }
+    }
+    if (total_rows > first && snap.rows < total_rows - first) {  // deleted tail rows
+        snap.rows = total_rows - first;
+        snap.present.resize(snap.rows, false);
+        for (idx_t c = 0; c < cols.size(); c++) {
+            snap.values[c].resize(snap.rows, 0);
+            snap.validity[c].resize((snap.rows + 63) / 64, 0);
         }
     }
 }
@@ -890,13 +1082,21 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
     auto &tm = DuckTransactionManager::Get(entry.catalog.GetAttached());
     // writers that finished before the snapshot below begins are in it
     const transaction_t lowest_active = tm.LowestActiveId();
+    const uint64_t total_rows = entry.GetStorage().GetTotalRows();  // before the snapshot (ReadRows)
     Connection con(*context.db);
+    RegisterContextState(*con.context);
     con.BeginTransaction();
     auto &snap_tx = DuckTransaction::Get(*con.context, entry.catalog);
     const transaction_t start = snap_tx.start_time;
     vector<transaction_t> folded;
     {
         lock_guard<mutex> g(attached.lock);
+        // writers that were active before this sync and may commit after its snapshot: those
+        // recorded before the table was attached too (CubitRegistry::NoteDirty)
+        for (auto &d : CubitRegistry::Dirty(entry.catalog.GetAttached(), lowest_active)) {
+            auto &w = attached.writers[d.first];
+            w = w || d.second;
+        }
         for (auto &w : attached.writers) {
             if (w.first < lowest_active) {
                 folded.push_back(w.first);
@@ -908,7 +1108,7 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
     vector<bool> present;  // presence of every row id of the table in this snapshot
     if (!rebuild && attached.table) {
         // rows appended since the partition was read, then which older rows remain
-        ReadRows(con, table_name, entry, attached.column_order, attached.gpu_rows, snap);
+        ReadRows(con, table_name, entry, attached.column_order, attached.gpu_rows, total_rows, snap);
         auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name) +
                              " WHERE rowid < " + to_string(attached.gpu_rows));
         if (res->HasError()) {
@@ -927,7 +1127,7 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
         }
     }
     if (rebuild || !attached.table) {
-        ReadRows(con, table_name, entry, attached.column_order, 0, snap);
+        ReadRows(con, table_name, entry, attached.column_order, 0, total_rows, snap);
         if (snap.rows == 0) {
             con.Commit();
             throw InvalidInputException("cubit: %s has no rows to attach", table_name);
@@ -1104,6 +1304,10 @@ DUCKDB_EXTENSION_API void cubit_init(duckdb::DatabaseInstance &db) {
                                                   {LogicalType::VARCHAR, LogicalType::VARCHAR, LogicalType::VARCHAR}));
     ExtensionUtil::RegisterFunction(db, attach);
     ExtensionUtil::RegisterFunction(db, PragmaFunction::PragmaCall("cubit_sync", CubitSync, {LogicalType::VARCHAR}));
+    // connections opened from now on carry the writer hook from the start; those already open
+    // (the one running LOAD among them) get it on their next optimized plan (CubitOptimize) —
+    // registered_state belongs to its connection's thread, so it is not touched from here
+    config.extension_callbacks.push_back(make_uniq<CubitExtensionCallback>());
 }
 
 DUCKDB_EXTENSION_API const char *cubit_version() {

@@ -238,6 +238,11 @@ int cubit_gather(cubit_ctx *ctx, const void *d_col, int type, const int64_t *d_r
  * widens while it fills the vector (the table-function mirror's windows). */
 int cubit_narrow_i32(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n, int64_t offset,
                      int32_t *d_out);
+/* cubit_narrow_i32 that checks the bound instead of trusting it: *d_overflow (device; the caller
+ * zeroes it) becomes 1 when some value lies outside [offset - 2^31, offset + 2^31), and the
+ * compacted copy must then not be used. */
+int cubit_narrow_i32_checked(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n,
+                             int64_t offset, int32_t *d_out, uint32_t *d_overflow);
 /* Fused probe + reduce: sum over ids of a[r]*b[r] as a 128-bit integer (lo, hi int64 at
  * d_out[0..1]) — Q6's sum(l_extendedprice*l_discount) (DECIMAL(38,4) storage). */
 int cubit_gather_sum_product(cubit_ctx *ctx, const int64_t *d_a, const int64_t *d_b, const int64_t *d_rowids,
@@ -329,6 +334,16 @@ int cubit_table_load_index(cubit_table *t, int col, const char *path);
 int cubit_table_set_deletes(cubit_table *t, const int64_t *rows, const uint64_t *ids, uint64_t n);
 int cubit_table_set_updates(cubit_table *t, int col, const int64_t *rows, const int64_t *values,
                             const uint64_t *versions, uint64_t n);
+/* Updates that may set NULL (UPDATE … SET x = NULL, or a NULL row given a value): as
+ * cubit_table_set_updates, plus valid[i] (1 = values[i], 0 = NULL; valid = NULL: every record
+ * carries its value). DuckDB keeps these as the validity column's update chain beside the value
+ * chain (InitializeUpdateValidity, src/storage/table/update_segment.cpp:588-600) and merges the
+ * newest visible record into the vector's mask (UpdateMergeValidity :94-99, FetchRowValidity
+ * :357-370). A reader that sees a SET NULL record finds the row in IS NULL and in no comparison,
+ * and its probe reports NULL; cubit_table_column_statistics reports has_null. A column
+ * registered without validity gets an all-valid one on the first SET NULL record. */
+int cubit_table_set_updates_nullable(cubit_table *t, int col, const int64_t *rows, const int64_t *values,
+                                     const uint8_t *valid, const uint64_t *versions, uint64_t n);
 /* Inserts: n disjoint row ranges [row_begin[i], row_end[i]) appended by one transaction each,
  * with its insert id (ChunkConstantInfo::insert_id / ChunkVectorInfo::inserted,
  * src/storage/table/chunk_info.cpp:36-53, 123-161); a reader sees a range when
@@ -358,8 +373,9 @@ int cubit_table_append(cubit_table *t, uint64_t n_new, const int *cols, const vo
                        const uint64_t *const *validity, uint32_t n_cols, uint64_t insert_id);
 /* Merge the update records of `col` with version < horizon into the base values and the
  * column's indexes (the checkpoint of update chains, UpdateSegment, update_segment.cpp;
- * CUBIT's merge of its update bitvectors): each row takes its newest merged value and becomes
- * valid, and the index bitvectors flip the rows whose predicate changed. Only snapshots with
+ * CUBIT's merge of its update bitvectors): each row takes its newest merged record — its value
+ * (the row becomes valid) or NULL (the row's validity bit clears and it leaves every index
+ * bitvector) — and the index bitvectors flip the rows whose predicate changed. Only snapshots with
  * start_time >= horizon may be served afterwards (as the reference folds versions only below
  * the lowest active start). Records at or past horizon stay. *n_merged = rows merged. */
 int cubit_table_merge_updates(cubit_table *t, int col, uint64_t horizon, uint64_t *n_merged);
@@ -379,9 +395,17 @@ int cubit_table_scan(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_
 int cubit_table_scan_tiles(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
                            int64_t *d_rowids, uint64_t capacity, uint64_t *d_count, uint32_t flags, uint64_t *d_dir,
                            uint32_t dir_cap, uint32_t *n_tiles, uint64_t *rows_per_tile);
-/* Probe column `col` at the scan's row ids (visible values for txn). */
+/* Probe column `col` at the scan's row ids (visible values for txn; a NULL row's slot as stored). */
 int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64_t *d_rowids, const uint64_t *d_count,
                       uint64_t max_n, int64_t *d_out);
+/* The probe with NULL-ness — ColumnData::FilterScan + Vector::Slice (column_data.cpp:305-309,
+ * vector.cpp:223-258) and FetchRow (column_data.cpp:452-461) hand back the vector's validity with
+ * its values: d_out[i] = the visible value of row d_rowids[i], 0 when it is NULL, and bit i of
+ * d_validity (LSB-first 64-bit words, DuckDB's ValidityMask layout; room for ⌈max_n / 64⌉ words,
+ * the first ⌈min(*d_count, max_n) / 64⌉ written, bits past the count 0) = the row is valid for
+ * txn, with its visible SET NULL / value records applied. */
+int cubit_table_probe_validity(cubit_table *t, int col, const cubit_txn *txn, const int64_t *d_rowids,
+                               const uint64_t *d_count, uint64_t max_n, int64_t *d_out, uint64_t *d_validity);
 /* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
 int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
 /* Column statistics — DataTable::GetStatistics behind seq_scan's `statistics` callback
@@ -403,7 +427,7 @@ int cubit_table_last_zones(cubit_table *t, uint32_t *evaluated, uint32_t *zones)
  * pins b to at most 4 values of an exact range index, b is decoded from that index instead
  * of gathered (CUBIT_SUM_GATHER_B forces the gather). d_out[0..1] = {lo, hi} of the 128-bit
  * sum; d_count (optional) = qualifying rows. Visible MVCC updates on a or b fall back to
- * scan + probe + sum (those columns must then be NOT NULL). */
+ * scan + probe (with validity when a column is nullable: NULL rows add nothing) + sum. */
 #define CUBIT_SUM_GATHER_B 1u
 #define CUBIT_SUM_NO_ZONEMAP 2u /* as CUBIT_SCAN_NO_ZONEMAP */
 /* When a was registered as DuckDB BITPACKING segments (cubit_table_add_bitpacked_column), the

@@ -55,6 +55,14 @@ int cubit_scan_max_threads(cubit_scan *scan, uint64_t *out);
 int cubit_scan_init_local(cubit_scan *scan, cubit_scan_local **out);
 /* out_columns[i] receives output column i (capacity 2,048 int64 each); *out_count the rows */
 int cubit_scan_function(cubit_scan *scan, cubit_scan_local *local, int64_t *const *out_columns, uint64_t *out_count);
+/* cubit_scan_function with each output column's validity: out_validity[i] (NULL, or either array
+ * NULL, to skip) receives 32 LSB-first words — the chunk's FlatVector::Validity
+ * (validity_mask.hpp:22,164-168), bit r = row r of the chunk valid, rows past *out_count set —
+ * and a NULL row's value is 0. The reference's scan hands the vector's mask out with its values
+ * (ColumnData::FilterScan + Vector::Slice, column_data.cpp:305-309, vector.cpp:223-258); the
+ * values-only call drops it. */
+int cubit_scan_function_validity(cubit_scan *scan, cubit_scan_local *local, int64_t *const *out_columns,
+                                 uint64_t *const *out_validity, uint64_t *out_count);
 int cubit_scan_batch_index(cubit_scan *scan, cubit_scan_local *local, uint64_t *out);
 int cubit_scan_progress(cubit_scan *scan, double *out);
 int cubit_scan_cardinality(cubit_table *table, uint64_t *estimated, uint64_t *max);

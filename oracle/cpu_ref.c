@@ -116,13 +116,17 @@ static void load_vector(const ocol *c, uint64_t first_row, uint64_t count, const
         out->valid = out->valid_buf;
     }
     /* update records are chronological; the visible value is the newest visible one
-     * (UpdatesForTransaction applies undo images newest→oldest: update_info.hpp:44-55) */
+     * (UpdatesForTransaction applies undo images newest→oldest: update_info.hpp:44-55). The
+     * validity column keeps its own chain, written by the same UPDATE (InitializeUpdateValidity,
+     * update_segment.cpp:588-600) and merged into the mask the same way (UpdateMergeValidity
+     * :94-99): a SET NULL record clears the row's bit. */
     for (uint64_t u = 0; u < c->n_updates; u++) {
         int64_t r = c->upd_rows[u];
         if (r < (int64_t)first_row || r >= (int64_t)(first_row + count)) continue;
         if (!use_inserted(st, tid, c->upd_version[u])) continue;
-        out->vals[r - first_row] = c->upd_values[u];
-        out->valid_buf[r - first_row] = 1;
+        const int ok = c->upd_valid ? c->upd_valid[u] != 0 : 1;
+        out->vals[r - first_row] = ok ? c->upd_values[u] : 0;
+        out->valid_buf[r - first_row] = (uint8_t)ok;
     }
     out->type = OTYPE_INT64;
     out->data = out->vals;
@@ -477,7 +481,7 @@ int oracle_fetch(const ocol *c, const omvcc *tx, const int64_t *rowids, uint64_t
                 const uint64_t u = order[k];
                 if (use_inserted(st, tid, c->upd_version[u])) { /* the newest visible record wins */
                     v = c->upd_values[u];
-                    valid = 1;
+                    valid = c->upd_valid ? c->upd_valid[u] != 0 : 1; /* FetchRowValidity :357-370 */
                 }
             }
         }

@@ -26,6 +26,7 @@ typedef struct {
     const int64_t *upd_rows;
     const int64_t *upd_values;
     const uint64_t *upd_version;
+    const uint8_t *upd_valid;  /* per record: 0 = SET NULL (validity update chain), NULL = all values */
 } ocol;
 
 typedef struct {

@@ -25,7 +25,7 @@ OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
 class OCol(C.Structure):
     _fields_ = [("type", C.c_int32), ("pad", C.c_int32), ("data", C.c_void_p), ("validity", C.c_void_p),
                 ("n_updates", C.c_uint64), ("upd_rows", C.c_void_p), ("upd_values", C.c_void_p),
-                ("upd_version", C.c_void_p)]
+                ("upd_version", C.c_void_p), ("upd_valid", C.c_void_p)]
 
 
 class OMvcc(C.Structure):
@@ -93,19 +93,21 @@ def lib():
 
 class Column:
     """A column as the oracle sees it: base values, optional validity words and a
-    chronological update list (rows, values, version ids)."""
+    chronological update list (rows, values, version ids[, valid flags: False = SET NULL])."""
 
-    def __init__(self, data: np.ndarray, validity: Optional[np.ndarray] = None,
-                 updates: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None):
+    def __init__(self, data: np.ndarray, validity: Optional[np.ndarray] = None, updates=None):
         self.data = np.ascontiguousarray(data)
         assert self.data.dtype in (np.int32, np.int64)
         self.validity = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
+        self.upd_valid = None
         if updates is None:
             self.upd = None
         else:
-            r, v, ver = updates
+            r, v, ver = updates[:3]
             self.upd = (np.ascontiguousarray(r, dtype=np.int64), np.ascontiguousarray(v, dtype=np.int64),
                         np.ascontiguousarray(ver, dtype=np.uint64))
+            if len(updates) > 3 and updates[3] is not None:
+                self.upd_valid = np.ascontiguousarray(updates[3], dtype=np.uint8)
 
     def ocol(self) -> OCol:
         c = OCol()
@@ -115,6 +117,7 @@ class Column:
         if self.upd is not None:
             c.n_updates = len(self.upd[0])
             c.upd_rows, c.upd_values, c.upd_version = (a.ctypes.data for a in self.upd)
+            c.upd_valid = self.upd_valid.ctypes.data if self.upd_valid is not None else None
         return c
 
 
@@ -168,12 +171,19 @@ def table_scan_mt(columns: Sequence[Column], plan, n_rows: int, threads: int, ro
     return int(n), int(sm.value)
 
 
-def fetch(column: Column, rowids: np.ndarray, row_base: int = 0, tx: Optional[Mvcc] = None) -> np.ndarray:
+def fetch(column: Column, rowids: np.ndarray, row_base: int = 0, tx: Optional[Mvcc] = None,
+          with_valid: bool = False):
+    """ColumnData::FetchRow per row id: values (0 at NULL rows), and with_valid=True also the
+    validity (bool per row) — (values, valid)."""
     rowids = np.ascontiguousarray(rowids, dtype=np.int64)
     out = np.empty(max(len(rowids), 1), dtype=np.int64)
+    valid = np.empty(max(len(rowids), 1), dtype=np.uint8)
     c = column.ocol()
-    lib().oracle_fetch(C.byref(c), C.pointer(tx.s) if tx is not None else None, rowids.ctypes.data, len(rowids),
-                       row_base, out.ctypes.data, None)
+    rc = lib().oracle_fetch(C.byref(c), C.pointer(tx.s) if tx is not None else None, rowids.ctypes.data,
+                            len(rowids), row_base, out.ctypes.data, valid.ctypes.data)
+    assert rc == 0
+    if with_valid:
+        return out[: len(rowids)], valid[: len(rowids)].astype(bool)
     return out[: len(rowids)]
 
 

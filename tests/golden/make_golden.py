@@ -17,6 +17,39 @@ def answer(sf):
     return {"revenue": lines[1], "source": str(p.relative_to(REF))}
 
 
+def sqllogic_script(rel):
+    """A .test file as data: its statements and queries in order — connection, SQL text, and
+    the outcome the file expects (ok / error, or the result rows with NULL as None) — plus the
+    session settings that shape the replay (immediate transaction mode, NULL ordering)."""
+    src = (REF / rel).read_text()
+    script, flags = [], {"immediate_transaction_mode": False, "nulls_first": False}
+    for block in re.split(r"\n\s*\n", src):
+        lines = [x for x in block.strip().split("\n") if x and not x.startswith("#")]
+        if not lines:
+            continue
+        head = lines[0].split()
+        if head[0] == "statement":
+            sql = " ".join(x.strip() for x in lines[1:] if x.strip() != "----")
+            if sql.upper().startswith("SET IMMEDIATE_TRANSACTION_MODE"):
+                flags["immediate_transaction_mode"] = True
+                continue
+            if sql.upper().startswith("SET DEFAULT_NULL_ORDER"):
+                flags["nulls_first"] = "nulls_first" in sql
+                continue
+            if sql.upper().startswith("PRAGMA"):
+                continue
+            script.append({"op": "statement", "con": head[2] if len(head) > 2 else "default", "sql": sql,
+                           "ok": head[1] == "ok"})
+        elif head[0] == "query":
+            sep = lines.index("----")
+            rows = [[None if v == "NULL" else int(v) for v in line.split("\t")] for line in lines[sep + 1:]]
+            script.append({"op": "query", "con": head[2] if len(head) > 2 else "default",
+                           "sql": " ".join(lines[1:sep]), "rows": rows})
+        else:
+            assert head[0] in ("require", "load"), head
+    return {"source": rel, **flags, "script": script}
+
+
 def main():
     tpch = {
         "q6_revenue": {sf: answer(sf) for sf in ("0.01", "0.1", "1", "100")},
@@ -232,7 +265,12 @@ def main():
                               "range": [-500, 500], "queries": neg},
            "many_matches": {"source": "test/sql/index/art/scan/test_art_many_matches.test", "blocks": blocks}}
     assert len(neg) == 3 and len(blocks) == 2 and all(len(b["counts"]) == 6 for b in blocks)
-    (OUT / "reference_cases.json").write_text(json.dumps({"zonemap_segment": zm, "interleaved_versions": iv,
+    # NULL-ness through updates (the validity column's update chain): the reference's NULL-update
+    # tests as scripts, replayed against the version model in tests/null_updates.py
+    nu = {name: sqllogic_script(f"test/sql/update/{name}.test")
+          for name in ("test_null_update", "null_update_merge", "null_update_merge_transaction",
+                       "test_update_many_updaters_nulls", "update_null_integers")}
+    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,

@@ -37,14 +37,19 @@ def q6_table(ctx, li):
     return t
 
 
-def drain(fn, n_tasks):
-    """Run n_tasks pipeline tasks; returns [(batch_index, chunk columns)]."""
+def drain(fn, n_tasks, validity=False):
+    """Run n_tasks pipeline tasks; returns [(batch_index, chunk columns)] — with validity=True
+    each column's bool mask follows the value columns (cubit_scan_function_validity)."""
     out, lock = [], threading.Lock()
 
     def task():
         local = fn.init_local()
         while True:
-            cols = fn.function(local)
+            if validity:
+                vals, masks = fn.function_validity(local)
+                cols = vals + masks
+            else:
+                cols = fn.function(local)
             if len(cols[0]) == 0:
                 return
             assert len(cols[0]) <= 2048
@@ -268,8 +273,8 @@ def test_window_transfer_compaction_round_trips(ctx):
     """Windows cross PCIe as int32 (value - offset) where a column's statistics allow it
     (cubit_narrow_i32) and as int64 otherwise; either way the chunks carry the exact values:
     row ids of a partition based at 2^40, a DATE-like int32 column, a DECIMAL-like int64 column
-    inside int32 range with negatives, one far outside it, and a column with NULL rows (kept
-    at 8 bytes: its stored slots are not bounded by the statistics)."""
+    inside int32 range with negatives, one far outside it, and a column with NULL rows (probed with
+    its validity: every row's value and NULL-ness equal the oracle's fetch, NULL rows as 0)."""
     from cubit_amd.datagen import validity_from_mask
 
     n = 1_500_007
@@ -290,15 +295,60 @@ def test_window_transfer_compaction_round_trips(ctx):
     t.build_index(0, L.INDEX_RANGE)
     fs = F.TableFilterSet({0: F.ConstantFilter("<", 30)})
     fn = CubitScanFunction(t, [ROW_ID, 1, 2, 3, 4, 0], [0, 1, 2, 3, 4], fs)
-    chunks = drain(fn, 3)
+    chunks = drain(fn, 3, validity=True)
     fn.close()
     keep = np.flatnonzero(key < 30)
     assert np.array_equal(ordered(chunks, 0), keep.astype(np.int64) + base)
     assert np.array_equal(ordered(chunks, 1), small[keep])
     assert np.array_equal(ordered(chunks, 2), big[keep])
     assert np.array_equal(ordered(chunks, 3), date[keep].astype(np.int64))
-    got = ordered(chunks, 4)
-    assert np.array_equal(got[valid[keep]], nulls[keep][valid[keep]])
+    for c in range(4):
+        assert ordered(chunks, 5 + c).all()  # columns without NULLs: every row valid
+    ref_vals, ref_valid = O.fetch(O.Column(nulls, validity_from_mask(valid)), keep, with_valid=True)
+    assert np.array_equal(ordered(chunks, 9), ref_valid)
+    assert np.array_equal(ordered(chunks, 4), ref_vals)
+    t.close()
+
+
+@pytest.mark.parametrize("tasks", [1, 4])
+def test_nullable_projection_and_unpruned_is_null_filter(ctx, tasks):
+    """SELECT b, c, rowid … WHERE a < k AND c IS NULL with c not pruned (DuckDB keeps a filter
+    column that is also projected): b and c carry their validity through the chunks — c is NULL on
+    every row, b on its own NULL rows, including rows whose NULL-ness an update record changed for
+    this transaction (ColumnData::FilterScan + Slice, column_data.cpp:305-309)."""
+    from cubit_amd.datagen import validity_from_mask
+
+    n = 1_000_003
+    rng = np.random.default_rng(77)
+    a = rng.integers(0, 100, n).astype(np.int32)
+    b = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    bv = rng.random(n) > 0.3
+    c = rng.integers(0, 5, n).astype(np.int32)
+    cv = rng.random(n) > 0.5
+    t = CubitTable(ctx, n, row_base=11)
+    t.add_column(0, a)
+    t.add_column(1, b, validity_from_mask(bv))
+    t.add_column(2, c, validity_from_mask(cv))
+    t.build_index(0, L.INDEX_RANGE)
+    me = TXN_START + 3
+    urows = np.sort(rng.choice(n, 4000, replace=False)).astype(np.int64)
+    uvals = rng.integers(0, 1000, len(urows)).astype(np.int64)
+    uok = rng.random(len(urows)) > 0.5
+    t.set_updates(1, urows, uvals, np.full(len(urows), me, np.uint64), valid=uok)
+    txn = L.Txn(2, me)
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 40), 2: F.IsNullFilter()})
+    fn = CubitScanFunction(t, [0, 1, 2, ROW_ID], [3, 1, 2], fs, txn=txn)
+    chunks = drain(fn, tasks, validity=True)  # rowid, b, c, then their masks
+    fn.close()
+    keep = np.flatnonzero((a < 40) & ~cv)
+    assert np.array_equal(ordered(chunks, 0), keep + 11)
+    assert ordered(chunks, 3).all()
+    tx = O.Mvcc(2, me)
+    ocol_b = O.Column(b, validity_from_mask(bv), (urows, uvals, np.full(len(urows), me, np.uint64), uok))
+    rv, rvalid = O.fetch(ocol_b, keep, tx=tx, with_valid=True)
+    assert np.array_equal(ordered(chunks, 4), rvalid) and np.array_equal(ordered(chunks, 1), rv)
+    assert not ordered(chunks, 5).any() and not ordered(chunks, 2).any()  # c IS NULL on every row
+    assert (~rvalid).any() and rvalid.any() and len(keep) > 100_000
     t.close()
 
 
