@@ -327,6 +327,12 @@ int cubit_row_group_size(void) { return (int)kRowGroupSize; }
 uint64_t cubit_padded_words(uint64_t n_rows) { return padded_words(n_rows); }
 const char* cubit_last_error(void) { return g_last_error.c_str(); }
 
+int cubit_device_count(int* n) {
+    if (!n) return fail(CUBIT_ERR_INVALID, "null argument");
+    HIP_CHECK(hipGetDeviceCount(n));
+    return CUBIT_OK;
+}
+
 int cubit_ctx_create(int device, cubit_ctx** out) {
     if (!out) return fail(CUBIT_ERR_INVALID, "out is null");
     int n = 0;

@@ -78,6 +78,7 @@ GPU_SIGNATURES = {
     "cubit_row_group_size": (C.c_int, []),
     "cubit_padded_words": (_U64, [_U64]),
     "cubit_last_error": (C.c_char_p, []),
+    "cubit_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "cubit_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "cubit_ctx_destroy": (C.c_int, [_P]),
     "cubit_ctx_set_stream": (C.c_int, [_P, _P]),
@@ -167,6 +168,11 @@ SCAN_SIGNATURES = {
     "cubit_scan_last_error": (C.c_char_p, []),
     "cubit_scan_init_global": (C.c_int, [_P, C.POINTER(_U64), _U32, C.POINTER(_U64), _U32, C.POINTER(FilterNode),
                                          _U32, C.POINTER(Txn), C.POINTER(_P)]),
+    "cubit_scan_init_global_multi": (C.c_int, [C.POINTER(_P), _U32, C.POINTER(_U64), _U32, C.POINTER(_U64), _U32,
+                                               C.POINTER(FilterNode), _U32, C.POINTER(Txn), C.POINTER(_P)]),
+    "cubit_scan_cardinality_multi": (C.c_int, [C.POINTER(_P), _U32, C.POINTER(_U64), C.POINTER(_U64)]),
+    "cubit_scan_statistics_multi": (C.c_int, [C.POINTER(_P), _U32, _U64, C.POINTER(_I64), C.POINTER(_I64),
+                                              C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "cubit_scan_max_threads": (C.c_int, [_P, C.POINTER(_U64)]),
     "cubit_scan_init_local": (C.c_int, [_P, C.POINTER(_P)]),
     "cubit_scan_function": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_U64)]),

@@ -18,21 +18,29 @@ ROW_ID = 2 ** 64 - 1  # COLUMN_IDENTIFIER_ROW_ID
 VECTOR_SIZE = 2048
 
 
+def _handles(tables):
+    """A partition or a row-ordered list of partitions → (ctypes array of handles, count)."""
+    ts = list(tables) if isinstance(tables, (list, tuple)) else [tables]
+    return (C.c_void_p * len(ts))(*[t.handle.value if isinstance(t.handle, C.c_void_p) else t.handle for t in ts]), len(ts)
+
+
 def cardinality(table):
-    """TableScanCardinality: (estimated, max) rows of the partition (bind time)."""
+    """TableScanCardinality: (estimated, max) rows of the partition(s) (bind time)."""
     lib = L.scan_lib()
     e, m = C.c_uint64(), C.c_uint64()
-    L.check_scan(lib.cubit_scan_cardinality(table.handle, C.byref(e), C.byref(m)))
+    hs, n = _handles(table)
+    L.check_scan(lib.cubit_scan_cardinality_multi(hs, n, C.byref(e), C.byref(m)))
     return int(e.value), int(m.value)
 
 
 def statistics(table, column_id: int):
-    """TableScanStatistics: (min, max, has_null, has_no_null) of a storage column, or None for
-    the row id (the reference returns no statistics)."""
+    """TableScanStatistics: (min, max, has_null, has_no_null) of a storage column over the
+    partition(s), or None for the row id (the reference returns no statistics)."""
     lib = L.scan_lib()
     lo, hi = C.c_int64(), C.c_int64()
     hn, hv = C.c_int(), C.c_int()
-    rc = lib.cubit_scan_statistics(table.handle, column_id, C.byref(lo), C.byref(hi), C.byref(hn), C.byref(hv))
+    hs, n = _handles(table)
+    rc = lib.cubit_scan_statistics_multi(hs, n, column_id, C.byref(lo), C.byref(hi), C.byref(hn), C.byref(hv))
     if rc == L.ERR_UNSUPPORTED and column_id == ROW_ID:
         return None
     L.check_scan(rc)
@@ -59,7 +67,8 @@ class LocalState:
 
 class CubitScanFunction:
     """init_global: run the GPU scan (+ probes) for the given column_ids / projection_ids /
-    filters; then any number of local states drain it chunk by chunk."""
+    filters; then any number of local states drain it chunk by chunk. `table` is one partition
+    or a row-ordered list of them (cubit_scan_init_global_multi: one cursor over all)."""
 
     def __init__(self, table, column_ids: Sequence[int], projection_ids: Optional[Sequence[int]] = None,
                  filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
@@ -72,9 +81,10 @@ class CubitScanFunction:
         nodes = serialize(filter_set, residual).nodes if (filter_set or residual) else []
         arr = to_ctypes(nodes)
         h = C.c_void_p()
-        L.check_scan(self.lib.cubit_scan_init_global(table.handle, cols, len(column_ids), projc if proj else None,
-                                                      len(proj), arr if nodes else None, len(nodes),
-                                                      C.byref(txn) if txn is not None else None, C.byref(h)))
+        hs, n = _handles(table)
+        L.check_scan(self.lib.cubit_scan_init_global_multi(hs, n, cols, len(column_ids), projc if proj else None,
+                                                            len(proj), arr if nodes else None, len(nodes),
+                                                            C.byref(txn) if txn is not None else None, C.byref(h)))
         self.handle = h
         self.n_out = len(proj) if proj else len(column_ids)
 

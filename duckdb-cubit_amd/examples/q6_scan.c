@@ -2,7 +2,7 @@
  * q6_scan — TPC-H Q6 through the C ABI alone (no Python, no PyTorch): what a C/C++ host such
  * as a DuckDB extension does with libcubitgpu.so and libcubit_scan.so.
  *
- *   q6_scan <sf> [threads]      e.g. q6_scan 1, q6_scan 100 16
+ *   q6_scan <sf> [threads] [--partitions N]      e.g. q6_scan 1, q6_scan 100 16, q6_scan 100 8 --partitions 8
  *
  * 1. generates lineitem's Q6 columns with libcubit_datagen (the repo's dbgen restatement);
  * 2. registers them on the GPU and builds the bitmap indexes (cubit_table_add_column /
@@ -16,12 +16,18 @@
  *    init_global, then `threads` pipeline tasks (pthreads), each with its own local state,
  *    draining 2,048-row chunks of (l_extendedprice, l_discount) into a partial revenue —
  *    timed end to end (best of 3) and checked against the fused revenue; one more line.
+ * 6. with --partitions N: lineitem held as N row-range partitions, partition p on device
+ *    p mod (devices visible) with a context each — one process driving every GPU of the node —
+ *    and the same pipeline over all of them through one cursor (cubit_scan_init_global_multi:
+ *    each partition decodes and probes on its own device, windows are copied from their own
+ *    device, no device-to-device exchange); timed and checked the same way; one more line.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <inttypes.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <time.h>
 
 #include "cubit_gpu.h"
@@ -96,7 +102,55 @@ static void *pipeline_task(void *arg) {
     return NULL;
 }
 
+/* `threads` pipeline tasks over one init_global (best of 3 end to end); returns the best time */
+static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cubit_filter_node *q6, uint32_t nn,
+                           int threads, uint64_t want_rows, __int128 want_rev, double *init_ms) {
+    const uint64_t proj_ids[] = {3, 1};
+    double best = 1e30;
+    task_t *tasks = calloc((size_t)threads, sizeof(task_t));
+    pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
+    for (int rep = 0; rep < 3; ++rep) {
+        const double t0 = now_s();
+        cubit_scan *ps;
+        CHECK_SCAN(cubit_scan_init_global_multi(parts, n_parts, proj_ids, 2, NULL, 0, q6, nn, NULL, &ps));
+        const double t1 = now_s();
+        for (int i = 0; i < threads; ++i) {
+            tasks[i] = (task_t){ps, 0, 0, 0};
+            if (pthread_create(&th[i], NULL, pipeline_task, &tasks[i]) != 0) exit(1);
+        }
+        uint64_t rows_p = 0;
+        __int128 rev_p = 0;
+        for (int i = 0; i < threads; ++i) {
+            pthread_join(th[i], NULL);
+            CHECK_SCAN(tasks[i].rc);
+            rows_p += tasks[i].rows;
+            rev_p += tasks[i].revenue;
+        }
+        const double t2 = now_s();
+        CHECK_SCAN(cubit_scan_destroy(ps));
+        if (t2 - t0 < best) {
+            best = t2 - t0;
+            *init_ms = (t1 - t0) * 1e3;
+        }
+        if (rows_p != want_rows || rev_p != want_rev) {
+            fprintf(stderr, "pipeline: %" PRIu64 " rows, revenue differs from the fused sum\n", rows_p);
+            exit(1);
+        }
+    }
+    free(tasks);
+    free(th);
+    return best;
+}
+
 int main(int argc, char **argv) {
+    int n_partitions = 0;
+    for (int i = 1; i + 1 < argc; ++i)
+        if (!strcmp(argv[i], "--partitions")) {
+            n_partitions = atoi(argv[i + 1]);
+            for (int j = i; j + 2 < argc; ++j) argv[j] = argv[j + 2];  /* drop the option */
+            argc -= 2;
+            break;
+        }
     const double sf = argc > 1 ? atof(argv[1]) : 1.0;
     const int64_t orders = cubit_tpch_orders(sf);
     const int64_t n = cubit_tpch_lineitem_rows(sf, 0, orders, 0);
@@ -197,44 +251,43 @@ int main(int argc, char **argv) {
     /* 5. the query as a pipeline of `threads` tasks over the callbacks */
     const int threads = argc > 2 ? atoi(argv[2]) : 0;
     if (threads > 0) {
-        const uint64_t proj_ids[] = {3, 1};
-        double best = 1e30, best_init = 0;
-        uint64_t rows_p = 0;
-        __int128 rev_p = 0;
-        task_t *tasks = calloc((size_t)threads, sizeof(task_t));
-        pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
-        for (int rep = 0; rep < 3; ++rep) {
-            const double t0 = now_s();
-            cubit_scan *ps;
-            CHECK_SCAN(cubit_scan_init_global(t, proj_ids, 2, NULL, 0, q6, nn, NULL, &ps));
-            const double t1 = now_s();
-            for (int i = 0; i < threads; ++i) {
-                tasks[i] = (task_t){ps, 0, 0, 0};
-                if (pthread_create(&th[i], NULL, pipeline_task, &tasks[i]) != 0) return 1;
-            }
-            rows_p = 0;
-            rev_p = 0;
-            for (int i = 0; i < threads; ++i) {
-                pthread_join(th[i], NULL);
-                CHECK_SCAN(tasks[i].rc);
-                rows_p += tasks[i].rows;
-                rev_p += tasks[i].revenue;
-            }
-            const double t2 = now_s();
-            CHECK_SCAN(cubit_scan_destroy(ps));
-            if (t2 - t0 < best) {
-                best = t2 - t0;
-                best_init = t1 - t0;
-            }
-            if (rows_p != q || rev_p != rev) {
-                fprintf(stderr, "pipeline: %" PRIu64 " rows, revenue differs from the fused sum\n", rows_p);
-                return 1;
-            }
-        }
+        double init_ms = 0;
+        const double best = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms);
         printf("pipeline threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64 " rows_per_s %.4e revenue_match 1\n",
-               threads, best_init * 1e3, best * 1e3, rows_p, rows_p / best);
-        free(tasks);
-        free(th);
+               threads, init_ms, best * 1e3, q, q / best);
+    }
+
+    /* 6. the same pipeline over N row-range partitions, one context each, spread over the devices */
+    if (threads > 0 && n_partitions > 0) {
+        int n_dev = 1;
+        CHECK(cubit_device_count(&n_dev));
+        cubit_ctx **pctx = calloc((size_t)n_partitions, sizeof(cubit_ctx *));
+        cubit_table **pt = calloc((size_t)n_partitions, sizeof(cubit_table *));
+        for (int p = 0; p < n_partitions; ++p) {
+            const int64_t b = n * p / n_partitions, e = n * (p + 1) / n_partitions;
+            CHECK(cubit_ctx_create(p % n_dev, &pctx[p]));
+            CHECK(cubit_table_create(pctx[p], (uint64_t)(e - b), b, &pt[p]));
+            CHECK(cubit_table_add_column(pt[p], 0, CUBIT_TYPE_INT32, shipdate + b, NULL, 0));
+            CHECK(cubit_table_add_column(pt[p], 1, CUBIT_TYPE_INT64, discount + b, NULL, 0));
+            CHECK(cubit_table_add_column(pt[p], 2, CUBIT_TYPE_INT64, quantity + b, NULL, 0));
+            CHECK(cubit_table_add_column(pt[p], 3, CUBIT_TYPE_INT64, extprice + b, NULL, 0));
+            CHECK(cubit_table_build_index(pt[p], 0, CUBIT_INDEX_RANGE, edges, (uint32_t)ne));
+            CHECK(cubit_table_build_index(pt[p], 1, CUBIT_INDEX_RANGE, NULL, 0));
+            CHECK(cubit_table_build_index(pt[p], 2, CUBIT_INDEX_RANGE, NULL, 0));
+        }
+        for (int p = 0; p < n_partitions; ++p) CHECK(cubit_sync(pctx[p]));
+        double init_ms = 0;
+        const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms);
+        printf("partitioned_pipeline partitions %d devices %d threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64
+               " rows_per_s %.4e revenue_match 1\n",
+               n_partitions, n_dev < n_partitions ? n_dev : n_partitions, threads, init_ms, best * 1e3, q, q / best);
+        CHECK_SCAN(cubit_scan_release_cached(NULL, NULL));
+        for (int p = 0; p < n_partitions; ++p) {
+            CHECK(cubit_table_destroy(pt[p]));
+            CHECK(cubit_ctx_destroy(pctx[p]));
+        }
+        free(pt);
+        free(pctx);
     }
     CHECK(cubit_dev_free(ctx, d_ids));
     CHECK(cubit_dev_free(ctx, d_cnt));

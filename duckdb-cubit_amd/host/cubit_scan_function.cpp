@@ -159,16 +159,19 @@ idx_t window_rows() {
 }
 
 struct Window {
-    uint32_t first, last;  // index range [first, last) into the non-empty tiles
-    idx_t off, len;        // the window's rows in the ordered output
+    uint32_t part;         // the partition the window's tiles belong to
+    uint32_t first, last;  // index range [first, last) into that partition's non-empty tiles
+    idx_t off, len;        // the window's rows in the partition's ordered output
 };
 
-struct CubitScanGlobalState : public GlobalTableFunctionState {
-    cubit_ctx* ctx = nullptr;
-    std::vector<column_t> column_ids;
-    std::vector<idx_t> emit;  // positions of column_ids that reach the output
+// The device side of one partition's scan: its ordered row ids, the probed columns and the
+// non-empty tiles' runs.
+struct PartScan {
+    CubitPartition part;
     idx_t count = 0;
     idx_t rows_per_tile = 0;
+    uint64_t tile_base = 0;   // tiles of the earlier partitions: batch index = tile_base + tile
+    PooledBuffer d_cnt, d_dir;
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
     // transfer compaction per emitted position: the window copies move int32 (value - offset)
@@ -177,8 +180,8 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     std::vector<int64_t> offset;
     std::vector<PooledBuffer> d_narrow;
     // the compaction bound is checked on the device (cubit_narrow_i32_checked): one flag word per
-    // emitted position, read once before the first window copy; a column whose flag is set goes
-    // back to the 8-byte copy
+    // emitted position, read once before the partition's first window copy; a column whose flag
+    // is set goes back to the 8-byte copy
     PooledBuffer d_overflow;
     std::once_flag overflow_checked;
     // NULL-ness per emitted position: a column whose statistics admit NULLs (update records
@@ -188,7 +191,14 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
-    std::vector<Window> windows;
+};
+
+struct CubitScanGlobalState : public GlobalTableFunctionState {
+    std::vector<std::unique_ptr<PartScan>> parts;  // row order
+    std::vector<column_t> column_ids;
+    std::vector<idx_t> emit;  // positions of column_ids that reach the output
+    idx_t count = 0;          // all partitions
+    std::vector<Window> windows;  // partition by partition, each in tile order
     idx_t max_window = 0;
     std::atomic<uint32_t> next{0};
     std::atomic<idx_t> emitted{0};
@@ -198,27 +208,144 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     }
     ~CubitScanGlobalState() override {
         // probes launched by init_global may still read the buffers returned to the pool
-        if (ctx) cubit_sync(ctx);
+        for (auto& p : parts)
+            if (p->part.ctx) cubit_sync(p->part.ctx);
     }
 };
 
 struct CubitScanLocalState : public LocalTableFunctionState {
     int64_t window = -1;           // claimed window, -1 = none yet
-    uint32_t tile_slot = 0;        // current tile (index into tiles)
+    uint32_t tile_slot = 0;        // current tile (index into the window partition's tiles)
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
     std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
     uint64_t valid_word0 = 0;              // ordered-output word of host_valid[e][0]
-    // this task's copy stream (ordered after init_global's device work): the tasks' window
-    // copies run side by side instead of queueing on the context stream
-    cubit_ctx* ctx = nullptr;
-    void* copy_stream = nullptr;
+    // this task's copy stream per partition (ordered after init_global's device work on the
+    // partition's context): the tasks' window copies run side by side, each from its own device
+    std::vector<std::pair<cubit_ctx*, void*>> streams;
     ~CubitScanLocalState() override {
-        if (copy_stream) cubit_copy_stream_destroy(ctx, copy_stream);
+        for (auto& s : streams)
+            if (s.second) cubit_copy_stream_destroy(s.first, s.second);
     }
 };
 
 int64_t* device_ptr(PooledBuffer& b) { return b.i64(); }
+
+// The decode of one partition into a buffer sized by a guess (an eighth of its rows), launched
+// and not waited for; the count and directory are read after every partition has been launched,
+// so the partitions' devices decode side by side.
+void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn, uint64_t cap) {
+    cubit_ctx* ctx = P.part.ctx;
+    if (!P.d_cnt.p) P.d_cnt.allocate(device_pool(), ctx, 16);
+    // this scan's tile directory, copied out within the scan call: other pipeline tasks or
+    // queries may scan on the same context right after it (cubit_table_scan_tiles)
+    const uint32_t dir_cap = (uint32_t)((P.part.n_rows + 131071) / 131072 + 1);
+    if (!P.d_dir.p) P.d_dir.allocate(device_pool(), ctx, 2ull * dir_cap * 8);
+    P.d_ids.allocate(device_pool(), ctx, std::max<uint64_t>(cap, 1) * 8);
+    uint32_t n_tiles = 0;
+    check(cubit_table_scan_tiles(P.part.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
+                                 device_ptr(P.d_ids), P.d_ids.bytes / 8, static_cast<uint64_t*>(P.d_cnt.p),
+                                 CUBIT_SCAN_ORDERED, static_cast<uint64_t*>(P.d_dir.p), dir_cap, &n_tiles,
+                                 &P.rows_per_tile),
+          "cubit_table_scan_tiles");
+    P.tiles.assign(n_tiles, 0);  // the directory's size until FinishDecode reads it
+}
+
+// Count and tile runs of a launched decode; a filter that kept more rows than the guess runs
+// a second time with the exact count.
+void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn) {
+    cubit_ctx* ctx = P.part.ctx;
+    check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
+    if (P.count > P.d_ids.bytes / 8) {
+        LaunchDecode(P, nodes, txn, P.count);
+        idx_t again = 0;
+        check(cubit_memcpy_d2h(ctx, &again, P.d_cnt.p, 8), "count");
+        if (again != P.count) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
+    }
+    const uint32_t n_tiles = P.count ? (uint32_t)P.tiles.size() : 0;  // nothing qualified: no run
+    P.tiles.clear();
+    std::vector<uint64_t> dir(2 * (size_t)n_tiles);
+    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
+    // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
+    idx_t off = 0;
+    for (uint32_t t = 0; t < n_tiles; ++t) {
+        const uint64_t len = dir[2 * t + 1];
+        if (!len) continue;
+        if (len > P.count - off)
+            throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile directory does not describe this scan's output");
+        P.tiles.push_back(t);
+        P.tile_off.push_back(off);
+        P.tile_len.push_back(len);
+        off += len;
+    }
+    if (off != P.count)
+        throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(off) + " of " +
+                                               std::to_string(P.count) + " row ids");
+}
+
+// Probe every emitted storage column at the partition's ordered row ids (ColumnData::FilterScan
+// semantics, column_data.cpp:305-309: values with their validity), on the device; the copies of
+// the first window wait for them in stream order. The statistics (DataTable::GetStatistics,
+// update records of any version included) say which columns can hold a NULL: those probe with
+// their validity, which also leaves 0 in a NULL row's value. Then the transfer compaction: a
+// column whose values all lie within 2^31 of an offset crosses PCIe as int32 (row ids: the
+// partition's rows below 2^31, offset row_base; probed columns: their statistics' range, widened
+// by any update records — a NULL row holds 0 after the validity probe, inside that window too).
+// The device checks the bound as it narrows.
+void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
+                  const cubit_txn* txn) {
+    cubit_ctx* ctx = P.part.ctx;
+    cubit_table* table = P.part.table;
+    const size_t n_emit = emit.size();
+    P.d_cols.resize(n_emit);
+    P.nullable.assign(n_emit, false);
+    P.d_valid.resize(n_emit);
+    P.narrow.assign(n_emit, false);
+    P.offset.assign(n_emit, 0);
+    P.d_narrow.resize(n_emit);
+    if (P.count == 0) return;
+    std::vector<int64_t> st_min(n_emit, 0), st_max(n_emit, 0);
+    uint64_t* d_cnt = static_cast<uint64_t*>(P.d_cnt.p);
+    for (size_t e = 0; e < n_emit; ++e) {
+        const column_t col = column_ids[emit[e]];
+        if (col == COLUMN_IDENTIFIER_ROW_ID) continue;
+        int hn = 0, hv = 0;
+        check(cubit_table_column_statistics(table, (int)col, &st_min[e], &st_max[e], &hn, &hv),
+              "cubit_table_column_statistics");
+        P.nullable[e] = hn != 0;
+        P.d_cols[e].allocate(device_pool(), ctx, P.count * 8);
+        if (P.nullable[e]) {
+            P.d_valid[e].allocate(device_pool(), ctx, (P.count + 63) / 64 * 8);
+            check(cubit_table_probe_validity(table, (int)col, txn, device_ptr(P.d_ids), d_cnt, P.count,
+                                             device_ptr(P.d_cols[e]), static_cast<uint64_t*>(P.d_valid[e].p)),
+                  "cubit_table_probe_validity");
+        } else {
+            check(cubit_table_probe(table, (int)col, txn, device_ptr(P.d_ids), d_cnt, P.count, device_ptr(P.d_cols[e])),
+                  "cubit_table_probe");
+        }
+    }
+    P.d_overflow.allocate(device_pool(), ctx, n_emit * 4);
+    check(cubit_memset_d(ctx, P.d_overflow.p, 0, n_emit * 4), "overflow flags");
+    for (size_t e = 0; e < n_emit; ++e) {
+        const column_t col = column_ids[emit[e]];
+        bool fits;
+        int64_t off = 0;
+        if (col == COLUMN_IDENTIFIER_ROW_ID) {
+            fits = P.part.n_rows <= (uint64_t)INT32_MAX;
+            off = P.part.row_base;
+        } else {
+            fits = st_min[e] >= INT32_MIN && st_max[e] <= INT32_MAX;
+        }
+        if (!fits) continue;
+        P.narrow[e] = true;
+        P.offset[e] = off;
+        P.d_narrow[e].allocate(device_pool(), ctx, P.count * 4);
+        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+        check(cubit_narrow_i32_checked(ctx, device_ptr(src), d_cnt, P.count, off, static_cast<int32_t*>(P.d_narrow[e].p),
+                                       static_cast<uint32_t*>(P.d_overflow.p) + e),
+              "cubit_narrow_i32_checked");
+    }
+}
 
 std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
     auto& bind = static_cast<const CubitScanBindData&>(*input.bind_data);
@@ -229,126 +356,38 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     } else {
         for (idx_t i = 0; i < input.column_ids.size(); ++i) g->emit.push_back(i);
     }
-    cubit_ctx* ctx = bind.ctx;
-    g->ctx = ctx;
-    PooledBuffer d_cnt;
-    d_cnt.allocate(device_pool(), ctx, 16);
     const cubit_txn* txn = bind.has_txn ? &bind.txn : nullptr;
     const auto& nodes = input.filters ? input.filters->nodes : std::vector<cubit_filter_node>{};
-    // one decode into a buffer sized by a guess (an eighth of the rows); only a filter that
-    // keeps more rows than that runs a second time, with the exact count
-    uint64_t cap = std::max<uint64_t>(bind.n_rows / 8 + 4096, 1);
-    // this scan's tile directory, copied out within the scan call: other pipeline tasks or
-    // queries may scan on the same context right after it (cubit_table_scan_tiles)
-    const uint32_t dir_cap = (uint32_t)((bind.n_rows + 131071) / 131072 + 1);
-    PooledBuffer d_dir;
-    d_dir.allocate(device_pool(), ctx, 2ull * dir_cap * 8);
-    uint32_t n_tiles = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        g->d_ids.allocate(device_pool(), ctx, cap * 8);
-        cap = g->d_ids.bytes / 8;
-        check(cubit_table_scan_tiles(bind.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
-                                     device_ptr(g->d_ids), cap, static_cast<uint64_t*>(d_cnt.p), CUBIT_SCAN_ORDERED,
-                                     static_cast<uint64_t*>(d_dir.p), dir_cap, &n_tiles, &g->rows_per_tile),
-              "cubit_table_scan_tiles");
-        check(cubit_memcpy_d2h(ctx, &g->count, d_cnt.p, 8), "count");
-        if (g->count <= cap) break;
-        if (pass == 1) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
-        cap = g->count;
+    uint64_t tile_base = 0;
+    for (const CubitPartition& part : bind.parts) {
+        auto P = std::make_unique<PartScan>();
+        P->part = part;
+        P->tile_base = tile_base;
+        tile_base += (part.n_rows + 131071) / 131072;
+        g->parts.push_back(std::move(P));
     }
-    if (g->count == 0) n_tiles = 0;  // nothing qualified: no run to hand out, whatever the directory holds
-    std::vector<uint64_t> dir(2 * (size_t)n_tiles);
-    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), d_dir.p, dir.size() * 8), "directory");
-    // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
-    idx_t off = 0;
-    for (uint32_t t = 0; t < n_tiles; ++t) {
-        const uint64_t len = dir[2 * t + 1];
-        if (!len) continue;
-        if (len > g->count - off)
-            throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile directory does not describe this scan's output");
-        g->tiles.push_back(t);
-        g->tile_off.push_back(off);
-        g->tile_len.push_back(len);
-        off += len;
-    }
-    if (off != g->count)
-        throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(off) + " of " +
-                                               std::to_string(g->count) + " row ids");
-    for (uint32_t i = 0; i < g->tiles.size();) {
-        Window w{i, i, g->tile_off[i], 0};
-        const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
-        while (w.last < g->tiles.size() && (w.last == w.first || (w.len + g->tile_len[w.last] <= max_rows &&
-                                                                   w.last - w.first < max_tiles))) {
-            w.len += g->tile_len[w.last];
-            ++w.last;
-        }
-        g->max_window = std::max(g->max_window, w.len);
-        g->windows.push_back(w);
-        i = w.last;
-    }
-    // probe every emitted storage column at the ordered row ids (ColumnData::FilterScan
-    // semantics, column_data.cpp:305-309: values with their validity), on the device; the copies
-    // of the first window wait for them in stream order. The statistics (DataTable::GetStatistics,
-    // update records of any version included) say which columns can hold a NULL: those probe with
-    // their validity, which also leaves 0 in a NULL row's value.
-    const size_t n_emit = g->emit.size();
-    g->d_cols.resize(n_emit);
-    g->nullable.assign(n_emit, false);
-    g->d_valid.resize(n_emit);
-    std::vector<int64_t> st_min(n_emit, 0), st_max(n_emit, 0);
-    for (size_t e = 0; e < n_emit; ++e) {
-        const column_t col = g->column_ids[g->emit[e]];
-        if (col == COLUMN_IDENTIFIER_ROW_ID || g->count == 0) continue;
-        int hn = 0, hv = 0;
-        check(cubit_table_column_statistics(bind.table, (int)col, &st_min[e], &st_max[e], &hn, &hv),
-              "cubit_table_column_statistics");
-        g->nullable[e] = hn != 0;
-        g->d_cols[e].allocate(device_pool(), ctx, g->count * 8);
-        if (g->nullable[e]) {
-            g->d_valid[e].allocate(device_pool(), ctx, (g->count + 63) / 64 * 8);
-            check(cubit_table_probe_validity(bind.table, (int)col, txn, device_ptr(g->d_ids),
-                                             static_cast<uint64_t*>(d_cnt.p), g->count, device_ptr(g->d_cols[e]),
-                                             static_cast<uint64_t*>(g->d_valid[e].p)),
-                  "cubit_table_probe_validity");
-        } else {
-            check(cubit_table_probe(bind.table, (int)col, txn, device_ptr(g->d_ids), static_cast<uint64_t*>(d_cnt.p),
-                                    g->count, device_ptr(g->d_cols[e])),
-                  "cubit_table_probe");
+    // every partition's decode in flight before any count is read: one per device at a time
+    for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, P->part.n_rows / 8 + 4096);
+    for (auto& P : g->parts) FinishDecode(*P, nodes, txn);
+    for (auto& P : g->parts) LaunchProbes(*P, g->column_ids, g->emit, txn);
+    // windows: consecutive non-empty tiles of one partition, at most window_rows() rows and
+    // window_rows() / 4,096 tiles
+    const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
+    for (uint32_t p = 0; p < g->parts.size(); ++p) {
+        const PartScan& P = *g->parts[p];
+        g->count += P.count;
+        for (uint32_t i = 0; i < P.tiles.size();) {
+            Window w{p, i, i, P.tile_off[i], 0};
+            while (w.last < P.tiles.size() &&
+                   (w.last == w.first || (w.len + P.tile_len[w.last] <= max_rows && w.last - w.first < max_tiles))) {
+                w.len += P.tile_len[w.last];
+                ++w.last;
+            }
+            g->max_window = std::max(g->max_window, w.len);
+            g->windows.push_back(w);
+            i = w.last;
         }
     }
-    // transfer compaction: a column whose values all lie within 2^31 of an offset crosses PCIe
-    // as int32 (row ids: the partition's rows below 2^31, offset row_base; probed columns: their
-    // statistics' range, widened by any update records — a NULL row holds 0 after the validity
-    // probe, inside that window too). The device checks the bound as it narrows.
-    g->narrow.assign(n_emit, false);
-    g->offset.assign(n_emit, 0);
-    g->d_narrow.resize(n_emit);
-    if (g->count) {
-        g->d_overflow.allocate(device_pool(), ctx, n_emit * 4);
-        check(cubit_memset_d(ctx, g->d_overflow.p, 0, n_emit * 4), "overflow flags");
-    }
-    for (size_t e = 0; e < n_emit && g->count; ++e) {
-        const column_t col = g->column_ids[g->emit[e]];
-        bool fits = false;
-        int64_t off = 0;
-        if (col == COLUMN_IDENTIFIER_ROW_ID) {
-            fits = bind.n_rows <= (uint64_t)INT32_MAX;
-            off = bind.row_base;
-        } else {
-            fits = st_min[e] >= INT32_MIN && st_max[e] <= INT32_MAX;
-        }
-        if (!fits) continue;
-        g->narrow[e] = true;
-        g->offset[e] = off;
-        g->d_narrow[e].allocate(device_pool(), ctx, g->count * 4);
-        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g->d_ids : g->d_cols[e];
-        check(cubit_narrow_i32_checked(ctx, device_ptr(src), static_cast<uint64_t*>(d_cnt.p), g->count, off,
-                                       static_cast<int32_t*>(g->d_narrow[e].p),
-                                       static_cast<uint32_t*>(g->d_overflow.p) + e),
-              "cubit_narrow_i32_checked");
-    }
-    // d_cnt goes back to the pool while the probes may still read it: stream order on this
-    // context keeps a later user of the buffer behind them; other contexts never get it
     return g;
 }
 
@@ -358,10 +397,11 @@ std::unique_ptr<LocalTableFunctionState> CubitScanInitLocal(TableFunctionInitInp
 
 // TableScanParallelStateNext analogue: take the next window (row_group_collection.cpp hands
 // out row groups under a mutex; one atomic suffices here) and copy its rows of every emitted
-// column to this state's page-locked buffers. A state copies one window at a time: claiming
-// the next window and copying it while the current one is handed out measured slower at 8 and
-// 16 tasks, before and after the pinned pool reused its buffers (12.4 vs 5.09 ms at 8 tasks,
-// profiles/r04c_pipeline_prefetch_not_kept.txt; round 3: profiles/r03mn_*).
+// column to this state's page-locked buffers, from the window's partition on that partition's
+// device. A state copies one window at a time: claiming the next window and copying it while
+// the current one is handed out measured slower at 8 and 16 tasks, before and after the pinned
+// pool reused its buffers (12.4 vs 5.09 ms at 8 tasks, profiles/r04c_pipeline_prefetch_not_kept.txt;
+// round 3: profiles/r03mn_*).
 bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     const uint32_t w = g.next.fetch_add(1);
     if (w >= g.windows.size()) {
@@ -369,43 +409,48 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         return false;
     }
     const Window& win = g.windows[w];
-    if (!l.copy_stream) {
-        check(cubit_copy_stream_create(g.ctx, &l.copy_stream), "copy stream");
-        l.ctx = g.ctx;
+    PartScan& P = *g.parts[win.part];
+    if (l.streams.size() != g.parts.size()) l.streams.assign(g.parts.size(), {nullptr, nullptr});
+    auto& st = l.streams[win.part];
+    if (!st.second) {
+        check(cubit_copy_stream_create(P.part.ctx, &st.second), "copy stream");
+        st.first = P.part.ctx;
     }
-    // the device's verdict on the compaction bounds, once per scan before any window copy (the
-    // copy stream starts after init_global's work, the narrowing included)
-    std::call_once(g.overflow_checked, [&] {
-        if (!g.d_overflow.p) return;
+    void* stream = st.second;
+    // the device's verdict on the compaction bounds, once per partition before any of its window
+    // copies (the copy stream starts after init_global's work, the narrowing included)
+    std::call_once(P.overflow_checked, [&] {
+        if (!P.d_overflow.p) return;
         std::vector<uint32_t> ov(g.emit.size());
-        check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, ov.data(), g.d_overflow.p, ov.size() * 4), "overflow flags");
+        check(cubit_memcpy_d2h_stream(P.part.ctx, stream, ov.data(), P.d_overflow.p, ov.size() * 4), "overflow flags");
         for (size_t e = 0; e < ov.size(); ++e)
-            if (ov[e]) g.narrow[e] = false;
+            if (ov[e]) P.narrow[e] = false;
     });
     if (l.host.size() != g.emit.size()) {
         l.host.resize(g.emit.size());
         l.host_valid.resize(g.emit.size());
     }
-    // validity words covering the window's rows [off, off + len) of the ordered output
+    // validity words covering the window's rows [off, off + len) of the partition's output
     const uint64_t w0 = win.off / 64, w1 = (win.off + win.len + 63) / 64;
     l.valid_word0 = w0;
     for (size_t e = 0; e < g.emit.size(); ++e) {
-        if (!l.host[e].p) l.host[e].allocate(pinned_pool(), g.ctx, g.max_window * 8);
-        if (g.nullable[e]) {
+        // page-locked memory is filed under no context: any partition's copies may use it
+        if (!l.host[e].p) l.host[e].allocate(pinned_pool(), P.part.ctx, g.max_window * 8);
+        if (P.nullable[e]) {
             // + 2 words: a window may start and end inside a word, and the chunk fill reads one ahead
-            if (!l.host_valid[e].p) l.host_valid[e].allocate(pinned_pool(), g.ctx, (g.max_window / 64 + 3) * 8);
-            check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host_valid[e].p,
-                                          static_cast<const uint64_t*>(g.d_valid[e].p) + w0, (w1 - w0) * 8),
+            if (!l.host_valid[e].p) l.host_valid[e].allocate(pinned_pool(), P.part.ctx, (g.max_window / 64 + 3) * 8);
+            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host_valid[e].p,
+                                          static_cast<const uint64_t*>(P.d_valid[e].p) + w0, (w1 - w0) * 8),
                   "window validity copy");
         }
         const column_t col = g.column_ids[g.emit[e]];
-        if (g.narrow[e]) {
-            const int32_t* src = static_cast<const int32_t*>(g.d_narrow[e].p) + win.off;
-            check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, src, win.len * 4), "window copy");
+        if (P.narrow[e]) {
+            const int32_t* src = static_cast<const int32_t*>(P.d_narrow[e].p) + win.off;
+            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, src, win.len * 4), "window copy");
             continue;
         }
-        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? g.d_ids : g.d_cols[e];
-        check(cubit_memcpy_d2h_stream(g.ctx, l.copy_stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
+        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+        check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
               "window copy");
     }
     l.window = w;
@@ -440,21 +485,23 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
         if (l.window < 0 && !NextWindow(g, l)) return;
         if ((size_t)l.window >= g.windows.size()) return;
         const Window& win = g.windows[l.window];
+        const PartScan& P = *g.parts[win.part];
         if (l.tile_slot >= win.last) {
             if (!NextWindow(g, l)) return;
             continue;
         }
-        const idx_t len = g.tile_len[l.tile_slot];
+        const idx_t len = P.tile_len[l.tile_slot];
         if (l.pos < len) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
-            const idx_t at = g.tile_off[l.tile_slot] - win.off + l.pos;
+            const idx_t at = P.tile_off[l.tile_slot] - win.off + l.pos;
             for (size_t e = 0; e < g.emit.size(); ++e) {
-                if (g.nullable[e]) FillValidity(static_cast<const uint64_t*>(l.host_valid[e].p), win.off + at - 64 * l.valid_word0,
-                                                n, output.validity[e]);
-                if (g.narrow[e]) {  // widen the compacted transfer
+                if (P.nullable[e])
+                    FillValidity(static_cast<const uint64_t*>(l.host_valid[e].p), win.off + at - 64 * l.valid_word0, n,
+                                 output.validity[e]);
+                if (P.narrow[e]) {  // widen the compacted transfer
                     const int32_t* src = static_cast<const int32_t*>(l.host[e].p) + at;
                     int64_t* dst = output.data[e].data();
-                    const int64_t off = g.offset[e];
+                    const int64_t off = P.offset[e];
                     for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
                 } else {
                     std::memcpy(output.data[e].data(), l.host[e].i64() + at, n * sizeof(int64_t));
@@ -470,13 +517,16 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
     }
 }
 
-// batch index = tile index: a local state's tiles ascend (windows are claimed in order and
-// hold consecutive tiles), as PipelineExecutor::NextBatch requires (pipeline_executor.cpp:132)
+// batch index = the partition's tile base + tile index: a local state's tiles ascend (windows
+// are claimed in order — partition by partition — and hold consecutive tiles), as
+// PipelineExecutor::NextBatch requires (pipeline_executor.cpp:132)
 idx_t CubitScanGetBatchIndex(const FunctionData*, LocalTableFunctionState* lstate, GlobalTableFunctionState* gstate) {
     auto& g = static_cast<CubitScanGlobalState&>(*gstate);
     auto& l = static_cast<CubitScanLocalState&>(*lstate);
-    if (l.window < 0 || (size_t)l.window >= g.windows.size() || l.tile_slot >= g.tiles.size()) return 0;
-    return g.tiles[l.tile_slot];
+    if (l.window < 0 || (size_t)l.window >= g.windows.size()) return 0;
+    const PartScan& P = *g.parts[g.windows[l.window].part];
+    if (l.tile_slot >= P.tiles.size()) return 0;
+    return P.tile_base + P.tiles[l.tile_slot];
 }
 double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gstate) {
     auto& g = static_cast<const CubitScanGlobalState&>(*gstate);
@@ -486,7 +536,7 @@ double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gs
 
 // TableScanCardinality (table_scan.cpp:201-208): NodeStatistics(table rows, table rows +
 // transaction-local rows); transaction-local rows stay on the CPU, so both are
-// the partition's rows
+// the partitions' rows
 NodeStatistics CubitScanCardinality(const FunctionData* bind_data) {
     auto& bind = static_cast<const CubitScanBindData&>(*bind_data);
     NodeStatistics st;
@@ -495,15 +545,25 @@ NodeStatistics CubitScanCardinality(const FunctionData* bind_data) {
     return st;
 }
 
-// TableScanStatistics (table_scan.cpp:108-117) → DataTable::GetStatistics: none for the row id
+// TableScanStatistics (table_scan.cpp:108-117) → DataTable::GetStatistics: none for the row id;
+// over several partitions, the merge of theirs (BaseStatistics::Merge: min of mins, max of
+// maxes over the partitions holding a valid value, either NULL flag)
 bool CubitScanStatistics(const FunctionData* bind_data, column_t column_id, ColumnStatistics& out) {
     auto& bind = static_cast<const CubitScanBindData&>(*bind_data);
     if (column_id == COLUMN_IDENTIFIER_ROW_ID) return false;
-    int hn = 0, hv = 0;
-    check(cubit_table_column_statistics(bind.table, (int)column_id, &out.min, &out.max, &hn, &hv),
-          "cubit_table_column_statistics");
-    out.has_null = hn != 0;
-    out.has_no_null = hv != 0;
+    out = ColumnStatistics{};
+    for (const CubitPartition& part : bind.parts) {
+        int64_t mn = 0, mx = 0;
+        int hn = 0, hv = 0;
+        check(cubit_table_column_statistics(part.table, (int)column_id, &mn, &mx, &hn, &hv),
+              "cubit_table_column_statistics");
+        if (hv) {
+            out.min = out.has_no_null ? std::min(out.min, mn) : mn;
+            out.max = out.has_no_null ? std::max(out.max, mx) : mx;
+            out.has_no_null = true;
+        }
+        out.has_null = out.has_null || hn != 0;
+    }
     return true;
 }
 
@@ -558,19 +618,51 @@ extern "C" {
 
 const char* cubit_scan_last_error(void) { return g_scan_error.c_str(); }
 
+}  // extern "C"
+
+namespace {
+
+// The partitions of a scan, in row order: disjoint, ascending row ranges.
+void bind_partitions(cubit_table* const* tables, uint32_t n_tables, CubitScanBindData& bind) {
+    bind.parts.clear();
+    bind.n_rows = 0;
+    for (uint32_t i = 0; i < n_tables; ++i) {
+        if (!tables[i]) throw ScanError(CUBIT_ERR_INVALID, "null partition");
+        CubitPartition p;
+        p.table = tables[i];
+        check(cubit_table_info(tables[i], &p.n_rows, &p.row_base, &p.ctx), "cubit_table_info");
+        if (!bind.parts.empty()) {
+            const CubitPartition& q = bind.parts.back();
+            if (p.row_base < q.row_base + (int64_t)q.n_rows)
+                throw ScanError(CUBIT_ERR_INVALID, "partitions must hold disjoint row ranges in row order");
+        }
+        bind.n_rows += p.n_rows;
+        bind.parts.push_back(p);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
 int cubit_scan_init_global(cubit_table* table, const uint64_t* column_ids, uint32_t n_column_ids,
                            const uint64_t* projection_ids, uint32_t n_projection_ids, const cubit_filter_node* nodes,
                            uint32_t n_nodes, const cubit_txn* txn, cubit_scan** out) {
-    if (!table || !out || (n_column_ids && !column_ids)) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    if (!table) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    return cubit_scan_init_global_multi(&table, 1, column_ids, n_column_ids, projection_ids, n_projection_ids, nodes,
+                                        n_nodes, txn, out);
+}
+
+int cubit_scan_init_global_multi(cubit_table* const* tables, uint32_t n_tables, const uint64_t* column_ids,
+                                 uint32_t n_column_ids, const uint64_t* projection_ids, uint32_t n_projection_ids,
+                                 const cubit_filter_node* nodes, uint32_t n_nodes, const cubit_txn* txn,
+                                 cubit_scan** out) {
+    if (!tables || !n_tables || !out || (n_column_ids && !column_ids))
+        return scan_fail(CUBIT_ERR_INVALID, "null argument");
     try {
         auto s = std::make_unique<cubit_scan>();
         s->fn = GetCubitScanFunction();
-        uint64_t n = 0;
-        int64_t base = 0;
-        check(cubit_table_info(table, &n, &base, &s->bind.ctx), "cubit_table_info");
-        s->bind.table = table;
-        s->bind.n_rows = n;
-        s->bind.row_base = base;
+        bind_partitions(tables, n_tables, s->bind);
         if (txn) {
             s->bind.has_txn = true;
             s->bind.txn = *txn;
@@ -645,14 +737,17 @@ int cubit_scan_progress(cubit_scan* s, double* out) {
     return CUBIT_OK;
 }
 
-// bind-time callbacks: the bind data is the partition (no scan state needed)
+// bind-time callbacks: the bind data is the partitions (no scan state needed)
 int cubit_scan_cardinality(cubit_table* table, uint64_t* estimated, uint64_t* max) {
     if (!table) return scan_fail(CUBIT_ERR_INVALID, "null table");
+    return cubit_scan_cardinality_multi(&table, 1, estimated, max);
+}
+
+int cubit_scan_cardinality_multi(cubit_table* const* tables, uint32_t n_tables, uint64_t* estimated, uint64_t* max) {
+    if (!tables || !n_tables) return scan_fail(CUBIT_ERR_INVALID, "null table");
     try {
         CubitScanBindData bind;
-        int64_t base = 0;
-        check(cubit_table_info(table, &bind.n_rows, &base, &bind.ctx), "cubit_table_info");
-        bind.table = table;
+        bind_partitions(tables, n_tables, bind);
         const NodeStatistics st = GetCubitScanFunction().cardinality(&bind);
         if (estimated) *estimated = st.estimated_cardinality;
         if (max) *max = st.max_cardinality;
@@ -665,9 +760,15 @@ int cubit_scan_cardinality(cubit_table* table, uint64_t* estimated, uint64_t* ma
 int cubit_scan_statistics(cubit_table* table, uint64_t column_id, int64_t* min, int64_t* max, int* has_null,
                           int* has_no_null) {
     if (!table) return scan_fail(CUBIT_ERR_INVALID, "null table");
+    return cubit_scan_statistics_multi(&table, 1, column_id, min, max, has_null, has_no_null);
+}
+
+int cubit_scan_statistics_multi(cubit_table* const* tables, uint32_t n_tables, uint64_t column_id, int64_t* min,
+                                int64_t* max, int* has_null, int* has_no_null) {
+    if (!tables || !n_tables) return scan_fail(CUBIT_ERR_INVALID, "null table");
     try {
         CubitScanBindData bind;
-        bind.table = table;
+        bind_partitions(tables, n_tables, bind);
         ColumnStatistics st;
         if (!GetCubitScanFunction().statistics(&bind, column_id, st))
             return scan_fail(CUBIT_ERR_UNSUPPORTED, "no statistics for the row-id column");

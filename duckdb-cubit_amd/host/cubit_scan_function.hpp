@@ -135,12 +135,22 @@ struct TableFunction {
     bool filter_prune = false;
 };
 
-// bind data: the partition and the reading transaction (TransactionData{start_time, id})
-struct CubitScanBindData : public FunctionData {
+// One row-range partition of the table as libcubitgpu holds it: rows [row_base, row_base +
+// n_rows) on the device of `ctx`.
+struct CubitPartition {
     cubit_table* table = nullptr;
     cubit_ctx* ctx = nullptr;
     idx_t n_rows = 0;
     int64_t row_base = 0;
+};
+
+// bind data: the table's partitions in row order (one per device, or several per device) and the
+// reading transaction (TransactionData{start_time, id}). DuckDB scans one table through one
+// cursor over every row group (RowGroupCollection::InitializeParallelScan / NextParallelScan,
+// row_group_collection.cpp:174-224); the partitions play the row groups' part.
+struct CubitScanBindData : public FunctionData {
+    std::vector<CubitPartition> parts;
+    idx_t n_rows = 0;  // all partitions
     bool has_txn = false;
     cubit_txn txn{};
 };

@@ -129,6 +129,8 @@ typedef struct {
 } cubit_txn;
 
 /* ------------------------------------------------------------------ context */
+/* devices visible to the process (one context per device for a table held as partitions) */
+int cubit_device_count(int *n);
 int cubit_ctx_create(int device, cubit_ctx **out);
 int cubit_ctx_destroy(cubit_ctx *ctx);
 /* stream is a hipStream_t (NULL = the null stream). */

@@ -51,6 +51,19 @@ const char *cubit_scan_last_error(void);
 int cubit_scan_init_global(cubit_table *table, const uint64_t *column_ids, uint32_t n_column_ids,
                            const uint64_t *projection_ids, uint32_t n_projection_ids, const cubit_filter_node *nodes,
                            uint32_t n_nodes, const cubit_txn *txn, cubit_scan **out);
+/* One scan over a table held as n_tables partitions (cubit_table_create row ranges: disjoint and
+ * ascending in row order, CUBIT_ERR_INVALID otherwise), each on its own context — one device per
+ * partition, or several partitions per device. DuckDB scans a table through one cursor over all
+ * of its row groups (RowGroupCollection::InitializeParallelScan / NextParallelScan,
+ * src/storage/table/row_group_collection.cpp:174-224): here every partition decodes and probes
+ * on its own device (launched before any count is read, so the devices work side by side), the
+ * windows of all partitions form one cursor in row order, each window is copied device-to-host
+ * from its own partition, and batch index = the partition's first tile (the tiles of the earlier
+ * partitions, ⌈n_rows / 131,072⌉ each) + its tile. No device-to-device exchange. */
+int cubit_scan_init_global_multi(cubit_table *const *tables, uint32_t n_tables, const uint64_t *column_ids,
+                                 uint32_t n_column_ids, const uint64_t *projection_ids, uint32_t n_projection_ids,
+                                 const cubit_filter_node *nodes, uint32_t n_nodes, const cubit_txn *txn,
+                                 cubit_scan **out);
 int cubit_scan_max_threads(cubit_scan *scan, uint64_t *out);
 int cubit_scan_init_local(cubit_scan *scan, cubit_scan_local **out);
 /* out_columns[i] receives output column i (capacity 2,048 int64 each); *out_count the rows */
@@ -68,6 +81,11 @@ int cubit_scan_progress(cubit_scan *scan, double *out);
 int cubit_scan_cardinality(cubit_table *table, uint64_t *estimated, uint64_t *max);
 int cubit_scan_statistics(cubit_table *table, uint64_t column_id, int64_t *min, int64_t *max, int *has_null,
                           int *has_no_null);
+/* the same over the partitions of one table: rows summed; statistics merged (min of the
+ * partitions' minima and max of their maxima over those holding a valid value, either NULL flag) */
+int cubit_scan_cardinality_multi(cubit_table *const *tables, uint32_t n_tables, uint64_t *estimated, uint64_t *max);
+int cubit_scan_statistics_multi(cubit_table *const *tables, uint32_t n_tables, uint64_t column_id, int64_t *min,
+                                int64_t *max, int *has_null, int *has_no_null);
 /* Buffers of finished scans are kept for the next one (page-locked host windows and device
  * result buffers; at most CUBIT_SCAN_CACHE_MB MiB pinned — default 256 — and 16x that on the
  * device). This frees every cached buffer and reports what was cached (either pointer may be

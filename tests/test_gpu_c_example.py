@@ -45,3 +45,16 @@ def test_c_example_links_against_the_abi():
     out = subprocess.run(["ldd", str(EXE)], capture_output=True, text=True)
     for lib in ("libcubitgpu.so", "libcubit_scan.so", "libcubit_datagen.so"):
         assert lib in out.stdout, out.stdout
+
+
+@pytest.mark.gpu
+def test_q6_from_c_over_partitions(golden):
+    """q6_scan --partitions N: lineitem as N row-range partitions with a context each (spread
+    over the visible devices), the pipeline over all of them through one cursor
+    (cubit_scan_init_global_multi): every Q6 row, the fused revenue."""
+    out = subprocess.run([str(EXE), "1", "4", "--partitions", "3"], capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr
+    line = [x for x in out.stdout.splitlines() if x.startswith("partitioned_pipeline")][0].split()[1:]
+    got = dict(zip(line[0::2], line[1::2]))
+    assert int(got["partitions"]) == 3 and int(got["threads"]) == 4
+    assert int(got["rows"]) == fp_count(golden) and got["revenue_match"] == "1"

@@ -105,3 +105,86 @@ def test_partitioned_probe_at_global_row_ids(ctx):
         assert np.array_equal(out.download(np.int64, len(rows)), li.l_extendedprice[rows - li.row_base])
     for t, _ in parts:
         t.close()
+
+
+@pytest.mark.parametrize("world,tasks", [(8, 1), (8, 4), (3, 4)])
+def test_table_function_over_partitions(golden, world, tasks):
+    """One table-function scan over all partitions (cubit_scan_init_global_multi), each on its
+    own context — as one process driving one device per partition would hold them, here all on
+    device 0: one cursor in row order over every partition's windows (RowGroupCollection's
+    NextParallelScan over all row groups, row_group_collection.cpp:174-224), each window copied
+    from its own partition, batch index = the partition's first tile + its tile. The chunks
+    equal the whole-table oracle, SF1's Q6 fingerprint and its revenue; every task's batch
+    indexes ascend."""
+    import threading
+
+    from cubit_amd import scan_function as S
+    from cubit_amd.scan_function import ROW_ID, CubitScanFunction
+
+    ctxs = [Context(0) for _ in range(world)]
+    orders = datagen.tpch_orders(1)
+    parts = []
+    for r in range(world):
+        ob, oe = parallel.partition_orders(orders, r, world)
+        li = datagen.tpch_lineitem(1, ob, oe)
+        t = CubitTable(ctxs[r], li.n_rows, li.row_base)
+        for c, arr in enumerate((li.l_shipdate, li.l_discount, li.l_quantity, li.l_extendedprice)):
+            t.add_column(c, arr)
+        t.build_index(0, L.INDEX_RANGE, MONTHS)
+        t.build_index(1, L.INDEX_RANGE)
+        t.build_index(2, L.INDEX_RANGE)
+        parts.append((t, li))
+    tables = [t for t, _ in parts]
+    whole = lineitem(1)
+    assert S.cardinality(tables) == (whole.n_rows, whole.n_rows)
+    assert S.statistics(tables, 3) == (int(whole.l_extendedprice.min()), int(whole.l_extendedprice.max()), False, True)
+    fn = CubitScanFunction(tables, [0, 1, 2, 3, ROW_ID], [4, 3, 1], F.q6_filter_set())
+    assert fn.max_threads() >= min(tasks, 2)
+    per_task, lock = {}, threading.Lock()
+
+    def task(k):
+        local = fn.init_local()
+        seen = []
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                break
+            seen.append((fn.get_batch_index(local), cols))
+        with lock:
+            per_task[k] = seen
+
+    th = [threading.Thread(target=task, args=(k,)) for k in range(tasks)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    tile_base = np.cumsum([0] + [(li.n_rows + 131071) // 131072 for _, li in parts])
+    chunks = []
+    for seen in per_task.values():
+        idx = [b for b, _ in seen]
+        assert idx == sorted(idx)
+        for b, cols in seen:
+            p = int(np.searchsorted(tile_base, b, side="right")) - 1
+            li = parts[p][1]
+            assert np.all((cols[0] - li.row_base) // 131072 + tile_base[p] == b)
+        chunks += seen
+    chunks.sort(key=lambda bc: (bc[0], bc[1][0][0]))
+    rows = np.concatenate([c[0] for _, c in chunks])
+    ref = O.table_scan([O.Column(whole.l_shipdate), O.Column(whole.l_discount), O.Column(whole.l_quantity)],
+                       F.serialize(F.q6_filter_set()), whole.n_rows)
+    assert np.array_equal(rows, ref)
+    fp = golden["tpch"]["fingerprints"]["sf1_q6"]
+    assert len(rows) == fp["count"] and int(rows.sum()) == fp["sum_rowid"] and O.xor_hash(rows) == fp["xor_hash"]
+    price = np.concatenate([c[1] for _, c in chunks])
+    disc = np.concatenate([c[2] for _, c in chunks])
+    assert np.array_equal(price, whole.l_extendedprice[ref]) and np.array_equal(disc, whole.l_discount[ref])
+    rev = int((price.astype(object) * disc.astype(object)).sum())
+    assert rev == revenue_from_answer(golden["tpch"]["q6_revenue"]["1"]["revenue"])
+    assert fn.progress() == pytest.approx(100.0)
+    fn.close()
+    with pytest.raises(L.CubitError):  # partitions out of row order
+        CubitScanFunction(tables[::-1], [ROW_ID], None, F.q6_filter_set())
+    for t in tables:
+        t.close()
+    for c in ctxs:
+        c.close()
