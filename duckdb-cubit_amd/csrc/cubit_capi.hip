@@ -961,6 +961,15 @@ extern "C" int cubit_narrow_i32(cubit_ctx* ctx, const int64_t* d_in, const uint6
     return CUBIT_OK;
 }
 
+extern "C" int cubit_narrow_checked(cubit_ctx* ctx, const int64_t* d_in, const uint64_t* d_count, uint64_t max_n,
+                                    int64_t offset, int width, void* d_out, uint32_t* d_overflow) {
+    if (!ctx || !d_in || !d_count || !d_out || !d_overflow) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (width != 1 && width != 2 && width != 4) return fail(CUBIT_ERR_INVALID, "width %d: 1, 2 or 4 bytes", width);
+    CUBIT_LOCK(ctx);
+    HIP_CHECK(launch_narrow_unsigned(d_in, d_count, max_n, offset, width, d_out, d_overflow, ctx->stream));
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_narrow_i32_checked(cubit_ctx* ctx, const int64_t* d_in, const uint64_t* d_count, uint64_t max_n,
                                         int64_t offset, int32_t* d_out, uint32_t* d_overflow) {
     if (!ctx || !d_in || !d_count || !d_out || !d_overflow) return fail(CUBIT_ERR_INVALID, "null argument");

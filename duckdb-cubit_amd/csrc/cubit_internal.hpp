@@ -185,6 +185,10 @@ hipError_t launch_bitpacked_compare(const uint8_t* bytes, const BpGroup* groups,
                                     const uint64_t* validity, int cmp, int64_t constant, int64_t constant2,
                                     uint64_t* out, hipStream_t stream, int simple_width = 0);
 // out[i] = (int32)(in[i] - offset), i < min(*d_count, max_n) (transfer compaction of a column)
+// out[i] = (unsigned width-byte)(in[i] - offset), width 1 / 2 / 4; *overflow = 1 when a value
+// falls outside [offset, offset + 2^(8·width))
+hipError_t launch_narrow_unsigned(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int width,
+                                  void* out, uint32_t* overflow, hipStream_t stream);
 // a narrower / unsigned column (CUBIT_TYPE_INT8 … UINT64) widened to its INT32 / INT64 storage
 hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hipStream_t stream);
 hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,

@@ -1159,12 +1159,66 @@ __device__ uint64_t lookback_recount(const EvalArgs& a, uint32_t b, int t, uint3
     return total;
 }
 // DBG (diagnostic builds, scripts/smallbench.hip; 0 in the library): 1 no spin, 2 no ids, 4 no
-// sleep, 8 no flag loads, 16 no LDS decode, 64 the staging loop without its LDS stores.
+// sleep, 8 no flag loads, 16 no LDS decode, 64 the staging loop without its LDS stores, 128 the
+// staging by rank (stage_by_rank) instead of the per-lane loop.
 // Measured and not kept (scripts/smallbench.hip; profiles/r03e_*, r03g_*, r03h_*): eight copies of
 // every flag, each reader on its own; a two-level walk (groups of 64 tiles + group totals); flag
 // loads issued before the LDS decode; a decoupled look-back (aggregate, then inclusive-prefix flags,
 // walks that stop at the nearest prefix) — slower at every size measured, 573 to 4,578 tiles (at
 // 4,578 the sum over every earlier flag costs 68.5 µs, the decoupled walk 91 µs).
+// Diagnostic (DBG 128): a wave's set bits of one word pair handed out by rank instead of by
+// word — lane l's two words are words 2l, 2l+1 of the wave's slice, `inc` its inclusive count
+// in the slice, `wtot` the slice's total and `base` its first stage slot; `row0` is the slice's
+// first row in the tile. Each lane takes ids k = lane, lane + 64, … : the owning lane by a binary
+// search over the lanes' inclusive counts (LDS), the word by its popcount, the bit by a popcount
+// walk over halves (no pdep on CDNA4). Trips per wave: ⌈wtot / 64⌉ instead of the largest
+// per-lane popcount of each word. Uses s_words' wave region for the words and s_inc's.
+template <int THREADS>
+__device__ __forceinline__ void stage_by_rank(uint64_t w0, uint64_t w1, uint32_t inc, uint32_t wtot, uint32_t base,
+                                              uint32_t row0, uint64_t* s_words, uint32_t* s_inc, uint32_t* s_stage,
+                                              int lane, int wave) {
+    uint64_t* sw = s_words + (uint32_t)wave * 128u;
+    uint32_t* si = s_inc + (uint32_t)wave * 64u;
+    sw[2 * lane] = w0;
+    sw[2 * lane + 1] = w1;
+    si[lane] = inc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (uint32_t k = (uint32_t)lane; k < wtot; k += 64u) {
+        // owner: the number of lanes whose inclusive count is <= k
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (si[l + step - 1] <= k) l += step;
+        const uint32_t ex = l ? si[l - 1] : 0u;
+        uint32_t rk = k - ex;
+        const uint64_t a0 = sw[2 * l], a1 = sw[2 * l + 1];
+        const uint32_t c0 = (uint32_t)__popcll(a0);
+        const bool second = rk >= c0;
+        uint64_t w = second ? a1 : a0;
+        rk -= second ? c0 : 0u;
+        uint32_t x = (uint32_t)w, pos = 0;
+        uint32_t c = (uint32_t)__popc(x);
+        if (rk >= c) {
+            rk -= c;
+            x = (uint32_t)(w >> 32);
+            pos = 32;
+        }
+#pragma unroll
+        for (uint32_t h = 16; h; h >>= 1) {
+            c = (uint32_t)__popc(x & ((1u << h) - 1u));
+            if (rk >= c) {
+                rk -= c;
+                x >>= h;
+                pos += h;
+            }
+        }
+        s_stage[base + k] = row0 + (2u * l + (second ? 1u : 0u)) * 64u + pos;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int K, int FORM, int STAGE, int WPC, int SAUX = 16, int DBG = 0, int THREADS = 512>
 __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_lookback(EvalArgs a,
                                                                                     uint64_t* __restrict__ dir) {
@@ -1233,7 +1287,17 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
 #pragma unroll
         for (int j = 0; j < NW; ++j) s_words[(uint32_t)j * THREADS + t] = r[j];
     }
-    if (!(DBG & 16) && staged && write_ids && tile_count) {
+    if ((DBG & 128) && staged && write_ids && tile_count) {
+        // every lane takes ids lane, lane + 64, … of its wave's slice of each pair
+#pragma unroll
+        for (int p = 0; p < PAIRS; ++p) {
+            const uint32_t inc = (incl >> (16 * p)) & 0xffffu;
+            const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            stage_by_rank<THREADS>(r[2 * p], r[2 * p + 1], inc, wtot, pair_off[p] - (inc - (uint32_t)(__popcll(r[2 * p]) + __popcll(r[2 * p + 1]))),
+                                   (uint32_t)(p * 2 * THREADS + 2 * wave * 64) * 64u, s_words, s_list_scratch, s_stage,
+                                   lane, wave);
+        }
+    } else if (!(DBG & 16) && staged && write_ids && tile_count) {
 #pragma unroll
         for (int p = 0; p < PAIRS; ++p) {
             uint32_t off = pair_off[p];
@@ -1262,15 +1326,20 @@ __global__ __launch_bounds__(THREADS, WPC * THREADS / 256) void eval_decode_look
     for (uint32_t j = t; !prefixed && j < b && !(DBG & 8); j += THREADS) {
         uint64_t f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t spins = 0;
+        bool gave_up = false;
         while (!(DBG & 1) && (f >> kFlagCntBits) != a.epoch) {
-            if (++spins >= spin_limit) {
-                s_expired = 1;  // stop waiting: the workgroup recounts below
-                f = 0;
+            // stop waiting once this thread's limit is reached or another thread of the workgroup
+            // gave up: the workgroup recounts every flag below anyway, so no further flag is
+            // worth a wait (without this each remaining unpublished flag cost another full limit)
+            if (++spins >= spin_limit || *static_cast<volatile uint32_t*>(&s_expired)) {
+                s_expired = 1;
+                gave_up = true;
                 break;
             }
             if (!(DBG & 4)) __builtin_amdgcn_s_sleep(2);
             f = __hip_atomic_load(a.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (gave_up) break;  // `pre` is replaced by the recount
         pre += f & kCntMask;
     }
     pre = wave_sum_flags(pre);
@@ -2464,6 +2533,30 @@ __global__ __launch_bounds__(256) void narrow_i32_kernel(const int64_t* __restri
     if (overflow && bad) *overflow = 1u;
 }
 
+// Transfer compaction to 1, 2 or 4 bytes: out[i] = (O)(in[i] - offset) as an unsigned O, for a
+// column whose values lie in [offset, offset + 2^(8·sizeof O)); `overflow` set when one does not.
+// 8 values per thread per step (one 16-byte store of bytes / halves, two of words).
+template <typename O>
+__global__ __launch_bounds__(256) void narrow_unsigned_kernel(const int64_t* __restrict__ in,
+                                                              const uint64_t* __restrict__ d_count, uint64_t max_n,
+                                                              int64_t offset, O* __restrict__ out,
+                                                              uint32_t* __restrict__ overflow) {
+    const uint64_t n = min(*d_count, max_n);
+    constexpr uint64_t kMax = sizeof(O) == 4 ? 0xffffffffull : (1ull << (8 * sizeof(O))) - 1;
+    bool bad = false;
+    for (uint64_t i = 8 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 8ull * gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (i + j < n) {
+                const uint64_t d = (uint64_t)in[i + j] - (uint64_t)offset;
+                bad |= d > kMax;
+                out[i + j] = (O)d;
+            }
+        }
+    }
+    if (overflow && bad) *overflow = 1u;
+}
+
 // out[i] = in[i] widened: a column registered with a narrower or unsigned type code
 // (cubit_table_add_column) is held as INT32 / INT64 values. 4 values per thread per step.
 template <typename S, typename D>
@@ -3085,6 +3178,24 @@ hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_
     if (max_n == 0) return hipSuccess;
     hipLaunchKernelGGL(narrow_i32_kernel, dim3(grid_for((max_n + 1) / 2)), dim3(256), 0, stream, in, d_count, max_n,
                        offset, out, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_unsigned(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int width,
+                                  void* out, uint32_t* overflow, hipStream_t stream) {
+    if (max_n == 0) return hipSuccess;
+    const dim3 grid(grid_for((max_n + 7) / 8)), block(256);
+    if (width == 1)
+        hipLaunchKernelGGL(narrow_unsigned_kernel<uint8_t>, grid, block, 0, stream, in, d_count, max_n, offset,
+                           static_cast<uint8_t*>(out), overflow);
+    else if (width == 2)
+        hipLaunchKernelGGL(narrow_unsigned_kernel<uint16_t>, grid, block, 0, stream, in, d_count, max_n, offset,
+                           static_cast<uint16_t*>(out), overflow);
+    else if (width == 4)
+        hipLaunchKernelGGL(narrow_unsigned_kernel<uint32_t>, grid, block, 0, stream, in, d_count, max_n, offset,
+                           static_cast<uint32_t*>(out), overflow);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

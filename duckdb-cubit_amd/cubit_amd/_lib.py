@@ -107,6 +107,7 @@ GPU_SIGNATURES = {
     "cubit_gather": (C.c_int, [_P, _P, C.c_int, _P, _P, _U64, _I64, _P]),
     "cubit_narrow_i32": (C.c_int, [_P, _P, _P, _U64, C.c_int64, _P]),
     "cubit_narrow_i32_checked": (C.c_int, [_P, _P, _P, _U64, C.c_int64, _P, _P]),
+    "cubit_narrow_checked": (C.c_int, [_P, _P, _P, _U64, C.c_int64, C.c_int, _P, _P]),
     "cubit_gather_sum_product": (C.c_int, [_P, _P, _P, _P, _P, _U64, _I64, _P]),
     "cubit_table_create": (C.c_int, [_P, _U64, _I64, C.POINTER(_P)]),
     "cubit_table_destroy": (C.c_int, [_P]),

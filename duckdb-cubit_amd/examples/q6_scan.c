@@ -17,7 +17,7 @@
  *    draining 2,048-row chunks of (l_extendedprice, l_discount) into a partial revenue —
  *    timed end to end (best of 3) and checked against the fused revenue; one more line.
  * 6. with --partitions N: lineitem held as N row-range partitions, partition p on device
- *    p mod (devices visible) with a context each — one process driving every GPU of the node —
+ *    p mod (devices visible), one context per device — one process driving every GPU of the node —
  *    and the same pipeline over all of them through one cursor (cubit_scan_init_global_multi:
  *    each partition decodes and probes on its own device, windows are copied from their own
  *    device, no device-to-device exchange); timed and checked the same way; one more line.
@@ -261,12 +261,13 @@ int main(int argc, char **argv) {
     if (threads > 0 && n_partitions > 0) {
         int n_dev = 1;
         CHECK(cubit_device_count(&n_dev));
-        cubit_ctx **pctx = calloc((size_t)n_partitions, sizeof(cubit_ctx *));
+        const int n_ctx = n_dev < n_partitions ? n_dev : n_partitions;
+        cubit_ctx **pctx = calloc((size_t)n_ctx, sizeof(cubit_ctx *));
         cubit_table **pt = calloc((size_t)n_partitions, sizeof(cubit_table *));
+        for (int d = 0; d < n_ctx; ++d) CHECK(cubit_ctx_create(d, &pctx[d]));
         for (int p = 0; p < n_partitions; ++p) {
             const int64_t b = n * p / n_partitions, e = n * (p + 1) / n_partitions;
-            CHECK(cubit_ctx_create(p % n_dev, &pctx[p]));
-            CHECK(cubit_table_create(pctx[p], (uint64_t)(e - b), b, &pt[p]));
+            CHECK(cubit_table_create(pctx[p % n_ctx], (uint64_t)(e - b), b, &pt[p]));
             CHECK(cubit_table_add_column(pt[p], 0, CUBIT_TYPE_INT32, shipdate + b, NULL, 0));
             CHECK(cubit_table_add_column(pt[p], 1, CUBIT_TYPE_INT64, discount + b, NULL, 0));
             CHECK(cubit_table_add_column(pt[p], 2, CUBIT_TYPE_INT64, quantity + b, NULL, 0));
@@ -275,17 +276,15 @@ int main(int argc, char **argv) {
             CHECK(cubit_table_build_index(pt[p], 1, CUBIT_INDEX_RANGE, NULL, 0));
             CHECK(cubit_table_build_index(pt[p], 2, CUBIT_INDEX_RANGE, NULL, 0));
         }
-        for (int p = 0; p < n_partitions; ++p) CHECK(cubit_sync(pctx[p]));
+        for (int d = 0; d < n_ctx; ++d) CHECK(cubit_sync(pctx[d]));
         double init_ms = 0;
         const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms);
         printf("partitioned_pipeline partitions %d devices %d threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64
                " rows_per_s %.4e revenue_match 1\n",
-               n_partitions, n_dev < n_partitions ? n_dev : n_partitions, threads, init_ms, best * 1e3, q, q / best);
+               n_partitions, n_ctx, threads, init_ms, best * 1e3, q, q / best);
         CHECK_SCAN(cubit_scan_release_cached(NULL, NULL));
-        for (int p = 0; p < n_partitions; ++p) {
-            CHECK(cubit_table_destroy(pt[p]));
-            CHECK(cubit_ctx_destroy(pctx[p]));
-        }
+        for (int p = 0; p < n_partitions; ++p) CHECK(cubit_table_destroy(pt[p]));
+        for (int d = 0; d < n_ctx; ++d) CHECK(cubit_ctx_destroy(pctx[d]));
         free(pt);
         free(pctx);
     }

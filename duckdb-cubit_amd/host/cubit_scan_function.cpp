@@ -174,12 +174,13 @@ struct PartScan {
     PooledBuffer d_cnt, d_dir;
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
-    // transfer compaction per emitted position: the window copies move int32 (value - offset)
-    // from d_narrow when every value fits, and the chunk fill widens them back
-    std::vector<bool> narrow;
+    // transfer compaction per emitted position: the window copies move `width` bytes per value
+    // (1, 2 or 4: value - offset as an unsigned integer, the smallest width the column's
+    // statistics allow; 0 = the 8-byte values) from d_narrow, and the chunk fill widens them back
+    std::vector<int> width;
     std::vector<int64_t> offset;
     std::vector<PooledBuffer> d_narrow;
-    // the compaction bound is checked on the device (cubit_narrow_i32_checked): one flag word per
+    // the compaction bound is checked on the device (cubit_narrow_checked): one flag word per
     // emitted position, read once before the partition's first window copy; a column whose flag
     // is set goes back to the 8-byte copy
     PooledBuffer d_overflow;
@@ -220,9 +221,19 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
     std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
     uint64_t valid_word0 = 0;              // ordered-output word of host_valid[e][0]
-    // this task's copy stream per partition (ordered after init_global's device work on the
-    // partition's context): the tasks' window copies run side by side, each from its own device
+    // this task's copy stream per context (ordered after init_global's device work on it):
+    // the tasks' window copies run side by side, each from its own device; partitions that share
+    // a context (several on one device) share the stream — a stream per partition and task put
+    // 64 streams on one device at 8 × 8 and ran 4x slower (profiles/r05d_partitioned_pipeline.txt)
     std::vector<std::pair<cubit_ctx*, void*>> streams;
+    void* stream_for(cubit_ctx* ctx) {
+        for (auto& s : streams)
+            if (s.first == ctx) return s.second;
+        void* st = nullptr;
+        check(cubit_copy_stream_create(ctx, &st), "copy stream");
+        streams.emplace_back(ctx, st);
+        return st;
+    }
     ~CubitScanLocalState() override {
         for (auto& s : streams)
             if (s.second) cubit_copy_stream_destroy(s.first, s.second);
@@ -290,8 +301,9 @@ void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
 // their validity, which also leaves 0 in a NULL row's value. Then the transfer compaction: a
 // column whose values all lie within 2^31 of an offset crosses PCIe as int32 (row ids: the
 // partition's rows below 2^31, offset row_base; probed columns: their statistics' range, widened
-// by any update records — a NULL row holds 0 after the validity probe, inside that window too).
-// The device checks the bound as it narrows.
+// by any update records — a NULL row holds 0 after the validity probe, so 0 joins the range of a
+// nullable column). The narrowest of 1, 2 and 4 bytes that holds the range is taken (Q6's
+// l_discount, 0 … 10, crosses as one byte). The device checks the bound as it narrows.
 void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
                   const cubit_txn* txn) {
     cubit_ctx* ctx = P.part.ctx;
@@ -300,7 +312,7 @@ void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const st
     P.d_cols.resize(n_emit);
     P.nullable.assign(n_emit, false);
     P.d_valid.resize(n_emit);
-    P.narrow.assign(n_emit, false);
+    P.width.assign(n_emit, 0);
     P.offset.assign(n_emit, 0);
     P.d_narrow.resize(n_emit);
     if (P.count == 0) return;
@@ -328,22 +340,24 @@ void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const st
     check(cubit_memset_d(ctx, P.d_overflow.p, 0, n_emit * 4), "overflow flags");
     for (size_t e = 0; e < n_emit; ++e) {
         const column_t col = column_ids[emit[e]];
-        bool fits;
-        int64_t off = 0;
+        int64_t lo, hi;
         if (col == COLUMN_IDENTIFIER_ROW_ID) {
-            fits = P.part.n_rows <= (uint64_t)INT32_MAX;
-            off = P.part.row_base;
+            lo = P.part.row_base;
+            hi = P.part.row_base + (int64_t)P.part.n_rows - 1;
         } else {
-            fits = st_min[e] >= INT32_MIN && st_max[e] <= INT32_MAX;
+            lo = P.nullable[e] ? std::min<int64_t>(st_min[e], 0) : st_min[e];
+            hi = P.nullable[e] ? std::max<int64_t>(st_max[e], 0) : st_max[e];
         }
-        if (!fits) continue;
-        P.narrow[e] = true;
-        P.offset[e] = off;
-        P.d_narrow[e].allocate(device_pool(), ctx, P.count * 4);
+        const uint64_t span = (uint64_t)hi - (uint64_t)lo;  // hi >= lo
+        const int width = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 32) ? 4 : 0;
+        if (!width) continue;
+        P.width[e] = width;
+        P.offset[e] = lo;
+        P.d_narrow[e].allocate(device_pool(), ctx, P.count * (uint64_t)width);
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
-        check(cubit_narrow_i32_checked(ctx, device_ptr(src), d_cnt, P.count, off, static_cast<int32_t*>(P.d_narrow[e].p),
-                                       static_cast<uint32_t*>(P.d_overflow.p) + e),
-              "cubit_narrow_i32_checked");
+        check(cubit_narrow_checked(ctx, device_ptr(src), d_cnt, P.count, lo, width, P.d_narrow[e].p,
+                                   static_cast<uint32_t*>(P.d_overflow.p) + e),
+              "cubit_narrow_checked");
     }
 }
 
@@ -410,13 +424,7 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     }
     const Window& win = g.windows[w];
     PartScan& P = *g.parts[win.part];
-    if (l.streams.size() != g.parts.size()) l.streams.assign(g.parts.size(), {nullptr, nullptr});
-    auto& st = l.streams[win.part];
-    if (!st.second) {
-        check(cubit_copy_stream_create(P.part.ctx, &st.second), "copy stream");
-        st.first = P.part.ctx;
-    }
-    void* stream = st.second;
+    void* stream = l.stream_for(P.part.ctx);
     // the device's verdict on the compaction bounds, once per partition before any of its window
     // copies (the copy stream starts after init_global's work, the narrowing included)
     std::call_once(P.overflow_checked, [&] {
@@ -424,7 +432,7 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         std::vector<uint32_t> ov(g.emit.size());
         check(cubit_memcpy_d2h_stream(P.part.ctx, stream, ov.data(), P.d_overflow.p, ov.size() * 4), "overflow flags");
         for (size_t e = 0; e < ov.size(); ++e)
-            if (ov[e]) P.narrow[e] = false;
+            if (ov[e]) P.width[e] = 0;
     });
     if (l.host.size() != g.emit.size()) {
         l.host.resize(g.emit.size());
@@ -444,9 +452,10 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
                   "window validity copy");
         }
         const column_t col = g.column_ids[g.emit[e]];
-        if (P.narrow[e]) {
-            const int32_t* src = static_cast<const int32_t*>(P.d_narrow[e].p) + win.off;
-            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, src, win.len * 4), "window copy");
+        if (P.width[e]) {
+            const int wd = P.width[e];
+            const char* src = static_cast<const char*>(P.d_narrow[e].p) + win.off * (uint64_t)wd;
+            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, src, win.len * (uint64_t)wd), "window copy");
             continue;
         }
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
@@ -477,6 +486,11 @@ void FillValidity(const uint64_t* words, uint64_t first, idx_t n, ValidityMask& 
     mask.all_valid = all == ~0ull;
 }
 
+template <typename U>
+void widen(const U* __restrict__ src, int64_t off, idx_t n, int64_t* __restrict__ dst) {
+    for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
+}
+
 void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
     auto& g = static_cast<CubitScanGlobalState&>(*data.global_state);
     auto& l = static_cast<CubitScanLocalState&>(*data.local_state);
@@ -498,13 +512,20 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
                 if (P.nullable[e])
                     FillValidity(static_cast<const uint64_t*>(l.host_valid[e].p), win.off + at - 64 * l.valid_word0, n,
                                  output.validity[e]);
-                if (P.narrow[e]) {  // widen the compacted transfer
-                    const int32_t* src = static_cast<const int32_t*>(l.host[e].p) + at;
-                    int64_t* dst = output.data[e].data();
-                    const int64_t off = P.offset[e];
-                    for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
-                } else {
-                    std::memcpy(output.data[e].data(), l.host[e].i64() + at, n * sizeof(int64_t));
+                int64_t* dst = output.Column(e);
+                const int64_t off = P.offset[e];
+                switch (P.width[e]) {  // widen the compacted transfer
+                case 1:
+                    widen(static_cast<const uint8_t*>(l.host[e].p) + at, off, n, dst);
+                    break;
+                case 2:
+                    widen(static_cast<const uint16_t*>(l.host[e].p) + at, off, n, dst);
+                    break;
+                case 4:
+                    widen(static_cast<const uint32_t*>(l.host[e].p) + at, off, n, dst);
+                    break;
+                default:
+                    std::memcpy(dst, l.host[e].i64() + at, n * sizeof(int64_t));
                 }
             }
             l.pos += n;
@@ -705,13 +726,15 @@ int cubit_scan_function_validity(cubit_scan* s, cubit_scan_local* l, int64_t* co
     if (!s || !l || !out_count) return scan_fail(CUBIT_ERR_INVALID, "null argument");
     try {
         TableFunctionInput in{&s->bind, l->lstate.get(), s->gstate.get()};
+        l->chunk.external = out_columns;  // values go straight into the caller's vectors
         s->fn.function(in, l->chunk);
+        l->chunk.external = nullptr;
     } catch (const ScanError& e) {
+        l->chunk.external = nullptr;
         return scan_fail(e.code, e.what());
     }
     const idx_t n = l->chunk.size();
     for (size_t c = 0; c < l->chunk.data.size(); ++c) {
-        if (out_columns && out_columns[c]) std::memcpy(out_columns[c], l->chunk.data[c].data(), n * sizeof(int64_t));
         if (out_validity && out_validity[c]) {
             const ValidityMask& m = l->chunk.validity[c];
             for (idx_t j = 0; j < STANDARD_VECTOR_SIZE / 64; ++j) out_validity[c][j] = m.all_valid ? ~0ull : m.words[j];

@@ -52,6 +52,10 @@ struct DataChunk {
     std::vector<std::vector<int64_t>> data;
     std::vector<ValidityMask> validity;
     idx_t count = 0;
+    // caller-owned vectors of STANDARD_VECTOR_SIZE values per column (null entries: `data`), so a
+    // chunk is filled where its consumer reads it instead of being copied there afterwards
+    int64_t* const* external = nullptr;
+    int64_t* Column(idx_t c) { return external && external[c] ? external[c] : data[c].data(); }
     void Initialize(idx_t n_columns) {
         data.assign(n_columns, std::vector<int64_t>(STANDARD_VECTOR_SIZE));
         validity.assign(n_columns, ValidityMask{});

@@ -245,6 +245,13 @@ int cubit_narrow_i32(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_coun
  * compacted copy must then not be used. */
 int cubit_narrow_i32_checked(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n,
                              int64_t offset, int32_t *d_out, uint32_t *d_overflow);
+/* Transfer compaction to the width a column's statistics allow: d_out[i] = (unsigned, `width` =
+ * 1, 2 or 4 bytes)(d_in[i] - offset) for i < min(*d_count, max_n), for values in [offset, offset +
+ * 2^(8·width)) — e.g. l_discount's 0 … 10 as one byte, a partition's row ids as four. *d_overflow
+ * (device; the caller zeroes it) becomes 1 when a value lies outside, and the copy must then not
+ * be used. */
+int cubit_narrow_checked(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n, int64_t offset,
+                         int width, void *d_out, uint32_t *d_overflow);
 /* Fused probe + reduce: sum over ids of a[r]*b[r] as a 128-bit integer (lo, hi int64 at
  * d_out[0..1]) — Q6's sum(l_extendedprice*l_discount) (DECIMAL(38,4) storage). */
 int cubit_gather_sum_product(cubit_ctx *ctx, const int64_t *d_a, const int64_t *d_b, const int64_t *d_rowids,

@@ -383,6 +383,11 @@ int main(int argc, char** argv) {
                               hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 0>),
                                                  dim3(a.num_tiles), dim3(512), 0, st, a, dir);
                           }, true});
+            vs.push_back({"prefixed, ids staged by rank (DBG 128)", [&](EvalArgs& a, hipStream_t st) {
+                              a.tile_prefix = d_prefix;
+                              hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 128>),
+                                                 dim3(a.num_tiles), dim3(512), 0, st, a, dir);
+                          }, true});
             vs.push_back({"prefixed DBG staging loop without LDS stores", [&](EvalArgs& a, hipStream_t st) {
                               a.tile_prefix = d_prefix;
                               hipLaunchKernelGGL((eval_decode_lookback<1, FORM_CONJ, kLookbackStage, 3, 16, 64>),
