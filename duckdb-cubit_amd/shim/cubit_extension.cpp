@@ -7,9 +7,10 @@
 // Linking it needs libduckdb, which this repository does not build.
 //
 //   PRAGMA cubit_attach('lineitem', 'l_shipdate,l_discount,l_quantity,l_extendedprice'
-//                       [, 'l_shipdate=range:1994-01-01,1995-01-01;l_discount=range;…']);
-//     copies those columns to the GPU (one partition per table, every column from one
-//     snapshot) and builds the named bitmap indexes;
+//                       [, 'l_shipdate=range:1994-01-01,1995-01-01;l_discount=range;…' [, devices]]);
+//     copies those columns to the GPU (every column from one snapshot; one row-range partition
+//     per device, `devices` of them — 1 by default, 0 = every visible device) and builds the
+//     named bitmap indexes;
 //   PRAGMA cubit_sync('lineitem');
 //     brings the partition to the table's committed state (appended rows, committed deletes;
 //     every column again after an UPDATE of an attached one).
@@ -95,8 +96,16 @@ struct CubitIndexSpec {
 //    table in (one transaction for every column). A scan may use the partition only if its own
 //    snapshot includes that one (start_time >= sync_start).
 struct CubitAttached {
-    cubit_ctx *ctx = nullptr;
-    cubit_table *table = nullptr;
+    // one context per device in use; the table as row-range partitions in row order, partition i
+    // on ctxs[i] (one partition per device: PRAGMA cubit_attach's `devices`), scanned through
+    // one cursor (cubit_scan_init_global_multi)
+    vector<cubit_ctx *> ctxs;
+    vector<cubit_table *> parts;
+    vector<uint64_t> part_base;     // first row id of each partition
+    int devices = 1;                // devices the attach asked for (0 = every visible one)
+    bool Attached() const {
+        return !parts.empty();
+    }
     unordered_map<column_t, PhysicalType> columns;
     vector<column_t> column_order;  // attached storage columns, in upload order
     vector<CubitIndexSpec> indexes; // the attach's index specification
@@ -428,9 +437,14 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
     }
     vector<uint64_t> proj(input.projection_ids.begin(), input.projection_ids.end());
     auto g = make_uniq<CubitGlobalState>();
-    if (cubit_scan_init_global(bind.attached.table, cols.data(), (uint32_t)cols.size(), proj.data(),
-                               (uint32_t)proj.size(), nodes.data(), (uint32_t)nodes.size(), &txn,
-                               &g->scan) != CUBIT_OK) {
+    vector<cubit_table *> parts;
+    {
+        lock_guard<mutex> lk(bind.attached.lock);
+        parts = bind.attached.parts;
+    }
+    if (cubit_scan_init_global_multi(parts.data(), (uint32_t)parts.size(), cols.data(), (uint32_t)cols.size(),
+                                     proj.data(), (uint32_t)proj.size(), nodes.data(), (uint32_t)nodes.size(), &txn,
+                                     &g->scan) != CUBIT_OK) {
         throw InvalidInputException("cubit_scan: %s", cubit_scan_last_error());
     }
     uint64_t mt = 1;
@@ -529,10 +543,11 @@ static void CopyValidity(const uint64_t *words, Vector &dst, idx_t n) {
     for (idx_t j = 0; j < nw; j++) {
         all = all && words[j] == ~0ull;
     }
+    auto &mask = FlatVector::Validity(dst);
     if (all) {
+        mask.Reset();  // no buffer = every row valid, whatever an earlier chunk left (validity_mask.hpp:139-143)
         return;
     }
-    auto &mask = FlatVector::Validity(dst);
     mask.Initialize(STANDARD_VECTOR_SIZE);
     auto data = mask.GetData();
     for (idx_t j = 0; j < nw; j++) {
@@ -590,7 +605,8 @@ static double CubitProgress(ClientContext &context, const FunctionData *bind_dat
 static unique_ptr<NodeStatistics> CubitCardinality(ClientContext &context, const FunctionData *bind_data) {
     auto &bind = bind_data->Cast<CubitBindData>();
     uint64_t estimated = 0, max = 0;
-    if (cubit_scan_cardinality(bind.attached.table, &estimated, &max) != CUBIT_OK) {
+    auto &parts = bind.attached.parts;
+    if (cubit_scan_cardinality_multi(parts.data(), (uint32_t)parts.size(), &estimated, &max) != CUBIT_OK) {
         return nullptr;
     }
     return make_uniq<NodeStatistics>(estimated, max);
@@ -606,7 +622,9 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
     }
     int64_t lo = 0, hi = 0;
     int has_null = 0, has_no_null = 0;
-    if (cubit_scan_statistics(bind.attached.table, column_id, &lo, &hi, &has_null, &has_no_null) != CUBIT_OK) {
+    auto &parts = bind.attached.parts;
+    if (cubit_scan_statistics_multi(parts.data(), (uint32_t)parts.size(), column_id, &lo, &hi, &has_null,
+                                    &has_no_null) != CUBIT_OK) {
         return nullptr;
     }
     const auto &type = bind.table.GetColumn(LogicalIndex(column_id)).GetType();
@@ -654,7 +672,7 @@ static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &tabl
         return false;
     }
     lock_guard<mutex> g(attached.lock);
-    return attached.table && attached.writers.empty() && storage.GetTotalRows() == attached.gpu_rows &&
+    return attached.Attached() && attached.writers.empty() && storage.GetTotalRows() == attached.gpu_rows &&
            tx.start_time >= attached.sync_start;
 }
 
@@ -774,10 +792,19 @@ public:
             return;
         }
         auto &tx = tr->Cast<DuckTransaction>();
-        auto props = tx.GetUndoProperties();
+        if (noted_db == db.get() && noted_id == tx.transaction_id && noted_values) {
+            return;  // recorded with values changed: nothing the undo buffer says can add to it
+        }
+        if (!tx.ChangesMade()) {
+            return;
+        }
+        auto props = tx.GetUndoProperties();  // walks the undo buffer: once per statement at most
         if (!props.has_deletes && !props.has_updates) {
             return;
         }
+        noted_db = db.get();
+        noted_id = tx.transaction_id;
+        noted_values = props.has_updates;
         CubitRegistry::NoteDirty(*db, tx.transaction_id, props.has_updates);
         for (auto &kv : CubitRegistry::InDatabase(*db)) {
             lock_guard<mutex> g(kv.second->lock);
@@ -785,6 +812,11 @@ public:
             w = w || props.has_updates;
         }
     }
+
+private:
+    const AttachedDatabase *noted_db = nullptr;  // the writer this connection recorded last
+    transaction_t noted_id = 0;
+    bool noted_values = false;
 };
 
 static void RegisterContextState(ClientContext &context) {
@@ -1033,40 +1065,62 @@ static bool SampleMatches(cubit_ctx *ctx, cubit_table *t, column_t col, const ve
     return true;
 }
 
-// Upload a whole snapshot as a new partition and build its indexes. With `entry`, a column held
-// in persistent BITPACKING segments is registered from them (AttachBitpackedColumn).
-static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, DuckTableEntry *entry) {
-    if (attached.table) {
-        cubit_table_destroy(attached.table);
-        attached.table = nullptr;
+static void DestroyPartitions(CubitAttached &attached) {
+    for (auto t : attached.parts) {
+        cubit_table_destroy(t);
     }
-    Check(cubit_table_create(attached.ctx, snap.rows, 0, &attached.table));
+    attached.parts.clear();
+    attached.part_base.clear();
+}
+
+// Upload a whole snapshot as new partitions and build their indexes: rows split into one
+// contiguous range per context (boundaries on row groups of 122,880 rows = 1,920 bitvector words,
+// so every partition's validity words are the snapshot's own), partition i on ctxs[i]. With
+// `entry` and one partition, a column held in persistent BITPACKING segments is registered from
+// them (AttachBitpackedColumn). Every partition gets the same indexes (the every-distinct-value
+// default decided over the whole snapshot).
+static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, DuckTableEntry *entry) {
+    DestroyPartitions(attached);
+    const uint64_t rg = 122880, units = (snap.rows + rg - 1) / rg;
+    const uint64_t n_parts = std::max<uint64_t>(1, std::min<uint64_t>(attached.ctxs.size(), units));
+    vector<bool> few(attached.column_order.size());
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
-        const column_t col = attached.column_order[c];
-        const bool from_segments =
-            entry && AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, attached.table,
-                                           snap.validity[c].data()) &&
-            SampleMatches(attached.ctx, attached.table, col, snap.values[c], snap.validity[c], snap.rows);
-        if (!from_segments) {  // (re-)registering replaces a column taken from segments
-            const bool wide = WidePhysical(attached.columns[col]);
-            vector<int32_t> narrow;
-            if (!wide) {
-                narrow.assign(snap.values[c].begin(), snap.values[c].end());
+        few[c] = FewDistinct(snap.values[c], snap.validity[c]);
+    }
+    for (uint64_t p = 0; p < n_parts; p++) {
+        const uint64_t b = std::min(snap.rows, units * p / n_parts * rg);
+        const uint64_t e = std::min(snap.rows, units * (p + 1) / n_parts * rg);
+        cubit_table *t = nullptr;
+        Check(cubit_table_create(attached.ctxs[p], e - b, (int64_t)b, &t));
+        attached.parts.push_back(t);
+        attached.part_base.push_back(b);
+        for (idx_t c = 0; c < attached.column_order.size(); c++) {
+            const column_t col = attached.column_order[c];
+            const uint64_t *valid = snap.validity[c].data() + b / 64;
+            const bool from_segments =
+                entry && n_parts == 1 &&
+                AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
+                SampleMatches(attached.ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
+            if (!from_segments) {  // (re-)registering replaces a column taken from segments
+                const bool wide = WidePhysical(attached.columns[col]);
+                vector<int32_t> narrow;
+                if (!wide) {
+                    narrow.assign(snap.values[c].begin() + b, snap.values[c].begin() + e);
+                }
+                Check(cubit_table_add_column(t, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
+                                             wide ? (const void *)(snap.values[c].data() + b) : (const void *)narrow.data(),
+                                             valid, 0));
             }
-            Check(cubit_table_add_column(attached.table, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
-                                         wide ? (const void *)snap.values[c].data() : (const void *)narrow.data(),
-                                         snap.validity[c].data(), 0));
-        }
-        bool named = false;
-        for (auto &ix : attached.indexes) {
-            if (ix.column == col) {
-                Check(cubit_table_build_index(attached.table, (int)col, ix.encoding, ix.keys.data(),
-                                              (uint32_t)ix.keys.size()));
-                named = true;
+            bool named = false;
+            for (auto &ix : attached.indexes) {
+                if (ix.column == col) {
+                    Check(cubit_table_build_index(t, (int)col, ix.encoding, ix.keys.data(), (uint32_t)ix.keys.size()));
+                    named = true;
+                }
             }
-        }
-        if (!named && FewDistinct(snap.values[c], snap.validity[c])) {
-            Check(cubit_table_build_index(attached.table, (int)col, CUBIT_INDEX_RANGE, nullptr, 0));
+            if (!named && few[c]) {
+                Check(cubit_table_build_index(t, (int)col, CUBIT_INDEX_RANGE, nullptr, 0));
+            }
         }
     }
     attached.gpu_rows = snap.rows;
@@ -1106,7 +1160,7 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
     }
     CubitSnapshot snap;
     vector<bool> present;  // presence of every row id of the table in this snapshot
-    if (!rebuild && attached.table) {
+    if (!rebuild && attached.Attached()) {
         // rows appended since the partition was read, then which older rows remain
         ReadRows(con, table_name, entry, attached.column_order, attached.gpu_rows, total_rows, snap);
         auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name) +
@@ -1126,7 +1180,7 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
             rebuild = true;  // fewer rows than the partition: renumbered by a vacuum
         }
     }
-    if (rebuild || !attached.table) {
+    if (rebuild || !attached.Attached()) {
         ReadRows(con, table_name, entry, attached.column_order, 0, total_rows, snap);
         if (snap.rows == 0) {
             con.Commit();
@@ -1159,7 +1213,8 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
                 }
                 valid.push_back(snap.validity[c].data());
             }
-            Check(cubit_table_append(attached.table, snap.rows, cols.data(), data.data(), valid.data(),
+            // appended rows continue the last partition's row range
+            Check(cubit_table_append(attached.parts.back(), snap.rows, cols.data(), data.data(), valid.data(),
                                      (uint32_t)cols.size(), 0));
             attached.gpu_rows += snap.rows;
             present.insert(present.end(), snap.present.begin(), snap.present.end());
@@ -1172,8 +1227,19 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
             gone.push_back((int64_t)r);
         }
     }
-    vector<uint64_t> ids(gone.size(), 0);
-    Check(cubit_table_set_deletes(attached.table, gone.data(), ids.data(), gone.size()));
+    // per partition, as its local rows
+    for (size_t p = 0; p < attached.parts.size(); p++) {
+        const int64_t b = (int64_t)attached.part_base[p];
+        const int64_t e = p + 1 < attached.parts.size() ? (int64_t)attached.part_base[p + 1] : (int64_t)attached.gpu_rows;
+        vector<int64_t> local;
+        for (auto r : gone) {
+            if (r >= b && r < e) {
+                local.push_back(r - b);
+            }
+        }
+        vector<uint64_t> ids(local.size(), 0);
+        Check(cubit_table_set_deletes(attached.parts[p], local.data(), ids.data(), local.size()));
+    }
     lock_guard<mutex> g(attached.lock);
     for (auto w : folded) {
         attached.writers.erase(w);
@@ -1186,7 +1252,7 @@ static void CubitSync(ClientContext &context, const FunctionParameters &paramete
     const auto table_name = parameters.values[0].ToString();
     auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
     auto attached = CubitRegistry::Find(entry);
-    if (!attached || !attached->table) {
+    if (!attached || !attached->Attached()) {
         throw InvalidInputException("cubit_sync: %s is not attached", table_name);
     }
     SyncPartition(context, entry.Cast<DuckTableEntry>(), *attached, table_name, false);
@@ -1245,16 +1311,29 @@ static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string
 // one transaction, upload them and build the named indexes (by default an every-distinct-value
 // range index on the columns with few distinct values). Attaching again replaces the partition.
 static void CubitAttachImpl(ClientContext &context, const string &table_name, const string &column_list,
-                            const string &spec) {
+                            const string &spec, int devices = 1) {
     auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
     if (!entry.IsDuckTable()) {
         throw InvalidInputException("cubit_attach: %s is not a DuckDB table", table_name);
     }
     auto &duck = entry.Cast<DuckTableEntry>();
     auto &attached = CubitRegistry::Insert(entry);
-    if (!attached.ctx) {
-        Check(cubit_ctx_create(0, &attached.ctx));
+    // one context per device: `devices` of them (0 = every visible device), kept across attaches
+    int visible = 1;
+    Check(cubit_device_count(&visible));
+    const int want = devices <= 0 ? visible : std::min(devices, visible);
+    DestroyPartitions(attached);
+    while ((int)attached.ctxs.size() > want) {
+        cubit_scan_release_cached(nullptr, nullptr);  // pooled buffers of the context going away
+        cubit_ctx_destroy(attached.ctxs.back());
+        attached.ctxs.pop_back();
     }
+    while ((int)attached.ctxs.size() < want) {
+        cubit_ctx *c = nullptr;
+        Check(cubit_ctx_create((int)attached.ctxs.size(), &c));
+        attached.ctxs.push_back(c);
+    }
+    attached.devices = devices;
     {
         lock_guard<mutex> g(attached.lock);
         attached.columns.clear();
@@ -1288,6 +1367,13 @@ static void CubitAttachIndexed(ClientContext &context, const FunctionParameters 
                     parameters.values[2].ToString());
 }
 
+// PRAGMA cubit_attach(table, columns, index_spec, devices): the table as one row-range partition
+// per device (devices = 0: every visible device), scanned by one process through one cursor
+static void CubitAttachDevices(ClientContext &context, const FunctionParameters &parameters) {
+    CubitAttachImpl(context, parameters.values[0].ToString(), parameters.values[1].ToString(),
+                    parameters.values[2].ToString(), parameters.values[3].GetValue<int32_t>());
+}
+
 } // namespace duckdb
 
 extern "C" {
@@ -1302,6 +1388,9 @@ DUCKDB_EXTENSION_API void cubit_init(duckdb::DatabaseInstance &db) {
     attach.AddFunction(PragmaFunction::PragmaCall("cubit_attach", CubitAttach, {LogicalType::VARCHAR, LogicalType::VARCHAR}));
     attach.AddFunction(PragmaFunction::PragmaCall("cubit_attach", CubitAttachIndexed,
                                                   {LogicalType::VARCHAR, LogicalType::VARCHAR, LogicalType::VARCHAR}));
+    attach.AddFunction(PragmaFunction::PragmaCall(
+        "cubit_attach", CubitAttachDevices,
+        {LogicalType::VARCHAR, LogicalType::VARCHAR, LogicalType::VARCHAR, LogicalType::INTEGER}));
     ExtensionUtil::RegisterFunction(db, attach);
     ExtensionUtil::RegisterFunction(db, PragmaFunction::PragmaCall("cubit_sync", CubitSync, {LogicalType::VARCHAR}));
     // connections opened from now on carry the writer hook from the start; those already open
