@@ -265,12 +265,35 @@ def main():
                               "range": [-500, 500], "queries": neg},
            "many_matches": {"source": "test/sql/index/art/scan/test_art_many_matches.test", "blocks": blocks}}
     assert len(neg) == 3 and len(blocks) == 2 and all(len(b["counts"]) == 6 for b in blocks)
+    # test/sql/filter/test_transitive_filters.test: vals1(i, j) = (i, i), (i, i+1), (i, i-1) for
+    # i in 0 … 10; the 40 one-table queries `WHERE <i cmp constant> AND <j cmp i>` with their rows in
+    # the order the file lists them. DuckDB pushes the constant comparison into the scan and keeps
+    # the column-to-column comparison in a filter above it (the join queries are not taken).
+    tf_src = (REF / "test/sql/filter/test_transitive_filters.test").read_text()
+    for needle in ("CREATE TABLE vals1 AS SELECT i AS i, i AS j FROM range(0, 11, 1) t1(i)",
+                   "INSERT INTO vals1 SELECT i, i+1 FROM vals1",
+                   "INSERT INTO vals1 SELECT DISTINCT(i), i-1 FROM vals1 ORDER by i"):
+        assert needle in tf_src, needle
+    tf_rows = [[i, i] for i in range(11)] + [[i, i + 1] for i in range(11)] + [[i, i - 1] for i in range(11)]
+    tf_q = []
+    const_re = re.compile(r"^i(<=|>=|<|>|=)(-?\d+)$")
+    col_re = re.compile(r"^j(<=|>=|<|>|=)i$")
+    for where, body in re.findall(r"query II\nSELECT \* FROM vals1 WHERE ([^\n]*)\n----\n((?:[^\n]+\n?)*)", tf_src):
+        terms = [x.strip() for x in where.split(" AND ")]
+        c = [const_re.match(x) for x in terms if const_re.match(x)]
+        r = [col_re.match(x) for x in terms if col_re.match(x)]
+        assert len(c) == 1 and len(r) == 1, where
+        rows = [[int(v) for v in line.split("\t")] for line in body.strip().split("\n") if line]
+        tf_q.append({"where": where, "constant": [c[0].group(1), int(c[0].group(2))], "residual": r[0].group(1),
+                     "rows": rows})
+    assert len(tf_q) == 40, len(tf_q)
+    tf = {"source": "test/sql/filter/test_transitive_filters.test", "rows": tf_rows, "queries": tf_q}
     # NULL-ness through updates (the validity column's update chain): the reference's NULL-update
     # tests as scripts, replayed against the version model in tests/null_updates.py
     nu = {name: sqllogic_script(f"test/sql/update/{name}.test")
           for name in ("test_null_update", "null_update_merge", "null_update_merge_transaction",
                        "test_update_many_updaters_nulls", "update_null_integers")}
-    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "zonemap_segment": zm, "interleaved_versions": iv,
+    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,

@@ -164,3 +164,4 @@ def test_set_null_on_a_column_without_validity(ctx):
     vals, valid = t.fetch(0, rows)
     assert valid.tolist() == [False, True, False] and vals.tolist() == [0, 55, 0]
     t.close()
+

@@ -339,3 +339,32 @@ def test_table_filter_pushdown(ctx, golden, index):
             else:
                 assert cols[out_col][0][rows].tolist() == expect, name
         t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_transitive_filters_through_table_function(ctx, golden, encoding):
+    """test_transitive_filters.test's 40 one-table queries: the constant comparison on i pushed
+    into cubit_scan (plain, range- or equality-indexed i), i and j probed through the table
+    function, and the j-to-i comparison DuckDB evaluates above the scan applied to the chunks:
+    the file's rows in its order."""
+    from test_oracle_filters import transitive_filter_cases
+
+    i, j, cases = transitive_filter_cases(golden)
+    t = CubitTable(ctx, len(i))
+    t.add_column(0, i)
+    t.add_column(1, j)
+    if encoding is not None:
+        t.build_index(0, encoding)
+    for fs, residual, want, where in cases:
+        fn = CubitScanFunction(t, [0, 1, 2 ** 64 - 1], None, fs)
+        local = fn.init_local()
+        got = []
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                break
+            got += [[int(a), int(b), int(r)] for a, b, r in zip(*cols)]
+        fn.close()
+        got.sort(key=lambda x: x[2])  # batch order = row order
+        assert [[a, b] for a, b, _ in got if residual(b, a)] == want, (where, encoding)
+    t.close()

@@ -90,3 +90,4 @@ def test_null_records_count_in_the_update_list(golden):
                 to_null += sum(1 for r in recs if not r[2])
                 from_null += sum(1 for r in recs if r[2] and q.base[c][r[0]] is None)
     assert to_null > 0 and from_null > 0
+
