@@ -188,3 +188,85 @@ def test_table_function_over_partitions(golden, world, tasks):
         t.close()
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("tasks", [1, 3])
+def test_table_function_over_ragged_partitions(tasks):
+    """cubit_scan_init_global_multi over partitions of every awkward kind, on two contexts: an
+    empty one, one where nothing qualifies, one with NULL rows in the projected column (the
+    others have none: the NULL-ness decision and the transfer width are per partition), one
+    with a row base that is not a multiple of 64 and a single ragged tile, and a last one of
+    several windows. Every row's value and NULL-ness equal numpy's; batch indexes ascend per
+    task and lie in the partition's tiles."""
+    import threading
+
+    from cubit_amd.datagen import validity_from_mask
+    from cubit_amd.scan_function import ROW_ID, CubitScanFunction
+
+    rng = np.random.default_rng(11)
+    sizes = [0, 70_000, 300_001, 77, 900_000]
+    ctxs = [Context(0), Context(0)]
+    bases, b = [], 5
+    for n in sizes:
+        bases.append(b)
+        b += n + (3 if n == 77 else 0)  # a gap between two partitions' row ranges
+    parts, cols = [], []
+    for k, (n, base) in enumerate(zip(sizes, bases)):
+        a = rng.integers(0, 100, n).astype(np.int32)
+        if k == 1:
+            a[:] = 500  # nothing passes a < 50
+        v = rng.integers(-(1 << 35), 1 << 35, n).astype(np.int64)
+        valid = rng.random(n) > 0.3 if k == 2 else np.ones(n, bool)
+        t = CubitTable(ctxs[k % 2], n, base)
+        t.add_column(0, a)
+        t.add_column(1, v, validity_from_mask(valid) if k == 2 else None)
+        if n:
+            t.build_index(0, L.INDEX_RANGE)
+        parts.append(t)
+        cols.append((a, v, valid, base))
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 50)})
+    fn = CubitScanFunction(parts, [0, 1, ROW_ID], [2, 1], fs)
+    out, lock = [], threading.Lock()
+
+    def task():
+        local = fn.init_local()
+        last = -1
+        while True:
+            vals, masks = fn.function_validity(local)
+            if len(vals[0]) == 0:
+                return
+            bi = fn.get_batch_index(local)
+            assert bi >= last
+            last = bi
+            with lock:
+                out.append((bi, vals, masks))
+
+    th = [threading.Thread(target=task) for _ in range(tasks)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    out.sort(key=lambda x: (x[0], x[1][0][0]))
+    rows = np.concatenate([o[1][0] for o in out])
+    got_v = np.concatenate([o[1][1] for o in out])
+    got_ok = np.concatenate([o[2][1] for o in out])
+    want_rows, want_v, want_ok = [], [], []
+    tile_base = 0
+    for (a, v, valid, base), n in zip(cols, sizes):
+        keep = np.flatnonzero(a < 50)
+        want_rows.append(keep + base)
+        want_v.append(np.where(valid[keep], v[keep], 0))
+        want_ok.append(valid[keep])
+        for bi, vals, _ in out:
+            sel = (vals[0] >= base) & (vals[0] < base + n)
+            if sel.any():
+                assert np.all((vals[0][sel] - base) // 131072 + tile_base == bi)
+        tile_base += (n + 131071) // 131072
+    assert np.array_equal(rows, np.concatenate(want_rows))
+    assert np.array_equal(got_ok, np.concatenate(want_ok)) and np.array_equal(got_v, np.concatenate(want_v))
+    assert fn.progress() == pytest.approx(100.0)
+    fn.close()
+    for t in parts:
+        t.close()
+    for c in ctxs:
+        c.close()
