@@ -35,7 +35,10 @@ def gpu_table(ctx, q: NU.Query, encoding):
         data = np.array([0 if v is None else v for v in base], dtype=np.int32)
         valid = np.array([v is not None for v in base], dtype=bool)
         t.add_column(j, data, validity_from_mask(valid) if not valid.all() else None)
-        if encoding is not None:
+        if encoding == "bins":  # an every-value range index plus binned bitvectors beside it
+            t.build_index(j, L.INDEX_RANGE)
+            t.build_index(j, L.INDEX_BINS, [0, 2, 4, 8, 17, 100])
+        elif encoding is not None:
             t.build_index(j, encoding)
     return t
 
@@ -85,7 +88,7 @@ def check_query(t, q: NU.Query, nulls_first, label):
             assert t.count(fs, txn=txn) == len(want), (label, q.sql, c, flt)
 
 
-@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY, "bins"])
 @pytest.mark.parametrize("name", CASES)
 def test_null_update_scripts_on_gpu(ctx, golden, name, encoding):
     case = NU.cases(golden)[name]
@@ -103,7 +106,7 @@ def test_null_update_scripts_on_gpu(ctx, golden, name, encoding):
     t.close()
 
 
-@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY, "bins"])
 def test_null_update_merge_checkpoints_every_statement(ctx, golden, encoding):
     """null_update_merge.test with a checkpoint after every statement: each query's committed
     records are merged as soon as it has read them (NULL → value and value → NULL flips of the

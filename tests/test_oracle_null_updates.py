@@ -51,6 +51,13 @@ def predicates(q: NU.Query, col: str):
         for op, f in (("=", lambda v, k=k: v == k), ("<", lambda v, k=k: v < k), (">=", lambda v, k=k: v >= k),
                       ("!=", lambda v, k=k: v != k)):
             out.append((F.ConstantFilter(op, k), lambda v, f=f: v is not None and f(v)))
+    # ranges, on bin edges (the GPU test's binned index: 0, 2, 4, 8, 17, 100) and off them, and a
+    # NULL-or-value disjunction
+    for lo, hi in ((2, 8), (4, 17), (1, 3), (0, 100)):
+        out.append((F.ConjunctionAndFilter([F.ConstantFilter(">=", lo), F.ConstantFilter("<", hi)]),
+                    lambda v, lo=lo, hi=hi: v is not None and lo <= v < hi))
+    out.append((F.ConjunctionOrFilter([F.IsNullFilter(), F.ConstantFilter("<", 3)]),
+                lambda v: v is None or v < 3))
     return out
 
 
