@@ -23,30 +23,55 @@ def sqllogic_script(rel):
     session settings that shape the replay (immediate transaction mode, NULL ordering)."""
     src = (REF / rel).read_text()
     script, flags = [], {"immediate_transaction_mode": False, "nulls_first": False}
+    loop = None  # (variable, range, blocks) while inside loop ... endloop
+
+    def value(v):
+        if v == "NULL":
+            return None
+        return int(v) if re.fullmatch(r"-?\d+", v) else int(float(v))  # SUM as DOUBLE: "294912.000000"
+
+    def emit(lines):
+        head = lines[0].split()
+        con = head[2] if len(head) > 2 else "default"
+        if head[0] == "statement":
+            body = " ".join(x.strip() for x in lines[1:] if x.strip() != "----")
+            for sql in [s.strip() for s in body.split(";") if s.strip()]:  # one entry per statement
+                if sql.upper().startswith("SET IMMEDIATE_TRANSACTION_MODE"):
+                    flags["immediate_transaction_mode"] = True
+                elif sql.upper().startswith("SET DEFAULT_NULL_ORDER"):
+                    flags["nulls_first"] = "nulls_first" in sql
+                elif not sql.upper().startswith("PRAGMA"):
+                    script.append({"op": "statement", "con": con, "sql": sql, "ok": head[1] == "ok"})
+        elif head[0] == "query":
+            sep = lines.index("----")
+            rows = [[value(v) for v in line.split("\t")] for line in lines[sep + 1:]]
+            script.append({"op": "query", "con": con, "sql": " ".join(lines[1:sep]), "rows": rows})
+        else:
+            assert head[0] in ("require", "load"), head
+
     for block in re.split(r"\n\s*\n", src):
         lines = [x for x in block.strip().split("\n") if x and not x.startswith("#")]
         if not lines:
             continue
         head = lines[0].split()
-        if head[0] == "statement":
-            sql = " ".join(x.strip() for x in lines[1:] if x.strip() != "----")
-            if sql.upper().startswith("SET IMMEDIATE_TRANSACTION_MODE"):
-                flags["immediate_transaction_mode"] = True
+        if head[0] == "loop":
+            loop = (head[1], range(int(head[2]), int(head[3])), [])
+            lines = lines[1:]
+            if not lines:
                 continue
-            if sql.upper().startswith("SET DEFAULT_NULL_ORDER"):
-                flags["nulls_first"] = "nulls_first" in sql
-                continue
-            if sql.upper().startswith("PRAGMA"):
-                continue
-            script.append({"op": "statement", "con": head[2] if len(head) > 2 else "default", "sql": sql,
-                           "ok": head[1] == "ok"})
-        elif head[0] == "query":
-            sep = lines.index("----")
-            rows = [[None if v == "NULL" else int(v) for v in line.split("\t")] for line in lines[sep + 1:]]
-            script.append({"op": "query", "con": head[2] if len(head) > 2 else "default",
-                           "sql": " ".join(lines[1:sep]), "rows": rows})
-        else:
-            assert head[0] in ("require", "load"), head
+        if lines[-1].strip() == "endloop":
+            var, rng, blocks = loop
+            blocks.append(lines[:-1])
+            for i in rng:
+                for b in blocks:
+                    if b:
+                        emit([x.replace("${" + var + "}", str(i)) for x in b])
+            loop = None
+            continue
+        if loop is not None:
+            loop[2].append(lines)
+            continue
+        emit(lines)
     return {"source": rel, **flags, "script": script}
 
 
@@ -289,11 +314,20 @@ def main():
     assert len(tf_q) == 40, len(tf_q)
     tf = {"source": "test/sql/filter/test_transitive_filters.test", "rows": tf_rows, "queries": tf_q}
     # NULL-ness through updates (the validity column's update chain): the reference's NULL-update
-    # tests as scripts, replayed against the version model in tests/null_updates.py
+    # tests as scripts, replayed against the version model in tests/sql_replay.py
     nu = {name: sqllogic_script(f"test/sql/update/{name}.test")
           for name in ("test_null_update", "null_update_merge", "null_update_merge_transaction",
                        "test_update_many_updaters_nulls", "update_null_integers")}
-    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
+    # inserts, deletes and updates under concurrent transactions: the reference's MVCC scripts,
+    # replayed by tests/sql_replay.py (insert / delete stamps and update records)
+    mvcc = {Path(rel).stem: sqllogic_script(rel) for rel in (
+        "test/sql/update/test_update_delete_same_tuple.test", "test/sql/update/update_after_commit.test",
+        "test/sql/update/test_update_same_value.test", "test/sql/delete/test_delete.test",
+        "test/sql/delete/test_large_delete.test", "test/sql/delete/large_deletes_transactions.test",
+        "test/sql/delete/test_segment_deletes.test", "test/sql/transactions/test_multi_transaction_append.test",
+        "test/sql/transactions/test_multi_version_large.test", "test/sql/transactions/test_null_version.test",
+        "test/sql/transactions/test_transaction_local_data.test")}
+    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "mvcc_scripts": mvcc, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
