@@ -322,7 +322,11 @@ def main():
     # replayed by tests/sql_replay.py (insert / delete stamps and update records)
     mvcc = {Path(rel).stem: sqllogic_script(rel) for rel in (
         "test/sql/update/test_update_delete_same_tuple.test", "test/sql/update/update_after_commit.test",
-        "test/sql/update/test_update_same_value.test", "test/sql/delete/test_delete.test",
+        "test/sql/update/test_update_same_value.test", "test/sql/update/test_update.test",
+        "test/sql/update/test_update_mix.test", "test/sql/update/test_update_many_updaters.test",
+        "test/sql/update/test_cascading_updates.test", "test/sql/delete/test_truncate.test",
+        "test/sql/delete/test_large_delete_parallel.test", "test/sql/transactions/test_multi_version.test",
+        "test/sql/transactions/test_interleaved_versions.test", "test/sql/delete/test_delete.test",
         "test/sql/delete/test_large_delete.test", "test/sql/delete/large_deletes_transactions.test",
         "test/sql/delete/test_segment_deletes.test", "test/sql/transactions/test_multi_transaction_append.test",
         "test/sql/transactions/test_multi_version_large.test", "test/sql/transactions/test_null_version.test",

@@ -4,10 +4,11 @@ extracted by tests/golden/make_golden.py).
 
 Files replayed: test/sql/update/{test_null_update, null_update_merge, null_update_merge_transaction,
 test_update_many_updaters_nulls, update_null_integers, test_update_delete_same_tuple,
-update_after_commit, test_update_same_value}.test; test/sql/delete/{test_delete, test_large_delete,
-large_deletes_transactions, test_segment_deletes}.test; test/sql/transactions/{
-test_multi_transaction_append, test_multi_version_large, test_null_version,
-test_transaction_local_data}.test.
+update_after_commit, test_update_same_value, test_update, test_update_mix, test_update_many_updaters,
+test_cascading_updates}.test; test/sql/delete/{test_delete, test_large_delete,
+large_deletes_transactions, test_segment_deletes, test_truncate, test_large_delete_parallel}.test;
+test/sql/transactions/{test_multi_transaction_append, test_multi_version_large, test_null_version,
+test_transaction_local_data, test_multi_version, test_interleaved_versions}.test.
 
 The replay records each statement the way DuckDB's version machinery does:
 * INSERT appends rows stamped with the inserting transaction's id (ChunkVectorInfo::Append,
@@ -22,7 +23,9 @@ The replay records each statement the way DuckDB's version machinery does:
 Start times and commit ids come from one increasing counter; a transaction sees a version v when
 v < start_time or v == its transaction id (TransactionVersionOperator::UseInsertedVersion,
 chunk_info.cpp:11-14). BEGIN takes the snapshot at once under immediate_transaction_mode, else at the
-transaction's first statement; a statement outside BEGIN is its own transaction.
+transaction's first statement; a statement outside BEGIN is its own transaction. A failed statement
+inside BEGIN aborts the transaction (its effects are dropped) and the COMMIT or ROLLBACK that
+follows ends it; TRUNCATE is a DELETE of every row; CHECKPOINT is left to the tests (a merge).
 
 Each SELECT is handed to the caller as a `Query`: the snapshot and the whole version state at that
 moment (every row ever appended with its insert and delete stamps, and the update records). The
@@ -284,6 +287,7 @@ class Query:
     deleted: np.ndarray             # uint64 per row
     records: Dict[str, list]        # column -> [(rows, values, valid, version)] batches, chronological
     view: Frame                     # the replay's own answer: the visible rows, with "rowid"
+    horizon: int = 0                # the oldest snapshot still open: a checkpoint may merge below it
 
     @property
     def n_rows(self) -> int:
@@ -403,17 +407,15 @@ class Replay:
                         np.array([r[j] is not None for r in tups], bool)) for j, c in enumerate(self.cols)}
             self.append(cols, owner)
             return
-        m = re.match(r"INSERT INTO \w+ SELECT (\w+), NULL FROM range\((\d+)\) tbl\((\w+)\)", s, re.I)
-        if m:
-            n = int(m.group(2))
-            a, b = self.cols
-            self.append({a: (np.arange(n, dtype=np.int64), np.ones(n, bool)),
-                         b: (np.zeros(n, np.int64), np.zeros(n, bool))}, owner)
-            return
-        m = re.match(r"INSERT INTO \w+ SELECT \* FROM range\((\d+),\s*(\d+),\s*1\)", s, re.I)
-        if m:
-            v = np.arange(int(m.group(1)), int(m.group(2)), dtype=np.int64)
-            self.append({self.cols[0]: (v, np.ones(len(v), bool))}, owner)
+        m = re.match(r"INSERT INTO \w+ SELECT (.*) FROM range\((\d+)(?:,\s*(\d+)(?:,\s*1)?)?\)(?:\s*\w+\((\w+)\))?$", s, re.I)
+        if m:  # SELECT <expressions over the range variable> FROM range(lo, hi[, 1]) alias(var)
+            lo, hi = (0, int(m.group(2))) if m.group(3) is None else (int(m.group(2)), int(m.group(3)))
+            v = np.arange(lo, hi, dtype=np.int64)
+            f = {(m.group(4) or "range").lower(): (v, np.ones(len(v), bool)), "rowid": (v, np.ones(len(v), bool))}
+            items = [x.strip() for x in m.group(1).split(",")]
+            exprs = [parse_expr(m.group(4) or "range") for _ in self.cols] if items == ["*"] else [parse_expr(x) for x in items]
+            assert len(exprs) == len(self.cols), sql
+            self.append({c: e(f) for c, e in zip(self.cols, exprs)}, owner)
             return
         m = re.match(r"INSERT INTO (\w+) SELECT \* FROM (\w+)$", s, re.I)
         assert m and m.group(1) == m.group(2), sql
@@ -464,7 +466,8 @@ class Replay:
             recs.setdefault(col, []).append((r, v, ok, self.txns[owner].version))
         return Query(con, sql, rows, t.start, t.tid, list(self.cols),
                      {c: (self.vals[c].copy(), self.valid[c].copy()) for c in self.cols},
-                     self.versions(self.ins, 0), self.versions(self.dels, NOT_DELETED), recs, self.view(t))
+                     self.versions(self.ins, 0), self.versions(self.dels, NOT_DELETED), recs, self.view(t),
+                     min([t.start] + [a.start for a in self.active.values() if a.start is not None]))
 
     def run(self):
         """Yields a Query per SELECT of the script (a DML statement's outcome and row count are
@@ -485,11 +488,15 @@ class Replay:
                 self.active[con] = t
                 continue
             if up.rstrip(";") in ("COMMIT", "ROLLBACK"):
-                self.finish(self.active.pop(con), up.startswith("COMMIT"))
+                t = self.active.pop(con)
+                if not t.aborted:  # COMMIT of an aborted transaction is its rollback
+                    self.finish(t, up.startswith("COMMIT"))
                 continue
             if up.startswith("INSERT") and not self.started and con not in self.active:
                 self.insert(sql, None)  # setup rows, before any snapshot: visible to all
                 continue
+            if up.startswith("TRUNCATE"):
+                sql, up = "DELETE FROM t", "DELETE FROM T"
             t = self.active.get(con) or self.new_txn(False)
             self.snapshot(t)
             if up.startswith(("UPDATE", "DELETE", "INSERT")):
@@ -505,8 +512,8 @@ class Replay:
                     assert ok and [[n]] == step["rows"], (sql, n, step["rows"])
                 if not t.explicit:
                     self.finish(t, ok)
-                elif not ok:  # a failed statement aborts its transaction
-                    self.finish(self.active.pop(con), False)
+                elif not ok:  # a failed statement aborts its transaction; ROLLBACK (or COMMIT) ends it
+                    self.finish(t, False)
                 continue
             assert step["op"] == "query", sql
             yield self.query_state(con, sql, step["rows"], t)

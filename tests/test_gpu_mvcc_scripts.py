@@ -155,6 +155,26 @@ def test_scripts_on_gpu(ctx, golden, group, name, encoding):
     dev.close()
 
 
+@pytest.mark.parametrize("encoding", [None, "bins"])
+@pytest.mark.parametrize("group,name", ALL)
+def test_scripts_with_a_checkpoint_after_every_query(ctx, golden, group, name, encoding):
+    """Every script with a checkpoint after each query: the committed records below the oldest
+    open snapshot merge into the base values, the validity and the index leaves, and the next query
+    hands over only the records at or above that horizon — every later query still reads the
+    file's rows."""
+    case = script(golden, group, name)
+    dev = DeviceScript(ctx, encoding)
+    merged = 0
+    for q in R.queries(case):
+        dev.sync(q, since=merged)
+        check_query(dev.t, q, case["nulls_first"], (name, encoding, "merge-each"), exhaustive=False)
+        horizon = max(merged, q.horizon)
+        for j in range(len(q.columns)):
+            dev.t.merge_updates(j, horizon)
+        merged = horizon
+    dev.close()
+
+
 @pytest.mark.parametrize("encoding", ENCODINGS)
 def test_null_update_merge_checkpoints_every_statement(ctx, golden, encoding):
     """null_update_merge.test with a checkpoint after every statement: each query's committed

@@ -21,7 +21,9 @@ NULL_CASES = ["test_null_update", "null_update_merge", "null_update_merge_transa
 MVCC_CASES = ["test_update_delete_same_tuple", "update_after_commit", "test_update_same_value", "test_delete",
               "test_large_delete", "large_deletes_transactions", "test_segment_deletes",
               "test_multi_transaction_append", "test_multi_version_large", "test_null_version",
-              "test_transaction_local_data"]
+              "test_transaction_local_data", "test_update", "test_update_mix", "test_update_many_updaters",
+              "test_cascading_updates", "test_truncate", "test_large_delete_parallel", "test_multi_version",
+              "test_interleaved_versions"]
 ALL = [("null_updates", n) for n in NULL_CASES] + [("mvcc_scripts", n) for n in MVCC_CASES]
 
 
