@@ -26,6 +26,7 @@
 #include <string>
 #include <tuple>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/cubit_gpu.h"
@@ -97,6 +98,9 @@ struct cubit_ctx {
     // (creating a HIP stream costs milliseconds; the table function's tasks take one per scan)
     std::vector<std::pair<hipStream_t, hipEvent_t>> copy_pool;
     std::unordered_map<hipStream_t, hipEvent_t> copy_live;
+    // copy events (cubit_copy_event_record): handed out and returned through a pool
+    std::vector<hipEvent_t> copy_ev_pool;
+    std::unordered_set<hipEvent_t> copy_ev_live;
     std::recursive_mutex mu;     // CUBIT_LOCK
 };
 
@@ -380,6 +384,8 @@ int cubit_ctx_destroy(cubit_ctx* ctx) {
         (void)hipStreamDestroy(se.first);
         (void)hipEventDestroy(se.second);
     }
+    for (hipEvent_t e : ctx->copy_ev_live) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->copy_ev_pool) (void)hipEventDestroy(e);
     for (auto& e : ctx->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -566,6 +572,57 @@ int cubit_memcpy_d2h_stream(cubit_ctx* ctx, void* stream, void* dst, const void*
     const hipStream_t s = static_cast<hipStream_t>(stream);
     HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    return CUBIT_OK;
+}
+
+int cubit_memcpy_d2h_async(cubit_ctx* ctx, void* stream, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+    return CUBIT_OK;
+}
+
+int cubit_copy_stream_sync(cubit_ctx* ctx, void* stream) {
+    if (!ctx || !stream) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return CUBIT_OK;
+}
+
+int cubit_copy_event_record(cubit_ctx* ctx, void* stream, void** event) {
+    if (!ctx || !stream || !event) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    if (int rc = set_device(ctx)) return rc;
+    hipEvent_t e = nullptr;
+    if (!ctx->copy_ev_pool.empty()) {
+        e = ctx->copy_ev_pool.back();
+        ctx->copy_ev_pool.pop_back();
+    } else {
+        HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    ctx->copy_ev_live.insert(e);
+    HIP_CHECK(hipEventRecord(e, static_cast<hipStream_t>(stream)));
+    *event = e;
+    return CUBIT_OK;
+}
+
+int cubit_copy_event_sync(cubit_ctx* ctx, void* event) {
+    if (!ctx || !event) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+    return CUBIT_OK;
+}
+
+int cubit_copy_event_destroy(cubit_ctx* ctx, void* event) {
+    if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
+    if (!event) return CUBIT_OK;
+    CUBIT_LOCK(ctx);
+    auto it = ctx->copy_ev_live.find(static_cast<hipEvent_t>(event));
+    if (it == ctx->copy_ev_live.end()) return fail(CUBIT_ERR_INVALID, "not a copy event of this context");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipEventSynchronize(*it));  // its copies are done before the event is reused
+    ctx->copy_ev_pool.push_back(*it);
+    ctx->copy_ev_live.erase(it);
     return CUBIT_OK;
 }
 
@@ -964,7 +1021,7 @@ extern "C" int cubit_narrow_i32(cubit_ctx* ctx, const int64_t* d_in, const uint6
 extern "C" int cubit_narrow_checked(cubit_ctx* ctx, const int64_t* d_in, const uint64_t* d_count, uint64_t max_n,
                                     int64_t offset, int width, void* d_out, uint32_t* d_overflow) {
     if (!ctx || !d_in || !d_count || !d_out || !d_overflow) return fail(CUBIT_ERR_INVALID, "null argument");
-    if (width != 1 && width != 2 && width != 4) return fail(CUBIT_ERR_INVALID, "width %d: 1, 2 or 4 bytes", width);
+    if (width < 1 || width > 4) return fail(CUBIT_ERR_INVALID, "width %d: 1, 2, 3 or 4 bytes", width);
     CUBIT_LOCK(ctx);
     HIP_CHECK(launch_narrow_unsigned(d_in, d_count, max_n, offset, width, d_out, d_overflow, ctx->stream));
     return CUBIT_OK;

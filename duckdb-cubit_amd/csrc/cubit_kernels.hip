@@ -2535,7 +2535,11 @@ __global__ __launch_bounds__(256) void narrow_i32_kernel(const int64_t* __restri
 
 // Transfer compaction to 1, 2 or 4 bytes: out[i] = (O)(in[i] - offset) as an unsigned O, for a
 // column whose values lie in [offset, offset + 2^(8·sizeof O)); `overflow` set when one does not.
-// 8 values per thread per step (one 16-byte store of bytes / halves, two of words).
+// 8 values per thread per step: four 16-byte loads, and the 8 narrowed values packed into one
+// 8-byte (bytes), one 16-byte (halves) or two 16-byte (words) stores, so a wave's store covers
+// 512 B – 2 KB contiguously — the shape that matters when `out` is page-locked host memory
+// written across PCIe (a wave of scattered 1-byte stores ran the link at ~3 GB/s). `in` and
+// `out` 16-byte aligned (launch_narrow_unsigned falls back to the scalar form otherwise).
 template <typename O>
 __global__ __launch_bounds__(256) void narrow_unsigned_kernel(const int64_t* __restrict__ in,
                                                               const uint64_t* __restrict__ d_count, uint64_t max_n,
@@ -2545,14 +2549,118 @@ __global__ __launch_bounds__(256) void narrow_unsigned_kernel(const int64_t* __r
     constexpr uint64_t kMax = sizeof(O) == 4 ? 0xffffffffull : (1ull << (8 * sizeof(O))) - 1;
     bool bad = false;
     for (uint64_t i = 8 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 8ull * gridDim.x * blockDim.x) {
+        if (i + 8 <= n) {
+            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(in + i);
+            uint64_t d[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (i + j < n) {
-                const uint64_t d = (uint64_t)in[i + j] - (uint64_t)offset;
+            for (int j = 0; j < 4; ++j) {
+                const ulonglong2 v = src[j];
+                d[2 * j] = v.x - (uint64_t)offset;
+                d[2 * j + 1] = v.y - (uint64_t)offset;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bad |= d[j] > kMax;
+            if constexpr (sizeof(O) == 1) {
+                uint64_t p = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) p |= (d[j] & 0xff) << (8 * j);
+                *reinterpret_cast<uint64_t*>(out + i) = p;
+            } else if constexpr (sizeof(O) == 2) {
+                ulonglong2 p{0, 0};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    p.x |= (d[j] & 0xffff) << (16 * j);
+                    p.y |= (d[4 + j] & 0xffff) << (16 * j);
+                }
+                *reinterpret_cast<ulonglong2*>(out + i) = p;
+            } else {
+                ulonglong2* dst = reinterpret_cast<ulonglong2*>(out + i);
+                dst[0] = ulonglong2{(d[0] & 0xffffffffull) | (d[1] << 32), (d[2] & 0xffffffffull) | (d[3] << 32)};
+                dst[1] = ulonglong2{(d[4] & 0xffffffffull) | (d[5] << 32), (d[6] & 0xffffffffull) | (d[7] << 32)};
+            }
+        } else {
+            for (uint64_t k = i; k < n; ++k) {
+                const uint64_t d = (uint64_t)in[k] - (uint64_t)offset;
                 bad |= d > kMax;
-                out[i + j] = (O)d;
+                out[k] = (O)d;
             }
         }
+    }
+    if (overflow && bad) *overflow = 1u;
+}
+
+// Three bytes per value (a column whose range spans < 2^24, e.g. l_extendedprice in cents):
+// value k of the output at bytes [3k, 3k + 3), little-endian. 8 values per thread per step,
+// packed into three 8-byte stores (a wave's 1.5 KB contiguous). `in` 16-byte and `out` 8-byte
+// aligned (launch_narrow_unsigned falls back to byte stores otherwise).
+__global__ __launch_bounds__(256) void narrow_u24_kernel(const int64_t* __restrict__ in,
+                                                         const uint64_t* __restrict__ d_count, uint64_t max_n,
+                                                         int64_t offset, uint8_t* __restrict__ out,
+                                                         uint32_t* __restrict__ overflow) {
+    const uint64_t n = min(*d_count, max_n);
+    constexpr uint64_t kMax = (1ull << 24) - 1;
+    bool bad = false;
+    for (uint64_t i = 8 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x); i < n; i += 8ull * gridDim.x * blockDim.x) {
+        if (i + 8 <= n) {
+            const ulonglong2* src = reinterpret_cast<const ulonglong2*>(in + i);
+            uint64_t d[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const ulonglong2 v = src[j];
+                d[2 * j] = v.x - (uint64_t)offset;
+                d[2 * j + 1] = v.y - (uint64_t)offset;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bad |= d[j] > kMax;
+                d[j] &= kMax;
+            }
+            uint64_t* dst = reinterpret_cast<uint64_t*>(out + 3 * i);
+            dst[0] = d[0] | (d[1] << 24) | (d[2] << 48);
+            dst[1] = (d[2] >> 16) | (d[3] << 8) | (d[4] << 32) | (d[5] << 56);
+            dst[2] = (d[5] >> 8) | (d[6] << 16) | (d[7] << 40);
+        } else {
+            for (uint64_t k = i; k < n; ++k) {
+                const uint64_t d = (uint64_t)in[k] - (uint64_t)offset;
+                bad |= d > kMax;
+                out[3 * k] = (uint8_t)d;
+                out[3 * k + 1] = (uint8_t)(d >> 8);
+                out[3 * k + 2] = (uint8_t)(d >> 16);
+            }
+        }
+    }
+    if (overflow && bad) *overflow = 1u;
+}
+
+__global__ __launch_bounds__(256) void narrow_u24_scalar_kernel(const int64_t* __restrict__ in,
+                                                                const uint64_t* __restrict__ d_count, uint64_t max_n,
+                                                                int64_t offset, uint8_t* __restrict__ out,
+                                                                uint32_t* __restrict__ overflow) {
+    const uint64_t n = min(*d_count, max_n);
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = (uint64_t)in[i] - (uint64_t)offset;
+        bad |= d > 0xffffffull;
+        out[3 * i] = (uint8_t)d;
+        out[3 * i + 1] = (uint8_t)(d >> 8);
+        out[3 * i + 2] = (uint8_t)(d >> 16);
+    }
+    if (overflow && bad) *overflow = 1u;
+}
+
+// The same for operands of any alignment: one value per store.
+template <typename O>
+__global__ __launch_bounds__(256) void narrow_unsigned_scalar_kernel(const int64_t* __restrict__ in,
+                                                                     const uint64_t* __restrict__ d_count,
+                                                                     uint64_t max_n, int64_t offset, O* __restrict__ out,
+                                                                     uint32_t* __restrict__ overflow) {
+    const uint64_t n = min(*d_count, max_n);
+    constexpr uint64_t kMax = sizeof(O) == 4 ? 0xffffffffull : (1ull << (8 * sizeof(O))) - 1;
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = (uint64_t)in[i] - (uint64_t)offset;
+        bad |= d > kMax;
+        out[i] = (O)d;
     }
     if (overflow && bad) *overflow = 1u;
 }
@@ -3181,20 +3289,36 @@ hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_
     return hipGetLastError();
 }
 
+template <typename O>
+static void narrow_unsigned_launch(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, O* out,
+                                   uint32_t* overflow, hipStream_t stream) {
+    const bool aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+    if (aligned)
+        hipLaunchKernelGGL(narrow_unsigned_kernel<O>, dim3(grid_for((max_n + 7) / 8)), dim3(256), 0, stream, in, d_count,
+                           max_n, offset, out, overflow);
+    else
+        hipLaunchKernelGGL(narrow_unsigned_scalar_kernel<O>, dim3(grid_for(max_n)), dim3(256), 0, stream, in, d_count,
+                           max_n, offset, out, overflow);
+}
+
 hipError_t launch_narrow_unsigned(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int width,
                                   void* out, uint32_t* overflow, hipStream_t stream) {
     if (max_n == 0) return hipSuccess;
-    const dim3 grid(grid_for((max_n + 7) / 8)), block(256);
     if (width == 1)
-        hipLaunchKernelGGL(narrow_unsigned_kernel<uint8_t>, grid, block, 0, stream, in, d_count, max_n, offset,
-                           static_cast<uint8_t*>(out), overflow);
+        narrow_unsigned_launch(in, d_count, max_n, offset, static_cast<uint8_t*>(out), overflow, stream);
     else if (width == 2)
-        hipLaunchKernelGGL(narrow_unsigned_kernel<uint16_t>, grid, block, 0, stream, in, d_count, max_n, offset,
-                           static_cast<uint16_t*>(out), overflow);
+        narrow_unsigned_launch(in, d_count, max_n, offset, static_cast<uint16_t*>(out), overflow, stream);
     else if (width == 4)
-        hipLaunchKernelGGL(narrow_unsigned_kernel<uint32_t>, grid, block, 0, stream, in, d_count, max_n, offset,
-                           static_cast<uint32_t*>(out), overflow);
-    else
+        narrow_unsigned_launch(in, d_count, max_n, offset, static_cast<uint32_t*>(out), overflow, stream);
+    else if (width == 3) {
+        uint8_t* o = static_cast<uint8_t*>(out);
+        if (reinterpret_cast<uintptr_t>(in) % 16 == 0 && reinterpret_cast<uintptr_t>(o) % 8 == 0)
+            hipLaunchKernelGGL(narrow_u24_kernel, dim3(grid_for((max_n + 7) / 8)), dim3(256), 0, stream, in, d_count,
+                               max_n, offset, o, overflow);
+        else
+            hipLaunchKernelGGL(narrow_u24_scalar_kernel, dim3(grid_for(max_n)), dim3(256), 0, stream, in, d_count, max_n,
+                               offset, o, overflow);
+    } else
         return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -99,6 +99,11 @@ GPU_SIGNATURES = {
     "cubit_copy_stream_create": (C.c_int, [_P, C.POINTER(_P)]),
     "cubit_copy_stream_destroy": (C.c_int, [_P, _P]),
     "cubit_memcpy_d2h_stream": (C.c_int, [_P, _P, _P, _P, _U64]),
+    "cubit_memcpy_d2h_async": (C.c_int, [_P, _P, _P, _P, _U64]),
+    "cubit_copy_stream_sync": (C.c_int, [_P, _P]),
+    "cubit_copy_event_record": (C.c_int, [_P, _P, C.POINTER(_P)]),
+    "cubit_copy_event_sync": (C.c_int, [_P, _P]),
+    "cubit_copy_event_destroy": (C.c_int, [_P, _P]),
     "cubit_build_bitvector": (C.c_int, [_P, _P, C.c_int, _P, _U64, C.c_int, _I64, _P]),
     "cubit_bitvector_eval": (
         C.c_int,

@@ -79,6 +79,7 @@ typedef struct {
     uint64_t rows;
     __int128 revenue;
     int rc;
+    double scan_s, consume_s; /* time inside cubit_scan_function / in the aggregate */
 } task_t;
 
 static void *pipeline_task(void *arg) {
@@ -88,13 +89,18 @@ static void *pipeline_task(void *arg) {
     if (tk->rc != CUBIT_OK) return NULL;
     int64_t *cols[2] = {malloc(2048 * 8), malloc(2048 * 8)};
     uint64_t got = 0;
+    double t = now_s();
     do {
         tk->rc = cubit_scan_function(tk->scan, local, cols, &got);
+        const double t1 = now_s();
+        tk->scan_s += t1 - t;
         if (tk->rc != CUBIT_OK) break;
         __int128 s = 0;
         for (uint64_t i = 0; i < got; ++i) s += (__int128)cols[0][i] * cols[1][i];
         tk->revenue += s;
         tk->rows += got;
+        t = now_s();
+        tk->consume_s += t - t1;
     } while (got);
     cubit_scan_local_destroy(local);
     free(cols[0]);
@@ -104,7 +110,7 @@ static void *pipeline_task(void *arg) {
 
 /* `threads` pipeline tasks over one init_global (best of 3 end to end); returns the best time */
 static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cubit_filter_node *q6, uint32_t nn,
-                           int threads, uint64_t want_rows, __int128 want_rev, double *init_ms) {
+                           int threads, uint64_t want_rows, __int128 want_rev, double *init_ms, double split_ms[2]) {
     const uint64_t proj_ids[] = {3, 1};
     double best = 1e30;
     task_t *tasks = calloc((size_t)threads, sizeof(task_t));
@@ -115,22 +121,27 @@ static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cu
         CHECK_SCAN(cubit_scan_init_global_multi(parts, n_parts, proj_ids, 2, NULL, 0, q6, nn, NULL, &ps));
         const double t1 = now_s();
         for (int i = 0; i < threads; ++i) {
-            tasks[i] = (task_t){ps, 0, 0, 0};
+            tasks[i] = (task_t){ps, 0, 0, 0, 0, 0};
             if (pthread_create(&th[i], NULL, pipeline_task, &tasks[i]) != 0) exit(1);
         }
         uint64_t rows_p = 0;
         __int128 rev_p = 0;
+        double scan_s = 0, consume_s = 0;
         for (int i = 0; i < threads; ++i) {
             pthread_join(th[i], NULL);
             CHECK_SCAN(tasks[i].rc);
             rows_p += tasks[i].rows;
             rev_p += tasks[i].revenue;
+            scan_s += tasks[i].scan_s;
+            consume_s += tasks[i].consume_s;
         }
         const double t2 = now_s();
         CHECK_SCAN(cubit_scan_destroy(ps));
         if (t2 - t0 < best) {
             best = t2 - t0;
             *init_ms = (t1 - t0) * 1e3;
+            split_ms[0] = scan_s * 1e3 / threads; /* per task: inside the callbacks */
+            split_ms[1] = consume_s * 1e3 / threads; /* per task: the aggregate's own work */
         }
         if (rows_p != want_rows || rev_p != want_rev) {
             fprintf(stderr, "pipeline: %" PRIu64 " rows, revenue differs from the fused sum\n", rows_p);
@@ -251,10 +262,25 @@ int main(int argc, char **argv) {
     /* 5. the query as a pipeline of `threads` tasks over the callbacks */
     const int threads = argc > 2 ? atoi(argv[2]) : 0;
     if (threads > 0) {
-        double init_ms = 0;
-        const double best = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms);
-        printf("pipeline threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64 " rows_per_s %.4e revenue_match 1\n",
-               threads, init_ms, best * 1e3, q, q / best);
+        double init_ms = 0, split[2] = {0, 0};
+        const double best = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms, split);
+        printf("pipeline threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64 " rows_per_s %.4e revenue_match 1"
+               " task_scan_ms %.3f task_aggregate_ms %.3f\n",
+               threads, init_ms, best * 1e3, q, q / best, split[0], split[1]);
+        /* the link's own device-to-host rate into page-locked memory (one 64 MiB copy, best of 3):
+         * the floor the pipeline's window copies share */
+        const uint64_t link_bytes = (uint64_t)n * 8 < (64ull << 20) ? (uint64_t)n * 8 : (64ull << 20);
+        void *h_link;
+        CHECK(cubit_host_alloc(ctx, link_bytes, &h_link));
+        double link_best = 1e30;
+        for (int rep = 0; rep < 3; ++rep) {
+            const double l0 = now_s();
+            CHECK(cubit_memcpy_d2h(ctx, h_link, d_ids, link_bytes));
+            const double l1 = now_s();
+            if (l1 - l0 < link_best) link_best = l1 - l0;
+        }
+        CHECK(cubit_host_free(ctx, h_link));
+        printf("link_d2h bytes %" PRIu64 " ms %.3f gb_per_s %.2f\n", link_bytes, link_best * 1e3, link_bytes / link_best / 1e9);
     }
 
     /* 6. the same pipeline over N row-range partitions, one context each, spread over the devices */
@@ -277,11 +303,11 @@ int main(int argc, char **argv) {
             CHECK(cubit_table_build_index(pt[p], 2, CUBIT_INDEX_RANGE, NULL, 0));
         }
         for (int d = 0; d < n_ctx; ++d) CHECK(cubit_sync(pctx[d]));
-        double init_ms = 0;
-        const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms);
+        double init_ms = 0, split[2] = {0, 0};
+        const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms, split);
         printf("partitioned_pipeline partitions %d devices %d threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64
-               " rows_per_s %.4e revenue_match 1\n",
-               n_partitions, n_ctx, threads, init_ms, best * 1e3, q, q / best);
+               " rows_per_s %.4e revenue_match 1 task_scan_ms %.3f task_aggregate_ms %.3f\n",
+               n_partitions, n_ctx, threads, init_ms, best * 1e3, q, q / best, split[0], split[1]);
         CHECK_SCAN(cubit_scan_release_cached(NULL, NULL));
         for (int p = 0; p < n_partitions; ++p) CHECK(cubit_table_destroy(pt[p]));
         for (int d = 0; d < n_ctx; ++d) CHECK(cubit_ctx_destroy(pctx[d]));

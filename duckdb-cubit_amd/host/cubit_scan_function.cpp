@@ -162,7 +162,22 @@ struct Window {
     uint32_t part;         // the partition the window's tiles belong to
     uint32_t first, last;  // index range [first, last) into that partition's non-empty tiles
     idx_t off, len;        // the window's rows in the partition's ordered output
+    uint32_t group = 0;    // staged partitions: the group of copies that brings the window's rows
 };
+
+// Staging: init_global copies every emitted column's transfer form (and validity words) to
+// page-locked host memory on ONE copy stream per partition, in row order, in groups of consecutive
+// windows of about kStageGroupBytes, each group closed by an event. A pipeline task that claims a
+// window waits for its group's event and reads the rows in place. One stream of multi-megabyte
+// copies runs the link at its own rate (56.6 GB/s for one 64 MiB copy on the MI355X box); the
+// tasks' concurrent per-window copies (0.5–1 MB each on up to 16 streams) reached ~20 GB/s
+// (profiles/r05k_*). Partitions whose staged bytes exceed CUBIT_SCAN_STAGE_MB (default 1024) are
+// copied per window by the task that claims it, as before.
+constexpr uint64_t kStageGroupBytes = 4ull << 20;
+uint64_t stage_cap_bytes() {  // read per init_global
+    const char* e = std::getenv("CUBIT_SCAN_STAGE_MB");
+    return (e && *e ? std::strtoull(e, nullptr, 10) : 1024ull) << 20;
+}
 
 // The device side of one partition's scan: its ordered row ids, the probed columns and the
 // non-empty tiles' runs.
@@ -175,7 +190,7 @@ struct PartScan {
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
     // transfer compaction per emitted position: the window copies move `width` bytes per value
-    // (1, 2 or 4: value - offset as an unsigned integer, the smallest width the column's
+    // (1, 2, 3 or 4: value - offset as an unsigned integer, the smallest width the column's
     // statistics allow; 0 = the 8-byte values) from d_narrow, and the chunk fill widens them back
     std::vector<int> width;
     std::vector<int64_t> offset;
@@ -192,6 +207,19 @@ struct PartScan {
     std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
+    // staging (see kStageGroupBytes): the copy stream, the host copies of every emitted column's
+    // transfer form and validity words, the overflow flags copied ahead of them, one event per
+    // group; `unstaged[e]` marks a column whose compaction overflowed (copied per window instead)
+    bool staged = false;
+    void* stage_stream = nullptr;
+    std::vector<PooledBuffer> h_stage, h_stage_valid;
+    PooledBuffer h_flags;
+    std::vector<void*> group_ev;
+    std::vector<bool> unstaged;
+    ~PartScan() {
+        for (void* ev : group_ev) cubit_copy_event_destroy(part.ctx, ev);
+        if (stage_stream) cubit_copy_stream_destroy(part.ctx, stage_stream);
+    }
 };
 
 struct CubitScanGlobalState : public GlobalTableFunctionState {
@@ -220,7 +248,11 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
     std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
-    uint64_t valid_word0 = 0;              // ordered-output word of host_valid[e][0]
+    uint64_t valid_word0 = 0;              // ordered-output word of src_valid[e][0]
+    // per emitted position: the window's first row on the host (its own copy, or the partition's
+    // staged rows) and the validity word valid_word0
+    std::vector<const char*> src;
+    std::vector<const uint64_t*> src_valid;
     // this task's copy stream per context (ordered after init_global's device work on it):
     // the tasks' window copies run side by side, each from its own device; partitions that share
     // a context (several on one device) share the stream — a stream per partition and task put
@@ -302,8 +334,9 @@ void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
 // column whose values all lie within 2^31 of an offset crosses PCIe as int32 (row ids: the
 // partition's rows below 2^31, offset row_base; probed columns: their statistics' range, widened
 // by any update records — a NULL row holds 0 after the validity probe, so 0 joins the range of a
-// nullable column). The narrowest of 1, 2 and 4 bytes that holds the range is taken (Q6's
-// l_discount, 0 … 10, crosses as one byte). The device checks the bound as it narrows.
+// nullable column). The narrowest of 1, 2, 3 and 4 bytes that holds the range is taken (Q6's
+// l_discount, 0 … 10, crosses as one byte, l_extendedprice as three). The device checks the bound
+// as it narrows.
 void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
                   const cubit_txn* txn) {
     cubit_ctx* ctx = P.part.ctx;
@@ -349,7 +382,7 @@ void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const st
             hi = P.nullable[e] ? std::max<int64_t>(st_max[e], 0) : st_max[e];
         }
         const uint64_t span = (uint64_t)hi - (uint64_t)lo;  // hi >= lo
-        const int width = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 32) ? 4 : 0;
+        const int width = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 24) ? 3 : span < (1ull << 32) ? 4 : 0;
         if (!width) continue;
         P.width[e] = width;
         P.offset[e] = lo;
@@ -359,6 +392,72 @@ void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const st
                                    static_cast<uint32_t*>(P.d_overflow.p) + e),
               "cubit_narrow_checked");
     }
+}
+
+// Bytes per row of an emitted column's transfer form: its compacted width, or the 8-byte value.
+uint64_t transfer_bytes(const PartScan& P, size_t e) { return P.width[e] ? (uint64_t)P.width[e] : 8; }
+
+// The transfer form of emitted position e on the device.
+const char* transfer_src(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit, size_t e) {
+    if (P.width[e]) return static_cast<const char*>(P.d_narrow[e].p);
+    PooledBuffer& src = column_ids[emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+    return static_cast<const char*>(src.p);
+}
+
+// Enqueue the staging copies of partition p (see kStageGroupBytes) and set its windows' groups.
+void Stage(CubitScanGlobalState& g, uint32_t p) {
+    PartScan& P = *g.parts[p];
+    const size_t n_emit = g.emit.size();
+    if (P.count == 0 || n_emit == 0) return;
+    uint64_t row_bytes = 0, total = 0;
+    for (size_t e = 0; e < n_emit; ++e) {
+        row_bytes += transfer_bytes(P, e);
+        total += P.count * transfer_bytes(P, e) + (P.nullable[e] ? (P.count + 63) / 64 * 8 : 0);
+    }
+    if (total > stage_cap_bytes()) return;
+    cubit_ctx* ctx = P.part.ctx;
+    check(cubit_copy_stream_create(ctx, &P.stage_stream), "staging stream");  // after the probes and narrowing
+    P.h_stage.resize(n_emit);
+    P.h_stage_valid.resize(n_emit);
+    P.unstaged.assign(n_emit, false);
+    // + 8 bytes: the 3-byte widen reads 4
+    for (size_t e = 0; e < n_emit; ++e) {
+        P.h_stage[e].allocate(pinned_pool(), ctx, P.count * transfer_bytes(P, e) + 8);
+        if (P.nullable[e]) P.h_stage_valid[e].allocate(pinned_pool(), ctx, ((P.count + 63) / 64 + 2) * 8);
+    }
+    P.h_flags.allocate(pinned_pool(), ctx, n_emit * 4);
+    check(cubit_memcpy_d2h_async(ctx, P.stage_stream, P.h_flags.p, P.d_overflow.p, n_emit * 4), "staged flags");
+    const uint64_t rows_per_group = std::max<uint64_t>(kStageGroupBytes / std::max<uint64_t>(row_bytes, 1), 1);
+    auto flush = [&](idx_t off, idx_t len) {
+        for (size_t e = 0; e < n_emit; ++e) {
+            const uint64_t b = transfer_bytes(P, e);
+            check(cubit_memcpy_d2h_async(ctx, P.stage_stream, static_cast<char*>(P.h_stage[e].p) + off * b,
+                                         transfer_src(P, g.column_ids, g.emit, e) + off * b, len * b),
+                  "staged copy");
+            if (P.nullable[e]) {
+                const uint64_t w0 = off / 64, w1 = (off + len + 63) / 64;
+                check(cubit_memcpy_d2h_async(ctx, P.stage_stream, static_cast<uint64_t*>(P.h_stage_valid[e].p) + w0,
+                                             static_cast<const uint64_t*>(P.d_valid[e].p) + w0, (w1 - w0) * 8),
+                      "staged validity copy");
+            }
+        }
+        void* ev = nullptr;
+        check(cubit_copy_event_record(ctx, P.stage_stream, &ev), "staged group event");
+        P.group_ev.push_back(ev);
+    };
+    idx_t g_off = 0, g_len = 0;
+    for (Window& w : g.windows) {
+        if (w.part != p) continue;
+        if (g_len && g_len + w.len > rows_per_group) {
+            flush(g_off, g_len);
+            g_off += g_len;
+            g_len = 0;
+        }
+        w.group = (uint32_t)P.group_ev.size();
+        g_len += w.len;
+    }
+    if (g_len) flush(g_off, g_len);
+    P.staged = true;
 }
 
 std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
@@ -402,6 +501,7 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
             i = w.last;
         }
     }
+    for (uint32_t p = 0; p < g->parts.size(); ++p) Stage(*g, p);
     return g;
 }
 
@@ -424,6 +524,47 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     }
     const Window& win = g.windows[w];
     PartScan& P = *g.parts[win.part];
+    if (l.host.size() != g.emit.size()) {
+        l.host.resize(g.emit.size());
+        l.host_valid.resize(g.emit.size());
+        l.src.resize(g.emit.size());
+        l.src_valid.resize(g.emit.size());
+    }
+    const uint64_t w0 = win.off / 64;
+    l.valid_word0 = w0;
+    l.window = w;
+    l.tile_slot = win.first;
+    l.pos = 0;
+    if (P.staged) {
+        check(cubit_copy_event_sync(P.part.ctx, P.group_ev[win.group]), "staged group");
+        // the flags were copied ahead of every group: a column whose compaction overflowed goes
+        // back to the 8-byte values, copied per window
+        std::call_once(P.overflow_checked, [&] {
+            const uint32_t* ov = static_cast<const uint32_t*>(P.h_flags.p);
+            for (size_t e = 0; e < g.emit.size(); ++e)
+                if (ov[e] && P.width[e]) {
+                    P.width[e] = 0;
+                    P.unstaged[e] = true;
+                }
+        });
+        bool copied = false;
+        for (size_t e = 0; e < g.emit.size(); ++e) {
+            if (P.nullable[e]) l.src_valid[e] = static_cast<const uint64_t*>(P.h_stage_valid[e].p) + w0;
+            if (!P.unstaged[e]) {
+                l.src[e] = static_cast<const char*>(P.h_stage[e].p) + win.off * transfer_bytes(P, e);
+                continue;
+            }
+            if (!l.host[e].p) l.host[e].allocate(pinned_pool(), P.part.ctx, g.max_window * 8);
+            PooledBuffer& src = g.column_ids[g.emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+            check(cubit_memcpy_d2h_async(P.part.ctx, l.stream_for(P.part.ctx), l.host[e].p, device_ptr(src) + win.off,
+                                         win.len * 8),
+                  "window copy");
+            l.src[e] = static_cast<const char*>(l.host[e].p);
+            copied = true;
+        }
+        if (copied) check(cubit_copy_stream_sync(P.part.ctx, l.stream_for(P.part.ctx)), "window copies");
+        return true;
+    }
     void* stream = l.stream_for(P.part.ctx);
     // the device's verdict on the compaction bounds, once per partition before any of its window
     // copies (the copy stream starts after init_global's work, the narrowing included)
@@ -434,37 +575,32 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         for (size_t e = 0; e < ov.size(); ++e)
             if (ov[e]) P.width[e] = 0;
     });
-    if (l.host.size() != g.emit.size()) {
-        l.host.resize(g.emit.size());
-        l.host_valid.resize(g.emit.size());
-    }
     // validity words covering the window's rows [off, off + len) of the partition's output
-    const uint64_t w0 = win.off / 64, w1 = (win.off + win.len + 63) / 64;
-    l.valid_word0 = w0;
+    const uint64_t w1 = (win.off + win.len + 63) / 64;
     for (size_t e = 0; e < g.emit.size(); ++e) {
         // page-locked memory is filed under no context: any partition's copies may use it
         if (!l.host[e].p) l.host[e].allocate(pinned_pool(), P.part.ctx, g.max_window * 8);
         if (P.nullable[e]) {
             // + 2 words: a window may start and end inside a word, and the chunk fill reads one ahead
             if (!l.host_valid[e].p) l.host_valid[e].allocate(pinned_pool(), P.part.ctx, (g.max_window / 64 + 3) * 8);
-            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host_valid[e].p,
-                                          static_cast<const uint64_t*>(P.d_valid[e].p) + w0, (w1 - w0) * 8),
+            check(cubit_memcpy_d2h_async(P.part.ctx, stream, l.host_valid[e].p,
+                                         static_cast<const uint64_t*>(P.d_valid[e].p) + w0, (w1 - w0) * 8),
                   "window validity copy");
+            l.src_valid[e] = static_cast<const uint64_t*>(l.host_valid[e].p);
         }
+        l.src[e] = static_cast<const char*>(l.host[e].p);
         const column_t col = g.column_ids[g.emit[e]];
         if (P.width[e]) {
             const int wd = P.width[e];
             const char* src = static_cast<const char*>(P.d_narrow[e].p) + win.off * (uint64_t)wd;
-            check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, src, win.len * (uint64_t)wd), "window copy");
+            check(cubit_memcpy_d2h_async(P.part.ctx, stream, l.host[e].p, src, win.len * (uint64_t)wd), "window copy");
             continue;
         }
         PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
-        check(cubit_memcpy_d2h_stream(P.part.ctx, stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
+        check(cubit_memcpy_d2h_async(P.part.ctx, stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
               "window copy");
     }
-    l.window = w;
-    l.tile_slot = win.first;
-    l.pos = 0;
+    check(cubit_copy_stream_sync(P.part.ctx, stream), "window copies");  // one wait for the window's columns
     return true;
 }
 
@@ -491,6 +627,16 @@ void widen(const U* __restrict__ src, int64_t off, idx_t n, int64_t* __restrict_
     for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
 }
 
+// three little-endian bytes per value; the window buffer holds 8 bytes per row, so the 4-byte
+// load of the last value stays inside it
+void widen24(const uint8_t* __restrict__ src, int64_t off, idx_t n, int64_t* __restrict__ dst) {
+    for (idx_t k = 0; k < n; ++k) {
+        uint32_t v;
+        std::memcpy(&v, src + 3 * k, 4);
+        dst[k] = off + (int64_t)(v & 0xffffffu);
+    }
+}
+
 void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
     auto& g = static_cast<CubitScanGlobalState&>(*data.global_state);
     auto& l = static_cast<CubitScanLocalState&>(*data.local_state);
@@ -509,23 +655,24 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
             const idx_t at = P.tile_off[l.tile_slot] - win.off + l.pos;
             for (size_t e = 0; e < g.emit.size(); ++e) {
-                if (P.nullable[e])
-                    FillValidity(static_cast<const uint64_t*>(l.host_valid[e].p), win.off + at - 64 * l.valid_word0, n,
-                                 output.validity[e]);
+                if (P.nullable[e]) FillValidity(l.src_valid[e], win.off + at - 64 * l.valid_word0, n, output.validity[e]);
                 int64_t* dst = output.Column(e);
                 const int64_t off = P.offset[e];
                 switch (P.width[e]) {  // widen the compacted transfer
                 case 1:
-                    widen(static_cast<const uint8_t*>(l.host[e].p) + at, off, n, dst);
+                    widen(reinterpret_cast<const uint8_t*>(l.src[e]) + at, off, n, dst);
                     break;
                 case 2:
-                    widen(static_cast<const uint16_t*>(l.host[e].p) + at, off, n, dst);
+                    widen(reinterpret_cast<const uint16_t*>(l.src[e]) + at, off, n, dst);
+                    break;
+                case 3:
+                    widen24(reinterpret_cast<const uint8_t*>(l.src[e]) + 3 * at, off, n, dst);
                     break;
                 case 4:
-                    widen(static_cast<const uint32_t*>(l.host[e].p) + at, off, n, dst);
+                    widen(reinterpret_cast<const uint32_t*>(l.src[e]) + at, off, n, dst);
                     break;
                 default:
-                    std::memcpy(dst, l.host[e].i64() + at, n * sizeof(int64_t));
+                    std::memcpy(dst, reinterpret_cast<const int64_t*>(l.src[e]) + at, n * sizeof(int64_t));
                 }
             }
             l.pos += n;

@@ -195,11 +195,21 @@ int cubit_sync(cubit_ctx *ctx);
 /* Copy streams: a stream of the context's device whose work starts after everything enqueued
  * on the context stream before the call (one pipeline task of the table-function mirror copies
  * its windows on its own, so the tasks' copies overlap instead of queueing on one stream).
- * cubit_memcpy_d2h_stream copies on it and waits for the copy. Destroyed streams go back to a
- * pool of the context (creating a HIP stream costs milliseconds) and are freed with it. */
+ * cubit_memcpy_d2h_stream copies on it and waits for the copy; cubit_memcpy_d2h_async only
+ * enqueues it, and cubit_copy_stream_sync waits for everything enqueued on the stream (the
+ * copies of one window's columns, one wait). Destroyed streams go back to a pool of the context
+ * (creating a HIP stream costs milliseconds) and are freed with it. */
 int cubit_copy_stream_create(cubit_ctx *ctx, void **stream);
 int cubit_copy_stream_destroy(cubit_ctx *ctx, void *stream);
 int cubit_memcpy_d2h_stream(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
+int cubit_memcpy_d2h_async(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
+int cubit_copy_stream_sync(cubit_ctx *ctx, void *stream);
+/* An event marking everything enqueued on a copy stream so far (pooled per context):
+ * cubit_copy_event_sync waits for it — a consumer thread waits for one staged group of copies,
+ * not for the whole stream; cubit_copy_event_destroy waits too and returns it to the pool. */
+int cubit_copy_event_record(cubit_ctx *ctx, void *stream, void **event);
+int cubit_copy_event_sync(cubit_ctx *ctx, void *event);
+int cubit_copy_event_destroy(cubit_ctx *ctx, void *event);
 /* Synchronise the context stream and report any pending HIP error. */
 int cubit_ctx_check(cubit_ctx *ctx);
 /* Tile directory of the last row-id materialisation on this context (device pointer, valid
@@ -246,8 +256,9 @@ int cubit_narrow_i32(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_coun
 int cubit_narrow_i32_checked(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n,
                              int64_t offset, int32_t *d_out, uint32_t *d_overflow);
 /* Transfer compaction to the width a column's statistics allow: d_out[i] = (unsigned, `width` =
- * 1, 2 or 4 bytes)(d_in[i] - offset) for i < min(*d_count, max_n), for values in [offset, offset +
- * 2^(8·width)) — e.g. l_discount's 0 … 10 as one byte, a partition's row ids as four. *d_overflow
+ * 1, 2, 3 or 4 bytes, little-endian, packed)(d_in[i] - offset) for i < min(*d_count, max_n), for
+ * values in [offset, offset + 2^(8·width)) — e.g. l_discount's 0 … 10 as one byte,
+ * l_extendedprice's cents as three, a partition's row ids as four. *d_overflow
  * (device; the caller zeroes it) becomes 1 when a value lies outside, and the copy must then not
  * be used. */
 int cubit_narrow_checked(cubit_ctx *ctx, const int64_t *d_in, const uint64_t *d_count, uint64_t max_n, int64_t offset,

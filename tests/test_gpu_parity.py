@@ -733,3 +733,44 @@ def test_candidate_check_off_key_constants(ctx, dtype):
         assert np.array_equal(t.scan(fs, txn=L.Txn(10, TXN_START + 1)), ref), (c, cmp)
     t.close()
     t2.close()
+
+
+@pytest.mark.parametrize("width", [1, 2, 3, 4])
+@pytest.mark.parametrize("shift", [0, 1])
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 4099, 1_000_003])
+def test_narrow_checked_round_trips(ctx, width, shift, n):
+    """cubit_narrow_checked (the table function's transfer compaction): value - offset as an
+    unsigned 1 / 2 / 3 / 4-byte little-endian integer, exact for every value in range, the overflow flag clear; one
+    value past the range sets it. shift = 1 puts both operands off 16-byte alignment (the
+    one-value-per-store form); lengths around the 8-value packing cover the tail; max_n below the
+    count leaves the rest untouched."""
+    rng = np.random.default_rng(n * 7 + width + shift)
+    for offset in (-12345, 2 ** 40):
+        vals = offset + rng.integers(0, 2 ** (8 * width), n, dtype=np.uint64).astype(np.int64)
+        vals[0] = offset + 2 ** (8 * width) - 1  # the top of the range
+        d_in = ctx.upload(np.concatenate([np.zeros(shift, np.int64), vals]))
+        d_cnt = ctx.upload(np.array([n], np.uint64))
+        out = ctx.upload(np.full((n + 1) * width, 0xAB, np.uint8))
+        flag = ctx.upload(np.zeros(4, np.uint32))
+        def run(max_n):
+            L.check(ctx.lib.cubit_narrow_checked(ctx.handle, d_in.addr + 8 * shift, d_cnt.ptr, max_n, offset, width,
+                                                 out.addr + width * shift, flag.ptr))
+            ctx.sync()
+            raw = out.download(np.uint8, (n + 1) * width)[width * shift:width * shift + n * width]
+            by = raw.reshape(n, width).astype(np.uint64)
+            vals_out = sum(by[:, k] << np.uint64(8 * k) for k in range(width))
+            return vals_out, int(flag.download(np.uint32, 1)[0])
+
+        got, bad = run(n)
+        assert bad == 0
+        assert np.array_equal(got.astype(np.int64) + offset, vals), (width, shift, n, offset)
+        if n > 8:  # max_n below the count: only the first max_n written
+            out.free()
+            out = ctx.upload(np.full((n + 1) * width, 0xAB, np.uint8))
+            got, _ = run(n // 2)
+            assert np.array_equal(got[:n // 2].astype(np.int64) + offset, vals[:n // 2])
+            assert (got[n // 2:] == sum(0xAB << (8 * k) for k in range(width))).all()
+        vals[n - 1] = offset + 2 ** (8 * width)  # one past the range
+        d_in.free()
+        d_in = ctx.upload(np.concatenate([np.zeros(shift, np.int64), vals]))
+        assert run(n)[1] == 1

@@ -1,7 +1,12 @@
 """The TableFunction mirror (include/cubit_scan.h) driven the way DuckDB's pipeline drives
 seq_scan: N tasks with their own local state call `function` until it returns an empty
 chunk (PhysicalTableScan::GetData, physical_table_scan.cpp:82-103); an order-preserving sink
-sorts chunks by batch index (table_scan.cpp:179-189)."""
+sorts chunks by batch index (table_scan.cpp:179-189).
+
+Every test runs twice: with the partition's rows staged to the host by init_global on one copy
+stream in groups (the default), and with CUBIT_SCAN_STAGE_MB=0, where each task copies the window it
+claims."""
+import os
 import threading
 
 import numpy as np
@@ -24,6 +29,20 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(autouse=True, params=["staged", "per_window"])
+def staging(request):
+    old = os.environ.get("CUBIT_SCAN_STAGE_MB")
+    if request.param == "per_window":
+        os.environ["CUBIT_SCAN_STAGE_MB"] = "0"
+    else:
+        os.environ.pop("CUBIT_SCAN_STAGE_MB", None)
+    yield request.param
+    if old is None:
+        os.environ.pop("CUBIT_SCAN_STAGE_MB", None)
+    else:
+        os.environ["CUBIT_SCAN_STAGE_MB"] = old
 
 
 def q6_table(ctx, li):
