@@ -590,7 +590,7 @@ int cubit_copy_stream_sync(cubit_ctx* ctx, void* stream) {
 }
 
 int cubit_copy_event_record(cubit_ctx* ctx, void* stream, void** event) {
-    if (!ctx || !stream || !event) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (!ctx || !event) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
     if (int rc = set_device(ctx)) return rc;
     hipEvent_t e = nullptr;
@@ -601,8 +601,15 @@ int cubit_copy_event_record(cubit_ctx* ctx, void* stream, void** event) {
         HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     ctx->copy_ev_live.insert(e);
-    HIP_CHECK(hipEventRecord(e, static_cast<hipStream_t>(stream)));
+    HIP_CHECK(hipEventRecord(e, stream ? static_cast<hipStream_t>(stream) : ctx->stream));
     *event = e;
+    return CUBIT_OK;
+}
+
+int cubit_copy_stream_wait_event(cubit_ctx* ctx, void* stream, void* event) {
+    if (!ctx || !stream || !event) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_CHECK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0));
     return CUBIT_OK;
 }
 

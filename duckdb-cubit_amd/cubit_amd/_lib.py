@@ -103,6 +103,7 @@ GPU_SIGNATURES = {
     "cubit_copy_stream_sync": (C.c_int, [_P, _P]),
     "cubit_copy_event_record": (C.c_int, [_P, _P, C.POINTER(_P)]),
     "cubit_copy_event_sync": (C.c_int, [_P, _P]),
+    "cubit_copy_stream_wait_event": (C.c_int, [_P, _P, _P]),
     "cubit_copy_event_destroy": (C.c_int, [_P, _P]),
     "cubit_build_bitvector": (C.c_int, [_P, _P, C.c_int, _P, _U64, C.c_int, _I64, _P]),
     "cubit_bitvector_eval": (

@@ -15,7 +15,8 @@
  * 5. with [threads]: the whole query through the callbacks as a DuckDB pipeline runs it —
  *    init_global, then `threads` pipeline tasks (pthreads), each with its own local state,
  *    draining 2,048-row chunks of (l_extendedprice, l_discount) into a partial revenue —
- *    timed end to end (best of 3) and checked against the fused revenue; one more line.
+ *    timed end to end (best of Q6_REPS runs, default 3; the median beside it) and checked against
+ *    the fused revenue; one more line.
  * 6. with --partitions N: lineitem held as N row-range partitions, partition p on device
  *    p mod (devices visible), one context per device — one process driving every GPU of the node —
  *    and the same pipeline over all of them through one cursor (cubit_scan_init_global_multi:
@@ -108,14 +109,19 @@ static void *pipeline_task(void *arg) {
     return NULL;
 }
 
-/* `threads` pipeline tasks over one init_global (best of 3 end to end); returns the best time */
+/* `threads` pipeline tasks over one init_global (best of Q6_REPS end to end); returns the best
+ * time, the median in *median_ms */
 static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cubit_filter_node *q6, uint32_t nn,
-                           int threads, uint64_t want_rows, __int128 want_rev, double *init_ms, double split_ms[2]) {
+                           int threads, uint64_t want_rows, __int128 want_rev, double *init_ms, double split_ms[2],
+                           double *median_ms) {
     const uint64_t proj_ids[] = {3, 1};
     double best = 1e30;
     task_t *tasks = calloc((size_t)threads, sizeof(task_t));
     pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
-    for (int rep = 0; rep < 3; ++rep) {
+    const char *reps_env = getenv("Q6_REPS");
+    const int reps = reps_env && atoi(reps_env) > 0 ? atoi(reps_env) : 3;
+    double *times = calloc((size_t)reps, sizeof(double));
+    for (int rep = 0; rep < reps; ++rep) {
         const double t0 = now_s();
         cubit_scan *ps;
         CHECK_SCAN(cubit_scan_init_global_multi(parts, n_parts, proj_ids, 2, NULL, 0, q6, nn, NULL, &ps));
@@ -137,6 +143,7 @@ static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cu
         }
         const double t2 = now_s();
         CHECK_SCAN(cubit_scan_destroy(ps));
+        times[rep] = t2 - t0;
         if (t2 - t0 < best) {
             best = t2 - t0;
             *init_ms = (t1 - t0) * 1e3;
@@ -148,6 +155,14 @@ static double run_pipeline(cubit_table *const *parts, uint32_t n_parts, const cu
             exit(1);
         }
     }
+    for (int i = 1; i < reps; ++i) /* insertion sort: the median */
+        for (int j = i; j > 0 && times[j] < times[j - 1]; --j) {
+            const double x = times[j];
+            times[j] = times[j - 1];
+            times[j - 1] = x;
+        }
+    *median_ms = times[reps / 2] * 1e3;
+    free(times);
     free(tasks);
     free(th);
     return best;
@@ -262,11 +277,11 @@ int main(int argc, char **argv) {
     /* 5. the query as a pipeline of `threads` tasks over the callbacks */
     const int threads = argc > 2 ? atoi(argv[2]) : 0;
     if (threads > 0) {
-        double init_ms = 0, split[2] = {0, 0};
-        const double best = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms, split);
+        double init_ms = 0, split[2] = {0, 0}, median_ms = 0;
+        const double best = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms, split, &median_ms);
         printf("pipeline threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64 " rows_per_s %.4e revenue_match 1"
-               " task_scan_ms %.3f task_aggregate_ms %.3f\n",
-               threads, init_ms, best * 1e3, q, q / best, split[0], split[1]);
+               " task_scan_ms %.3f task_aggregate_ms %.3f median_ms %.3f\n",
+               threads, init_ms, best * 1e3, q, q / best, split[0], split[1], median_ms);
         /* the link's own device-to-host rate into page-locked memory (one 64 MiB copy, best of 3):
          * the floor the pipeline's window copies share */
         const uint64_t link_bytes = (uint64_t)n * 8 < (64ull << 20) ? (uint64_t)n * 8 : (64ull << 20);
@@ -281,6 +296,34 @@ int main(int argc, char **argv) {
         }
         CHECK(cubit_host_free(ctx, h_link));
         printf("link_d2h bytes %" PRIu64 " ms %.3f gb_per_s %.2f\n", link_bytes, link_best * 1e3, link_bytes / link_best / 1e9);
+    }
+
+    /* 5b. Q6_AB=1: staged and per-window copies alternated run by run in this process (paired
+     * comparison: the box's other tenants load both alike), best and median of each */
+    if (threads > 0 && getenv("Q6_AB") && atoi(getenv("Q6_AB")) == 1) {
+        const char *reps_env = getenv("Q6_REPS");
+        const int reps = reps_env && atoi(reps_env) > 0 ? atoi(reps_env) : 3;
+        double ab[2][64];
+        int k = 0;
+        for (; k < reps && k < 64; ++k)
+            for (int mode = 0; mode < 2; ++mode) {
+                setenv("CUBIT_SCAN_STAGE_MB", mode ? "0" : "1024", 1);
+                setenv("Q6_REPS", "1", 1);
+                double init_ms = 0, split[2] = {0, 0}, median_ms = 0;
+                ab[mode][k] = run_pipeline(&t, 1, q6, nn, threads, q, rev, &init_ms, split, &median_ms) * 1e3;
+            }
+        if (reps_env) setenv("Q6_REPS", reps_env, 1);
+        unsetenv("CUBIT_SCAN_STAGE_MB");
+        for (int mode = 0; mode < 2; ++mode) {
+            for (int i = 1; i < k; ++i)
+                for (int j = i; j > 0 && ab[mode][j] < ab[mode][j - 1]; --j) {
+                    const double x = ab[mode][j];
+                    ab[mode][j] = ab[mode][j - 1];
+                    ab[mode][j - 1] = x;
+                }
+            printf("pipeline_ab %s threads %d runs %d best_ms %.3f median_ms %.3f\n", mode ? "per_window" : "staged",
+                   threads, k, ab[mode][0], ab[mode][k / 2]);
+        }
     }
 
     /* 6. the same pipeline over N row-range partitions, one context each, spread over the devices */
@@ -303,11 +346,11 @@ int main(int argc, char **argv) {
             CHECK(cubit_table_build_index(pt[p], 2, CUBIT_INDEX_RANGE, NULL, 0));
         }
         for (int d = 0; d < n_ctx; ++d) CHECK(cubit_sync(pctx[d]));
-        double init_ms = 0, split[2] = {0, 0};
-        const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms, split);
+        double init_ms = 0, split[2] = {0, 0}, median_ms = 0;
+        const double best = run_pipeline(pt, (uint32_t)n_partitions, q6, nn, threads, q, rev, &init_ms, split, &median_ms);
         printf("partitioned_pipeline partitions %d devices %d threads %d init_global_ms %.3f total_ms %.3f rows %" PRIu64
-               " rows_per_s %.4e revenue_match 1 task_scan_ms %.3f task_aggregate_ms %.3f\n",
-               n_partitions, n_ctx, threads, init_ms, best * 1e3, q, q / best, split[0], split[1]);
+               " rows_per_s %.4e revenue_match 1 task_scan_ms %.3f task_aggregate_ms %.3f median_ms %.3f\n",
+               n_partitions, n_ctx, threads, init_ms, best * 1e3, q, q / best, split[0], split[1], median_ms);
         CHECK_SCAN(cubit_scan_release_cached(NULL, NULL));
         for (int p = 0; p < n_partitions; ++p) CHECK(cubit_table_destroy(pt[p]));
         for (int d = 0; d < n_ctx; ++d) CHECK(cubit_ctx_destroy(pctx[d]));

@@ -30,8 +30,11 @@ void check(int rc, const char* what) {
 // Buffers outlive one scan: pinning or allocating ~100 MB costs milliseconds, more than the
 // work, and DuckDB runs init_global once per query. Freed buffers wait here and a request takes
 // the smallest one that fits without wasting more than half of it. The cap bounds what an idle
-// process keeps (CUBIT_SCAN_CACHE_MB, default 256 MiB of page-locked and 4 GiB of device
-// memory); cubit_scan_release_cached() frees everything cached. Never destroyed (the process
+// process keeps (CUBIT_SCAN_CACHE_MB, default 1 GiB of page-locked and 16 GiB of device
+// memory: the probes are sized by the decode's capacity guess, an eighth of the partition's rows,
+// and a 4 GiB cap evicted — hipFree — a query's buffers between its runs: SF100 Q6 over 4
+// partitions 5.3 ms against 3.1 with room, profiles/r05n_*); cubit_scan_release_cached() frees
+// everything cached. Never destroyed (the process
 // exit releases the pages; a static destructor could run after the HIP runtime's).
 class BufferPool {
   public:
@@ -107,11 +110,11 @@ size_t cache_cap_mb(size_t dflt) {
     return (e && *e ? std::strtoull(e, nullptr, 10) : dflt) << 20;
 }
 BufferPool& pinned_pool() {
-    static BufferPool* p = new BufferPool(true, cache_cap_mb(256));
+    static BufferPool* p = new BufferPool(true, cache_cap_mb(1024));
     return *p;
 }
 BufferPool& device_pool() {
-    static BufferPool* p = new BufferPool(false, cache_cap_mb(256) * 16);
+    static BufferPool* p = new BufferPool(false, cache_cap_mb(1024) * 16);
     return *p;
 }
 
@@ -166,14 +169,16 @@ struct Window {
 };
 
 // Staging: init_global copies every emitted column's transfer form (and validity words) to
-// page-locked host memory on ONE copy stream per partition, in row order, in groups of consecutive
-// windows of about kStageGroupBytes, each group closed by an event. A pipeline task that claims a
-// window waits for its group's event and reads the rows in place. One stream of multi-megabyte
+// page-locked host memory on ONE copy stream per device, in row order, in about kStageGroups
+// groups of consecutive windows per partition: each group's probes and narrowing run on the
+// context stream, the copy stream waits for them, copies the group and records an event. A
+// pipeline task that claims a window waits for its group's event and reads the rows in place. One stream of multi-megabyte
 // copies runs the link at its own rate (56.6 GB/s for one 64 MiB copy on the MI355X box); the
 // tasks' concurrent per-window copies (0.5–1 MB each on up to 16 streams) reached ~20 GB/s
 // (profiles/r05k_*). Partitions whose staged bytes exceed CUBIT_SCAN_STAGE_MB (default 1024) are
 // copied per window by the task that claims it, as before.
-constexpr uint64_t kStageGroupBytes = 4ull << 20;
+constexpr uint64_t kStageGroups = 8;
+
 uint64_t stage_cap_bytes() {  // read per init_global
     const char* e = std::getenv("CUBIT_SCAN_STAGE_MB");
     return (e && *e ? std::strtoull(e, nullptr, 10) : 1024ull) << 20;
@@ -207,18 +212,17 @@ struct PartScan {
     std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
-    // staging (see kStageGroupBytes): the copy stream, the host copies of every emitted column's
-    // transfer form and validity words, the overflow flags copied ahead of them, one event per
-    // group; `unstaged[e]` marks a column whose compaction overflowed (copied per window instead)
+    // staging (see kStageGroupBytes): the host copies of every emitted column's transfer form and
+    // validity words, each group's overflow flags, and its events
     bool staged = false;
-    void* stage_stream = nullptr;
     std::vector<PooledBuffer> h_stage, h_stage_valid;
-    PooledBuffer h_flags;
-    std::vector<void*> group_ev;
-    std::vector<bool> unstaged;
+    PooledBuffer h_flags;                  // per group: one overflow flag per emitted column
+    std::vector<void*> probe_ev, group_ev;  // per group: probes done (context stream), copies done
+    std::vector<uint64_t> group_word;      // per group: its first validity word
+    std::vector<idx_t> group_off;          // per group: its first row (bit 0 of that word)
     ~PartScan() {
         for (void* ev : group_ev) cubit_copy_event_destroy(part.ctx, ev);
-        if (stage_stream) cubit_copy_stream_destroy(part.ctx, stage_stream);
+        for (void* ev : probe_ev) cubit_copy_event_destroy(part.ctx, ev);
     }
 };
 
@@ -231,6 +235,18 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     idx_t max_window = 0;
     std::atomic<uint32_t> next{0};
     std::atomic<idx_t> emitted{0};
+    // one staging copy stream per context, shared by the partitions on that device (their copies
+    // run in row order on it; a stream per partition put several copy streams on one device's
+    // four hardware queues and measured slower)
+    std::vector<std::pair<cubit_ctx*, void*>> stage_streams;
+    void* StageStream(cubit_ctx* ctx) {
+        for (auto& s : stage_streams)
+            if (s.first == ctx) return s.second;
+        void* st = nullptr;
+        check(cubit_copy_stream_create(ctx, &st), "staging stream");  // after the probes and narrowing
+        stage_streams.emplace_back(ctx, st);
+        return st;
+    }
     idx_t MaxThreads() const override {
         const idx_t hw = std::max<unsigned>(1, std::thread::hardware_concurrency());
         return std::max<idx_t>(1, std::min<idx_t>(windows.size(), hw));
@@ -239,6 +255,8 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
         // probes launched by init_global may still read the buffers returned to the pool
         for (auto& p : parts)
             if (p->part.ctx) cubit_sync(p->part.ctx);
+        parts.clear();  // their staging events first
+        for (auto& s : stage_streams) cubit_copy_stream_destroy(s.first, s.second);
     }
 };
 
@@ -248,11 +266,13 @@ struct CubitScanLocalState : public LocalTableFunctionState {
     idx_t pos = 0;                 // next row of the tile's run to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
     std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
-    uint64_t valid_word0 = 0;              // ordered-output word of src_valid[e][0]
     // per emitted position: the window's first row on the host (its own copy, or the partition's
-    // staged rows) and the validity word valid_word0
+    // staged rows), the transfer width of the window's values, and validity words whose bit 0 is
+    // the partition's output row valid_bit0
     std::vector<const char*> src;
+    std::vector<int> width;
     std::vector<const uint64_t*> src_valid;
+    idx_t valid_bit0 = 0;
     // this task's copy stream per context (ordered after init_global's device work on it):
     // the tasks' window copies run side by side, each from its own device; partitions that share
     // a context (several on one device) share the stream — a stream per partition and task put
@@ -295,20 +315,27 @@ void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
 }
 
 // Count and tile runs of a launched decode; a filter that kept more rows than the guess runs
-// a second time with the exact count.
-void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn) {
+// a second time with the exact count (returns true then: the probes must run again). h_meta: the
+// count and the directory already copied to the host (BeginMeta), or null to read them here.
+bool FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn,
+                  const uint64_t* h_meta) {
     cubit_ctx* ctx = P.part.ctx;
-    check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
+    bool again_decoded = false;
+    if (h_meta) P.count = h_meta[0];
+    else check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
     if (P.count > P.d_ids.bytes / 8) {
         LaunchDecode(P, nodes, txn, P.count);
         idx_t again = 0;
         check(cubit_memcpy_d2h(ctx, &again, P.d_cnt.p, 8), "count");
         if (again != P.count) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
+        h_meta = nullptr;
+        again_decoded = true;
     }
     const uint32_t n_tiles = P.count ? (uint32_t)P.tiles.size() : 0;  // nothing qualified: no run
     P.tiles.clear();
     std::vector<uint64_t> dir(2 * (size_t)n_tiles);
-    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
+    if (n_tiles && h_meta) std::memcpy(dir.data(), h_meta + 1, dir.size() * 8);
+    else if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
     // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
     idx_t off = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {
@@ -324,53 +351,31 @@ void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
     if (off != P.count)
         throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(off) + " of " +
                                                std::to_string(P.count) + " row ids");
+    return again_decoded;
 }
 
-// Probe every emitted storage column at the partition's ordered row ids (ColumnData::FilterScan
-// semantics, column_data.cpp:305-309: values with their validity), on the device; the copies of
-// the first window wait for them in stream order. The statistics (DataTable::GetStatistics,
-// update records of any version included) say which columns can hold a NULL: those probe with
-// their validity, which also leaves 0 in a NULL row's value. Then the transfer compaction: a
-// column whose values all lie within 2^31 of an offset crosses PCIe as int32 (row ids: the
-// partition's rows below 2^31, offset row_base; probed columns: their statistics' range, widened
-// by any update records — a NULL row holds 0 after the validity probe, so 0 joins the range of a
-// nullable column). The narrowest of 1, 2, 3 and 4 bytes that holds the range is taken (Q6's
-// l_discount, 0 … 10, crosses as one byte, l_extendedprice as three). The device checks the bound
-// as it narrows.
-void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
-                  const cubit_txn* txn) {
+// The transfer plan of a partition's emitted columns, and their device buffers. The statistics
+// (DataTable::GetStatistics, update records of any version included) say which columns can hold
+// a NULL: those probe with their validity, which also leaves 0 in a NULL row's value. The
+// transfer compaction: a column whose values all lie within 2^32 of an offset crosses PCIe as
+// value - offset in the fewest of 1, 2, 3 and 4 bytes that hold the range (row ids: the
+// partition's rows, offset row_base; probed columns: their statistics' range, widened by any
+// update records — a NULL row holds 0 after the validity probe, so 0 joins the range of a
+// nullable column). Q6's l_discount (0 … 10) crosses as one byte, l_extendedprice as three. The
+// device checks the bound as it narrows (one flag per group and column). Validity words: one
+// run of words per group (`valid_words` in all), a group's bit 0 at its first row.
+void PlanTransfer(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
+                  uint64_t n_groups, uint64_t valid_words) {
     cubit_ctx* ctx = P.part.ctx;
     cubit_table* table = P.part.table;
     const size_t n_emit = emit.size();
+    const uint64_t n = P.count;
     P.d_cols.resize(n_emit);
     P.nullable.assign(n_emit, false);
     P.d_valid.resize(n_emit);
     P.width.assign(n_emit, 0);
     P.offset.assign(n_emit, 0);
     P.d_narrow.resize(n_emit);
-    if (P.count == 0) return;
-    std::vector<int64_t> st_min(n_emit, 0), st_max(n_emit, 0);
-    uint64_t* d_cnt = static_cast<uint64_t*>(P.d_cnt.p);
-    for (size_t e = 0; e < n_emit; ++e) {
-        const column_t col = column_ids[emit[e]];
-        if (col == COLUMN_IDENTIFIER_ROW_ID) continue;
-        int hn = 0, hv = 0;
-        check(cubit_table_column_statistics(table, (int)col, &st_min[e], &st_max[e], &hn, &hv),
-              "cubit_table_column_statistics");
-        P.nullable[e] = hn != 0;
-        P.d_cols[e].allocate(device_pool(), ctx, P.count * 8);
-        if (P.nullable[e]) {
-            P.d_valid[e].allocate(device_pool(), ctx, (P.count + 63) / 64 * 8);
-            check(cubit_table_probe_validity(table, (int)col, txn, device_ptr(P.d_ids), d_cnt, P.count,
-                                             device_ptr(P.d_cols[e]), static_cast<uint64_t*>(P.d_valid[e].p)),
-                  "cubit_table_probe_validity");
-        } else {
-            check(cubit_table_probe(table, (int)col, txn, device_ptr(P.d_ids), d_cnt, P.count, device_ptr(P.d_cols[e])),
-                  "cubit_table_probe");
-        }
-    }
-    P.d_overflow.allocate(device_pool(), ctx, n_emit * 4);
-    check(cubit_memset_d(ctx, P.d_overflow.p, 0, n_emit * 4), "overflow flags");
     for (size_t e = 0; e < n_emit; ++e) {
         const column_t col = column_ids[emit[e]];
         int64_t lo, hi;
@@ -378,18 +383,57 @@ void LaunchProbes(PartScan& P, const std::vector<column_t>& column_ids, const st
             lo = P.part.row_base;
             hi = P.part.row_base + (int64_t)P.part.n_rows - 1;
         } else {
-            lo = P.nullable[e] ? std::min<int64_t>(st_min[e], 0) : st_min[e];
-            hi = P.nullable[e] ? std::max<int64_t>(st_max[e], 0) : st_max[e];
+            int hn = 0, hv = 0;
+            check(cubit_table_column_statistics(table, (int)col, &lo, &hi, &hn, &hv), "cubit_table_column_statistics");
+            P.nullable[e] = hn != 0;
+            if (P.nullable[e]) {
+                lo = std::min<int64_t>(lo, 0);
+                hi = std::max<int64_t>(hi, 0);
+            }
+            P.d_cols[e].allocate(device_pool(), ctx, n * 8);
+            if (P.nullable[e]) P.d_valid[e].allocate(device_pool(), ctx, valid_words * 8);
         }
         const uint64_t span = (uint64_t)hi - (uint64_t)lo;  // hi >= lo
         const int width = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 24) ? 3 : span < (1ull << 32) ? 4 : 0;
         if (!width) continue;
         P.width[e] = width;
         P.offset[e] = lo;
-        P.d_narrow[e].allocate(device_pool(), ctx, P.count * (uint64_t)width);
-        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
-        check(cubit_narrow_checked(ctx, device_ptr(src), d_cnt, P.count, lo, width, P.d_narrow[e].p,
-                                   static_cast<uint32_t*>(P.d_overflow.p) + e),
+        P.d_narrow[e].allocate(device_pool(), ctx, n * (uint64_t)width + 16);
+    }
+    P.d_overflow.allocate(device_pool(), ctx, std::max<uint64_t>(n_groups, 1) * n_emit * 4);
+    check(cubit_memset_d(ctx, P.d_overflow.p, 0, std::max<uint64_t>(n_groups, 1) * n_emit * 4), "overflow flags");
+}
+
+// Probe every emitted storage column at rows [off, off + len) of the partition's ordered row ids
+// (ColumnData::FilterScan semantics, column_data.cpp:305-309: values with their validity, the
+// validity from word `valid_word`), then narrow them (flags of group `group`); all on the
+// context stream.
+void ProbeRange(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
+                const cubit_txn* txn, idx_t off, idx_t len, uint64_t valid_word, uint64_t group) {
+    cubit_ctx* ctx = P.part.ctx;
+    cubit_table* table = P.part.table;
+    const size_t n_emit = emit.size();
+    uint64_t* d_cnt = static_cast<uint64_t*>(P.d_cnt.p);  // ≥ off + len: the kernels take min(count, len)
+    for (size_t e = 0; e < n_emit; ++e) {
+        const column_t col = column_ids[emit[e]];
+        if (col == COLUMN_IDENTIFIER_ROW_ID) continue;
+        if (P.nullable[e]) {
+            check(cubit_table_probe_validity(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len,
+                                             device_ptr(P.d_cols[e]) + off,
+                                             static_cast<uint64_t*>(P.d_valid[e].p) + valid_word),
+                  "cubit_table_probe_validity");
+        } else {
+            check(cubit_table_probe(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len,
+                                    device_ptr(P.d_cols[e]) + off),
+                  "cubit_table_probe");
+        }
+    }
+    for (size_t e = 0; e < n_emit; ++e) {
+        if (!P.width[e]) continue;
+        PooledBuffer& src = column_ids[emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+        check(cubit_narrow_checked(ctx, device_ptr(src) + off, d_cnt, len, P.offset[e], P.width[e],
+                                   static_cast<char*>(P.d_narrow[e].p) + off * (uint64_t)P.width[e],
+                                   static_cast<uint32_t*>(P.d_overflow.p) + group * n_emit + e),
               "cubit_narrow_checked");
     }
 }
@@ -404,59 +448,77 @@ const char* transfer_src(PartScan& P, const std::vector<column_t>& column_ids, c
     return static_cast<const char*>(src.p);
 }
 
-// Enqueue the staging copies of partition p (see kStageGroupBytes) and set its windows' groups.
-void Stage(CubitScanGlobalState& g, uint32_t p) {
+// The probes, compaction and (staged) copies of partition p. Staged (see kStageGroups): the
+// partition's windows are cut into groups; per group the probes and narrowing run on the context
+// stream and close with an event, the staging stream waits for it and copies the group's rows —
+// the link starts on the first group while the device probes the next. Not staged: one probe
+// over every row, and each task copies the window it claims.
+void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
     PartScan& P = *g.parts[p];
     const size_t n_emit = g.emit.size();
-    if (P.count == 0 || n_emit == 0) return;
-    uint64_t row_bytes = 0, total = 0;
-    for (size_t e = 0; e < n_emit; ++e) {
-        row_bytes += transfer_bytes(P, e);
-        total += P.count * transfer_bytes(P, e) + (P.nullable[e] ? (P.count + 63) / 64 * 8 : 0);
-    }
-    if (total > stage_cap_bytes()) return;
-    cubit_ctx* ctx = P.part.ctx;
-    check(cubit_copy_stream_create(ctx, &P.stage_stream), "staging stream");  // after the probes and narrowing
-    P.h_stage.resize(n_emit);
-    P.h_stage_valid.resize(n_emit);
-    P.unstaged.assign(n_emit, false);
-    // + 8 bytes: the 3-byte widen reads 4
-    for (size_t e = 0; e < n_emit; ++e) {
-        P.h_stage[e].allocate(pinned_pool(), ctx, P.count * transfer_bytes(P, e) + 8);
-        if (P.nullable[e]) P.h_stage_valid[e].allocate(pinned_pool(), ctx, ((P.count + 63) / 64 + 2) * 8);
-    }
-    P.h_flags.allocate(pinned_pool(), ctx, n_emit * 4);
-    check(cubit_memcpy_d2h_async(ctx, P.stage_stream, P.h_flags.p, P.d_overflow.p, n_emit * 4), "staged flags");
-    const uint64_t rows_per_group = std::max<uint64_t>(kStageGroupBytes / std::max<uint64_t>(row_bytes, 1), 1);
-    auto flush = [&](idx_t off, idx_t len) {
-        for (size_t e = 0; e < n_emit; ++e) {
-            const uint64_t b = transfer_bytes(P, e);
-            check(cubit_memcpy_d2h_async(ctx, P.stage_stream, static_cast<char*>(P.h_stage[e].p) + off * b,
-                                         transfer_src(P, g.column_ids, g.emit, e) + off * b, len * b),
-                  "staged copy");
-            if (P.nullable[e]) {
-                const uint64_t w0 = off / 64, w1 = (off + len + 63) / 64;
-                check(cubit_memcpy_d2h_async(ctx, P.stage_stream, static_cast<uint64_t*>(P.h_stage_valid[e].p) + w0,
-                                             static_cast<const uint64_t*>(P.d_valid[e].p) + w0, (w1 - w0) * 8),
-                      "staged validity copy");
-            }
-        }
-        void* ev = nullptr;
-        check(cubit_copy_event_record(ctx, P.stage_stream, &ev), "staged group event");
-        P.group_ev.push_back(ev);
-    };
-    idx_t g_off = 0, g_len = 0;
+    // groups of consecutive windows: about an eighth of the partition each (each group costs a
+    // probe and a narrowing launch per column, a few microseconds apiece), at least 2^18 rows
+    std::vector<idx_t> g_off, g_len;
+    const uint64_t rows_per_group = std::max<uint64_t>((P.count + kStageGroups - 1) / kStageGroups, 1ull << 18);
     for (Window& w : g.windows) {
         if (w.part != p) continue;
-        if (g_len && g_len + w.len > rows_per_group) {
-            flush(g_off, g_len);
-            g_off += g_len;
-            g_len = 0;
+        if (g_off.empty() || g_len.back() + w.len > rows_per_group) {
+            g_off.push_back(w.off);
+            g_len.push_back(0);
         }
-        w.group = (uint32_t)P.group_ev.size();
-        g_len += w.len;
+        w.group = (uint32_t)g_off.size() - 1;
+        g_len.back() += w.len;
     }
-    if (g_len) flush(g_off, g_len);
+    uint64_t words = 0;
+    for (idx_t len : g_len) words += (len + 63) / 64;
+    PlanTransfer(P, g.column_ids, g.emit, g_off.size(), std::max<uint64_t>(words, (P.count + 63) / 64));
+    if (P.count == 0 || n_emit == 0) return;
+    uint64_t total = 0;
+    for (size_t e = 0; e < n_emit; ++e)
+        total += P.count * transfer_bytes(P, e) + (P.nullable[e] ? words * 8 : 0);
+    if (total > stage_cap_bytes()) {  // one probe over every row, validity words in row order
+        ProbeRange(P, g.column_ids, g.emit, txn, 0, P.count, 0, 0);
+        return;
+    }
+    cubit_ctx* ctx = P.part.ctx;
+    P.h_stage.resize(n_emit);
+    P.h_stage_valid.resize(n_emit);
+    for (size_t e = 0; e < n_emit; ++e) {
+        P.h_stage[e].allocate(pinned_pool(), ctx, P.count * transfer_bytes(P, e) + 8);  // + 8: the 3-byte widen reads 4
+        if (P.nullable[e]) P.h_stage_valid[e].allocate(pinned_pool(), ctx, (words + 2) * 8);
+    }
+    P.h_flags.allocate(pinned_pool(), ctx, g_off.size() * n_emit * 4);
+    P.group_word.clear();
+    void* st = nullptr;
+    uint64_t wb = 0;
+    for (size_t k = 0; k < g_off.size(); ++k) {
+        const idx_t off = g_off[k], len = g_len[k];
+        ProbeRange(P, g.column_ids, g.emit, txn, off, len, wb, k);
+        void* probed = nullptr;
+        check(cubit_copy_event_record(ctx, nullptr, &probed), "probe event");  // on the context stream
+        P.probe_ev.push_back(probed);
+        if (!st) st = g.StageStream(ctx);
+        check(cubit_copy_stream_wait_event(ctx, st, probed), "staging wait");
+        check(cubit_memcpy_d2h_async(ctx, st, static_cast<uint32_t*>(P.h_flags.p) + k * n_emit,
+                                     static_cast<const uint32_t*>(P.d_overflow.p) + k * n_emit, n_emit * 4),
+              "staged flags");
+        for (size_t e = 0; e < n_emit; ++e) {
+            const uint64_t b = transfer_bytes(P, e);
+            check(cubit_memcpy_d2h_async(ctx, st, static_cast<char*>(P.h_stage[e].p) + off * b,
+                                         transfer_src(P, g.column_ids, g.emit, e) + off * b, len * b),
+                  "staged copy");
+            if (P.nullable[e])
+                check(cubit_memcpy_d2h_async(ctx, st, static_cast<uint64_t*>(P.h_stage_valid[e].p) + wb,
+                                             static_cast<const uint64_t*>(P.d_valid[e].p) + wb, (len + 63) / 64 * 8),
+                      "staged validity copy");
+        }
+        void* ev = nullptr;
+        check(cubit_copy_event_record(ctx, st, &ev), "staged group event");
+        P.group_ev.push_back(ev);
+        P.group_word.push_back(wb);
+        P.group_off.push_back(off);
+        wb += (len + 63) / 64;
+    }
     P.staged = true;
 }
 
@@ -481,8 +543,7 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     }
     // every partition's decode in flight before any count is read: one per device at a time
     for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, P->part.n_rows / 8 + 4096);
-    for (auto& P : g->parts) FinishDecode(*P, nodes, txn);
-    for (auto& P : g->parts) LaunchProbes(*P, g->column_ids, g->emit, txn);
+    for (auto& P : g->parts) FinishDecode(*P, nodes, txn, nullptr);
     // windows: consecutive non-empty tiles of one partition, at most window_rows() rows and
     // window_rows() / 4,096 tiles
     const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
@@ -501,7 +562,7 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
             i = w.last;
         }
     }
-    for (uint32_t p = 0; p < g->parts.size(); ++p) Stage(*g, p);
+    for (uint32_t p = 0; p < g->parts.size(); ++p) ProbeAndStage(*g, p, txn);
     return g;
 }
 
@@ -524,36 +585,32 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     }
     const Window& win = g.windows[w];
     PartScan& P = *g.parts[win.part];
-    if (l.host.size() != g.emit.size()) {
-        l.host.resize(g.emit.size());
-        l.host_valid.resize(g.emit.size());
-        l.src.resize(g.emit.size());
-        l.src_valid.resize(g.emit.size());
+    const size_t n_emit = g.emit.size();
+    if (l.host.size() != n_emit) {
+        l.host.resize(n_emit);
+        l.host_valid.resize(n_emit);
+        l.src.resize(n_emit);
+        l.width.resize(n_emit);
+        l.src_valid.resize(n_emit);
     }
-    const uint64_t w0 = win.off / 64;
-    l.valid_word0 = w0;
     l.window = w;
     l.tile_slot = win.first;
     l.pos = 0;
     if (P.staged) {
         check(cubit_copy_event_sync(P.part.ctx, P.group_ev[win.group]), "staged group");
-        // the flags were copied ahead of every group: a column whose compaction overflowed goes
-        // back to the 8-byte values, copied per window
-        std::call_once(P.overflow_checked, [&] {
-            const uint32_t* ov = static_cast<const uint32_t*>(P.h_flags.p);
-            for (size_t e = 0; e < g.emit.size(); ++e)
-                if (ov[e] && P.width[e]) {
-                    P.width[e] = 0;
-                    P.unstaged[e] = true;
-                }
-        });
+        // the group's overflow flags came with it: a column whose compaction overflowed in this
+        // group is copied per window as its 8-byte values instead
+        const uint32_t* ov = static_cast<const uint32_t*>(P.h_flags.p) + (uint64_t)win.group * n_emit;
+        l.valid_bit0 = P.group_off[win.group];
         bool copied = false;
-        for (size_t e = 0; e < g.emit.size(); ++e) {
-            if (P.nullable[e]) l.src_valid[e] = static_cast<const uint64_t*>(P.h_stage_valid[e].p) + w0;
-            if (!P.unstaged[e]) {
+        for (size_t e = 0; e < n_emit; ++e) {
+            if (P.nullable[e]) l.src_valid[e] = static_cast<const uint64_t*>(P.h_stage_valid[e].p) + P.group_word[win.group];
+            l.width[e] = P.width[e];
+            if (!(P.width[e] && ov[e])) {
                 l.src[e] = static_cast<const char*>(P.h_stage[e].p) + win.off * transfer_bytes(P, e);
                 continue;
             }
+            l.width[e] = 0;
             if (!l.host[e].p) l.host[e].allocate(pinned_pool(), P.part.ctx, g.max_window * 8);
             PooledBuffer& src = g.column_ids[g.emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
             check(cubit_memcpy_d2h_async(P.part.ctx, l.stream_for(P.part.ctx), l.host[e].p, device_ptr(src) + win.off,
@@ -570,14 +627,15 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     // copies (the copy stream starts after init_global's work, the narrowing included)
     std::call_once(P.overflow_checked, [&] {
         if (!P.d_overflow.p) return;
-        std::vector<uint32_t> ov(g.emit.size());
+        std::vector<uint32_t> ov(n_emit);
         check(cubit_memcpy_d2h_stream(P.part.ctx, stream, ov.data(), P.d_overflow.p, ov.size() * 4), "overflow flags");
         for (size_t e = 0; e < ov.size(); ++e)
             if (ov[e]) P.width[e] = 0;
     });
     // validity words covering the window's rows [off, off + len) of the partition's output
-    const uint64_t w1 = (win.off + win.len + 63) / 64;
-    for (size_t e = 0; e < g.emit.size(); ++e) {
+    const uint64_t w0 = win.off / 64, w1 = (win.off + win.len + 63) / 64;
+    l.valid_bit0 = w0 * 64;
+    for (size_t e = 0; e < n_emit; ++e) {
         // page-locked memory is filed under no context: any partition's copies may use it
         if (!l.host[e].p) l.host[e].allocate(pinned_pool(), P.part.ctx, g.max_window * 8);
         if (P.nullable[e]) {
@@ -589,14 +647,14 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
             l.src_valid[e] = static_cast<const uint64_t*>(l.host_valid[e].p);
         }
         l.src[e] = static_cast<const char*>(l.host[e].p);
-        const column_t col = g.column_ids[g.emit[e]];
+        l.width[e] = P.width[e];
         if (P.width[e]) {
             const int wd = P.width[e];
             const char* src = static_cast<const char*>(P.d_narrow[e].p) + win.off * (uint64_t)wd;
             check(cubit_memcpy_d2h_async(P.part.ctx, stream, l.host[e].p, src, win.len * (uint64_t)wd), "window copy");
             continue;
         }
-        PooledBuffer& src = col == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
+        PooledBuffer& src = g.column_ids[g.emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
         check(cubit_memcpy_d2h_async(P.part.ctx, stream, l.host[e].p, device_ptr(src) + win.off, win.len * 8),
               "window copy");
     }
@@ -627,8 +685,8 @@ void widen(const U* __restrict__ src, int64_t off, idx_t n, int64_t* __restrict_
     for (idx_t k = 0; k < n; ++k) dst[k] = off + (int64_t)src[k];
 }
 
-// three little-endian bytes per value; the window buffer holds 8 bytes per row, so the 4-byte
-// load of the last value stays inside it
+// three little-endian bytes per value; the buffers hold at least 8 bytes past the last value, so
+// its 4-byte load stays inside them
 void widen24(const uint8_t* __restrict__ src, int64_t off, idx_t n, int64_t* __restrict__ dst) {
     for (idx_t k = 0; k < n; ++k) {
         uint32_t v;
@@ -655,10 +713,10 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
             const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
             const idx_t at = P.tile_off[l.tile_slot] - win.off + l.pos;
             for (size_t e = 0; e < g.emit.size(); ++e) {
-                if (P.nullable[e]) FillValidity(l.src_valid[e], win.off + at - 64 * l.valid_word0, n, output.validity[e]);
+                if (P.nullable[e]) FillValidity(l.src_valid[e], win.off + at - l.valid_bit0, n, output.validity[e]);
                 int64_t* dst = output.Column(e);
                 const int64_t off = P.offset[e];
-                switch (P.width[e]) {  // widen the compacted transfer
+                switch (l.width[e]) {  // widen the compacted transfer
                 case 1:
                     widen(reinterpret_cast<const uint8_t*>(l.src[e]) + at, off, n, dst);
                     break;

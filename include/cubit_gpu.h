@@ -204,11 +204,15 @@ int cubit_copy_stream_destroy(cubit_ctx *ctx, void *stream);
 int cubit_memcpy_d2h_stream(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
 int cubit_memcpy_d2h_async(cubit_ctx *ctx, void *stream, void *dst, const void *src, uint64_t bytes);
 int cubit_copy_stream_sync(cubit_ctx *ctx, void *stream);
-/* An event marking everything enqueued on a copy stream so far (pooled per context):
- * cubit_copy_event_sync waits for it — a consumer thread waits for one staged group of copies,
- * not for the whole stream; cubit_copy_event_destroy waits too and returns it to the pool. */
+/* An event marking everything enqueued so far on a copy stream, or on the context stream when
+ * `stream` is NULL (pooled per context): cubit_copy_event_sync waits for it on the host — a
+ * consumer thread waits for one staged group of copies, not for the whole stream;
+ * cubit_copy_stream_wait_event makes a copy stream wait for it on the device — the copies of a
+ * group start when that group's probes are done; cubit_copy_event_destroy waits too and returns
+ * it to the pool. */
 int cubit_copy_event_record(cubit_ctx *ctx, void *stream, void **event);
 int cubit_copy_event_sync(cubit_ctx *ctx, void *event);
+int cubit_copy_stream_wait_event(cubit_ctx *ctx, void *stream, void *event);
 int cubit_copy_event_destroy(cubit_ctx *ctx, void *event);
 /* Synchronise the context stream and report any pending HIP error. */
 int cubit_ctx_check(cubit_ctx *ctx);

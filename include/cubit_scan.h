@@ -87,7 +87,7 @@ int cubit_scan_cardinality_multi(cubit_table *const *tables, uint32_t n_tables, 
 int cubit_scan_statistics_multi(cubit_table *const *tables, uint32_t n_tables, uint64_t column_id, int64_t *min,
                                 int64_t *max, int *has_null, int *has_no_null);
 /* Buffers of finished scans are kept for the next one (page-locked host windows and device
- * result buffers; at most CUBIT_SCAN_CACHE_MB MiB pinned — default 256 — and 16x that on the
+ * result buffers; at most CUBIT_SCAN_CACHE_MB MiB pinned — default 1024 — and 16x that on the
  * device). This frees every cached buffer and reports what was cached (either pointer may be
  * NULL); call it before destroying a context whose scans are done. */
 int cubit_scan_release_cached(uint64_t *pinned_bytes, uint64_t *device_bytes);
