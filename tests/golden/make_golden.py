@@ -250,6 +250,24 @@ def main():
     zt = {"source": "test/sql/filter/test_zonemap.test_slow", "rows": 100000000,
           "queries": [{"sql": q, "tree": trees[q], "count": c} for q, c in zip(zt_sql, zt_counts)]}
     assert len(zt["queries"]) == 6
+    # test/sql/filter/filter_cache.test: integers(a) = generate_series(0, 9999) x generate_series(0, 9)
+    # (each a ten times); the nested subqueries' WHERE clauses reach the scan as one filter: the
+    # plain comparisons as the TableFilterSet ("where", ANDed), the OR as a residual tree
+    fc_case = sqllogic_script("test/sql/filter/filter_cache.test")
+    assert any("generate_series(0, 9999, 1) tbl(a), generate_series(0, 9, 1) tbl2(b)" in st["sql"]
+               for st in fc_case["script"])
+    fc_counts = [st["rows"][0][0] for st in fc_case["script"] if st["op"] == "query"]
+    fc_shapes = [
+        {"sql": "a<5", "where": [[0, "<", 5]], "tree": None},
+        {"sql": "((a>1 AND a<10) OR a>9995) AND a<5", "where": [[0, "<", 5]],
+         "tree": ["or", ["and", [0, ">", 1], [0, "<", 10]], [0, ">", 9995]]},
+        {"sql": "((a <> 3 AND a<50) OR (a > 9995)) AND a>1 AND a<20 AND a<5",
+         "where": [[0, ">", 1], [0, "<", 20], [0, "<", 5]],
+         "tree": ["or", ["and", [0, "!=", 3], [0, "<", 50]], [0, ">", 9995]]},
+    ]
+    assert len(fc_counts) == len(fc_shapes)
+    fc = {"source": "test/sql/filter/filter_cache.test", "values": [0, 10000], "repeat": 10,
+          "queries": [dict(q, count=c) for q, c in zip(fc_shapes, fc_counts)]}
     # test/sql/filter/test_obsolete_filters.test: integers(a, b) = (1,10) (2,12) (3,14) (4,16)
     # (5,NULL) (NULL,NULL); every query whose WHERE is an AND of comparisons of a with integer
     # constants — redundant, subsumed and contradictory ones, all pushed into the scan as one
@@ -336,7 +354,7 @@ def main():
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,
                                                           "many_updaters": mu, "block_boundary_update": bb,
-                                                          "zonemap_or_trees": zt, "obsolete_filters": ob,
+                                                          "zonemap_or_trees": zt, "obsolete_filters": ob, "filter_cache": fc,
                                                           "art_scans": art},
                                                          indent=1, sort_keys=True) + "\n")
 

@@ -6,9 +6,10 @@ import pytest
 from cubit_amd import _lib as L
 from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
-from cubit_amd.scan_function import CubitScanFunction
+from cubit_amd.scan_function import ROW_ID, CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import (art_scan_cases, block_boundary_states, filter_pushdown_tables, many_updaters_reads, multi_version_views,
+from test_oracle_tpch import (art_scan_cases, block_boundary_states, filter_cache_filters, filter_cache_table,
+                              filter_pushdown_tables, many_updaters_reads, multi_version_views,
                               obsolete_filter_columns, obsolete_filter_sets, residual_from_json, update_case_views,
                               zonemap_table)
 
@@ -220,6 +221,35 @@ def test_zonemap_or_trees(ctx, golden, a_index):
             else:
                 mask = ((a > 500) & (b == 1)) | (b < 2)
             assert np.array_equal(t.scan(None, res, capacity=1024), np.flatnonzero(mask)), q["sql"]
+    t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_filter_cache(ctx, golden, encoding):
+    """test/sql/filter/filter_cache.test: the nested subqueries' filters as one scan (comparisons
+    pushed, the OR of ranges as a residual) — count(*) equals the file's, through the count
+    kernel and the table function, and the rows equal numpy's."""
+    a = filter_cache_table(golden)
+    t = CubitTable(ctx, len(a))
+    t.add_column(0, a)
+    if encoding is not None:
+        t.build_index(0, encoding)
+    for q in golden["cases"]["filter_cache"]["queries"]:
+        fs, res = filter_cache_filters(q)
+        assert t.count(fs, res) == q["count"], (q["sql"], encoding)
+        fn = CubitScanFunction(t, [0, ROW_ID], None, fs, res)
+        local = fn.init_local()
+        got = []
+        while True:
+            cols = fn.function(local)
+            if len(cols[0]) == 0:
+                break
+            got += cols[1].tolist()
+        fn.close()
+        mask = a < 5
+        if q["tree"]:
+            mask &= ((a > 1) & (a < 10) | (a > 9995)) if q["count"] == 30 else ((a != 3) & (a < 50) | (a > 9995)) & (a > 1) & (a < 20)
+        assert sorted(got) == np.flatnonzero(mask).tolist(), (q["sql"], encoding)
     t.close()
 
 

@@ -412,6 +412,28 @@ def test_zonemap_or_trees_reference_case(golden):
         assert n == q["count"], q["sql"]
 
 
+def filter_cache_table(golden):
+    """filter_cache.test's integers: every a in [0, 10000) ten times (a cross product's rows)."""
+    c = golden["cases"]["filter_cache"]
+    lo, hi = c["values"]
+    return np.repeat(np.arange(lo, hi, dtype=np.int32), c["repeat"])
+
+
+def filter_cache_filters(q):
+    """A filter_cache query as (TableFilterSet of its plain comparisons, residual OR tree or None)."""
+    return where_filters(q["where"]), (residual_from_json(q["tree"]) if q["tree"] else None)
+
+
+def test_filter_cache_reference_case(golden):
+    """test/sql/filter/filter_cache.test: nested subqueries' filters combined into one scan —
+    comparisons pushed, an OR of ranges as the residual — count the file's rows."""
+    a = filter_cache_table(golden)
+    for q in golden["cases"]["filter_cache"]["queries"]:
+        fs, res = filter_cache_filters(q)
+        rows = O.table_scan([O.Column(a)], F.serialize(fs, res), len(a))
+        assert len(rows) == q["count"], q["sql"]
+
+
 def obsolete_filter_sets(golden):
     """test_obsolete_filters.test's integer queries as (WHERE text, TableFilterSet of the AND
     chain on column a, expected (a, b) rows sorted)."""
