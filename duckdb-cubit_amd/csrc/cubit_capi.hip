@@ -1115,6 +1115,7 @@ struct Updates {
     bool valid_at(uint64_t i) const { return h_valids.empty() || h_valids[i]; }
     std::vector<uint64_t> distinct_versions;  // sorted
     uint64_t n = 0;
+    bool unique_rows = true;  // one record per row (the checkpoint fast path merges the list as is)
     // distinct updated values, sorted: the update statistics the planner widens the index
     // statistics with (DuckDB's zonemaps consult update statistics the same way,
     // standard_column_data.cpp:50-57)
@@ -1999,7 +2000,11 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
     Updates u;
     u.n = n;
     for (uint64_t i = 0; valids && i < n; ++i) u.any_null |= valids[i] == 0;
+    u.h_rows.reserve(n);
+    u.h_values.reserve(n);
+    u.h_versions.reserve(n);
     for (uint64_t i : order) {
+        if (!u.h_rows.empty() && u.h_rows.back() == rows[i]) u.unique_rows = false;
         u.h_rows.push_back(rows[i]);
         u.h_values.push_back(values[i]);
         u.h_versions.push_back(versions[i]);
@@ -2383,8 +2388,9 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
 // with version < horizon — visible to every snapshot the caller still serves (start_time ≥
 // horizon, as DuckDB's lowest active start bounds what a checkpoint may fold) — leaves the
 // update list: each row takes its newest such value (records of a row are chronological; the
-// merged records are the row's prefix below horizon) and becomes valid, and every index
-// bitvector of the column flips the rows whose predicate changed (merge_rows_kernel). Records
+// merged records are the row's prefix below horizon) and its NULL-ness, and every index bitvector
+// of the column whose membership can change is rewritten for each 64-row word holding a merged
+// row (merge_words_kernel). Records
 // at or past horizon stay in the list. *n_merged (optional) = rows whose base changed.
 extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horizon, uint64_t* n_merged) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
@@ -2398,49 +2404,78 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     hipStream_t s = t->ctx->stream;
     Column& c = cit->second;
     const Updates& u = uit->second;
+    // The merged records: each row's newest record below horizon. When every record is below it
+    // and each row has one record (a checkpoint after the writers committed: the common case),
+    // that is the update list itself, already on the device, and nothing is left.
+    const bool all = u.unique_rows && u.distinct_versions.back() < horizon;
     std::vector<int64_t> m_rows, m_vals, k_rows, k_vals;
     std::vector<uint8_t> m_valid, k_valid;
     std::vector<uint64_t> k_vers;
-    bool m_null = false;
-    for (uint64_t i = 0; i < u.n;) {
-        uint64_t j = i;
-        while (j < u.n && u.h_rows[j] == u.h_rows[i]) ++j;
-        uint64_t p = i;  // merged prefix [i, p)
-        while (p < j && u.h_versions[p] < horizon) ++p;
-        if (p > i) {
-            const int64_t v = u.h_values[p - 1];
-            const bool ok = u.valid_at(p - 1);  // the newest merged record decides value and NULL-ness
-            if (ok && c.type == CUBIT_TYPE_INT32 && (v < INT32_MIN || v > INT32_MAX))
-                return fail(CUBIT_ERR_INVALID, "row %lld: value %lld does not fit an INT32 column",
-                            (long long)u.h_rows[i], (long long)v);
-            m_rows.push_back(u.h_rows[i]);
-            m_vals.push_back(ok ? v : 0);
-            m_valid.push_back(ok ? 1 : 0);
-            m_null |= !ok;
+    bool m_null = all && u.any_null;
+    uint64_t m = all ? u.n : 0;
+    if (!all) {
+        for (uint64_t i = 0; i < u.n;) {
+            uint64_t j = i;
+            while (j < u.n && u.h_rows[j] == u.h_rows[i]) ++j;
+            uint64_t p = i;  // merged prefix [i, p)
+            while (p < j && u.h_versions[p] < horizon) ++p;
+            if (p > i) {
+                const int64_t v = u.h_values[p - 1];
+                const bool ok = u.valid_at(p - 1);  // the newest merged record decides value and NULL-ness
+                m_rows.push_back(u.h_rows[i]);
+                m_vals.push_back(ok ? v : 0);
+                m_valid.push_back(ok ? 1 : 0);
+                m_null |= !ok;
+            }
+            for (uint64_t q = p; q < j; ++q) {
+                k_rows.push_back(u.h_rows[q]);
+                k_vals.push_back(u.h_values[q]);
+                k_vers.push_back(u.h_versions[q]);
+                k_valid.push_back(u.valid_at(q) ? 1 : 0);
+            }
+            i = j;
         }
-        for (uint64_t q = p; q < j; ++q) {
-            k_rows.push_back(u.h_rows[q]);
-            k_vals.push_back(u.h_values[q]);
-            k_vers.push_back(u.h_versions[q]);
-            k_valid.push_back(u.valid_at(q) ? 1 : 0);
-        }
-        i = j;
+        m = m_rows.size();
     }
-    if (m_rows.empty()) return CUBIT_OK;
+    if (m == 0) return CUBIT_OK;
+    // the merged values' distinct valid values: the statistics and exact keys they add
+    std::vector<int64_t> added;
+    if (all) {
+        added = u.stat_values;  // the records' distinct valid values, computed when they were set
+    } else {
+        std::vector<int64_t> valid_vals;
+        for (uint64_t i = 0; i < m; ++i)
+            if (m_valid[i]) valid_vals.push_back(m_vals[i]);
+        added = distinct_sorted(valid_vals.data(), valid_vals.size());
+    }
+    if (c.type == CUBIT_TYPE_INT32 && !added.empty() && (added.front() < INT32_MIN || added.back() > INT32_MAX))
+        return fail(CUBIT_ERR_INVALID, "merged value %lld does not fit an INT32 column",
+                    (long long)(added.front() < INT32_MIN ? added.front() : added.back()));
     HIP_CHECK(hipStreamSynchronize(s));
-    drop_zones(t);  // the merge flips index bits in place
+    drop_zones(t);  // the merge rewrites index words in place
     if (int rc = own_column(t, c, std::max<uint64_t>(t->n_rows, c.cap_rows))) return rc;
     if (m_null)
         if (int rc = ensure_validity(t, c)) return rc;
     c.drop_packed();  // merged values are not in the segments
-    const uint64_t m = m_rows.size();
     DevBuf d_rows, d_vals, d_valid;
-    if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess ||
-        (m_null && hipMalloc(&d_valid.p, m) != hipSuccess))
-        return fail(CUBIT_ERR_OOM, "merge list allocation failed");
-    HIP_CHECK(hipMemcpyAsync(d_rows.p, m_rows.data(), m * 8, hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(d_vals.p, m_vals.data(), m * 8, hipMemcpyHostToDevice, s));
-    if (m_null) HIP_CHECK(hipMemcpyAsync(d_valid.p, m_valid.data(), m, hipMemcpyHostToDevice, s));
+    const int64_t* rows_p;
+    const int64_t* vals_p;
+    const uint8_t* valid_p;
+    if (all) {
+        rows_p = static_cast<const int64_t*>(u.rows->p);
+        vals_p = static_cast<const int64_t*>(u.values->p);
+        valid_p = u.any_null ? u.d_valids() : nullptr;  // a NULL record holds value 0 (store_updates)
+    } else {
+        if (hipMalloc(&d_rows.p, m * 8) != hipSuccess || hipMalloc(&d_vals.p, m * 8) != hipSuccess ||
+            (m_null && hipMalloc(&d_valid.p, m) != hipSuccess))
+            return fail(CUBIT_ERR_OOM, "merge list allocation failed");
+        HIP_CHECK(hipMemcpyAsync(d_rows.p, m_rows.data(), m * 8, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_vals.p, m_vals.data(), m * 8, hipMemcpyHostToDevice, s));
+        if (m_null) HIP_CHECK(hipMemcpyAsync(d_valid.p, m_valid.data(), m, hipMemcpyHostToDevice, s));
+        rows_p = static_cast<const int64_t*>(d_rows.p);
+        vals_p = static_cast<const int64_t*>(d_vals.p);
+        valid_p = m_null ? static_cast<const uint8_t*>(d_valid.p) : nullptr;
+    }
     Index* ixs[2] = {t->idx.count(col) ? &t->idx[col] : nullptr, t->bins.count(col) ? &t->bins[col] : nullptr};
     MergeIndex mi[2] = {};
     DevBuf d_keys[2], d_bvs[2];
@@ -2457,16 +2492,12 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         mi[x].n_keys = (uint32_t)ix->keys.size();
         mi[x].encoding = ix->encoding == CUBIT_INDEX_RANGE ? 0 : ix->encoding == CUBIT_INDEX_EQUALITY ? 1 : 2;
     }
-    HIP_CHECK(launch_merge_rows(static_cast<const int64_t*>(d_rows.p), static_cast<const int64_t*>(d_vals.p),
-                                static_cast<const uint8_t*>(d_valid.p), m, const_cast<void*>(c.data), c.type,
-                                const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
+    // every 64-row word holding merged rows, rewritten by one wave (rows ascend, each once)
+    HIP_CHECK(launch_merge_words(rows_p, vals_p, valid_p, m, t->n_rows, const_cast<void*>(c.data), c.type,
+                                 const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
     HIP_CHECK(hipStreamSynchronize(s));
     // statistics and exact keys for the merged values (a merged NULL leaves the index bounds:
     // they only have to contain the valid values)
-    std::vector<int64_t> valid_vals;
-    for (uint64_t i = 0; i < m; ++i)
-        if (m_valid[i]) valid_vals.push_back(m_vals[i]);
-    const std::vector<int64_t> added = distinct_sorted(valid_vals.data(), valid_vals.size());
     for (Index* ix : ixs) {
         if (!ix || added.empty()) continue;
         const bool was_empty = ix->empty;
@@ -2477,9 +2508,12 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         if (int rc = maintain_exact_keys(t, col, *ix, added, old_min, was_empty)) return rc;
     }
     // the records left (each row's suffix at or past horizon), still grouped and chronological
-    if (int rc = store_updates(t, col, k_rows.data(), k_vals.data(), k_vers.data(), k_rows.size(), k_valid.data()))
+    if (k_rows.empty()) {
+        t->upd.erase(col);
+    } else if (int rc = store_updates(t, col, k_rows.data(), k_vals.data(), k_vers.data(), k_rows.size(),
+                                      k_valid.data())) {
         return rc;
-    if (k_rows.empty()) t->upd.erase(col);
+    }
     drop_derived(t);
     if (n_merged) *n_merged = m;
     return CUBIT_OK;

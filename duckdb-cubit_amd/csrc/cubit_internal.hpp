@@ -261,9 +261,9 @@ struct MergeIndex {
 };
 hipError_t launch_splice_bits(uint64_t* dst, const uint64_t* src, uint64_t bit_off, uint64_t n_bits,
                               hipStream_t stream);
-// valids: per merged row 1 = the value, 0 = NULL (nullptr: every row valid; a NULL needs `validity`)
-hipError_t launch_merge_rows(const int64_t* rows, const int64_t* values, const uint8_t* valids, uint64_t m, void* col,
-                             int type, uint64_t* validity, const MergeIndex& ix0, const MergeIndex& ix1,
-                             hipStream_t stream);
-
+// merge by 64-row words: the m merged records' rows ascend, each row once; valids: per record
+// 1 = the value, 0 = NULL (nullptr: every row valid; a NULL needs `validity`)
+hipError_t launch_merge_words(const int64_t* rows, const int64_t* values, const uint8_t* valids, uint64_t m,
+                              uint64_t n_rows, void* col, int type, uint64_t* validity, MergeIndex ix0, MergeIndex ix1,
+                              hipStream_t stream);
 }  // namespace cubit
