@@ -411,3 +411,44 @@ def test_scan_tiles_returns_this_scans_directory(ctx):
     rc, *_ = scan_tiles(7, tiles - 1)
     assert rc == L.ERR_CAPACITY
     t.close()
+
+
+def test_q6_over_an_empty_lineitem(ctx):
+    """test/sql/tpch/tpch_sf0.test runs every TPC-H query over dbgen(sf=0): Q6's filter over an
+    empty lineitem (indexes built on no rows) gives no rows through the scan, the count, the fused
+    sum and the table function (one partition, and an empty partition beside a non-empty one)."""
+    from cubit_amd import scan_function as S
+
+    def q6_empty():
+        t = CubitTable(ctx, 0)
+        t.add_column(0, np.empty(0, np.int32))
+        for c in (1, 2, 3):
+            t.add_column(c, np.empty(0, np.int64))
+        months = [F.date(y, m, 1) for y in range(1992, 1999) for m in range(1, 13)] + [F.date(1999, 1, 1)]
+        t.build_index(0, L.INDEX_RANGE, months)
+        t.build_index(1, L.INDEX_RANGE)
+        t.build_index(2, L.INDEX_RANGE)
+        return t
+
+    t = q6_empty()
+    fs = F.q6_filter_set()
+    assert t.scan(fs).tolist() == [] and t.count(fs) == 0
+    assert t.sum_product(3, 1, fs) == (0, 0)
+    assert S.cardinality(t) == (0, 0)
+    fn = CubitScanFunction(t, [0, 1, 2, 3, ROW_ID], [4, 3, 1], F.q6_filter_set(0, 1, 2))
+    assert len(fn.function(fn.init_local())[0]) == 0
+    assert fn.progress() == 100.0
+    fn.close()
+    # an empty partition in front of the SF0.01 lineitem: the cursor steps over it
+    li = lineitem(0.01)
+    full = CubitTable(ctx, li.n_rows, 0)
+    for c, arr in enumerate((li.l_shipdate, li.l_discount, li.l_quantity, li.l_extendedprice)):
+        full.add_column(c, arr)
+    fn = CubitScanFunction([t, full], [0, 1, 2, 3, ROW_ID], [4], F.q6_filter_set(0, 1, 2))
+    rows = ordered(drain(fn, 2), 0)
+    fn.close()
+    ref = O.table_scan([O.Column(li.l_shipdate), O.Column(li.l_discount), O.Column(li.l_quantity)],
+                       F.serialize(F.q6_filter_set()), li.n_rows)
+    assert np.array_equal(rows, ref) and len(rows) == 1191
+    full.close()
+    t.close()
