@@ -2954,6 +2954,7 @@ __device__ __forceinline__ uint32_t upper_key(const int64_t* keys, uint32_t n, i
 // [min a, max b) of the records' symmetric differences; equality / bins: each record's old and
 // new key. Rows past n_rows read as not present.
 constexpr uint32_t kMergeLdsKeys = 1024;
+constexpr int kMergeBatch = 4;  // words whose 64 values a wave loads together
 
 __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restrict__ rows,
                                                           const int64_t* __restrict__ values,
@@ -2962,7 +2963,7 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                                                           MergeIndex ix0, MergeIndex ix1) {
     // both indexes' keys and bitvector pointers in LDS (up to kMergeLdsKeys each): a word's
     // rewrite walks its keys one after another, and from global memory each step waited for a
-    // dependent load of the key and of the bitvector pointer (19 ms for 4.4 M words at 25 keys)
+    // dependent load of the key and of the bitvector pointer
     __shared__ int64_t s_keys[2][kMergeLdsKeys];
     __shared__ uint64_t* s_bvs[2][kMergeLdsKeys];
     for (int x = 0; x < 2; ++x) {
@@ -2977,102 +2978,146 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
     for (uint64_t i0 = ((uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 64; i0 < m; i0 += waves * 64) {
-        const uint64_t ic = i0 + lane;
-        const bool in_chunk = ic < m;
-        const uint64_t my_word = in_chunk ? (uint64_t)rows[ic] >> 6 : 0;
-        const bool starts_word = in_chunk && (ic == 0 || ((uint64_t)rows[ic - 1] >> 6) != my_word);
+        // the chunk's records and the next chunk's (a word starting here may run into it), each
+        // record loaded once; a word's records then come by shuffles, and the old values of its
+        // rows from the one load of the word's 64 values — one round of loads per batch of words
+        const uint64_t ic = i0 + lane, inx = i0 + 64 + lane;
+        const bool in_c = ic < m, in_n = inx < m;
+        const int64_t row_c = in_c ? rows[ic] : -1, row_n = in_n ? rows[inx] : -1;
+        const int64_t val_c = in_c ? values[ic] : 0, val_n = in_n ? values[inx] : 0;
+        const int ok_c = in_c && (!valids || valids[ic]), ok_n = in_n && (!valids || valids[inx]);
+        const int64_t before = i0 > 0 ? rows[i0 - 1] : -1;  // the record ahead of the chunk
+        int64_t prev_row = __shfl_up(row_c, 1, 64);
+        if (lane == 0) prev_row = before;
+        const bool starts_word = in_c && (prev_row < 0 || ((uint64_t)prev_row >> 6) != ((uint64_t)row_c >> 6));
         uint64_t todo = __ballot(starts_word);
         while (todo) {
-            const uint64_t r0 = i0 + (uint64_t)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint64_t word = (uint64_t)rows[r0] >> 6;
-            const bool same = r0 + lane < m && ((uint64_t)rows[r0 + lane] >> 6) == word;
-            const uint64_t cnt = (uint64_t)__popcll(__ballot(same));  // the word's records: a prefix
-            const bool has_rec = lane < cnt;
-            int64_t rrow = 0, nv = 0, ov = 0;
-            bool nvalid = false;
-            uint32_t pos = 0;
-            const uint64_t old_vword = validity ? validity[word] : ~0ull;
-            if (has_rec) {
-                rrow = rows[r0 + lane];
-                nv = values[r0 + lane];
-                nvalid = !valids || valids[r0 + lane];
-                pos = (uint32_t)(rrow & 63);
-                ov = type == 0 ? (int64_t)static_cast<const int32_t*>(col)[rrow] : static_cast<const int64_t*>(col)[rrow];
+            uint32_t s[kMergeBatch];
+            uint64_t wd[kMergeBatch];
+            int nb = 0;
+            for (; nb < kMergeBatch && todo; ++nb) {
+                s[nb] = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                wd[nb] = (uint64_t)__shfl(row_c, (int)s[nb], 64) >> 6;
             }
-            const bool ovalid = has_rec && ((old_vword >> pos) & 1ull);
-            // the records' rows and new NULL-ness as word masks (OR over the wave)
-            uint64_t rec_bits = has_rec ? 1ull << pos : 0, new_bits = has_rec && nvalid ? 1ull << pos : 0;
-    #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                rec_bits |= __shfl_xor(rec_bits, d, 64);
-                new_bits |= __shfl_xor(new_bits, d, 64);
+            int64_t colv[kMergeBatch];
+            uint64_t vw[kMergeBatch];
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                colv[j] = 0;
+                vw[j] = ~0ull;
+                if (j < nb) {
+                    const uint64_t row = wd[j] * 64 + lane;
+                    if (row < n_rows)
+                        colv[j] = type == 0 ? (int64_t)static_cast<const int32_t*>(col)[row]
+                                            : static_cast<const int64_t*>(col)[row];
+                    if (validity) vw[j] = validity[wd[j]];
+                }
             }
-            const uint64_t vword = (old_vword & ~rec_bits) | new_bits;
-            if (has_rec) {
-                if (type == 0) static_cast<int32_t*>(col)[rrow] = nvalid ? (int32_t)nv : 0;
-                else static_cast<int64_t*>(col)[rrow] = nvalid ? nv : 0;
-            }
-            if (validity && lane == 0) validity[word] = vword;
-            // each row's merged value: a record's (records ascend by row, so the row's record is the
-            // popcount of the record rows below it), else the column's, which no lane writes
-            const uint64_t row = word * 64 + lane;
-            const bool mine = (rec_bits >> lane) & 1ull;
-            const int64_t from_rec = __shfl(nv, (int)__popcll(rec_bits & ((1ull << lane) - 1ull)), 64);
-            const bool present = row < n_rows && ((vword >> lane) & 1ull);
-            int64_t v = 0;
-            if (present)
-                v = mine ? from_rec
-                         : (type == 0 ? (int64_t)static_cast<const int32_t*>(col)[row] : static_cast<const int64_t*>(col)[row]);
-            for (int x = 0; x < 2; ++x) {
-                const MergeIndex& gix = x ? ix1 : ix0;
-                if (!gix.bvs) continue;
-                const uint32_t n = gix.n_keys;
-                const bool lds = n <= kMergeLdsKeys;
-                const MergeIndex ix{lds ? s_keys[x] : gix.keys, lds ? s_bvs[x] : gix.bvs, n, gix.encoding};
-                if (ix.encoding == 0) {  // range: L(k) = {valid, v < k}
-                    uint32_t a = n, b = 0;  // the union of the records' flipped key intervals
-                    if (has_rec) {
-                        uint32_t ra = n, rb = n;
-                        if (ovalid && nvalid) {
-                            const int64_t lo = ov < nv ? ov : nv, hi = ov < nv ? nv : ov;
-                            ra = upper_key(ix.keys, n, lo);
-                            rb = upper_key(ix.keys, n, hi);
-                        } else if (ovalid) {
-                            ra = upper_key(ix.keys, n, ov);
-                        } else if (nvalid) {
-                            ra = upper_key(ix.keys, n, nv);
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                if (j >= nb) break;
+                const uint64_t word = wd[j];
+                // the word's records: chunk lanes s[j] … and on into the next chunk (a prefix)
+                const uint32_t cnt = (uint32_t)__popcll(__ballot(in_c && ((uint64_t)row_c >> 6) == word)) +
+                                     (uint32_t)__popcll(__ballot(in_n && ((uint64_t)row_n >> 6) == word));
+                const uint32_t q = s[j] + lane;  // this lane's record, 0 … 127 over the two chunks
+                const int64_t r_a = __shfl(row_c, (int)(q & 63), 64), r_b = __shfl(row_n, (int)(q & 63), 64);
+                const int64_t v_a = __shfl(val_c, (int)(q & 63), 64), v_b = __shfl(val_n, (int)(q & 63), 64);
+                const int o_a = __shfl(ok_c, (int)(q & 63), 64), o_b = __shfl(ok_n, (int)(q & 63), 64);
+                const bool has_rec = lane < cnt;
+                const int64_t rrow = q < 64 ? r_a : r_b;
+                const int64_t nv = q < 64 ? v_a : v_b;
+                const bool nvalid = (q < 64 ? o_a : o_b) != 0;
+                const uint32_t pos = has_rec ? (uint32_t)(rrow & 63) : 0;
+                const int64_t ov = __shfl(colv[j], (int)pos, 64);  // the row's old value
+                const uint64_t old_vword = vw[j];
+                const bool ovalid = has_rec && ((old_vword >> pos) & 1ull);
+                // the records' rows and new NULL-ness as word masks (OR over the wave)
+                uint64_t rec_bits = has_rec ? 1ull << pos : 0, new_bits = has_rec && nvalid ? 1ull << pos : 0;
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) {
+                    rec_bits |= __shfl_xor(rec_bits, d, 64);
+                    new_bits |= __shfl_xor(new_bits, d, 64);
+                }
+                const uint64_t vword = (old_vword & ~rec_bits) | new_bits;
+                if (has_rec) {
+                    if (type == 0) static_cast<int32_t*>(col)[rrow] = nvalid ? (int32_t)nv : 0;
+                    else static_cast<int64_t*>(col)[rrow] = nvalid ? nv : 0;
+                }
+                if (validity && lane == 0) validity[word] = vword;
+                // each row's merged value: its record's (records ascend by row: the row's record is
+                // the popcount of the record rows below it), else its old value
+                const uint64_t row = word * 64 + lane;
+                const bool mine = (rec_bits >> lane) & 1ull;
+                const int64_t from_rec = __shfl(nv, (int)__popcll(rec_bits & ((1ull << lane) - 1ull)), 64);
+                const bool present = row < n_rows && ((vword >> lane) & 1ull);
+                const int64_t v = present ? (mine ? from_rec : colv[j]) : 0;
+                for (int x = 0; x < 2; ++x) {
+                    const MergeIndex& gix = x ? ix1 : ix0;
+                    if (!gix.bvs) continue;
+                    const uint32_t n = gix.n_keys;
+                    const bool lds = n <= kMergeLdsKeys;
+                    const MergeIndex ix{lds ? s_keys[x] : gix.keys, lds ? s_bvs[x] : gix.bvs, n, gix.encoding};
+                    if (ix.encoding == 0) {  // range: L(k) = {valid, v < k}
+                        // the union of the records' flipped key intervals (keys searched in LDS when
+                        // cached there: called with the LDS array itself, the searches are ds_reads)
+                        auto interval = [&](const int64_t* keys, uint32_t& ra, uint32_t& rb) {
+                            ra = n;
+                            rb = n;
+                            if (ovalid && nvalid) {
+                                const int64_t lo = ov < nv ? ov : nv, hi = ov < nv ? nv : ov;
+                                ra = upper_key(keys, n, lo);
+                                rb = upper_key(keys, n, hi);
+                            } else if (ovalid) {
+                                ra = upper_key(keys, n, ov);
+                            } else if (nvalid) {
+                                ra = upper_key(keys, n, nv);
+                            }
+                        };
+                        uint32_t a = n, b = 0;
+                        if (has_rec) {
+                            uint32_t ra, rb;
+                            if (lds) interval(s_keys[x], ra, rb);
+                            else interval(gix.keys, ra, rb);
+                            if (ra < rb) {
+                                a = ra;
+                                b = rb;
+                            }
                         }
-                        if (ra < rb) {
-                            a = ra;
-                            b = rb;
+#pragma unroll
+                        for (int d = 32; d >= 1; d >>= 1) {
+                            a = min(a, (uint32_t)__shfl_xor((int)a, d, 64));
+                            b = max(b, (uint32_t)__shfl_xor((int)b, d, 64));
                         }
-                    }
-    #pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) {
-                        a = min(a, (uint32_t)__shfl_xor((int)a, d, 64));
-                        b = max(b, (uint32_t)__shfl_xor((int)b, d, 64));
-                    }
-                    for (uint32_t k = a; k < b; ++k) {
-                        const uint64_t bits = __ballot(present && v < ix.keys[k]);
-                        if (lane == 0) ix.bvs[k][word] = bits;
-                    }
-                } else {  // equality E(k) = {valid, v == k}; bins B_i = {valid, e_i <= v < e_i+1}
-                    // each record's old and new bitvector (-1: none), rewritten one record at a time
-                    auto which = [&](bool ok, int64_t val) -> int32_t {
-                        if (!ok) return -1;
-                        const uint32_t k = upper_key(ix.keys, n, val);
-                        if (ix.encoding == 1) return (k > 0 && ix.keys[k - 1] == val) ? (int32_t)k - 1 : -1;
-                        return (k == 0 || k == n) ? -1 : (int32_t)k - 1;
-                    };
-                    const int32_t ko = has_rec ? which(ovalid, ov) : -1, kn = has_rec ? which(nvalid, nv) : -1;
-                    for (uint32_t j = 0; j < cnt; ++j) {
-                        for (int side = 0; side < 2; ++side) {
-                            const int32_t k = __shfl(side ? kn : ko, (int)j, 64);
-                            if (k < 0) continue;
-                            const bool in = ix.encoding == 1 ? v == ix.keys[k] : (ix.keys[k] <= v && v < ix.keys[k + 1]);
-                            const uint64_t bits = __ballot(present && in);
-                            if (lane == 0) ix.bvs[k][word] = bits;
+                        if (lds) {  // explicit LDS reads (through a generic pointer they issue as flat loads)
+                            for (uint32_t k = a; k < b; ++k) {
+                                const uint64_t bits = __ballot(present && v < s_keys[x][k]);
+                                if (lane == 0) s_bvs[x][k][word] = bits;
+                            }
+                        } else {
+                            for (uint32_t k = a; k < b; ++k) {
+                                const uint64_t bits = __ballot(present && v < ix.keys[k]);
+                                if (lane == 0) ix.bvs[k][word] = bits;
+                            }
+                        }
+                    } else {  // equality E(k) = {valid, v == k}; bins B_i = {valid, e_i <= v < e_i+1}
+                        // each record's old and new bitvector (-1: none), rewritten one record at a time
+                        auto which = [&](bool ok, int64_t val) -> int32_t {
+                            if (!ok) return -1;
+                            const uint32_t k = upper_key(ix.keys, n, val);
+                            if (ix.encoding == 1) return (k > 0 && ix.keys[k - 1] == val) ? (int32_t)k - 1 : -1;
+                            return (k == 0 || k == n) ? -1 : (int32_t)k - 1;
+                        };
+                        const int32_t ko = has_rec ? which(ovalid, ov) : -1, kn = has_rec ? which(nvalid, nv) : -1;
+                        for (uint32_t jj = 0; jj < cnt; ++jj) {
+                            for (int side = 0; side < 2; ++side) {
+                                const int32_t k = __shfl(side ? kn : ko, (int)jj, 64);
+                                if (k < 0) continue;
+                                const bool in = ix.encoding == 1 ? v == ix.keys[k] : (ix.keys[k] <= v && v < ix.keys[k + 1]);
+                                const uint64_t bits = __ballot(present && in);
+                                if (lane == 0) ix.bvs[k][word] = bits;
+                            }
                         }
                     }
                 }
