@@ -203,8 +203,9 @@ struct PartScan {
     std::vector<int64_t> offset;
     std::vector<PooledBuffer> d_narrow;
     // the compaction bound is checked on the device (cubit_narrow_checked): one flag word per
-    // emitted position, read once before the partition's first window copy; a column whose flag
-    // is set goes back to the 8-byte copy
+    // group and emitted position — staged, copied with the group and read by the tasks that claim
+    // its windows; per-window copies, read once before the partition's first window — and a
+    // column whose flag is set goes back to its 8-byte values
     PooledBuffer d_overflow;
     std::once_flag overflow_checked;
     // NULL-ness per emitted position: a column whose statistics admit NULLs (update records
@@ -214,7 +215,7 @@ struct PartScan {
     std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
-    // staging (see kStageGroupBytes): the host copies of every emitted column's transfer form and
+    // staging (see kStageGroups): the host copies of every emitted column's transfer form and
     // validity words, each group's overflow flags, and its events
     bool staged = false;
     std::vector<PooledBuffer> h_stage, h_stage_valid;
@@ -317,27 +318,20 @@ void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
 }
 
 // Count and tile runs of a launched decode; a filter that kept more rows than the guess runs
-// a second time with the exact count (returns true then: the probes must run again). h_meta: the
-// count and the directory already copied to the host (BeginMeta), or null to read them here.
-bool FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn,
-                  const uint64_t* h_meta) {
+// a second time with the exact count.
+void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn) {
     cubit_ctx* ctx = P.part.ctx;
-    bool again_decoded = false;
-    if (h_meta) P.count = h_meta[0];
-    else check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
+    check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
     if (P.count > P.d_ids.bytes / 8) {
         LaunchDecode(P, nodes, txn, P.count);
         idx_t again = 0;
         check(cubit_memcpy_d2h(ctx, &again, P.d_cnt.p, 8), "count");
         if (again != P.count) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
-        h_meta = nullptr;
-        again_decoded = true;
     }
     const uint32_t n_tiles = P.count ? (uint32_t)P.tiles.size() : 0;  // nothing qualified: no run
     P.tiles.clear();
     std::vector<uint64_t> dir(2 * (size_t)n_tiles);
-    if (n_tiles && h_meta) std::memcpy(dir.data(), h_meta + 1, dir.size() * 8);
-    else if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
+    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
     // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
     idx_t off = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {
@@ -353,7 +347,6 @@ bool FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
     if (off != P.count)
         throw ScanError(CUBIT_ERR_INVALID, "cubit_scan: tile runs cover " + std::to_string(off) + " of " +
                                                std::to_string(P.count) + " row ids");
-    return again_decoded;
 }
 
 // The transfer plan of a partition's emitted columns, and their device buffers. The statistics
@@ -545,7 +538,7 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
     }
     // every partition's decode in flight before any count is read: one per device at a time
     for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, P->part.n_rows / 8 + 4096);
-    for (auto& P : g->parts) FinishDecode(*P, nodes, txn, nullptr);
+    for (auto& P : g->parts) FinishDecode(*P, nodes, txn);
     // windows: consecutive non-empty tiles of one partition, at most window_rows() rows and
     // window_rows() / 4,096 tiles
     const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
@@ -573,12 +566,12 @@ std::unique_ptr<LocalTableFunctionState> CubitScanInitLocal(TableFunctionInitInp
 }
 
 // TableScanParallelStateNext analogue: take the next window (row_group_collection.cpp hands
-// out row groups under a mutex; one atomic suffices here) and copy its rows of every emitted
-// column to this state's page-locked buffers, from the window's partition on that partition's
-// device. A state copies one window at a time: claiming the next window and copying it while
-// the current one is handed out measured slower at 8 and 16 tasks, before and after the pinned
-// pool reused its buffers (12.4 vs 5.09 ms at 8 tasks, profiles/r04c_pipeline_prefetch_not_kept.txt;
-// round 3: profiles/r03mn_*).
+// out row groups under a mutex; one atomic suffices here). Staged partitions: wait for the
+// window's group and point at its rows in the staged buffers. Otherwise: copy the window's rows
+// of every emitted column to this state's page-locked buffers, from the window's partition on
+// that partition's device, one window at a time (claiming the next window and copying it while
+// the current one is handed out measured slower at 8 and 16 tasks: 12.4 vs 5.09 ms,
+// profiles/r04c_pipeline_prefetch_not_kept.txt; round 3: profiles/r03mn_*).
 bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     const uint32_t w = g.next.fetch_add(1);
     if (w >= g.windows.size()) {
