@@ -4,11 +4,16 @@ a larger size and for a fixed wall-clock budget, with fresh seeds — random pus
 TableFilterSets and residual AND/OR trees over range / equality / edge-keyed range + bins /
 unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
 updates from a writer; each scan under a random decode kernel (AUTO, pair-claimed, run-claimed,
-look-back). Every result is compared with the oracle; prints one summary line.
+look-back). Every result is compared with the oracle; every third filter also runs through the
+table function (random projection with the row id, 1-4 pipeline tasks, staged or per-window
+copies): row ids, values and NULL-ness against the oracle's scan and fetch. Prints one summary
+line.
 
   python scripts/fuzz_soak.py [seconds] [rows] [first seed]
 """
+import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -20,9 +25,55 @@ sys.path[:0] = [str(ROOT / "duckdb-cubit_amd"), str(ROOT), str(ROOT / "tests")]
 from cubit_amd import _lib as L  # noqa: E402
 from cubit_amd import filters as F  # noqa: E402
 from cubit_amd.datagen import validity_from_mask  # noqa: E402
+from cubit_amd.scan_function import ROW_ID, CubitScanFunction  # noqa: E402
 from cubit_amd.table import Context, CubitTable  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from test_gpu_planner_fuzz import TXN_START, rand_const_filter, rand_residual  # noqa: E402
+
+
+def table_function_check(t, rng, fs, residual, txn, ref, ocols, row_base, tx, label):
+    """The scan through the table-function callbacks: the emitted storage columns' values and
+    NULL-ness and the row ids, against the oracle (row ids: its scan; values: its fetch)."""
+    keep = [int(c) for c in rng.permutation(4)[: int(rng.integers(0, 5))]]
+    column_ids = [0, 1, 2, 3, ROW_ID]
+    projection = [4] + keep
+    if rng.random() < 0.5:
+        os.environ["CUBIT_SCAN_STAGE_MB"] = "0"  # per-window copies
+    else:
+        os.environ.pop("CUBIT_SCAN_STAGE_MB", None)
+    fn = CubitScanFunction(t, column_ids, projection, fs, residual, txn=txn)
+    parts, lock = [], threading.Lock()
+
+    def task():
+        local = fn.init_local()
+        while True:
+            vals, masks = fn.function_validity(local)
+            if len(vals[0]) == 0:
+                return
+            with lock:
+                parts.append((vals, masks))
+
+    th = [threading.Thread(target=task) for _ in range(int(rng.integers(1, 5)))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    fn.close()
+    os.environ.pop("CUBIT_SCAN_STAGE_MB", None)
+    if not parts:
+        if len(ref):
+            raise AssertionError(f"{label}: table function returned no rows, oracle {len(ref)}")
+        return
+    ids = np.concatenate([p[0][0] for p in parts])
+    o = np.argsort(ids, kind="stable")
+    if not np.array_equal(ids[o], ref):
+        raise AssertionError(f"{label}: table function rows {len(ids)} vs {len(ref)}")
+    for k, c in enumerate(keep, start=1):
+        vals = np.concatenate([p[0][k] for p in parts])[o]
+        valid = np.concatenate([p[1][k] for p in parts])[o]
+        rv, rvalid = O.fetch(ocols[c], ref, row_base=row_base, tx=tx, with_valid=True)
+        if not (np.array_equal(valid, rvalid) and np.array_equal(vals[valid], rv[rvalid].astype(np.int64))):
+            raise AssertionError(f"{label}: table function column {c} differs from the oracle's fetch")
 
 
 def round_(ctx, seed, n, with_updates):
@@ -90,6 +141,9 @@ def round_(ctx, seed, n, with_updates):
             c = t.count(fs, txn=L.Txn(start, tid))
             if c != len(ref):
                 raise AssertionError(f"seed {seed} case {i}: count {c} vs {len(ref)}")
+        if i % 3 == 0:
+            table_function_check(t, rng, fs, residual, L.Txn(start, tid), ref, ocols, row_base,
+                                 O.Mvcc(start, tid, deleted=deleted), f"seed {seed} case {i}")
         checks += 1
     ctx.set_decode_kernel(L.DECODE_AUTO)
     t.close()
