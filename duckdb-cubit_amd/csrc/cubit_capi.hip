@@ -505,7 +505,8 @@ int cubit_dev_free(cubit_ctx* ctx, void* dptr) {
 int cubit_host_alloc(cubit_ctx* ctx, uint64_t bytes, void** hptr) {
     if (!ctx || !hptr) return fail(CUBIT_ERR_INVALID, "null argument");
     if (int rc = set_device(ctx)) return rc;
-    if (hipHostMalloc(hptr, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess)
+    // portable: the table function's pinned pool serves copies from every device's partitions
+    if (hipHostMalloc(hptr, std::max<uint64_t>(bytes, 16), hipHostMallocPortable) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
     return CUBIT_OK;
 }
