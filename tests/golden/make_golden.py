@@ -28,7 +28,11 @@ def sqllogic_script(rel):
     def value(v):
         if v == "NULL":
             return None
-        return int(v) if re.fullmatch(r"-?\d+", v) else int(float(v))  # SUM as DOUBLE: "294912.000000"
+        if re.fullmatch(r"-?\d+", v):
+            return int(v)
+        if re.fullmatch(r"-?\d+\.\d*", v):
+            return int(float(v))  # SUM as DOUBLE: "294912.000000"
+        return v  # text (an EXPLAIN's plan line): kept as the file has it
 
     def emit(lines):
         head = lines[0].split()
@@ -307,6 +311,30 @@ def main():
     art = {"negative_range": {"source": "test/sql/index/art/scan/test_art_negative_range_scan.test",
                               "range": [-500, 500], "queries": neg},
            "many_matches": {"source": "test/sql/index/art/scan/test_art_many_matches.test", "blocks": blocks}}
+    # test_art_adaptive_scan.test: 42 x 2050 then 43 … 5042 appended, COUNT(i) WHERE i = 42; and
+    # test_art_range_scan.test's USMALLINT parts: rows 1 … 19 (resp. 134), x > 20 (resp. 135) empty,
+    # then 256 (resp. 256, 257) appended after the index and found. Each step: rows appended (None:
+    # the table's first rows), then the query's expected rows / count from the file.
+    ad = sqllogic_script("test/sql/index/art/scan/test_art_adaptive_scan.test")
+    ad_sql = " ".join(st["sql"] for st in ad["script"])
+    assert "SELECT 42 AS i FROM range(2050)" in ad_sql and "SELECT 42 + 1 + range FROM range(5000)" in ad_sql
+    ad_count = [st["rows"] for st in ad["script"] if st["op"] == "query" and st["sql"].startswith("SELECT COUNT(i)")]
+    rs = sqllogic_script("test/sql/index/art/scan/test_art_range_scan.test")
+    rs_q = [st for st in rs["script"] if st["op"] == "query" and "x >" in st["sql"] and "'" not in st["sql"]]
+    rs_sql = " ".join(st["sql"] for st in rs["script"])
+    assert "SELECT i FROM range(1, 20) tbl(i)" in rs_sql and "SELECT i FROM range(1, 135) tbl(i)" in rs_sql
+    assert [q["sql"] for q in rs_q] == ["SELECT x FROM test WHERE x > 20;"] * 2 + ["SELECT x FROM test WHERE x > 135;"] * 2
+    art["appended"] = [
+        {"source": "test/sql/index/art/scan/test_art_adaptive_scan.test", "type": "int32",
+         "steps": [{"append": {"repeat": [42, 2050]}, "then": {"range": [43, 5043]}, "filter": ["=", 42],
+                    "count": ad_count[0][0][0]}]},
+        {"source": "test/sql/index/art/scan/test_art_range_scan.test (node 48)", "type": "uint16",
+         "steps": [{"append": {"range": [1, 20]}, "filter": [">", 20], "rows": [r[0] for r in rs_q[0]["rows"]]},
+                   {"append": {"values": [256]}, "filter": [">", 20], "rows": [r[0] for r in rs_q[1]["rows"]]}]},
+        {"source": "test/sql/index/art/scan/test_art_range_scan.test (node 256)", "type": "uint16",
+         "steps": [{"append": {"range": [1, 135]}, "filter": [">", 135], "rows": [r[0] for r in rs_q[2]["rows"]]},
+                   {"append": {"values": [256, 257]}, "filter": [">", 135], "rows": [r[0] for r in rs_q[3]["rows"]]}]},
+    ]
     assert len(neg) == 3 and len(blocks) == 2 and all(len(b["counts"]) == 6 for b in blocks)
     # test/sql/filter/test_transitive_filters.test: vals1(i, j) = (i, i), (i, i+1), (i, i-1) for
     # i in 0 … 10; the 40 one-table queries `WHERE <i cmp constant> AND <j cmp i>` with their rows in

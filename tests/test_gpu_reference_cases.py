@@ -8,7 +8,7 @@ from cubit_amd import filters as F
 from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import ROW_ID, CubitScanFunction
 from cubit_amd.table import Context, CubitTable
-from test_oracle_tpch import (art_scan_cases, block_boundary_states, filter_cache_filters, filter_cache_table,
+from test_oracle_tpch import (art_appended_cases, art_scan_cases, block_boundary_states, filter_cache_filters, filter_cache_table,
                               filter_pushdown_tables, many_updaters_reads, multi_version_views,
                               obsolete_filter_columns, obsolete_filter_sets, residual_from_json, update_case_views,
                               zonemap_table)
@@ -251,6 +251,37 @@ def test_filter_cache(ctx, golden, encoding):
             mask &= ((a > 1) & (a < 10) | (a > 9995)) if q["count"] == 30 else ((a != 3) & (a < 50) | (a > 9995)) & (a > 1) & (a < 20)
         assert sorted(got) == np.flatnonzero(mask).tolist(), (q["sql"], encoding)
     t.close()
+
+
+@pytest.mark.parametrize("encoding", [L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_art_scans_over_appended_rows(ctx, golden, encoding):
+    """test_art_range_scan.test's integer parts: an indexed USMALLINT key column created empty (the
+    PRIMARY KEY's index exists before any row), rows appended (cubit_table_append maintains the
+    index: new keys, values above the old range), each query's rows as the file has them; and
+    test_art_adaptive_scan.test: 2,050 rows of 42 and 5,000 others, indexed after, COUNT = 2050."""
+    for source, dtype, steps in art_appended_cases(golden):
+        t = CubitTable(ctx, 0)
+        t.add_column(0, np.empty(0, np.dtype(dtype)))
+        if "adaptive" not in source:
+            t.build_index(0, encoding)  # the index exists before the rows
+        v = np.zeros(0, np.int64)
+        for add, fs, count, rows in steps:
+            t.append({0: add.astype(np.int32)})
+            v = np.concatenate([v, add])
+            if "adaptive" in source:
+                t.build_index(0, encoding)  # CREATE INDEX after the inserts
+            got = t.scan(fs)
+            assert np.array_equal(got, np.flatnonzero(fs_mask(fs, v))), (source, encoding)
+            if count is not None:
+                assert t.count(fs) == count, (source, encoding)
+            else:
+                assert v[got].tolist() == rows, (source, encoding)
+        t.close()
+
+
+def fs_mask(fs, v):
+    (flt,) = fs.filters.values()
+    return {">": v > flt.constant, "=": v == flt.constant}[flt.comparison]
 
 
 @pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE])

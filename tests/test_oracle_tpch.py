@@ -490,6 +490,43 @@ def test_art_scans_reference_case(golden):
             assert got == want, (kind, want)
 
 
+def art_appended_cases(golden):
+    """test_art_adaptive_scan.test and test_art_range_scan.test's integer parts as (source, dtype,
+    steps): each step's appended values, its filter as a TableFilterSet, and the file's answer
+    ("count" or the rows)."""
+    def values(spec):
+        if "repeat" in spec:
+            v, k = spec["repeat"]
+            return np.full(k, v, np.int64)
+        if "range" in spec:
+            return np.arange(*spec["range"], dtype=np.int64)
+        return np.array(spec["values"], np.int64)
+
+    for case in golden["cases"]["art_scans"]["appended"]:
+        steps = []
+        for st in case["steps"]:
+            add = values(st["append"])
+            if "then" in st:
+                add = np.concatenate([add, values(st["then"])])
+            op, k = st["filter"]
+            steps.append((add, F.TableFilterSet({0: F.ConstantFilter(op, k)}), st.get("count"), st.get("rows")))
+        yield case["source"], case["type"], steps
+
+
+def test_art_appended_reference_cases(golden):
+    """The ART scans over rows inserted after the index (test_art_range_scan.test) or before it
+    (test_art_adaptive_scan.test) on the oracle: each step's answer from the file."""
+    for source, _, steps in art_appended_cases(golden):
+        v = np.zeros(0, np.int64)
+        for add, fs, count, rows in steps:
+            v = np.concatenate([v, add])
+            got = O.table_scan([O.Column(v)], F.serialize(fs), len(v))
+            if count is not None:
+                assert len(got) == count, source
+            else:
+                assert v[got].tolist() == rows, source
+
+
 def filter_pushdown_tables(golden):
     """The tables of test/optimizer/pushdown/table_filter_pushdown.test as (name, columns
     [(values, valid mask or None, physical width)], queries [(TableFilterSet, result column,
