@@ -640,6 +640,13 @@ int cubit_memset_d(cubit_ctx* ctx, void* dst, int value, uint64_t bytes) {
     return CUBIT_OK;
 }
 
+int cubit_memcpy_d2d(cubit_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || ((!dst || !src) && bytes)) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (!bytes) return CUBIT_OK;
+    HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return CUBIT_OK;
+}
+
 int cubit_ctx_check(cubit_ctx* ctx) {
     if (!ctx) return fail(CUBIT_ERR_INVALID, "ctx is null");
     HIP_CHECK(hipStreamSynchronize(ctx->stream));

@@ -95,6 +95,7 @@ GPU_SIGNATURES = {
     "cubit_memcpy_h2d": (C.c_int, [_P, _P, _P, _U64]),
     "cubit_memcpy_d2h": (C.c_int, [_P, _P, _P, _U64]),
     "cubit_memset_d": (C.c_int, [_P, _P, C.c_int, _U64]),
+    "cubit_memcpy_d2d": (C.c_int, [_P, _P, _P, _U64]),
     "cubit_sync": (C.c_int, [_P]),
     "cubit_copy_stream_create": (C.c_int, [_P, C.POINTER(_P)]),
     "cubit_copy_stream_destroy": (C.c_int, [_P, _P]),

@@ -3,6 +3,8 @@
 #include "cubit_scan_function.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -171,15 +173,22 @@ struct Window {
 };
 
 // Staging: init_global copies every emitted column's transfer form (and validity words) to
-// page-locked host memory on ONE copy stream per device, in row order, in about kStageGroups
-// groups of consecutive windows per partition: each group's probes and narrowing run on the
-// context stream, the copy stream waits for them, copies the group and records an event. A
+// page-locked host memory on ONE copy stream per device, in row order, in about stage_groups()
+// groups of consecutive windows per partition: each group's probes and narrowing fill its block
+// on the context stream, the copy stream waits for them, copies the block and records an event. A
 // pipeline task that claims a window waits for its group's event and reads the rows in place. One stream of multi-megabyte
 // copies runs the link at its own rate (56.6 GB/s for one 64 MiB copy on the MI355X box); the
 // tasks' concurrent per-window copies (0.5–1 MB each on up to 16 streams) reached ~20 GB/s
 // (profiles/r05k_*). Partitions whose staged bytes exceed CUBIT_SCAN_STAGE_MB (default 1024) are
 // copied per window by the task that claims it, as before.
-constexpr uint64_t kStageGroups = 8;
+uint64_t stage_groups() {  // 8; CUBIT_SCAN_STAGE_GROUPS overrides (diagnostic)
+    static const uint64_t n = [] {
+        const char* e = std::getenv("CUBIT_SCAN_STAGE_GROUPS");
+        const uint64_t v = e && *e ? std::strtoull(e, nullptr, 10) : 8;
+        return std::max<uint64_t>(v, 1);
+    }();
+    return n;
+}
 
 uint64_t stage_cap_bytes() {  // read per init_global
     const char* e = std::getenv("CUBIT_SCAN_STAGE_MB");
@@ -203,9 +212,9 @@ struct PartScan {
     std::vector<int64_t> offset;
     std::vector<PooledBuffer> d_narrow;
     // the compaction bound is checked on the device (cubit_narrow_checked): one flag word per
-    // group and emitted position — staged, copied with the group and read by the tasks that claim
-    // its windows; per-window copies, read once before the partition's first window — and a
-    // column whose flag is set goes back to its 8-byte values
+    // group and emitted position — staged, at the head of the group's block and read by the tasks
+    // that claim its windows; per-window copies, read once before the partition's first window —
+    // and a column whose flag is set goes back to its 8-byte values
     PooledBuffer d_overflow;
     std::once_flag overflow_checked;
     // NULL-ness per emitted position: a column whose statistics admit NULLs (update records
@@ -215,14 +224,14 @@ struct PartScan {
     std::vector<PooledBuffer> d_valid;
     std::vector<uint32_t> tiles;         // non-empty tiles, ascending
     std::vector<idx_t> tile_off, tile_len;  // per non-empty tile: its run in the ordered output
-    // staging (see kStageGroups): the host copies of every emitted column's transfer form and
-    // validity words, each group's overflow flags, and its events
+    // staging (see stage_groups()): per group one block (BlockLayout) on the device and its copy
+    // in page-locked memory, both laid out back to back; the group's events
     bool staged = false;
-    std::vector<PooledBuffer> h_stage, h_stage_valid;
-    PooledBuffer h_flags;                  // per group: one overflow flag per emitted column
+    PooledBuffer d_block, h_block;
+    std::vector<uint64_t> blk_off;          // per group: its block's first byte (+ the end)
+    std::vector<uint64_t> col_rel, val_rel;  // per group × emitted position: its regions in the block
     std::vector<void*> probe_ev, group_ev;  // per group: probes done (context stream), copies done
-    std::vector<uint64_t> group_word;      // per group: its first validity word
-    std::vector<idx_t> group_off;          // per group: its first row (bit 0 of that word)
+    std::vector<idx_t> group_off;          // per group: its first row (bit 0 of its validity words)
     ~PartScan() {
         for (void* ev : group_ev) cubit_copy_event_destroy(part.ctx, ev);
         for (void* ev : probe_ev) cubit_copy_event_destroy(part.ctx, ev);
@@ -349,28 +358,25 @@ void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
                                                std::to_string(P.count) + " row ids");
 }
 
-// The transfer plan of a partition's emitted columns, and their device buffers. The statistics
-// (DataTable::GetStatistics, update records of any version included) say which columns can hold
-// a NULL: those probe with their validity, which also leaves 0 in a NULL row's value. The
-// transfer compaction: a column whose values all lie within 2^32 of an offset crosses PCIe as
-// value - offset in the fewest of 1, 2, 3 and 4 bytes that hold the range (row ids: the
-// partition's rows, offset row_base; probed columns: their statistics' range, widened by any
-// update records — a NULL row holds 0 after the validity probe, so 0 joins the range of a
-// nullable column). Q6's l_discount (0 … 10) crosses as one byte, l_extendedprice as three. The
-// device checks the bound as it narrows (one flag per group and column). Validity words: one
-// run of words per group (`valid_words` in all), a group's bit 0 at its first row.
-void PlanTransfer(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
-                  uint64_t n_groups, uint64_t valid_words) {
-    cubit_ctx* ctx = P.part.ctx;
-    cubit_table* table = P.part.table;
+// The transfer plan of a partition's emitted columns. The statistics (DataTable::GetStatistics,
+// update records of any version included) say which columns can hold a NULL: those probe with
+// their validity, which also leaves 0 in a NULL row's value. The transfer compaction: a column
+// whose values all lie within 2^32 of an offset crosses PCIe as value - offset in the fewest of
+// 1, 2, 3 and 4 bytes that hold the range (row ids: the partition's rows, offset row_base;
+// probed columns: their statistics' range, widened by any update records — a NULL row holds 0
+// after the validity probe, so 0 joins the range of a nullable column). Q6's l_discount (0 … 10)
+// crosses as one byte, l_extendedprice as three. The device checks the bound as it narrows (one
+// flag per group and column).
+void PlanWidths(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit) {
     const size_t n_emit = emit.size();
-    const uint64_t n = P.count;
-    P.d_cols.resize(n_emit);
     P.nullable.assign(n_emit, false);
-    P.d_valid.resize(n_emit);
     P.width.assign(n_emit, 0);
     P.offset.assign(n_emit, 0);
-    P.d_narrow.resize(n_emit);
+    // CUBIT_SCAN_TEST_SHIFT_OFFSET=1 (tests only): every compacted column's offset one above its
+    // minimum, so the device flags the groups that hold the minimum and their windows take the
+    // 8-byte fallback
+    const char* shift_env = std::getenv("CUBIT_SCAN_TEST_SHIFT_OFFSET");
+    const int64_t shift = shift_env && *shift_env == '1' ? 1 : 0;
     for (size_t e = 0; e < n_emit; ++e) {
         const column_t col = column_ids[emit[e]];
         int64_t lo, hi;
@@ -379,32 +385,55 @@ void PlanTransfer(PartScan& P, const std::vector<column_t>& column_ids, const st
             hi = P.part.row_base + (int64_t)P.part.n_rows - 1;
         } else {
             int hn = 0, hv = 0;
-            check(cubit_table_column_statistics(table, (int)col, &lo, &hi, &hn, &hv), "cubit_table_column_statistics");
+            check(cubit_table_column_statistics(P.part.table, (int)col, &lo, &hi, &hn, &hv),
+                  "cubit_table_column_statistics");
             P.nullable[e] = hn != 0;
             if (P.nullable[e]) {
                 lo = std::min<int64_t>(lo, 0);
                 hi = std::max<int64_t>(hi, 0);
             }
-            P.d_cols[e].allocate(device_pool(), ctx, n * 8);
-            if (P.nullable[e]) P.d_valid[e].allocate(device_pool(), ctx, valid_words * 8);
         }
         const uint64_t span = (uint64_t)hi - (uint64_t)lo;  // hi >= lo
         const int width = span < (1ull << 8) ? 1 : span < (1ull << 16) ? 2 : span < (1ull << 24) ? 3 : span < (1ull << 32) ? 4 : 0;
         if (!width) continue;
         P.width[e] = width;
-        P.offset[e] = lo;
-        P.d_narrow[e].allocate(device_pool(), ctx, n * (uint64_t)width + 16);
+        P.offset[e] = lo + shift;
     }
-    P.d_overflow.allocate(device_pool(), ctx, std::max<uint64_t>(n_groups, 1) * n_emit * 4);
-    check(cubit_memset_d(ctx, P.d_overflow.p, 0, std::max<uint64_t>(n_groups, 1) * n_emit * 4), "overflow flags");
+}
+
+// Bytes per row of an emitted column's transfer form: its compacted width, or the 8-byte value.
+uint64_t transfer_bytes(const PartScan& P, size_t e) { return P.width[e] ? (uint64_t)P.width[e] : 8; }
+
+constexpr uint64_t round16(uint64_t b) { return (b + 15) & ~15ull; }
+
+// One group's staging block (offsets from the block's first byte, every region 16-byte aligned):
+// the overflow flags (one word per emitted position), each emitted column's transfer form (+ 16
+// bytes: the 3-byte widen reads past the last value), then the validity words of each nullable
+// column (+ 2 words: the chunk fill reads one word ahead). Returns the block's size.
+uint64_t BlockLayout(const PartScan& P, idx_t len, uint64_t* col_rel, uint64_t* val_rel) {
+    const size_t n_emit = P.width.size();
+    uint64_t rel = round16(n_emit * 4);
+    for (size_t e = 0; e < n_emit; ++e) {
+        col_rel[e] = rel;
+        rel += round16(len * transfer_bytes(P, e) + 16);
+    }
+    for (size_t e = 0; e < n_emit; ++e) {
+        val_rel[e] = rel;
+        if (P.nullable[e]) rel += round16(((len + 63) / 64 + 2) * 8);
+    }
+    return rel;
 }
 
 // Probe every emitted storage column at rows [off, off + len) of the partition's ordered row ids
-// (ColumnData::FilterScan semantics, column_data.cpp:305-309: values with their validity, the
-// validity from word `valid_word`), then narrow them (flags of group `group`); all on the
-// context stream.
+// (ColumnData::FilterScan semantics, column_data.cpp:305-309: values with their validity), then
+// narrow them; all on the context stream. Per emitted position: values to `cols[e]` (a narrowed
+// column: to d_cols, read by the narrowing and by the 8-byte fallback), validity words to
+// `valid[e]`, the transfer form to `out[e]` and the overflow flag to `flags + e`. The row id
+// column's transfer form is its narrowing, or (width 0) a copy of the ids when `out` is a staging
+// block (`copy_ids`).
 void ProbeRange(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit,
-                const cubit_txn* txn, idx_t off, idx_t len, uint64_t valid_word, uint64_t group) {
+                const cubit_txn* txn, idx_t off, idx_t len, int64_t* const* cols, uint64_t* const* valid,
+                char* const* out, uint32_t* flags, bool copy_ids) {
     cubit_ctx* ctx = P.part.ctx;
     cubit_table* table = P.part.table;
     const size_t n_emit = emit.size();
@@ -413,48 +442,42 @@ void ProbeRange(PartScan& P, const std::vector<column_t>& column_ids, const std:
         const column_t col = column_ids[emit[e]];
         if (col == COLUMN_IDENTIFIER_ROW_ID) continue;
         if (P.nullable[e]) {
-            check(cubit_table_probe_validity(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len,
-                                             device_ptr(P.d_cols[e]) + off,
-                                             static_cast<uint64_t*>(P.d_valid[e].p) + valid_word),
+            check(cubit_table_probe_validity(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len, cols[e], valid[e]),
                   "cubit_table_probe_validity");
         } else {
-            check(cubit_table_probe(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len,
-                                    device_ptr(P.d_cols[e]) + off),
+            check(cubit_table_probe(table, (int)col, txn, device_ptr(P.d_ids) + off, d_cnt, len, cols[e]),
                   "cubit_table_probe");
         }
     }
     for (size_t e = 0; e < n_emit; ++e) {
-        if (!P.width[e]) continue;
-        PooledBuffer& src = column_ids[emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
-        check(cubit_narrow_checked(ctx, device_ptr(src) + off, d_cnt, len, P.offset[e], P.width[e],
-                                   static_cast<char*>(P.d_narrow[e].p) + off * (uint64_t)P.width[e],
-                                   static_cast<uint32_t*>(P.d_overflow.p) + group * n_emit + e),
-              "cubit_narrow_checked");
+        const bool rowid = column_ids[emit[e]] == COLUMN_IDENTIFIER_ROW_ID;
+        if (P.width[e]) {
+            const int64_t* src = rowid ? device_ptr(P.d_ids) + off : cols[e];
+            check(cubit_narrow_checked(ctx, src, d_cnt, len, P.offset[e], P.width[e], out[e], flags + e),
+                  "cubit_narrow_checked");
+        } else if (rowid && copy_ids) {
+            check(cubit_memcpy_d2d(ctx, out[e], device_ptr(P.d_ids) + off, len * 8), "row id copy");
+        }
     }
 }
 
-// Bytes per row of an emitted column's transfer form: its compacted width, or the 8-byte value.
-uint64_t transfer_bytes(const PartScan& P, size_t e) { return P.width[e] ? (uint64_t)P.width[e] : 8; }
-
-// The transfer form of emitted position e on the device.
-const char* transfer_src(PartScan& P, const std::vector<column_t>& column_ids, const std::vector<idx_t>& emit, size_t e) {
-    if (P.width[e]) return static_cast<const char*>(P.d_narrow[e].p);
-    PooledBuffer& src = column_ids[emit[e]] == COLUMN_IDENTIFIER_ROW_ID ? P.d_ids : P.d_cols[e];
-    return static_cast<const char*>(src.p);
-}
-
-// The probes, compaction and (staged) copies of partition p. Staged (see kStageGroups): the
-// partition's windows are cut into groups; per group the probes and narrowing run on the context
-// stream and close with an event, the staging stream waits for it and copies the group's rows —
-// the link starts on the first group while the device probes the next. Not staged: one probe
-// over every row, and each task copies the window it claims.
+// The probes, compaction and (staged) copies of partition p. Staged (see stage_groups()): the
+// partition's windows are cut into groups, each with one staging block on the device and its
+// image in page-locked memory; per group the probes and narrowing fill the block on the context
+// stream and close with an event, and the staging stream waits for it and copies the block in
+// ONE copy — the link starts on the first group while the device probes the next (one copy per
+// column and a separate flags copy left ≈ 35 µs of gaps per group on the link,
+// profiles/r05ae_*). Not staged: one probe over every row into partition-wide buffers, and each
+// task copies the window it claims.
 void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
     PartScan& P = *g.parts[p];
+    cubit_ctx* ctx = P.part.ctx;
     const size_t n_emit = g.emit.size();
+    PlanWidths(P, g.column_ids, g.emit);
     // groups of consecutive windows: about an eighth of the partition each (each group costs a
     // probe and a narrowing launch per column, a few microseconds apiece), at least 2^18 rows
     std::vector<idx_t> g_off, g_len;
-    const uint64_t rows_per_group = std::max<uint64_t>((P.count + kStageGroups - 1) / kStageGroups, 1ull << 18);
+    const uint64_t rows_per_group = std::max<uint64_t>((P.count + stage_groups() - 1) / stage_groups(), 1ull << 18);
     for (Window& w : g.windows) {
         if (w.part != p) continue;
         if (g_off.empty() || g_len.back() + w.len > rows_per_group) {
@@ -464,55 +487,70 @@ void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
         w.group = (uint32_t)g_off.size() - 1;
         g_len.back() += w.len;
     }
-    uint64_t words = 0;
-    for (idx_t len : g_len) words += (len + 63) / 64;
-    PlanTransfer(P, g.column_ids, g.emit, g_off.size(), std::max<uint64_t>(words, (P.count + 63) / 64));
+    const size_t n_groups = g_off.size();
+    P.col_rel.assign(n_groups * n_emit, 0);
+    P.val_rel.assign(n_groups * n_emit, 0);
+    P.blk_off.assign(n_groups + 1, 0);
+    for (size_t k = 0; k < n_groups; ++k)
+        P.blk_off[k + 1] = P.blk_off[k] + BlockLayout(P, g_len[k], &P.col_rel[k * n_emit], &P.val_rel[k * n_emit]);
+    P.d_cols.resize(n_emit);
+    P.d_valid.resize(n_emit);
+    P.d_narrow.resize(n_emit);
     if (P.count == 0 || n_emit == 0) return;
-    uint64_t total = 0;
+    const bool staged = P.blk_off[n_groups] <= stage_cap_bytes();
+    // partition-wide values of every probed column that the staging does not take whole: the
+    // narrowed ones (their 8-byte fallback) and, not staged, all
     for (size_t e = 0; e < n_emit; ++e)
-        total += P.count * transfer_bytes(P, e) + (P.nullable[e] ? words * 8 : 0);
-    if (total > stage_cap_bytes()) {  // one probe over every row, validity words in row order
-        ProbeRange(P, g.column_ids, g.emit, txn, 0, P.count, 0, 0);
+        if (g.column_ids[g.emit[e]] != COLUMN_IDENTIFIER_ROW_ID && (P.width[e] || !staged))
+            P.d_cols[e].allocate(device_pool(), ctx, P.count * 8);
+    std::vector<int64_t*> cols(n_emit, nullptr);
+    std::vector<uint64_t*> valid(n_emit, nullptr);
+    std::vector<char*> out(n_emit, nullptr);
+    if (!staged) {  // one probe over every row, validity words in row order
+        for (size_t e = 0; e < n_emit; ++e) {
+            cols[e] = device_ptr(P.d_cols[e]);
+            if (P.nullable[e]) {
+                P.d_valid[e].allocate(device_pool(), ctx, ((P.count + 63) / 64 + 2) * 8);
+                valid[e] = static_cast<uint64_t*>(P.d_valid[e].p);
+            }
+            if (P.width[e]) {
+                P.d_narrow[e].allocate(device_pool(), ctx, P.count * (uint64_t)P.width[e] + 16);
+                out[e] = static_cast<char*>(P.d_narrow[e].p);
+            }
+        }
+        P.d_overflow.allocate(device_pool(), ctx, n_emit * 4);
+        check(cubit_memset_d(ctx, P.d_overflow.p, 0, n_emit * 4), "overflow flags");
+        ProbeRange(P, g.column_ids, g.emit, txn, 0, P.count, cols.data(), valid.data(), out.data(),
+                   static_cast<uint32_t*>(P.d_overflow.p), false);
         return;
     }
-    cubit_ctx* ctx = P.part.ctx;
-    P.h_stage.resize(n_emit);
-    P.h_stage_valid.resize(n_emit);
-    for (size_t e = 0; e < n_emit; ++e) {
-        P.h_stage[e].allocate(pinned_pool(), ctx, P.count * transfer_bytes(P, e) + 8);  // + 8: the 3-byte widen reads 4
-        if (P.nullable[e]) P.h_stage_valid[e].allocate(pinned_pool(), ctx, (words + 2) * 8);
-    }
-    P.h_flags.allocate(pinned_pool(), ctx, g_off.size() * n_emit * 4);
-    P.group_word.clear();
-    void* st = nullptr;
-    uint64_t wb = 0;
-    for (size_t k = 0; k < g_off.size(); ++k) {
+    P.d_block.allocate(device_pool(), ctx, P.blk_off[n_groups]);
+    P.h_block.allocate(pinned_pool(), ctx, P.blk_off[n_groups]);
+    void* st = g.StageStream(ctx);
+    for (size_t k = 0; k < n_groups; ++k) {
         const idx_t off = g_off[k], len = g_len[k];
-        ProbeRange(P, g.column_ids, g.emit, txn, off, len, wb, k);
+        char* blk = static_cast<char*>(P.d_block.p) + P.blk_off[k];
+        for (size_t e = 0; e < n_emit; ++e) {
+            char* region = blk + P.col_rel[k * n_emit + e];
+            const bool rowid = g.column_ids[g.emit[e]] == COLUMN_IDENTIFIER_ROW_ID;
+            cols[e] = rowid ? nullptr : P.width[e] ? device_ptr(P.d_cols[e]) + off : reinterpret_cast<int64_t*>(region);
+            valid[e] = P.nullable[e] ? reinterpret_cast<uint64_t*>(blk + P.val_rel[k * n_emit + e]) : nullptr;
+            out[e] = region;
+        }
+        check(cubit_memset_d(ctx, blk, 0, n_emit * 4), "overflow flags");
+        ProbeRange(P, g.column_ids, g.emit, txn, off, len, cols.data(), valid.data(), out.data(),
+                   reinterpret_cast<uint32_t*>(blk), true);
         void* probed = nullptr;
         check(cubit_copy_event_record(ctx, nullptr, &probed), "probe event");  // on the context stream
         P.probe_ev.push_back(probed);
-        if (!st) st = g.StageStream(ctx);
         check(cubit_copy_stream_wait_event(ctx, st, probed), "staging wait");
-        check(cubit_memcpy_d2h_async(ctx, st, static_cast<uint32_t*>(P.h_flags.p) + k * n_emit,
-                                     static_cast<const uint32_t*>(P.d_overflow.p) + k * n_emit, n_emit * 4),
-              "staged flags");
-        for (size_t e = 0; e < n_emit; ++e) {
-            const uint64_t b = transfer_bytes(P, e);
-            check(cubit_memcpy_d2h_async(ctx, st, static_cast<char*>(P.h_stage[e].p) + off * b,
-                                         transfer_src(P, g.column_ids, g.emit, e) + off * b, len * b),
-                  "staged copy");
-            if (P.nullable[e])
-                check(cubit_memcpy_d2h_async(ctx, st, static_cast<uint64_t*>(P.h_stage_valid[e].p) + wb,
-                                             static_cast<const uint64_t*>(P.d_valid[e].p) + wb, (len + 63) / 64 * 8),
-                      "staged validity copy");
-        }
+        check(cubit_memcpy_d2h_async(ctx, st, static_cast<char*>(P.h_block.p) + P.blk_off[k], blk,
+                                     P.blk_off[k + 1] - P.blk_off[k]),
+              "staged block");
         void* ev = nullptr;
         check(cubit_copy_event_record(ctx, st, &ev), "staged group event");
         P.group_ev.push_back(ev);
-        P.group_word.push_back(wb);
         P.group_off.push_back(off);
-        wb += (len + 63) / 64;
     }
     P.staged = true;
 }
@@ -536,9 +574,14 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         tile_base += (part.n_rows + 131071) / 131072;
         g->parts.push_back(std::move(P));
     }
+    // CUBIT_SCAN_PHASES=1: the host time of init_global's phases on stderr (diagnostic)
+    static const bool phases = std::getenv("CUBIT_SCAN_PHASES") != nullptr;
+    auto t0 = std::chrono::steady_clock::now(), t1 = t0, t2 = t0;
     // every partition's decode in flight before any count is read: one per device at a time
     for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, P->part.n_rows / 8 + 4096);
+    if (phases) t1 = std::chrono::steady_clock::now();
     for (auto& P : g->parts) FinishDecode(*P, nodes, txn);
+    if (phases) t2 = std::chrono::steady_clock::now();
     // windows: consecutive non-empty tiles of one partition, at most window_rows() rows and
     // window_rows() / 4,096 tiles
     const idx_t max_rows = window_rows(), max_tiles = max_rows / 4096;
@@ -558,6 +601,12 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         }
     }
     for (uint32_t p = 0; p < g->parts.size(); ++p) ProbeAndStage(*g, p, txn);
+    if (phases) {
+        const auto t3 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        std::fprintf(stderr, "cubit_scan phases launch_decode_us %.1f finish_decode_us %.1f probe_stage_us %.1f\n",
+                     us(t0, t1), us(t1, t2), us(t2, t3));
+    }
     return g;
 }
 
@@ -592,17 +641,19 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     l.tile_slot = win.first;
     l.pos = 0;
     if (P.staged) {
-        check(cubit_copy_event_sync(P.part.ctx, P.group_ev[win.group]), "staged group");
-        // the group's overflow flags came with it: a column whose compaction overflowed in this
-        // group is copied per window as its 8-byte values instead
-        const uint32_t* ov = static_cast<const uint32_t*>(P.h_flags.p) + (uint64_t)win.group * n_emit;
-        l.valid_bit0 = P.group_off[win.group];
+        const uint32_t k = win.group;
+        check(cubit_copy_event_sync(P.part.ctx, P.group_ev[k]), "staged group");
+        // the group's overflow flags came at the head of its block: a column whose compaction
+        // overflowed in this group is copied per window as its 8-byte values instead
+        const char* blk = static_cast<const char*>(P.h_block.p) + P.blk_off[k];
+        const uint32_t* ov = reinterpret_cast<const uint32_t*>(blk);
+        l.valid_bit0 = P.group_off[k];
         bool copied = false;
         for (size_t e = 0; e < n_emit; ++e) {
-            if (P.nullable[e]) l.src_valid[e] = static_cast<const uint64_t*>(P.h_stage_valid[e].p) + P.group_word[win.group];
+            if (P.nullable[e]) l.src_valid[e] = reinterpret_cast<const uint64_t*>(blk + P.val_rel[k * n_emit + e]);
             l.width[e] = P.width[e];
             if (!(P.width[e] && ov[e])) {
-                l.src[e] = static_cast<const char*>(P.h_stage[e].p) + win.off * transfer_bytes(P, e);
+                l.src[e] = blk + P.col_rel[k * n_emit + e] + (win.off - P.group_off[k]) * transfer_bytes(P, e);
                 continue;
             }
             l.width[e] = 0;

@@ -191,6 +191,9 @@ int cubit_host_free(cubit_ctx *ctx, void *hptr);
 int cubit_memcpy_h2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memcpy_d2h(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_memset_d(cubit_ctx *ctx, void *dst, int value, uint64_t bytes);
+/* Device → device copy enqueued on the context stream (not waited for): the table-function
+ * mirror packs a group's 8-byte row ids into its staging block with it. */
+int cubit_memcpy_d2d(cubit_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int cubit_sync(cubit_ctx *ctx);
 /* Copy streams: a stream of the context's device whose work starts after everything enqueued
  * on the context stream before the call (one pipeline task of the table-function mirror copies

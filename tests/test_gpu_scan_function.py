@@ -329,6 +329,41 @@ def test_window_transfer_compaction_round_trips(ctx):
     t.close()
 
 
+def test_compaction_overflow_falls_back_to_8_byte_values(ctx, monkeypatch):
+    """The device checks the compaction bound as it narrows: with every compacted column's offset
+    moved one above its minimum (CUBIT_SCAN_TEST_SHIFT_OFFSET), the groups (staged) or the
+    partition (per window) holding a minimum are flagged and their windows cross as 8-byte values —
+    the chunks still carry the exact values, row ids included."""
+    from cubit_amd.datagen import validity_from_mask
+
+    n = 2_000_003
+    rng = np.random.default_rng(5)
+    key = rng.integers(0, 100, n).astype(np.int32)
+    price = rng.integers(90_000, 10_000_000, n).astype(np.int64)
+    disc = rng.integers(0, 11, n).astype(np.int64)
+    nul = rng.integers(-5, 5, n).astype(np.int64)
+    ok = rng.random(n) > 0.1
+    t = CubitTable(ctx, n, row_base=3)
+    t.add_column(0, key)
+    t.add_column(1, price)
+    t.add_column(2, disc)
+    t.add_column(3, nul, validity_from_mask(ok))
+    t.build_index(0, L.INDEX_RANGE)
+    monkeypatch.setenv("CUBIT_SCAN_TEST_SHIFT_OFFSET", "1")
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 60)})
+    fn = CubitScanFunction(t, [0, 1, 2, 3, ROW_ID], [4, 1, 2, 3], fs)  # row ids first: ordered() sorts by them
+    chunks = drain(fn, 4, validity=True)
+    fn.close()
+    keep = np.flatnonzero(key < 60)
+    assert np.array_equal(ordered(chunks, 0), keep.astype(np.int64) + 3)
+    assert np.array_equal(ordered(chunks, 1), price[keep])
+    assert np.array_equal(ordered(chunks, 2), disc[keep])
+    ref_vals, ref_valid = O.fetch(O.Column(nul, validity_from_mask(ok)), keep, with_valid=True)
+    assert np.array_equal(ordered(chunks, 7), ref_valid)
+    assert np.array_equal(ordered(chunks, 3), ref_vals)
+    t.close()
+
+
 @pytest.mark.parametrize("tasks", [1, 4])
 def test_nullable_projection_and_unpruned_is_null_filter(ctx, tasks):
     """SELECT b, c, rowid … WHERE a < k AND c IS NULL with c not pruned (DuckDB keeps a filter
