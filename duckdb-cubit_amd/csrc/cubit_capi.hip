@@ -3545,7 +3545,104 @@ int zone_plan(cubit_table* t, const ExprP& e, std::vector<uint32_t>& live, bool*
     return CUBIT_OK;
 }
 
+// [lo, hi) of the values a comparison keeps (NE: the interval it removes); false for NE.
+bool cmp_interval(int cmp, int64_t c, double* lo, double* hi) {
+    const double inf = std::numeric_limits<double>::infinity(), x = (double)c;
+    *lo = -inf;
+    *hi = inf;
+    switch (cmp) {
+    case CUBIT_CMP_EQ: *lo = x; *hi = x + 1; return true;
+    case CUBIT_CMP_NE: *lo = x; *hi = x + 1; return false;
+    case CUBIT_CMP_LT: *hi = x; return true;
+    case CUBIT_CMP_LE: *hi = x + 1; return true;
+    case CUBIT_CMP_GT: *lo = x + 1; return true;
+    default: *lo = x; return true;  // GE
+    }
+}
+
+// Estimated fraction of the partition's rows a filter tree (prefix nodes from i; i ends past the
+// subtree) keeps, on the planner's cost model (interval_selectivity: per-zone min / max, values
+// uniform within a zone, columns independent). An AND folds its constant children on one column
+// into one interval (a pushed TableFilterSet's `a <= v AND v < b`); an OR keeps 1 - Π(1 - s);
+// IS NULL counts the zones that hold a NULL. MVCC deletes only lower the true fraction.
+double tree_selectivity(cubit_table* t, const cubit_filter_node* nodes, uint32_t& i, int* rc) {
+    const cubit_filter_node& f = nodes[i++];
+    double lo, hi;
+    switch (f.kind) {
+    case CUBIT_FILTER_AND: {
+        std::map<int, std::pair<double, double>> iv;
+        double sel = 1.0;
+        for (int k = 0; k < f.n_children && !*rc; ++k) {
+            const cubit_filter_node& c = nodes[i];
+            if (c.kind == CUBIT_FILTER_CONSTANT && c.cmp != CUBIT_CMP_NE) {
+                cmp_interval(c.cmp, c.constant, &lo, &hi);
+                const double inf = std::numeric_limits<double>::infinity();
+                auto& r = iv.emplace(c.column, std::make_pair(-inf, inf)).first->second;
+                r.first = std::max(r.first, lo);
+                r.second = std::min(r.second, hi);
+                ++i;
+            } else {
+                sel *= tree_selectivity(t, nodes, i, rc);
+            }
+        }
+        for (const auto& kv : iv) {
+            if (*rc) break;
+            sel *= kv.second.second <= kv.second.first ? 0.0
+                                                       : interval_selectivity(t, kv.first, kv.second.first, kv.second.second, rc);
+        }
+        return sel;
+    }
+    case CUBIT_FILTER_OR: {
+        double none = 1.0;
+        for (int k = 0; k < f.n_children && !*rc; ++k) none *= 1.0 - tree_selectivity(t, nodes, i, rc);
+        return 1.0 - none;
+    }
+    case CUBIT_FILTER_CONSTANT: {
+        const bool in = cmp_interval(f.cmp, f.constant, &lo, &hi);
+        const double s = interval_selectivity(t, f.column, lo, hi, rc);
+        return in ? s : 1.0 - s;
+    }
+    case CUBIT_FILTER_IS_NULL: {
+        if (!t->cols.at(f.column).validity || t->n_rows == 0) return 0.0;
+        if ((*rc = ensure_zones(t, {}, {f.column}))) return 1.0;
+        const auto& fl = t->col_zones.at(f.column).fl;
+        double rows = 0.0;
+        for (uint32_t z = 0; z < (uint32_t)fl.size(); ++z)
+            if (!(fl[z] & 2)) rows += (double)std::min<uint64_t>(kZoneRows, t->n_rows - (uint64_t)z * kZoneRows);
+        return std::min(1.0, rows / (double)t->n_rows);
+    }
+    default:  // IS NOT NULL
+        return 1.0;
+    }
+}
+
 }  // namespace
+
+extern "C" int cubit_table_estimate_rows(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_nodes,
+                                         uint64_t* rows) {
+    if (!t || !rows || (n_nodes && !nodes)) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    *rows = t->n_rows;
+    if (n_nodes == 0 || t->n_rows == 0) return CUBIT_OK;
+    Planner shape{t, nodes, n_nodes};
+    if (shape.subtree_end(0) != (int)n_nodes) return fail(CUBIT_ERR_INVALID, "malformed filter tree");
+    for (uint32_t k = 0; k < n_nodes; ++k) {
+        const cubit_filter_node& f = nodes[k];
+        if (f.kind < CUBIT_FILTER_CONSTANT || f.kind > CUBIT_FILTER_AND)
+            return fail(CUBIT_ERR_INVALID, "filter node kind %d", f.kind);
+        if (f.kind != CUBIT_FILTER_OR && f.kind != CUBIT_FILTER_AND && !t->cols.count(f.column))
+            return fail(CUBIT_ERR_INVALID, "filter references unregistered column %d", f.column);
+        if (f.kind == CUBIT_FILTER_CONSTANT && (f.cmp < 0 || f.cmp > 5))
+            return fail(CUBIT_ERR_INVALID, "comparison %d", f.cmp);
+    }
+    if (int rc = set_device(t->ctx)) return rc;
+    int rc = CUBIT_OK;
+    uint32_t i = 0;
+    const double s = std::min(1.0, std::max(0.0, tree_selectivity(t, nodes, i, &rc)));
+    if (rc) return rc;
+    *rows = std::min<uint64_t>(t->n_rows, (uint64_t)std::ceil(s * (double)t->n_rows));
+    return CUBIT_OK;
+}
 
 namespace {
 

@@ -138,6 +138,7 @@ GPU_SIGNATURES = {
     "cubit_table_probe": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P]),
     "cubit_table_probe_validity": (C.c_int, [_P, C.c_int, C.POINTER(Txn), _P, _P, _U64, _P, _P]),
     "cubit_table_last_plan": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
+    "cubit_table_estimate_rows": (C.c_int, [_P, C.POINTER(FilterNode), _U32, C.POINTER(_U64)]),
     "cubit_table_last_zones": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
     "cubit_table_use_packed_filter": (C.c_int, [_P, C.c_int]),
     "cubit_table_last_packed": (C.c_int, [_P, C.POINTER(_U32)]),
@@ -187,6 +188,7 @@ SCAN_SIGNATURES = {
     "cubit_scan_function_validity": (C.c_int, [_P, _P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_U64)]),
     "cubit_scan_batch_index": (C.c_int, [_P, _P, C.POINTER(_U64)]),
     "cubit_scan_progress": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "cubit_scan_decodes": (C.c_int, [_P, C.POINTER(_U32)]),
     "cubit_scan_cardinality": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_U64)]),
     "cubit_scan_statistics": (C.c_int, [_P, _U64, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(C.c_int),
                                         C.POINTER(C.c_int)]),

@@ -116,6 +116,13 @@ class CubitScanFunction:
         L.check_scan(self.lib.cubit_scan_batch_index(self.handle, local.handle, C.byref(v)))
         return int(v.value)
 
+    def decodes(self) -> int:
+        """Decode launches init_global made (cubit_scan_decodes): one per partition unless the
+        filter kept more than twice the estimated rows."""
+        v = C.c_uint32()
+        L.check_scan(self.lib.cubit_scan_decodes(self.handle, C.byref(v)))
+        return int(v.value)
+
     def progress(self) -> float:
         v = C.c_double()
         L.check_scan(self.lib.cubit_scan_progress(self.handle, C.byref(v)))

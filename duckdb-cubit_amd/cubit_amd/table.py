@@ -331,6 +331,15 @@ class CubitTable:
             raise L.CubitError(L.ERR_CAPACITY, f"{n} rows qualify, capacity {cap}")
         return out.download(np.int64, n)
 
+    def estimate_rows(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None) -> int:
+        """The planner's estimate of the qualifying rows (cubit_table_estimate_rows: zone
+        statistics, no scan)."""
+        plan = serialize(filter_set, residual)
+        nodes = to_ctypes(plan.nodes)
+        v = C.c_uint64()
+        L.check(self.lib.cubit_table_estimate_rows(self.handle, nodes, len(plan.nodes), C.byref(v)))
+        return int(v.value)
+
     def count(self, filter_set: Optional[TableFilterSet] = None, residual: Optional[Residual] = None,
               txn: Optional[L.Txn] = None, zonemap: bool = True) -> int:
         plan = serialize(filter_set, residual)

@@ -202,6 +202,7 @@ struct PartScan {
     idx_t count = 0;
     idx_t rows_per_tile = 0;
     uint64_t tile_base = 0;   // tiles of the earlier partitions: batch index = tile_base + tile
+    uint32_t decodes = 0;     // decode launches (a second one only when the capacity fell short)
     PooledBuffer d_cnt, d_dir;
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
@@ -272,6 +273,11 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     }
 };
 
+bool phases_enabled() {
+    static const bool on = std::getenv("CUBIT_SCAN_PHASES") != nullptr;
+    return on;
+}
+
 struct CubitScanLocalState : public LocalTableFunctionState {
     int64_t window = -1;           // claimed window, -1 = none yet
     uint32_t tile_slot = 0;        // current tile (index into the window partition's tiles)
@@ -298,7 +304,13 @@ struct CubitScanLocalState : public LocalTableFunctionState {
         streams.emplace_back(ctx, st);
         return st;
     }
+    // CUBIT_SCAN_PHASES=1 (diagnostic): windows claimed and the time spent waiting for their
+    // staged groups / copies, on stderr when the state goes away
+    uint32_t n_windows = 0;
+    double wait_us = 0;
     ~CubitScanLocalState() override {
+        if (phases_enabled() && n_windows)
+            std::fprintf(stderr, "cubit_scan task windows %u wait_us %.1f\n", n_windows, wait_us);
         for (auto& s : streams)
             if (s.second) cubit_copy_stream_destroy(s.first, s.second);
     }
@@ -306,11 +318,12 @@ struct CubitScanLocalState : public LocalTableFunctionState {
 
 int64_t* device_ptr(PooledBuffer& b) { return b.i64(); }
 
-// The decode of one partition into a buffer sized by a guess (an eighth of its rows), launched
-// and not waited for; the count and directory are read after every partition has been launched,
-// so the partitions' devices decode side by side.
+// The decode of one partition into a buffer of `cap` row ids, launched and not waited for; the
+// count and directory are read after every partition has been launched, so the partitions'
+// devices decode side by side.
 void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn, uint64_t cap) {
     cubit_ctx* ctx = P.part.ctx;
+    ++P.decodes;
     if (!P.d_cnt.p) P.d_cnt.allocate(device_pool(), ctx, 16);
     // this scan's tile directory, copied out within the scan call: other pipeline tasks or
     // queries may scan on the same context right after it (cubit_table_scan_tiles)
@@ -326,7 +339,21 @@ void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, cons
     P.tiles.assign(n_tiles, 0);  // the directory's size until FinishDecode reads it
 }
 
-// Count and tile runs of a launched decode; a filter that kept more rows than the guess runs
+// The first decode's capacity: twice the planner's estimate of the qualifying rows
+// (cubit_table_estimate_rows: zone statistics, no scan), at least an eighth of the partition, at
+// most all of it — so a filter keeping half the rows decodes once into a buffer of every row
+// (device memory is pooled across queries, and an unfilled buffer costs no bandwidth). Only an
+// estimate off by more than 2x (correlated columns) takes the second pass.
+uint64_t DecodeCapacity(const PartScan& P, const std::vector<cubit_filter_node>& nodes) {
+    const uint64_t n = P.part.n_rows;
+    uint64_t est = n;
+    if (!nodes.empty())
+        check(cubit_table_estimate_rows(P.part.table, nodes.data(), (uint32_t)nodes.size(), &est),
+              "cubit_table_estimate_rows");
+    return std::min<uint64_t>(n + 1, std::max<uint64_t>(n / 8, 2 * est) + 4096);
+}
+
+// Count and tile runs of a launched decode; a filter that kept more rows than the capacity runs
 // a second time with the exact count.
 void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn) {
     cubit_ctx* ctx = P.part.ctx;
@@ -575,10 +602,10 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         g->parts.push_back(std::move(P));
     }
     // CUBIT_SCAN_PHASES=1: the host time of init_global's phases on stderr (diagnostic)
-    static const bool phases = std::getenv("CUBIT_SCAN_PHASES") != nullptr;
+    const bool phases = phases_enabled();
     auto t0 = std::chrono::steady_clock::now(), t1 = t0, t2 = t0;
     // every partition's decode in flight before any count is read: one per device at a time
-    for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, P->part.n_rows / 8 + 4096);
+    for (auto& P : g->parts) LaunchDecode(*P, nodes, txn, DecodeCapacity(*P, nodes));
     if (phases) t1 = std::chrono::steady_clock::now();
     for (auto& P : g->parts) FinishDecode(*P, nodes, txn);
     if (phases) t2 = std::chrono::steady_clock::now();
@@ -640,9 +667,16 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     l.window = w;
     l.tile_slot = win.first;
     l.pos = 0;
+    ++l.n_windows;
+    const bool timed = phases_enabled();
+    const auto t_claim = timed ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+    auto waited = [&] {
+        if (timed) l.wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_claim).count();
+    };
     if (P.staged) {
         const uint32_t k = win.group;
         check(cubit_copy_event_sync(P.part.ctx, P.group_ev[k]), "staged group");
+        waited();
         // the group's overflow flags came at the head of its block: a column whose compaction
         // overflowed in this group is copied per window as its 8-byte values instead
         const char* blk = static_cast<const char*>(P.h_block.p) + P.blk_off[k];
@@ -705,6 +739,7 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
               "window copy");
     }
     check(cubit_copy_stream_sync(P.part.ctx, stream), "window copies");  // one wait for the window's columns
+    waited();
     return true;
 }
 
@@ -1022,7 +1057,13 @@ int cubit_scan_function_validity(cubit_scan* s, cubit_scan_local* l, int64_t* co
     for (size_t c = 0; c < l->chunk.data.size(); ++c) {
         if (out_validity && out_validity[c]) {
             const ValidityMask& m = l->chunk.validity[c];
-            for (idx_t j = 0; j < STANDARD_VECTOR_SIZE / 64; ++j) out_validity[c][j] = m.all_valid ? ~0ull : m.words[j];
+            // the chunk's words; rows past n read as valid (the words past ⌈n / 64⌉ hold an earlier
+            // chunk's bits)
+            for (idx_t j = 0; j < STANDARD_VECTOR_SIZE / 64; ++j) {
+                uint64_t w = m.all_valid || j * 64 >= n ? ~0ull : m.words[j];
+                if (j * 64 < n && n - j * 64 < 64) w |= ~0ull << (n - j * 64);
+                out_validity[c][j] = w;
+            }
         }
     }
     *out_count = n;
@@ -1036,6 +1077,14 @@ int cubit_scan_function(cubit_scan* s, cubit_scan_local* l, int64_t* const* out_
 int cubit_scan_batch_index(cubit_scan* s, cubit_scan_local* l, uint64_t* out) {
     if (!s || !l || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
     *out = s->fn.get_batch_index(&s->bind, l->lstate.get(), s->gstate.get());
+    return CUBIT_OK;
+}
+
+int cubit_scan_decodes(cubit_scan* s, uint32_t* out) {
+    if (!s || !out) return scan_fail(CUBIT_ERR_INVALID, "null argument");
+    uint32_t n = 0;
+    for (const auto& P : static_cast<CubitScanGlobalState*>(s->gstate.get())->parts) n += P->decodes;
+    *out = n;
     return CUBIT_OK;
 }
 

@@ -433,6 +433,13 @@ int cubit_table_probe(cubit_table *t, int col, const cubit_txn *txn, const int64
  * txn, with its visible SET NULL / value records applied. */
 int cubit_table_probe_validity(cubit_table *t, int col, const cubit_txn *txn, const int64_t *d_rowids,
                                const uint64_t *d_count, uint64_t max_n, int64_t *d_out, uint64_t *d_validity);
+/* Estimated qualifying rows of a filter tree (the nodes cubit_table_scan takes), from the
+ * per-zone min / max statistics the zonemaps use (values uniform within a zone, columns
+ * independent) — the cardinality estimate a caller sizes its row-id buffer by, as DuckDB's
+ * TableScanInitGlobal sizes nothing but the planner estimates a filtered scan's rows from column
+ * statistics (table_scan.cpp:88-106, TableFilter::CheckStatistics). No kernel beyond the zone
+ * statistics (computed once per table version); exactness never depends on it. */
+int cubit_table_estimate_rows(cubit_table *t, const cubit_filter_node *nodes, uint32_t n_nodes, uint64_t *rows);
 /* Bitvectors the last cubit_table_scan read per 64-row word (K) — for roofline bytes. */
 int cubit_table_last_plan(cubit_table *t, uint32_t *n_leaves, uint32_t *n_passes);
 /* Column statistics — DataTable::GetStatistics behind seq_scan's `statistics` callback

@@ -78,6 +78,10 @@ int cubit_scan_function_validity(cubit_scan *scan, cubit_scan_local *local, int6
                                  uint64_t *const *out_validity, uint64_t *out_count);
 int cubit_scan_batch_index(cubit_scan *scan, cubit_scan_local *local, uint64_t *out);
 int cubit_scan_progress(cubit_scan *scan, double *out);
+/* Decode launches init_global made, summed over the partitions: one per partition unless a
+ * filter kept more than twice the rows cubit_table_estimate_rows predicted (then one more with
+ * the exact count). Diagnostic: the reference's scan has no second pass to count. */
+int cubit_scan_decodes(cubit_scan *scan, uint32_t *out);
 int cubit_scan_cardinality(cubit_table *table, uint64_t *estimated, uint64_t *max);
 int cubit_scan_statistics(cubit_table *table, uint64_t column_id, int64_t *min, int64_t *max, int *has_null,
                           int *has_no_null);

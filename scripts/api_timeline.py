@@ -7,9 +7,9 @@ from pathlib import Path
 
 d = Path(sys.argv[1])
 run = int(sys.argv[2]) if len(sys.argv) > 2 else -1
-k = list(csv.DictReader(open(next(d.glob("*kernel_trace.csv")))))
-m = list(csv.DictReader(open(next(d.glob("*memory_copy_trace.csv")))))
-a = list(csv.DictReader(open(next(d.glob("*hip_api_trace.csv")))))
+k = list(csv.DictReader(open(next(d.rglob("*kernel_trace.csv")))))
+m = list(csv.DictReader(open(next(d.rglob("*memory_copy_trace.csv")))))
+a = list(csv.DictReader(open(next(d.rglob("*hip_api_trace.csv")))))
 dec = sorted(int(r["Start_Timestamp"]) for r in k if "eval_decode" in r["Kernel_Name"])
 s = dec[run]
 e = dec[run + 1] if run != -1 and run + 1 < len(dec) else s + 4_000_000

@@ -15,6 +15,13 @@
 #   dist1                      the bench as one torchrun rank over RCCL (the N > 1 code path)
 #   dist2                      two gloo ranks sharing the GPU (strong scaling rehearsal)
 #   distg:<n>                  n gloo ranks sharing the GPU (n <= 4 here: the N = 8 case is the driver's)
+#   self:<n>[:<args>]          plain `python bench.py --gpus n` with no launcher (bench.py starts its own
+#                              n ranks), gloo, every rank on the one GPU (CUBIT_BENCH_SHARE_GPU=1)
+#   apitrace[:<sf>,<tasks>]    HIP API + kernel + copy trace of examples/q6_scan (default 100 8), then
+#                              scripts/api_timeline.py over runs 0..3 into $OUT/apitrace_runs.txt
+#   merge                      scripts/merge_timing.py (the merge at 612 M rows, phases on stderr)
+#   pipeline[:<sf>,<tasks>,...]  examples/q6_scan (default 100 8) with CUBIT_SCAN_PHASES=1 (init_global's
+#                              phases and each task's window waits on stderr), Q6_REPS=5
 #   run:<cmd,args>             any other command (e.g. run:./scripts/smallbench,10)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -70,6 +77,22 @@ for step in "$@"; do
       CUBIT_BENCH_SHARE_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$rest" \
           --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus "$rest" --steps 10 --warmup 3 --dist-backend gloo \
           --no-cpu-baseline > "$OUT/$n.bench_dist${rest}_gloo.json" 2> "$log" ;;
+    self)
+      nn=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      [ "$nn" -ge 2 ] && [ "$nn" -le 4 ] || { echo "self: 2 to 4 ranks" >&2; exit 2; }
+      CUBIT_BENCH_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus "$nn" --steps 10 --warmup 3 \
+          --dist-backend gloo --no-cpu-baseline ${a//,/ } > "$OUT/$n.bench_self${nn}_gloo.json" 2> "$log" ;;
+    apitrace)
+      a=${rest:-100,8}
+      timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
+          -d "$OUT/apitrace" -o q6 -- duckdb-cubit_amd/lib/q6_scan ${a//,/ } > "$log" 2>&1 &&
+      for r in 0 1 2 3; do echo "== run $r"; python scripts/api_timeline.py "$OUT/apitrace" $r; done \
+          > "$OUT/apitrace_runs.txt" 2>&1 ;;
+    pipeline)
+      a=${rest:-100,8}
+      CUBIT_SCAN_PHASES=1 Q6_REPS=5 timeout -k 10 300 duckdb-cubit_amd/lib/q6_scan ${a//,/ } > "$log" 2>&1 ;;
+    merge)
+      timeout -k 10 600 python -u scripts/merge_timing.py > "$log" 2>&1 ;;
     run)
       timeout -k 10 600 ${rest//,/ } > "$log" 2>&1 ;;
     *)

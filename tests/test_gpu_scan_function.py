@@ -114,6 +114,76 @@ def test_q6_through_table_function(ctx, golden, tasks):
         assert np.all(cols[0] // 131072 == b)
 
 
+@pytest.mark.parametrize("tasks", [1, 4])
+def test_non_selective_filter_decodes_once(ctx, tasks):
+    """init_global sizes its row-id buffer from the planner's estimate
+    (cubit_table_estimate_rows), so a filter keeping half the rows decodes once instead of
+    overflowing the old n/8 guess and decoding again; rows and probed values equal the oracle's.
+    A filter the estimate gets wrong (three copies of one column: independence predicts 1/8,
+    the filter keeps 1/2) still returns the oracle's rows, by the second pass."""
+    rng = np.random.default_rng(17)
+    n = 1_000_003
+    a = rng.integers(0, 1000, n).astype(np.int64)
+    b = rng.integers(-50, 50, n).astype(np.int32)
+    t = CubitTable(ctx, n, row_base=11)
+    t.add_column(0, a)
+    t.add_column(1, b)
+    t.add_column(2, a.copy())
+    t.build_index(0, L.INDEX_RANGE, [250, 500, 750])
+    fs = F.TableFilterSet({0: F.ConstantFilter("<", 500)})
+    est = t.estimate_rows(fs)
+    assert abs(est - n // 2) < n // 20
+    fn = CubitScanFunction(t, [0, 1, ROW_ID], [2, 1], fs)
+    chunks = drain(fn, tasks)
+    assert fn.decodes() == 1
+    ref = O.table_scan([O.Column(a), O.Column(b)], F.serialize(fs), n, row_base=11)
+    assert len(ref) > n // 3
+    assert np.array_equal(ordered(chunks, 0), ref)
+    assert np.array_equal(ordered(chunks, 1), b[ref - 11])
+    # correlated columns: three copies of a, each < 500, keep 1/2 while independence predicts
+    # 1/8 — the capacity (max(n/8, 2 · n/8)) falls short and the second pass returns the rows
+    t.add_column(3, a.copy())
+    fs3 = F.TableFilterSet({0: F.ConstantFilter("<", 500), 2: F.ConstantFilter("<", 500),
+                            3: F.ConstantFilter("<", 500)})
+    fn3 = CubitScanFunction(t, [0, 2, 3, ROW_ID], [3], fs3)
+    rows3 = ordered(drain(fn3, tasks), 0)
+    assert fn3.decodes() == 2
+    ref3 = np.flatnonzero(a < 500) + 11
+    assert np.array_equal(rows3, ref3)
+    fn.close()
+    fn3.close()
+    t.close()
+
+
+def test_estimate_rows_shapes(ctx):
+    """cubit_table_estimate_rows over the filter shapes the scan takes: constants on one column
+    folded into one interval, OR, IS NULL / IS NOT NULL, an empty interval, no filter."""
+    from cubit_amd.datagen import validity_from_mask
+
+    n = 262_144 * 4
+    v = np.arange(n, dtype=np.int64) % 1000
+    ok = np.ones(n, dtype=bool)
+    ok[: 131_072] = np.arange(131_072) % 2 == 0  # NULLs in the first zone only
+    t = CubitTable(ctx, n)
+    t.add_column(0, v, validity_from_mask(ok))
+    near = lambda got, want: abs(got - want) <= 0.02 * n  # noqa: E731
+    assert t.estimate_rows(None) == n
+    assert near(t.estimate_rows(F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 100),
+                                                                                 F.ConstantFilter("<", 300)])})),
+                n * 0.2)
+    assert t.estimate_rows(F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">=", 300),
+                                                                          F.ConstantFilter("<", 100)])})) == 0
+    assert near(t.estimate_rows(F.TableFilterSet({0: F.ConjunctionOrFilter([F.ConstantFilter("<", 100),
+                                                                             F.ConstantFilter(">=", 900)])})),
+                n * 0.19)
+    assert near(t.estimate_rows(F.TableFilterSet({0: F.ConstantFilter("!=", 5)})), n)
+    assert t.estimate_rows(F.TableFilterSet({0: F.IsNullFilter()})) == 131_072  # the zones holding a NULL
+    assert t.estimate_rows(F.TableFilterSet({0: F.IsNotNullFilter()})) == n
+    with pytest.raises(L.CubitError):
+        t.estimate_rows(F.TableFilterSet({5: F.ConstantFilter("<", 1)}))
+    t.close()
+
+
 def test_no_filter_full_scan_and_empty_result(ctx):
     n = 300_000
     a = np.arange(n, dtype=np.int64) % 1000
