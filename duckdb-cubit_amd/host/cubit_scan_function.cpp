@@ -151,8 +151,9 @@ struct PooledBuffer {
 // of every emitted column, all on the device — and copies only the count and the tile
 // directory to the host. The ids and values then reach the host per *window* (consecutive
 // non-empty tiles of about window_rows() rows): the local state that claims a window copies its
-// range of every emitted column into its own page-locked buffer and hands the window's tiles
-// out as DataChunks. The reference hands out one row group per NextParallelScan and produces
+// range of every emitted column into its own page-locked buffer (or reads it where init_global
+// staged it) and hands the window's rows out as full DataChunks of 2,048, one batch index per
+// window. The reference hands out one row group per NextParallelScan and produces
 // its chunks on demand (table_scan.cpp:119-156); a window is the unit a GPU→host copy is worth.
 // Window size: at most window_rows() rows and window_rows() / 4,096 tiles (2^18 rows and 64
 // tiles by default; CUBIT_SCAN_WINDOW_ROWS sets the row bound, a power of two ≥ 2^14).
@@ -280,8 +281,7 @@ bool phases_enabled() {
 
 struct CubitScanLocalState : public LocalTableFunctionState {
     int64_t window = -1;           // claimed window, -1 = none yet
-    uint32_t tile_slot = 0;        // current tile (index into the window partition's tiles)
-    idx_t pos = 0;                 // next row of the tile's run to emit
+    idx_t pos = 0;                 // next row of the window to emit
     std::vector<PooledBuffer> host;  // per emitted position: the window's rows (page-locked)
     std::vector<PooledBuffer> host_valid;  // per nullable position: the window's validity words
     // per emitted position: the window's first row on the host (its own copy, or the partition's
@@ -665,8 +665,10 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
         l.src_valid.resize(n_emit);
     }
     l.window = w;
-    l.tile_slot = win.first;
     l.pos = 0;
+    // progress counts rows when their window is claimed, as TableScanProgress counts the row
+    // groups the parallel cursor has handed out (table_scan.cpp:158-177); one atomic per window
+    g.emitted.fetch_add(win.len, std::memory_order_relaxed);
     ++l.n_windows;
     const bool timed = phases_enabled();
     const auto t_claim = timed ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
@@ -819,55 +821,52 @@ void CubitScanFunc(TableFunctionInput& data, DataChunk& output) {
         if ((size_t)l.window >= g.windows.size()) return;
         const Window& win = g.windows[l.window];
         const PartScan& P = *g.parts[win.part];
-        if (l.tile_slot >= win.last) {
+        if (l.pos >= win.len) {
             if (!NextWindow(g, l)) return;
             continue;
         }
-        const idx_t len = P.tile_len[l.tile_slot];
-        if (l.pos < len) {
-            const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, len - l.pos);
-            const idx_t at = P.tile_off[l.tile_slot] - win.off + l.pos;
-            for (size_t e = 0; e < g.emit.size(); ++e) {
-                if (P.nullable[e]) FillValidity(l.src_valid[e], win.off + at - l.valid_bit0, n, output.validity[e]);
-                int64_t* dst = output.Column(e);
-                const int64_t off = P.offset[e];
-                switch (l.width[e]) {  // widen the compacted transfer
-                case 1:
-                    widen(reinterpret_cast<const uint8_t*>(l.src[e]) + at, off, n, dst);
-                    break;
-                case 2:
-                    widen(reinterpret_cast<const uint16_t*>(l.src[e]) + at, off, n, dst);
-                    break;
-                case 3:
-                    widen24(reinterpret_cast<const uint8_t*>(l.src[e]) + 3 * at, off, n, dst);
-                    break;
-                case 4:
-                    widen(reinterpret_cast<const uint32_t*>(l.src[e]) + at, off, n, dst);
-                    break;
-                default:
-                    std::memcpy(dst, reinterpret_cast<const int64_t*>(l.src[e]) + at, n * sizeof(int64_t));
-                }
+        // a chunk of up to 2,048 of the window's rows: they are contiguous in the partition's
+        // ordered output whatever tiles they come from, and one batch index covers the window
+        const idx_t n = std::min<idx_t>(STANDARD_VECTOR_SIZE, win.len - l.pos);
+        const idx_t at = l.pos;
+        for (size_t e = 0; e < g.emit.size(); ++e) {
+            if (P.nullable[e]) FillValidity(l.src_valid[e], win.off + at - l.valid_bit0, n, output.validity[e]);
+            int64_t* dst = output.Column(e);
+            const int64_t off = P.offset[e];
+            switch (l.width[e]) {  // widen the compacted transfer
+            case 1:
+                widen(reinterpret_cast<const uint8_t*>(l.src[e]) + at, off, n, dst);
+                break;
+            case 2:
+                widen(reinterpret_cast<const uint16_t*>(l.src[e]) + at, off, n, dst);
+                break;
+            case 3:
+                widen24(reinterpret_cast<const uint8_t*>(l.src[e]) + 3 * at, off, n, dst);
+                break;
+            case 4:
+                widen(reinterpret_cast<const uint32_t*>(l.src[e]) + at, off, n, dst);
+                break;
+            default:
+                std::memcpy(dst, reinterpret_cast<const int64_t*>(l.src[e]) + at, n * sizeof(int64_t));
             }
-            l.pos += n;
-            output.SetCardinality(n);
-            g.emitted.fetch_add(n);
-            return;
         }
-        ++l.tile_slot;
-        l.pos = 0;
+        l.pos += n;
+        output.SetCardinality(n);
+        return;
     }
 }
 
-// batch index = the partition's tile base + tile index: a local state's tiles ascend (windows
-// are claimed in order — partition by partition — and hold consecutive tiles), as
-// PipelineExecutor::NextBatch requires (pipeline_executor.cpp:132)
+// batch index = the partition's tile base + the window's first tile: one batch per window (a
+// morsel, as seq_scan's batch is one row group, table_scan.cpp:179-189), so a chunk may hold rows
+// of several tiles; a local state's batch indexes ascend (windows are claimed in order —
+// partition by partition — and hold consecutive tiles), as PipelineExecutor::NextBatch requires
+// (pipeline_executor.cpp:132)
 idx_t CubitScanGetBatchIndex(const FunctionData*, LocalTableFunctionState* lstate, GlobalTableFunctionState* gstate) {
     auto& g = static_cast<CubitScanGlobalState&>(*gstate);
     auto& l = static_cast<CubitScanLocalState&>(*lstate);
     if (l.window < 0 || (size_t)l.window >= g.windows.size()) return 0;
     const PartScan& P = *g.parts[g.windows[l.window].part];
-    if (l.tile_slot >= P.tiles.size()) return 0;
-    return P.tile_base + P.tiles[l.tile_slot];
+    return P.tile_base + P.tiles[g.windows[l.window].first];
 }
 double CubitScanProgress(const FunctionData*, const GlobalTableFunctionState* gstate) {
     auto& g = static_cast<const CubitScanGlobalState&>(*gstate);

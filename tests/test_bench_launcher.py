@@ -73,3 +73,25 @@ def test_bench_refuses_a_launcher_world_size_other_than_gpus():
     assert r.returncode != 0
     assert "WORLD_SIZE is 1" in r.stderr
     assert r.stdout == ""
+
+
+def test_cpu_baseline_times_the_whole_partition(li001, monkeypatch):
+    """bench.cpu_baseline over a whole partition: the box's CPU share of threads,
+    the 1-thread point, and the count / Σ row id checked against the scan it is compared with."""
+    from cubit_amd import filters as F
+    from oracle import oracle as O
+
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    cols = [O.Column(li001.l_shipdate), O.Column(li001.l_discount), O.Column(li001.l_quantity)]
+    plan = F.serialize(F.q6_filter_set())
+    ref = O.table_scan(cols, plan, li001.n_rows)
+    k = 20_000
+    sample = (cols, plan, k, None)
+    full = (cols, plan, li001.n_rows, None)
+    out = bench.cpu_baseline(sample, full, gpu=(len(ref), int(ref.sum())), min_seconds=0.3)
+    assert out["equals_gpu_count_and_rowid_sum"] is True
+    assert out["cores"] == min(3, out["host_cpus"]["affinity"])
+    assert str(li001.n_rows) in out["sample"] and out["sample"].startswith("the whole partition")
+    assert out["value"] > 0 and out["single_thread_value"] > 0
+    bad = bench.cpu_baseline(sample, full, gpu=(len(ref) + 1, int(ref.sum())), min_seconds=0.1)
+    assert bad["equals_gpu_count_and_rowid_sum"] is False

@@ -163,11 +163,17 @@ def test_table_function_over_partitions(golden, world, tasks):
     for seen in per_task.values():
         idx = [b for b, _ in seen]
         assert idx == sorted(idx)
-        for b, cols in seen:
-            p = int(np.searchsorted(tile_base, b, side="right")) - 1
-            li = parts[p][1]
-            assert np.all((cols[0] - li.row_base) // 131072 + tile_base[p] == b)
         chunks += seen
+    # batch index = the first tile (over the partitions' tiles) of the chunk's window: a chunk
+    # lies in one partition, in tiles from its batch index up to the next batch index present
+    bases = np.array([li.row_base for _, li in parts])
+    bs = sorted({b for b, _ in chunks})
+    nxt = {b: (bs[i + 1] if i + 1 < len(bs) else 1 << 62) for i, b in enumerate(bs)}
+    for b, cols in chunks:
+        p = np.searchsorted(bases, cols[0], side="right") - 1
+        assert np.all(p == p[0])
+        tiles = (cols[0] - bases[p[0]]) // 131072 + tile_base[p[0]]
+        assert np.all(tiles >= b) and np.all(tiles < nxt[b])
     chunks.sort(key=lambda bc: (bc[0], bc[1][0][0]))
     rows = np.concatenate([c[0] for _, c in chunks])
     ref = O.table_scan([O.Column(whole.l_shipdate), O.Column(whole.l_discount), O.Column(whole.l_quantity)],
@@ -257,10 +263,14 @@ def test_table_function_over_ragged_partitions(tasks):
         want_rows.append(keep + base)
         want_v.append(np.where(valid[keep], v[keep], 0))
         want_ok.append(valid[keep])
+        bs = sorted({bi for bi, _, _ in out})
         for bi, vals, _ in out:
             sel = (vals[0] >= base) & (vals[0] < base + n)
-            if sel.any():
-                assert np.all((vals[0][sel] - base) // 131072 + tile_base == bi)
+            if sel.any():  # a chunk lies in one partition, in its window's tiles
+                assert sel.all()
+                tiles = (vals[0] - base) // 131072 + tile_base
+                later = [x for x in bs if x > bi]
+                assert np.all(tiles >= bi) and np.all(tiles < (later[0] if later else 1 << 62))
         tile_base += (n + 131071) // 131072
     assert np.array_equal(rows, np.concatenate(want_rows))
     assert np.array_equal(got_ok, np.concatenate(want_ok)) and np.array_equal(got_v, np.concatenate(want_v))

@@ -84,6 +84,20 @@ def drain(fn, n_tasks, validity=False):
     return out
 
 
+def assert_window_batches(chunks, tile_of):
+    """Batch index = the first tile of the chunk's window (one batch per window, a morsel): every
+    chunk's rows lie in tiles >= its batch index and below the next batch index present, and
+    chunks are full — at most one chunk per batch holds fewer than 2,048 rows."""
+    bs = sorted({b for b, _ in chunks})
+    nxt = {b: (bs[i + 1] if i + 1 < len(bs) else np.iinfo(np.int64).max) for i, b in enumerate(bs)}
+    short = {}
+    for b, cols in chunks:
+        t = tile_of(cols[0])
+        assert np.all(t >= b) and np.all(t < nxt[b]), b
+        short[b] = short.get(b, 0) + (len(cols[0]) < 2048)
+    assert max(short.values(), default=0) <= 1
+
+
 def ordered(chunks, col):
     chunks = sorted(chunks, key=lambda bc: (bc[0], bc[1][0][0] if len(bc[1][0]) else 0))
     return np.concatenate([c[col] for _, c in chunks]) if chunks else np.empty(0, np.int64)
@@ -109,9 +123,7 @@ def test_q6_through_table_function(ctx, golden, tasks):
     rev = int((ordered(chunks, 1).astype(object) * ordered(chunks, 2).astype(object)).sum())
     assert rev == revenue_from_answer(golden["tpch"]["q6_revenue"]["0.1"]["revenue"])
     assert fn.progress() == pytest.approx(100.0)
-    # batch indexes are tiles: rows of batch b lie in tile b
-    for b, cols in chunks:
-        assert np.all(cols[0] // 131072 == b)
+    assert_window_batches(chunks, lambda ids: ids // 131072)
 
 
 @pytest.mark.parametrize("tasks", [1, 4])
@@ -265,9 +277,9 @@ def test_cardinality_and_statistics_callbacks(ctx):
 def test_windows_stream_in_batch_order_per_task(ctx):
     """A result of several copy windows (262,144 rows each) drained by 4 tasks: every task's
     batch indexes never decrease (PipelineExecutor::NextBatch refuses a lower one,
-    pipeline_executor.cpp:132-136), every chunk's rows lie in its batch's tile, and the rows
-    equal numpy's predicate. The filter keeps half the rows, more than init_global's first
-    guess (an eighth), so the decode runs a second time with the exact count."""
+    pipeline_executor.cpp:132-136), every chunk's rows lie in its batch's window, and the rows
+    equal numpy's predicate. The filter keeps half the rows: init_global's estimate sizes the
+    decode for them (one pass)."""
     from cubit_amd import scan_function as S
 
     n = 3_000_017
@@ -303,9 +315,9 @@ def test_windows_stream_in_batch_order_per_task(ctx):
     for k, seen in per_task.items():
         idx = [bi for bi, _ in seen]
         assert idx == sorted(idx), k
-        for bi, cols in seen:
-            assert np.all((cols[0] - 1_000) // 131072 == bi)
         chunks += seen
+    assert_window_batches(chunks, lambda ids: (ids - 1_000) // 131072)
+    assert fn.decodes() == 1
     want = np.flatnonzero(a < 500)
     assert np.array_equal(ordered(chunks, 0), want + 1_000)
     assert np.array_equal(ordered(chunks, 1), b[want])
