@@ -180,8 +180,9 @@ struct Window {
 // pipeline task that claims a window waits for its group's event and reads the rows in place. One stream of multi-megabyte
 // copies runs the link at its own rate (56.6 GB/s for one 64 MiB copy on the MI355X box); the
 // tasks' concurrent per-window copies (0.5–1 MB each on up to 16 streams) reached ~20 GB/s
-// (profiles/r05k_*). Partitions whose staged bytes exceed CUBIT_SCAN_STAGE_MB (default 1024) are
-// copied per window by the task that claims it, as before.
+// (profiles/r05k_*). CUBIT_SCAN_STAGE_MB (default 1024) bounds the bytes one scan stages over all
+// of its partitions: a partition past the budget, or whose blocks cannot be allocated, is copied
+// per window by the task that claims it.
 uint64_t stage_groups() {  // 8; CUBIT_SCAN_STAGE_GROUPS overrides (diagnostic)
     static const uint64_t n = [] {
         const char* e = std::getenv("CUBIT_SCAN_STAGE_GROUPS");
@@ -191,9 +192,10 @@ uint64_t stage_groups() {  // 8; CUBIT_SCAN_STAGE_GROUPS overrides (diagnostic)
     return n;
 }
 
-uint64_t stage_cap_bytes() {  // read per init_global
+uint64_t stage_cap_bytes() {  // read per init_global; MiB, fractions allowed (tests)
     const char* e = std::getenv("CUBIT_SCAN_STAGE_MB");
-    return (e && *e ? std::strtoull(e, nullptr, 10) : 1024ull) << 20;
+    const double mb = e && *e ? std::strtod(e, nullptr) : 1024.0;
+    return mb > 0 ? (uint64_t)(mb * 1048576.0) : 0;
 }
 
 // The device side of one partition's scan: its ordered row ids, the probed columns and the
@@ -247,6 +249,7 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     idx_t count = 0;          // all partitions
     std::vector<Window> windows;  // partition by partition, each in tile order
     idx_t max_window = 0;
+    uint64_t stage_left = 0;  // staging bytes the partitions not yet staged may still take
     std::atomic<uint32_t> next{0};
     std::atomic<idx_t> emitted{0};
     // one staging copy stream per context, shared by the partitions on that device (their copies
@@ -524,7 +527,21 @@ void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
     P.d_valid.resize(n_emit);
     P.d_narrow.resize(n_emit);
     if (P.count == 0 || n_emit == 0) return;
-    const bool staged = P.blk_off[n_groups] <= stage_cap_bytes();
+    // staged when the partition's blocks fit what is left of the scan's staging budget (one
+    // budget over all partitions: N partitions must not pin N budgets) and both the device and the
+    // page-locked block can be had; else each task copies the windows it claims
+    bool staged = P.blk_off[n_groups] <= g.stage_left;
+    if (staged) {
+        try {
+            P.d_block.allocate(device_pool(), ctx, P.blk_off[n_groups]);
+            P.h_block.allocate(pinned_pool(), ctx, P.blk_off[n_groups]);
+            g.stage_left -= P.blk_off[n_groups];
+        } catch (const ScanError&) {
+            P.d_block.reset();
+            P.h_block.reset();
+            staged = false;
+        }
+    }
     // partition-wide values of every probed column that the staging does not take whole: the
     // narrowed ones (their 8-byte fallback) and, not staged, all
     for (size_t e = 0; e < n_emit; ++e)
@@ -551,8 +568,6 @@ void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
                    static_cast<uint32_t*>(P.d_overflow.p), false);
         return;
     }
-    P.d_block.allocate(device_pool(), ctx, P.blk_off[n_groups]);
-    P.h_block.allocate(pinned_pool(), ctx, P.blk_off[n_groups]);
     void* st = g.StageStream(ctx);
     for (size_t k = 0; k < n_groups; ++k) {
         const idx_t off = g_off[k], len = g_len[k];
@@ -627,6 +642,7 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
             i = w.last;
         }
     }
+    g->stage_left = stage_cap_bytes();
     for (uint32_t p = 0; p < g->parts.size(); ++p) ProbeAndStage(*g, p, txn);
     if (phases) {
         const auto t3 = std::chrono::steady_clock::now();

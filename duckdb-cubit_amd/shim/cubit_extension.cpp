@@ -66,7 +66,9 @@
 #include "cubit_gpu.h"
 #include "cubit_scan.h"
 
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 
 namespace duckdb {
 
@@ -95,16 +97,53 @@ struct CubitIndexSpec {
 //  * the snapshot: `sync_start` is the start time of the transaction the last sync read the
 //    table in (one transaction for every column). A scan may use the partition only if its own
 //    snapshot includes that one (start_time >= sync_start).
-struct CubitAttached {
-    // one context per device in use; the table as row-range partitions in row order, partition i
-    // on ctxs[i] (one partition per device: PRAGMA cubit_attach's `devices`), scanned through
-    // one cursor (cubit_scan_init_global_multi)
+//
+// Lifetime: the contexts and the partitions are shared objects (CubitContexts,
+// CubitPartitionSet). A scan holds its partition set from init_global until its global state
+// goes away, and the bind-time callbacks hold it for their call, so an attach or a rebuilding sync
+// that swaps a new set in under `lock` never frees a table or a context that a running scan still
+// reads: the last holder does. Lock order: `lock`, then a set's `rw`.
+
+// One context per device in use, destroyed with the last partition set built on them.
+struct CubitContexts {
     vector<cubit_ctx *> ctxs;
+    ~CubitContexts() {
+        if (!ctxs.empty()) {
+            cubit_scan_release_cached(nullptr, nullptr);  // pooled buffers of the contexts going away
+        }
+        for (auto c : ctxs) {
+            cubit_ctx_destroy(c);
+        }
+    }
+};
+
+// The table as row-range partitions in row order, partition i on contexts->ctxs[i] (one partition
+// per device: PRAGMA cubit_attach's `devices`), scanned through one cursor
+// (cubit_scan_init_global_multi).
+struct CubitPartitionSet {
+    std::shared_ptr<CubitContexts> contexts;
     vector<cubit_table *> parts;
-    vector<uint64_t> part_base;     // first row id of each partition
-    int devices = 1;                // devices the attach asked for (0 = every visible one)
-    bool Attached() const {
-        return !parts.empty();
+    vector<uint64_t> part_base;  // first row id of each partition
+    // a scan's init_global — the only part of a scan that reads the tables; its chunks come from
+    // its own buffers — holds it shared; a sync's in-place appends and deletes hold it exclusive
+    std::shared_mutex rw;
+    ~CubitPartitionSet() {
+        for (auto t : parts) {
+            cubit_table_destroy(t);
+        }
+    }
+};
+
+struct CubitAttached {
+    std::shared_ptr<CubitContexts> contexts;   // the contexts the next set is built on
+    std::shared_ptr<CubitPartitionSet> set;    // the current partitions (under `lock`)
+    int devices = 1;                           // devices the attach asked for (0 = every visible one)
+    bool Attached() const {                    // under `lock`
+        return set && !set->parts.empty();
+    }
+    std::shared_ptr<CubitPartitionSet> Current() {
+        lock_guard<mutex> g(lock);
+        return set;
     }
     unordered_map<column_t, PhysicalType> columns;
     vector<column_t> column_order;  // attached storage columns, in upload order
@@ -118,6 +157,7 @@ struct CubitAttached {
     // attach for every still-active transaction that had already written (CubitRegistry::Dirty).
     unordered_map<transaction_t, bool> writers;
     mutex lock;  // scans, writers and syncs of different connections meet here
+    mutex sync_lock;  // one attach or sync of the table at a time
 };
 
 class CubitRegistry {
@@ -142,9 +182,13 @@ public:
     // Transactions that deleted or updated rows, per database, whether or not a table was
     // attached then: an attach must not miss a writer that started before it and commits after
     // its snapshot. Entries of finished transactions (id < LowestActiveId) are dropped.
-    static void NoteDirty(const AttachedDatabase &db, transaction_t id, bool values) {
+    static void NoteDirty(const AttachedDatabase &db, transaction_t id, bool values, transaction_t lowest_active) {
         lock_guard<mutex> g(lock);
-        auto &w = dirty()[&db][id];
+        auto &m = dirty()[&db];
+        for (auto it = m.begin(); it != m.end();) {  // finished writers: bounded however rare syncs are
+            it = it->first < lowest_active ? m.erase(it) : std::next(it);
+        }
+        auto &w = m[id];
         w = w || values;
     }
     static unordered_map<transaction_t, bool> Dirty(const AttachedDatabase &db, transaction_t lowest_active) {
@@ -378,6 +422,7 @@ struct CubitGlobalState : public GlobalTableFunctionState {
         return seq_global ? seq_global->MaxThreads() : max_threads;
     }
     cubit_scan *scan = nullptr;
+    std::shared_ptr<CubitPartitionSet> set;  // released after the scan (member order)
     idx_t max_threads = 1;
     vector<LogicalType> out_types;  // output chunk column types, in output order
     // set when the scan runs as seq_scan (the partition was not current at init_global)
@@ -399,23 +444,35 @@ struct CubitLocalState : public LocalTableFunctionState {
 };
 
 static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached);
+static bool PartitionCurrentLocked(ClientContext &context, DuckTableEntry &table, CubitAttached &attached);
 
-// the scan's columns are all on the GPU (a re-attach may have changed the column set)
-static bool ColumnsAttached(CubitAttached &attached, const vector<column_t> &column_ids) {
+// The partition set a scan may run on, taken with the freshness checks under one hold of the
+// attached table's lock (a sync cannot land between the check and the set), and with the set's
+// `rw` held shared until the scan's device work is launched: nullptr when the scan must be
+// seq_scan's (stale, or a scanned column not on the GPU).
+static std::shared_ptr<CubitPartitionSet> AcquireCurrent(ClientContext &context, DuckTableEntry &table,
+                                                         CubitAttached &attached, const vector<column_t> &column_ids,
+                                                         std::shared_lock<std::shared_mutex> &reading) {
     lock_guard<mutex> g(attached.lock);
-    for (auto c : column_ids) {
+    if (!PartitionCurrentLocked(context, table, attached)) {
+        return nullptr;
+    }
+    for (auto c : column_ids) {  // a re-attach may have changed the column set
         if (c != COLUMN_IDENTIFIER_ROW_ID && !attached.columns.count(c)) {
-            return false;
+            return nullptr;
         }
     }
-    return true;
+    reading = std::shared_lock<std::shared_mutex>(attached.set->rw);
+    return attached.set;
 }
 
 static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &context, TableFunctionInitInput &input) {
     auto &bind = input.bind_data->Cast<CubitBindData>();
     // the plan may be older than the partition's state (a prepared statement, a write committed
     // since planning): check again in the executing transaction, and run as seq_scan if stale
-    if (!CubitPartitionIsCurrent(context, bind.table, bind.attached) || !ColumnsAttached(bind.attached, input.column_ids)) {
+    std::shared_lock<std::shared_mutex> reading;
+    auto set = AcquireCurrent(context, bind.table, bind.attached, input.column_ids, reading);
+    if (!set) {
         auto g = make_uniq<CubitGlobalState>();
         TableFunctionInitInput seq_input(bind.seq_bind.get(), input.column_ids, input.projection_ids, input.filters);
         g->seq_global = bind.seq.init_global(context, seq_input);
@@ -437,16 +494,14 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
     }
     vector<uint64_t> proj(input.projection_ids.begin(), input.projection_ids.end());
     auto g = make_uniq<CubitGlobalState>();
-    vector<cubit_table *> parts;
-    {
-        lock_guard<mutex> lk(bind.attached.lock);
-        parts = bind.attached.parts;
-    }
+    g->set = set;
+    auto &parts = set->parts;
     if (cubit_scan_init_global_multi(parts.data(), (uint32_t)parts.size(), cols.data(), (uint32_t)cols.size(),
                                      proj.data(), (uint32_t)proj.size(), nodes.data(), (uint32_t)nodes.size(), &txn,
                                      &g->scan) != CUBIT_OK) {
         throw InvalidInputException("cubit_scan: %s", cubit_scan_last_error());
     }
+    reading.unlock();  // the chunks come from the scan's own buffers
     uint64_t mt = 1;
     cubit_scan_max_threads(g->scan, &mt);
     g->max_threads = mt;
@@ -605,7 +660,11 @@ static double CubitProgress(ClientContext &context, const FunctionData *bind_dat
 static unique_ptr<NodeStatistics> CubitCardinality(ClientContext &context, const FunctionData *bind_data) {
     auto &bind = bind_data->Cast<CubitBindData>();
     uint64_t estimated = 0, max = 0;
-    auto &parts = bind.attached.parts;
+    auto set = bind.attached.Current();  // held for the call: a re-attach may swap it meanwhile
+    if (!set) {
+        return nullptr;
+    }
+    auto &parts = set->parts;
     if (cubit_scan_cardinality_multi(parts.data(), (uint32_t)parts.size(), &estimated, &max) != CUBIT_OK) {
         return nullptr;
     }
@@ -622,7 +681,11 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
     }
     int64_t lo = 0, hi = 0;
     int has_null = 0, has_no_null = 0;
-    auto &parts = bind.attached.parts;
+    auto set = bind.attached.Current();
+    if (!set) {
+        return nullptr;
+    }
+    auto &parts = set->parts;
     if (cubit_scan_statistics_multi(parts.data(), (uint32_t)parts.size(), column_id, &lo, &hi, &has_null,
                                     &has_no_null) != CUBIT_OK) {
         return nullptr;
@@ -665,15 +728,19 @@ TableFunction GetCubitScanFunction() {
 //  * no writer of the table is outstanding (CubitAttached::writers: recorded when its statement
 //    ends or when it is planned) and every committed append is synced;
 //  * the transaction's snapshot includes the one the partition was read in.
-static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
+static bool PartitionCurrentLocked(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
     auto &tx = DuckTransaction::Get(context, table.catalog);
     auto &storage = table.GetStorage();
     if (tx.ChangesMade() || LocalStorage::Get(tx).Find(storage)) {
         return false;
     }
-    lock_guard<mutex> g(attached.lock);
     return attached.Attached() && attached.writers.empty() && storage.GetTotalRows() == attached.gpu_rows &&
            tx.start_time >= attached.sync_start;
+}
+
+static bool CubitPartitionIsCurrent(ClientContext &context, DuckTableEntry &table, CubitAttached &attached) {
+    lock_guard<mutex> g(attached.lock);
+    return PartitionCurrentLocked(context, table, attached);
 }
 
 // DELETE / UPDATE / INSERT … ON CONFLICT DO UPDATE planned on an attached table: remember the
@@ -805,7 +872,8 @@ public:
         noted_db = db.get();
         noted_id = tx.transaction_id;
         noted_values = props.has_updates;
-        CubitRegistry::NoteDirty(*db, tx.transaction_id, props.has_updates);
+        CubitRegistry::NoteDirty(*db, tx.transaction_id, props.has_updates,
+                                 DuckTransactionManager::Get(*db).LowestActiveId());
         for (auto &kv : CubitRegistry::InDatabase(*db)) {
             lock_guard<mutex> g(kv.second->lock);
             auto &w = kv.second->writers[tx.transaction_id];
@@ -1065,24 +1133,20 @@ static bool SampleMatches(cubit_ctx *ctx, cubit_table *t, column_t col, const ve
     return true;
 }
 
-static void DestroyPartitions(CubitAttached &attached) {
-    for (auto t : attached.parts) {
-        cubit_table_destroy(t);
-    }
-    attached.parts.clear();
-    attached.part_base.clear();
-}
-
-// Upload a whole snapshot as new partitions and build their indexes: rows split into one
+// Upload a whole snapshot as a new partition set and build its indexes: rows split into one
 // contiguous range per context (boundaries on row groups of 122,880 rows = 1,920 bitvector words,
-// so every partition's validity words are the snapshot's own), partition i on ctxs[i]. With
-// `entry` and one partition, a column held in persistent BITPACKING segments is registered from
-// them (AttachBitpackedColumn). Every partition gets the same indexes (the every-distinct-value
-// default decided over the whole snapshot).
-static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, DuckTableEntry *entry) {
-    DestroyPartitions(attached);
+// so every partition's validity words are the snapshot's own), partition i on the contexts' i-th.
+// With `entry` and one partition, a column held in persistent BITPACKING segments is registered
+// from them (AttachBitpackedColumn). Every partition gets the same indexes (the
+// every-distinct-value default decided over the whole snapshot). The set is not visible to scans
+// until the caller swaps it in.
+static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached, const CubitSnapshot &snap,
+                                                         DuckTableEntry *entry) {
+    auto set = std::make_shared<CubitPartitionSet>();
+    set->contexts = attached.contexts;
+    const auto &ctxs = set->contexts->ctxs;
     const uint64_t rg = 122880, units = (snap.rows + rg - 1) / rg;
-    const uint64_t n_parts = std::max<uint64_t>(1, std::min<uint64_t>(attached.ctxs.size(), units));
+    const uint64_t n_parts = std::max<uint64_t>(1, std::min<uint64_t>(ctxs.size(), units));
     vector<bool> few(attached.column_order.size());
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
         few[c] = FewDistinct(snap.values[c], snap.validity[c]);
@@ -1091,16 +1155,16 @@ static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, D
         const uint64_t b = std::min(snap.rows, units * p / n_parts * rg);
         const uint64_t e = std::min(snap.rows, units * (p + 1) / n_parts * rg);
         cubit_table *t = nullptr;
-        Check(cubit_table_create(attached.ctxs[p], e - b, (int64_t)b, &t));
-        attached.parts.push_back(t);
-        attached.part_base.push_back(b);
+        Check(cubit_table_create(ctxs[p], e - b, (int64_t)b, &t));
+        set->parts.push_back(t);
+        set->part_base.push_back(b);
         for (idx_t c = 0; c < attached.column_order.size(); c++) {
             const column_t col = attached.column_order[c];
             const uint64_t *valid = snap.validity[c].data() + b / 64;
             const bool from_segments =
                 entry && n_parts == 1 &&
                 AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
-                SampleMatches(attached.ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
+                SampleMatches(ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
             if (!from_segments) {  // (re-)registering replaces a column taken from segments
                 const bool wide = WidePhysical(attached.columns[col]);
                 vector<int32_t> narrow;
@@ -1123,7 +1187,30 @@ static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, D
             }
         }
     }
-    attached.gpu_rows = snap.rows;
+    return set;
+}
+
+// The committed deletes (row ids the snapshot lacks, visible to every snapshot the swap admits:
+// start_time >= the sync's) as each partition's delete list of local rows.
+static void SetDeletes(CubitPartitionSet &set, const vector<bool> &present, uint64_t rows) {
+    vector<int64_t> gone;
+    for (uint64_t r = 0; r < rows; r++) {
+        if (r >= present.size() || !present[r]) {
+            gone.push_back((int64_t)r);
+        }
+    }
+    for (size_t p = 0; p < set.parts.size(); p++) {
+        const int64_t b = (int64_t)set.part_base[p];
+        const int64_t e = p + 1 < set.parts.size() ? (int64_t)set.part_base[p + 1] : (int64_t)rows;
+        vector<int64_t> local;
+        for (auto r : gone) {
+            if (r >= b && r < e) {
+                local.push_back(r - b);
+            }
+        }
+        vector<uint64_t> ids(local.size(), 0);
+        Check(cubit_table_set_deletes(set.parts[p], local.data(), ids.data(), local.size()));
+    }
 }
 
 // Bring the partition to the table's committed state, reading every attached column in one
@@ -1133,6 +1220,7 @@ static void BuildPartition(CubitAttached &attached, const CubitSnapshot &snap, D
 // column is read again. Row ids the snapshot lacks are deletes, committed before it began.
 static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAttached &attached,
                           const string &table_name, bool rebuild) {
+    // the caller holds attached.sync_lock: syncs and attaches of this table run one at a time
     auto &tm = DuckTransactionManager::Get(entry.catalog.GetAttached());
     // writers that finished before the snapshot below begins are in it
     const transaction_t lowest_active = tm.LowestActiveId();
@@ -1143,6 +1231,8 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
     auto &snap_tx = DuckTransaction::Get(*con.context, entry.catalog);
     const transaction_t start = snap_tx.start_time;
     vector<transaction_t> folded;
+    std::shared_ptr<CubitPartitionSet> cur;
+    uint64_t gpu_rows = 0;
     {
         lock_guard<mutex> g(attached.lock);
         // writers that were active before this sync and may commit after its snapshot: those
@@ -1157,18 +1247,33 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
                 rebuild |= w.second;
             }
         }
+        if (attached.Attached()) {
+            cur = attached.set;
+            gpu_rows = attached.gpu_rows;  // only syncs change it, and they run one at a time
+        }
     }
+    // the end of every path: the partition state, the writers it folded and its snapshot, in one
+    // hold of the lock (and of the set's rw when it changes in place)
+    auto publish = [&](std::shared_ptr<CubitPartitionSet> next, uint64_t rows) {
+        lock_guard<mutex> g(attached.lock);
+        attached.set = std::move(next);
+        attached.gpu_rows = rows;
+        for (auto w : folded) {
+            attached.writers.erase(w);
+        }
+        attached.sync_start = start;
+    };
     CubitSnapshot snap;
     vector<bool> present;  // presence of every row id of the table in this snapshot
-    if (!rebuild && attached.Attached()) {
+    if (!rebuild && cur) {
         // rows appended since the partition was read, then which older rows remain
-        ReadRows(con, table_name, entry, attached.column_order, attached.gpu_rows, total_rows, snap);
+        ReadRows(con, table_name, entry, attached.column_order, gpu_rows, total_rows, snap);
         auto res = con.Query("SELECT rowid FROM " + KeywordHelper::WriteOptionallyQuoted(table_name) +
-                             " WHERE rowid < " + to_string(attached.gpu_rows));
+                             " WHERE rowid < " + to_string(gpu_rows));
         if (res->HasError()) {
             res->ThrowError();
         }
-        present.assign(attached.gpu_rows, false);
+        present.assign(gpu_rows, false);
         while (auto chunk = res->Fetch()) {
             chunk->Flatten();
             auto ids = FlatVector::GetData<int64_t>(chunk->data[0]);
@@ -1176,11 +1281,11 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
                 present[(uint64_t)ids[i]] = true;
             }
         }
-        if (snap.rows == 0 && entry.GetStorage().GetTotalRows() < attached.gpu_rows) {
+        if (snap.rows == 0 && entry.GetStorage().GetTotalRows() < gpu_rows) {
             rebuild = true;  // fewer rows than the partition: renumbered by a vacuum
         }
     }
-    if (rebuild || !attached.Attached()) {
+    if (rebuild || !cur) {
         ReadRows(con, table_name, entry, attached.column_order, 0, total_rows, snap);
         if (snap.rows == 0) {
             con.Commit();
@@ -1191,56 +1296,41 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
         // and a concurrent checkpoint does not vacuum deleted rows (:132-135); later appends show
         // as more rows than the snapshot's. Either keeps that column on decoded values, and the
         // sample check in BuildPartition backs this up.
-        BuildPartition(attached, snap, &entry);
+        auto next = BuildPartition(attached, snap, &entry);
         con.Commit();
-        present = snap.present;
-    } else {
-        con.Commit();
-        if (snap.rows) {
-            vector<int> cols;
-            vector<const void *> data;
-            vector<const uint64_t *> valid;
-            vector<vector<int32_t>> narrow;
-            narrow.reserve(attached.column_order.size());
-            for (idx_t c = 0; c < attached.column_order.size(); c++) {
-                const column_t col = attached.column_order[c];
-                cols.push_back((int)col);
-                if (WidePhysical(attached.columns[col])) {
-                    data.push_back(snap.values[c].data());
-                } else {
-                    narrow.emplace_back(snap.values[c].begin(), snap.values[c].end());
-                    data.push_back(narrow.back().data());
-                }
-                valid.push_back(snap.validity[c].data());
-            }
-            // appended rows continue the last partition's row range
-            Check(cubit_table_append(attached.parts.back(), snap.rows, cols.data(), data.data(), valid.data(),
-                                     (uint32_t)cols.size(), 0));
-            attached.gpu_rows += snap.rows;
-            present.insert(present.end(), snap.present.begin(), snap.present.end());
-        }
+        SetDeletes(*next, snap.present, snap.rows);
+        publish(std::move(next), snap.rows);  // scans still on the old set keep it until they end
+        return;
     }
-    // committed deletes: visible to every snapshot the swap admits (start_time >= start)
-    vector<int64_t> gone;
-    for (uint64_t r = 0; r < attached.gpu_rows; r++) {
-        if (r >= present.size() || !present[r]) {
-            gone.push_back((int64_t)r);
-        }
-    }
-    // per partition, as its local rows
-    for (size_t p = 0; p < attached.parts.size(); p++) {
-        const int64_t b = (int64_t)attached.part_base[p];
-        const int64_t e = p + 1 < attached.parts.size() ? (int64_t)attached.part_base[p + 1] : (int64_t)attached.gpu_rows;
-        vector<int64_t> local;
-        for (auto r : gone) {
-            if (r >= b && r < e) {
-                local.push_back(r - b);
-            }
-        }
-        vector<uint64_t> ids(local.size(), 0);
-        Check(cubit_table_set_deletes(attached.parts[p], local.data(), ids.data(), local.size()));
-    }
+    con.Commit();
+    // in place: appended rows continue the last partition's row range; no scan reads the tables
+    // meanwhile (the set's rw, exclusive) and none is admitted before the new state is published
     lock_guard<mutex> g(attached.lock);
+    std::unique_lock<std::shared_mutex> writing(cur->rw);
+    if (snap.rows) {
+        vector<int> cols;
+        vector<const void *> data;
+        vector<const uint64_t *> valid;
+        vector<vector<int32_t>> narrow;
+        narrow.reserve(attached.column_order.size());
+        for (idx_t c = 0; c < attached.column_order.size(); c++) {
+            const column_t col = attached.column_order[c];
+            cols.push_back((int)col);
+            if (WidePhysical(attached.columns[col])) {
+                data.push_back(snap.values[c].data());
+            } else {
+                narrow.emplace_back(snap.values[c].begin(), snap.values[c].end());
+                data.push_back(narrow.back().data());
+            }
+            valid.push_back(snap.validity[c].data());
+        }
+        Check(cubit_table_append(cur->parts.back(), snap.rows, cols.data(), data.data(), valid.data(),
+                                 (uint32_t)cols.size(), 0));
+        gpu_rows += snap.rows;
+        present.insert(present.end(), snap.present.begin(), snap.present.end());
+    }
+    SetDeletes(*cur, present, gpu_rows);
+    attached.gpu_rows = gpu_rows;
     for (auto w : folded) {
         attached.writers.erase(w);
     }
@@ -1252,9 +1342,10 @@ static void CubitSync(ClientContext &context, const FunctionParameters &paramete
     const auto table_name = parameters.values[0].ToString();
     auto &entry = Catalog::GetEntry<TableCatalogEntry>(context, INVALID_CATALOG, DEFAULT_SCHEMA, table_name);
     auto attached = CubitRegistry::Find(entry);
-    if (!attached || !attached->Attached()) {
+    if (!attached || !attached->Current()) {
         throw InvalidInputException("cubit_sync: %s is not attached", table_name);
     }
+    lock_guard<mutex> one(attached->sync_lock);
     SyncPartition(context, entry.Cast<DuckTableEntry>(), *attached, table_name, false);
 }
 
@@ -1319,23 +1410,25 @@ static void CubitAttachImpl(ClientContext &context, const string &table_name, co
     auto &duck = entry.Cast<DuckTableEntry>();
     auto &attached = CubitRegistry::Insert(entry);
     // one context per device: `devices` of them (0 = every visible device), kept across attaches
+    // with the same count; a new count gets new contexts, and the old ones go with the last
+    // partition set (and scan) built on them
     int visible = 1;
     Check(cubit_device_count(&visible));
     const int want = devices <= 0 ? visible : std::min(devices, visible);
-    DestroyPartitions(attached);
-    while ((int)attached.ctxs.size() > want) {
-        cubit_scan_release_cached(nullptr, nullptr);  // pooled buffers of the context going away
-        cubit_ctx_destroy(attached.ctxs.back());
-        attached.ctxs.pop_back();
+    lock_guard<mutex> one(attached.sync_lock);  // through the rebuild below
+    if (!attached.contexts || (int)attached.contexts->ctxs.size() != want) {
+        auto fresh = std::make_shared<CubitContexts>();
+        for (int d = 0; d < want; d++) {
+            cubit_ctx *c = nullptr;
+            Check(cubit_ctx_create(d, &c));
+            fresh->ctxs.push_back(c);
+        }
+        attached.contexts = std::move(fresh);
     }
-    while ((int)attached.ctxs.size() < want) {
-        cubit_ctx *c = nullptr;
-        Check(cubit_ctx_create((int)attached.ctxs.size(), &c));
-        attached.ctxs.push_back(c);
-    }
-    attached.devices = devices;
     {
         lock_guard<mutex> g(attached.lock);
+        attached.set.reset();  // not current until the rebuild below publishes the new set
+        attached.devices = devices;
         attached.columns.clear();
         attached.column_order.clear();
         for (auto name : StringUtil::Split(column_list, ',')) {

@@ -107,16 +107,20 @@ def test_partitioned_probe_at_global_row_ids(ctx):
         t.close()
 
 
-@pytest.mark.parametrize("world,tasks", [(8, 1), (8, 4), (3, 4)])
-def test_table_function_over_partitions(golden, world, tasks):
+@pytest.mark.parametrize("world,tasks,stage_mb", [(8, 1, None), (8, 4, None), (3, 4, None), (8, 4, "0.15")])
+def test_table_function_over_partitions(golden, world, tasks, stage_mb, monkeypatch):
     """One table-function scan over all partitions (cubit_scan_init_global_multi), each on its
     own context — as one process driving one device per partition would hold them, here all on
     device 0: one cursor in row order over every partition's windows (RowGroupCollection's
     NextParallelScan over all row groups, row_group_collection.cpp:174-224), each window copied
     from its own partition, batch index = the partition's first tile + its tile. The chunks
     equal the whole-table oracle, SF1's Q6 fingerprint and its revenue; every task's batch
-    indexes ascend."""
+    indexes ascend. stage_mb 0.15: one staging budget for the whole scan holds the first
+    partitions' blocks (≈ 57 KB each), the rest are copied per window."""
     import threading
+
+    if stage_mb is not None:
+        monkeypatch.setenv("CUBIT_SCAN_STAGE_MB", stage_mb)
 
     from cubit_amd import scan_function as S
     from cubit_amd.scan_function import ROW_ID, CubitScanFunction
