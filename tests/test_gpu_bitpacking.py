@@ -240,6 +240,40 @@ def test_gpu_reads_duckdb_written_segment(ctx, s):
     t.close()
 
 
+# ---------------------------------------------------------------- the FTS index's segments
+
+from test_oracle_bitpacking import FTS, FTS_BP, check_fts_invariants, fts_decoded, fts_segment  # noqa: E402
+
+
+def test_gpu_reads_the_fts_index_segments(ctx):
+    """The BITPACKING segments of the reference's huggingface_index.db FTS index (FOR groups of
+    7, 8 and 11 bits, CONSTANT_DELTA; tests/golden/bitpacking_reference_segments_fts.json)
+    through K5: each unpacked column equals the restatement's decode, the unpacked columns
+    satisfy the FTS definitions (docs.len = terms per doc, dict.df = distinct docs per term,
+    every termid present, Σ len / 153 = avgdl), and comparisons through the packed-segment filter
+    equal the oracle's scan."""
+    cols = fts_decoded()
+    for s in FTS_BP:
+        col = fts_segment(s)
+        n = s["count"]
+        t = CubitTable(ctx, n, row_base=0)
+        t.add_bitpacked_column(0, col.data, col.seg_off, col.seg_count, np.int64)
+        got = t.download_column(0)
+        assert np.array_equal(got, cols[s["name"]]), s["name"]
+        cols[s["name"]] = got
+        oc = O.Column(got)
+        mid = int(np.median(got))
+        for cmp, k in (("<", mid), (">=", mid), ("=", mid), ("<", int(got.min()) + 1)):
+            fs = F.TableFilterSet({0: F.ConstantFilter(cmp, k)})
+            ref = O.table_scan([oc], F.serialize(fs), n)
+            t.use_packed_filter(True)
+            assert np.array_equal(t.scan(fs), ref), (s["name"], cmp, k)
+            t.use_packed_filter(False)
+        t.close()
+    check_fts_invariants(cols)
+    assert FTS["stats_avgdl"] > 0
+
+
 # ---------------------------------------------------------------- every integral type
 
 from test_oracle_bitpacking import (FORCED, INT_DTYPES, bitwidth_tables, filter_pushdown_column,  # noqa: E402

@@ -112,13 +112,16 @@ def reference_segment(s):
 
 
 def packed_tail_masked(seg: bytes, tsize: int, count: int) -> bytes:
-    """A one-group FOR / DELTA_FOR segment with the packed bits past value `count` zeroed: DuckDB
-    packs whole 32-value blocks from a reused buffer, so those bits are left-overs, not data."""
+    """A FOR / DELTA_FOR segment with the packed bits of its last group past the segment's last
+    value zeroed: DuckDB packs whole 32-value blocks from a reused buffer, so those bits are
+    left-overs, not data."""
     b = bytearray(seg)
     end = int.from_bytes(b[:8], "little")
-    meta = int.from_bytes(b[end - 4:end], "little")
+    last = (count - 1) // 2048  # metadata words are read downward from `end`, one per group
+    meta = int.from_bytes(b[end - 4 * (last + 1):end - 4 * last], "little")
     mode, off = meta >> 24, meta & 0xFFFFFF
-    if mode not in (4, 5) or count > 2048:
+    count -= 2048 * last  # values of the last group
+    if mode not in (4, 5):
         return bytes(b)
     fields = 3 if mode == 4 else 2  # DELTA_FOR: FOR, width, delta offset; FOR: FOR, width
     width = int.from_bytes(b[off + tsize: off + 2 * tsize], "little", signed=True)
@@ -126,6 +129,10 @@ def packed_tail_masked(seg: bytes, tsize: int, count: int) -> bytes:
     blocks = (count + 31) // 32
     for bit in range(count * width, blocks * 32 * width):
         b[packed + bit // 8] &= ~(1 << (bit % 8)) & 0xFF
+    # and the alignment gap between the last group's data and the metadata words (FlushSegment
+    # moves the metadata down to the data's aligned end; the gap keeps what the buffer held)
+    data_end = packed + blocks * 32 * width // 8
+    b[data_end:end - 4 * (last + 1)] = bytes(max(0, end - 4 * (last + 1) - data_end))
     return bytes(b)
 
 
@@ -326,3 +333,96 @@ def test_all_null_group_is_not_bitpackable_under_forced_modes(mode):
     valid[2048:] = 0
     assert O.bp_compress(v, valid, mode) is None
     assert O.bp_compress(v, valid, "auto") is not None
+
+
+# ---------------------------------------------------------------- FTS index segments (wider FOR groups)
+
+FTS = json.loads((Path(__file__).resolve().parent / "golden" / "bitpacking_reference_segments_fts.json").read_text())
+FTS_BP = [s for s in FTS["segments"] if s["compression"] == "bitpacking"]
+
+
+def fts_segment(s):
+    """A fixture segment of bitpacking_reference_segments_fts.json as a one-segment BitpackedColumn."""
+    raw = np.frombuffer(bytes.fromhex(s["segment_hex"]), dtype=np.uint8)
+    data = np.zeros((len(raw) + 7) // 8 * 8 + 8, dtype=np.uint8)
+    data[: len(raw)] = raw
+    return O.BitpackedColumn(data, np.array([0], np.uint64), np.array([len(raw)], np.uint64),
+                             np.array([s["count"]], np.uint64), np.dtype(s["dtype"]))
+
+
+def rle_decode(s):
+    """An RLE segment of BIGINTs (src/storage/compression/rle.cpp:248-277, RLEScanState: the
+    8-byte header is the offset of the uint16 run lengths; the run values start at byte 8)."""
+    seg = bytes.fromhex(s["segment_hex"])
+    off = int.from_bytes(seg[:8], "little")
+    n_runs = (len(seg) - off) // 2
+    vals = np.frombuffer(seg[8:8 + 8 * n_runs], dtype="<i8")
+    runs = np.frombuffer(seg[off:off + 2 * n_runs], dtype="<u2")
+    out = np.repeat(vals, runs)
+    assert len(out) == s["count"]
+    return out
+
+
+def fts_decoded():
+    """Every FTS column: BITPACKING ones by the restatement, RLE ones by rle_decode."""
+    return {s["name"]: (O.bp_decode(fts_segment(s)) if s["compression"] == "bitpacking" else rle_decode(s))
+            for s in FTS["segments"]}
+
+
+def check_fts_invariants(cols):
+    """fts_indexing.cpp:83-149 over the decoded columns (see the fixture's `invariants`)."""
+    docid, termid = cols["terms.docid"], cols["terms.termid"]
+    assert np.array_equal(cols["docs.len"], np.bincount(docid, minlength=153))
+    assert np.array_equal(np.unique(termid), np.arange(1558))
+    pairs = np.unique(termid.astype(np.int64) * 1024 + docid)
+    assert np.array_equal(cols["dict.df"], np.bincount(pairs // 1024, minlength=1558))
+    assert abs(cols["docs.len"].sum() / 153 - FTS["stats_avgdl"]) < 1e-9
+
+
+def test_fts_segments_widths_and_modes():
+    """The FTS file adds FOR groups of 7, 8 and 11 bits (the storage_version.db segments are at
+    most 3 bits wide) and CONSTANT_DELTA groups, all with an 8-byte T."""
+    modes, widths = set(), set()
+    for s in FTS_BP:
+        seg = bytes.fromhex(s["segment_hex"])
+        end = int.from_bytes(seg[:8], "little")
+        for g in range((s["count"] + 2047) // 2048):
+            meta = int.from_bytes(seg[end - 4 * (g + 1):end - 4 * g], "little")
+            mode, off = meta >> 24, meta & 0xFFFFFF
+            modes.add(mode)
+            if mode == 5:  # FOR: frame of reference, then the width (T-sized fields)
+                widths.add(int.from_bytes(seg[off + 8:off + 16], "little", signed=True))
+    assert modes == {3, 5}  # CONSTANT_DELTA, FOR (bitpacking.cpp BitpackingMode)
+    assert {7, 8, 11} <= widths
+
+
+@pytest.mark.parametrize("s", FTS_BP, ids=[s["name"] for s in FTS_BP])
+def test_fts_segment_decodes_to_its_definition_and_statistics(s):
+    """Each segment decodes to the values the FTS definitions give where they fix them
+    (CONSTANT_DELTA columns; docs.len from the RLE column terms.docid) and to the minimum and
+    maximum its DataPointer stores."""
+    got = O.bp_decode(fts_segment(s))
+    assert int(got.min()) == s["statistics"]["min"] and int(got.max()) == s["statistics"]["max"]
+    vals = s["values"]
+    if isinstance(vals, dict):
+        vals = list(range(*vals["range"]))
+    if vals is not None:
+        assert got.tolist() == vals
+
+
+def test_fts_columns_satisfy_the_index_definitions():
+    """docs.len = terms per doc, dict.df = distinct docs per term, every termid present,
+    Σ len / 153 = stats.avgdl — over the restatement's decode of the FOR segments."""
+    check_fts_invariants(fts_decoded())
+
+
+@pytest.mark.parametrize("s", FTS_BP, ids=[s["name"] for s in FTS_BP])
+def test_fts_compressor_writes_duckdbs_bytes(s):
+    """The restatement's writer given the decoded values reproduces DuckDB's segment byte for
+    byte, up to the left-over bits past the last value of a 32-value block."""
+    got = O.bp_decode(fts_segment(s))
+    ours = O.bp_compress(got, None, "auto")
+    assert ours is not None and len(ours.seg_off) == 1
+    ref = packed_tail_masked(bytes.fromhex(s["segment_hex"]), 8, s["count"])
+    mine = packed_tail_masked(bytes(ours.data[: int(ours.seg_size[0])]), 8, s["count"])
+    assert mine == ref
