@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -235,9 +236,11 @@ struct PartScan {
     std::vector<uint64_t> blk_off;          // per group: its block's first byte (+ the end)
     std::vector<uint64_t> col_rel, val_rel;  // per group × emitted position: its regions in the block
     std::vector<void*> probe_ev, group_ev;  // per group: probes done (context stream), copies done
-    std::vector<idx_t> group_off;          // per group: its first row (bit 0 of its validity words)
+    std::vector<idx_t> group_off, group_len;  // per group: its first row (bit 0 of its validity words), rows
+    uint32_t groups_launched = 0;          // group_ev[k] exists for k below it (CubitScanGlobalState::stage_mu)
     ~PartScan() {
-        for (void* ev : group_ev) cubit_copy_event_destroy(part.ctx, ev);
+        for (void* ev : group_ev)
+            if (ev) cubit_copy_event_destroy(part.ctx, ev);
         for (void* ev : probe_ev) cubit_copy_event_destroy(part.ctx, ev);
     }
 };
@@ -256,6 +259,13 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
     // run in row order on it; a stream per partition put several copy streams on one device's
     // four hardware queues and measured slower)
     std::vector<std::pair<cubit_ctx*, void*>> stage_streams;
+    // the staged groups' device work (probes, narrowing, block copies, events) is launched by this
+    // thread after init_global has returned, so the pipeline's tasks start while it launches; a task
+    // that claims a window of a group not launched yet waits on stage_cv
+    std::thread stager;
+    std::mutex stage_mu;
+    std::condition_variable stage_cv;
+    std::string stage_error;  // a launch failed: every waiting task throws it
     void* StageStream(cubit_ctx* ctx) {
         for (auto& s : stage_streams)
             if (s.first == ctx) return s.second;
@@ -269,6 +279,7 @@ struct CubitScanGlobalState : public GlobalTableFunctionState {
         return std::max<idx_t>(1, std::min<idx_t>(windows.size(), hw));
     }
     ~CubitScanGlobalState() override {
+        if (stager.joinable()) stager.join();
         // probes launched by init_global may still read the buffers returned to the pool
         for (auto& p : parts)
             if (p->part.ctx) cubit_sync(p->part.ctx);
@@ -493,12 +504,13 @@ void ProbeRange(PartScan& P, const std::vector<column_t>& column_ids, const std:
 
 // The probes, compaction and (staged) copies of partition p. Staged (see stage_groups()): the
 // partition's windows are cut into groups, each with one staging block on the device and its
-// image in page-locked memory; per group the probes and narrowing fill the block on the context
-// stream and close with an event, and the staging stream waits for it and copies the block in
-// ONE copy — the link starts on the first group while the device probes the next (one copy per
-// column and a separate flags copy left ≈ 35 µs of gaps per group on the link,
-// profiles/r05ae_*). Not staged: one probe over every row into partition-wide buffers, and each
-// task copies the window it claims.
+// image in page-locked memory; here the groups are laid out and the blocks allocated, and the
+// stager thread launches each group's work (LaunchStagedGroups: the probes and narrowing fill the
+// block on the context stream and close with an event, and the staging stream waits for it and
+// copies the block in ONE copy — the link starts on the first group while the device probes the
+// next; one copy per column and a separate flags copy left ≈ 35 µs of gaps per group on the link,
+// profiles/r05ae_*). Not staged: one probe over every row into partition-wide buffers, launched
+// here, and each task copies the window it claims.
 void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
     PartScan& P = *g.parts[p];
     cubit_ctx* ctx = P.part.ctx;
@@ -568,9 +580,27 @@ void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
                    static_cast<uint32_t*>(P.d_overflow.p), false);
         return;
     }
+    g.StageStream(ctx);  // created here: the stager only looks it up
+    P.group_off = g_off;
+    P.group_len = g_len;
+    P.group_ev.assign(n_groups, nullptr);
+    P.staged = true;
+}
+
+// The staged groups of partition p, launched in row order (the stager thread): per group the
+// overflow flags are cleared, the probes and narrowing fill its device block on the context
+// stream, an event closes them, and the staging stream waits for it, copies the block into its
+// page-locked image and records the group's event.
+void LaunchStagedGroups(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
+    PartScan& P = *g.parts[p];
+    cubit_ctx* ctx = P.part.ctx;
+    const size_t n_emit = g.emit.size();
     void* st = g.StageStream(ctx);
-    for (size_t k = 0; k < n_groups; ++k) {
-        const idx_t off = g_off[k], len = g_len[k];
+    std::vector<int64_t*> cols(n_emit, nullptr);
+    std::vector<uint64_t*> valid(n_emit, nullptr);
+    std::vector<char*> out(n_emit, nullptr);
+    for (size_t k = 0; k < P.group_off.size(); ++k) {
+        const idx_t off = P.group_off[k], len = P.group_len[k];
         char* blk = static_cast<char*>(P.d_block.p) + P.blk_off[k];
         for (size_t e = 0; e < n_emit; ++e) {
             char* region = blk + P.col_rel[k * n_emit + e];
@@ -591,10 +621,13 @@ void ProbeAndStage(CubitScanGlobalState& g, uint32_t p, const cubit_txn* txn) {
               "staged block");
         void* ev = nullptr;
         check(cubit_copy_event_record(ctx, st, &ev), "staged group event");
-        P.group_ev.push_back(ev);
-        P.group_off.push_back(off);
+        {
+            std::lock_guard<std::mutex> lk(g.stage_mu);
+            P.group_ev[k] = ev;
+            P.groups_launched = (uint32_t)k + 1;
+        }
+        g.stage_cv.notify_all();
     }
-    P.staged = true;
 }
 
 std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitInput& input) {
@@ -643,7 +676,24 @@ std::unique_ptr<GlobalTableFunctionState> CubitScanInitGlobal(TableFunctionInitI
         }
     }
     g->stage_left = stage_cap_bytes();
-    for (uint32_t p = 0; p < g->parts.size(); ++p) ProbeAndStage(*g, p, txn);
+    bool any_staged = false;
+    for (uint32_t p = 0; p < g->parts.size(); ++p) {
+        ProbeAndStage(*g, p, txn);
+        any_staged |= g->parts[p]->staged;
+    }
+    if (any_staged) {
+        CubitScanGlobalState* gs = g.get();
+        gs->stager = std::thread([gs, txn] {
+            try {
+                for (uint32_t p = 0; p < gs->parts.size(); ++p)
+                    if (gs->parts[p]->staged) LaunchStagedGroups(*gs, p, txn);
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(gs->stage_mu);
+                gs->stage_error = e.what();
+            }
+            gs->stage_cv.notify_all();
+        });
+    }
     if (phases) {
         const auto t3 = std::chrono::steady_clock::now();
         auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -693,7 +743,14 @@ bool NextWindow(CubitScanGlobalState& g, CubitScanLocalState& l) {
     };
     if (P.staged) {
         const uint32_t k = win.group;
-        check(cubit_copy_event_sync(P.part.ctx, P.group_ev[k]), "staged group");
+        void* ev = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(g.stage_mu);
+            g.stage_cv.wait(lk, [&] { return P.groups_launched > k || !g.stage_error.empty(); });
+            if (P.groups_launched <= k) throw ScanError(CUBIT_ERR_DEVICE, "cubit_scan staging: " + g.stage_error);
+            ev = P.group_ev[k];
+        }
+        check(cubit_copy_event_sync(P.part.ctx, ev), "staged group");
         waited();
         // the group's overflow flags came at the head of its block: a column whose compaction
         // overflowed in this group is copied per window as its 8-byte values instead
