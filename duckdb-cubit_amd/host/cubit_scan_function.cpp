@@ -207,7 +207,7 @@ struct PartScan {
     idx_t rows_per_tile = 0;
     uint64_t tile_base = 0;   // tiles of the earlier partitions: batch index = tile_base + tile
     uint32_t decodes = 0;     // decode launches (a second one only when the capacity fell short)
-    PooledBuffer d_cnt, d_dir;
+    PooledBuffer d_cnt;  // the decode's count (2 words), then its tile directory: one read brings both
     PooledBuffer d_ids;                  // device: ordered row ids
     std::vector<PooledBuffer> d_cols;    // device: per emitted position, probed values
     // transfer compaction per emitted position: the window copies move `width` bytes per value
@@ -338,16 +338,15 @@ int64_t* device_ptr(PooledBuffer& b) { return b.i64(); }
 void LaunchDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn, uint64_t cap) {
     cubit_ctx* ctx = P.part.ctx;
     ++P.decodes;
-    if (!P.d_cnt.p) P.d_cnt.allocate(device_pool(), ctx, 16);
     // this scan's tile directory, copied out within the scan call: other pipeline tasks or
     // queries may scan on the same context right after it (cubit_table_scan_tiles)
     const uint32_t dir_cap = (uint32_t)((P.part.n_rows + 131071) / 131072 + 1);
-    if (!P.d_dir.p) P.d_dir.allocate(device_pool(), ctx, 2ull * dir_cap * 8);
+    if (!P.d_cnt.p) P.d_cnt.allocate(device_pool(), ctx, 16 + 2ull * dir_cap * 8);
     P.d_ids.allocate(device_pool(), ctx, std::max<uint64_t>(cap, 1) * 8);
     uint32_t n_tiles = 0;
     check(cubit_table_scan_tiles(P.part.table, nodes.empty() ? nullptr : nodes.data(), (uint32_t)nodes.size(), txn,
                                  device_ptr(P.d_ids), P.d_ids.bytes / 8, static_cast<uint64_t*>(P.d_cnt.p),
-                                 CUBIT_SCAN_ORDERED, static_cast<uint64_t*>(P.d_dir.p), dir_cap, &n_tiles,
+                                 CUBIT_SCAN_ORDERED, static_cast<uint64_t*>(P.d_cnt.p) + 2, dir_cap, &n_tiles,
                                  &P.rows_per_tile),
           "cubit_table_scan_tiles");
     P.tiles.assign(n_tiles, 0);  // the directory's size until FinishDecode reads it
@@ -371,17 +370,19 @@ uint64_t DecodeCapacity(const PartScan& P, const std::vector<cubit_filter_node>&
 // a second time with the exact count.
 void FinishDecode(PartScan& P, const std::vector<cubit_filter_node>& nodes, const cubit_txn* txn) {
     cubit_ctx* ctx = P.part.ctx;
-    check(cubit_memcpy_d2h(ctx, &P.count, P.d_cnt.p, 8), "count");
+    // the count and the directory in one read (the tile count is known from the launch)
+    std::vector<uint64_t> head(2 + 2 * P.tiles.size());
+    check(cubit_memcpy_d2h(ctx, head.data(), P.d_cnt.p, head.size() * 8), "count and directory");
+    P.count = head[0];
     if (P.count > P.d_ids.bytes / 8) {
         LaunchDecode(P, nodes, txn, P.count);
-        idx_t again = 0;
-        check(cubit_memcpy_d2h(ctx, &again, P.d_cnt.p, 8), "count");
-        if (again != P.count) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
+        head.assign(2 + 2 * P.tiles.size(), 0);
+        check(cubit_memcpy_d2h(ctx, head.data(), P.d_cnt.p, head.size() * 8), "count and directory");
+        if (head[0] != P.count) throw ScanError(CUBIT_ERR_CAPACITY, "cubit_table_scan: count changed between the passes");
     }
     const uint32_t n_tiles = P.count ? (uint32_t)P.tiles.size() : 0;  // nothing qualified: no run
     P.tiles.clear();
-    std::vector<uint64_t> dir(2 * (size_t)n_tiles);
-    if (n_tiles) check(cubit_memcpy_d2h(ctx, dir.data(), P.d_dir.p, dir.size() * 8), "directory");
+    const uint64_t* dir = head.data() + 2;
     // the ordered layout: tile t's run starts at the sum of the earlier tiles' lengths
     idx_t off = 0;
     for (uint32_t t = 0; t < n_tiles; ++t) {
