@@ -20,8 +20,14 @@
 #   apitrace[:<sf>,<tasks>]    HIP API + kernel + copy trace of examples/q6_scan (default 100 8), then
 #                              scripts/api_timeline.py over runs 0..3 into $OUT/apitrace_runs.txt
 #   merge                      scripts/merge_timing.py (the merge at 612 M rows, phases on stderr)
-#   pipeline[:<sf>,<tasks>,...]  examples/q6_scan (default 100 8) with CUBIT_SCAN_PHASES=1 (init_global's
-#                              phases and each task's window waits on stderr), Q6_REPS=5
+#   pipeline[:<args>]          examples/q6_scan (default 100 8) with CUBIT_SCAN_PHASES=1 (init_global's
+#                              phases and each task's window waits on stderr), Q6_REPS=5; leading
+#                              VAR=value args go to its environment (pipeline:CUBIT_SCAN_STAGE_MB=0,100,8;
+#                              pipeline:Q6_AB=1,Q6_REPS=20,100,16; pipeline:100,8,--partitions,4)
+#   trace:<cmd,args>           rocprofv3 --kernel-trace --memory-copy-trace --stats of a command
+#   pmc:<counters>:<cmd,args>  one rocprofv3 --pmc pass (counters joined by '+', within one pass's
+#                              limits: at most 8 SQ_, 4 TCC_, ...) over a command
+#   soak[:<args>]              scripts/fuzz_soak.py (default 150 2000003 20000)
 #   run:<cmd,args>             any other command (e.g. run:./scripts/smallbench,10)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -89,8 +95,21 @@ for step in "$@"; do
       for r in 0 1 2 3; do echo "== run $r"; python scripts/api_timeline.py "$OUT/apitrace" $r; done \
           > "$OUT/apitrace_runs.txt" 2>&1 ;;
     pipeline)
-      a=${rest:-100,8}
-      CUBIT_SCAN_PHASES=1 Q6_REPS=5 timeout -k 10 300 duckdb-cubit_amd/lib/q6_scan ${a//,/ } > "$log" 2>&1 ;;
+      envs=(); args=()
+      for x in ${rest//,/ }; do [[ $x == *=* ]] && envs+=("$x") || args+=("$x"); done
+      [ ${#args[@]} -eq 0 ] && args=(100 8)
+      env CUBIT_SCAN_PHASES=1 Q6_REPS=5 "${envs[@]}" timeout -k 10 300 duckdb-cubit_amd/lib/q6_scan "${args[@]}" \
+          > "$log" 2>&1 ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/trace$n" \
+          -o tr -- ${rest//,/ } > "$log" 2>&1 ;;
+    pmc)
+      c=${rest%%:*}; a=${rest#*:}
+      timeout -s KILL 300 rocprofv3 --pmc ${c//+/ } --output-format csv -d "$OUT/pmc$n" -o pmc -- ${a//,/ } \
+          > "$log" 2>&1 ;;
+    soak)
+      a=${rest:-150,2000003,20000}
+      timeout -k 10 400 python -u scripts/fuzz_soak.py ${a//,/ } > "$log" 2>&1 ;;
     merge)
       timeout -k 10 600 python -u scripts/merge_timing.py > "$log" 2>&1 ;;
     run)
