@@ -270,6 +270,9 @@ int run_eval(cubit_ctx* ctx, const EvalProgram& prog, uint64_t n_rows, int64_t r
     // the ticket word at once (768 tiles: 384 instead of 512, ≈11 ns each).
     const uint64_t work = a.num_tiles;
     const uint64_t max_grid = (uint64_t)ctx->n_cus * 2;
+    // (a grid of ceil(work / ceil(work / max_grid)) workgroups, every one the same number of tiles,
+    // measured slower: SF100 / 4 18.5 -> 21.0 µs, fewer workgroups than the last round's leave HBM
+    // unsaturated; profiles/r06k_balanced_grid_not_kept.txt)
     const unsigned grid = (unsigned)(work <= max_grid ? work : work <= 2 * max_grid ? (work + 1) / 2 : max_grid);
     if (tiles == 0) {  // no row: the count is 0 and no kernel runs
         if (start) ctx->n_timed--;

@@ -9,7 +9,9 @@
 #   tests:<f1>,<f2>            just those test files (verbose, fail fast)
 #   smoke                      __graft_entry__.smoke()
 #   bench[:<workload>[:<args>]]  python bench.py --workload <workload> <args>; args use ',' for
-#                              spaces (bench:q6:--steps,20) — default: the driver's N = 1 line
+#                              spaces (bench:q6:--steps,20), leading VAR=value args go to its
+#                              environment (bench:q6:CUBIT_BENCH_PARTITION=0/8,--steps,20) — default:
+#                              the driver's N = 1 line
 #   profile:<workload>[:<args>]  rocprofv3 --kernel-trace --stats over that bench, then one
 #                              --pmc pass each for FETCH_SIZE and WRITE_SIZE (never combined)
 #   dist1                      the bench as one torchrun rank over RCCL (the N > 1 code path)
@@ -55,8 +57,10 @@ for step in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
     bench)
       w=${rest%%:*}; a=${rest#*:}; [ "$a" = "$rest" ] && a=""
+      envs=(); args=()
+      for x in ${a//,/ }; do [[ $x == *=* && $x != --* ]] && envs+=("$x") || args+=("$x"); done
       if [ -n "$w" ]; then
-        timeout -k 10 600 python bench.py --workload "$w" ${a//,/ } > "$OUT/$n.bench_$w.json" 2> "$log"
+        env "${envs[@]}" timeout -k 10 600 python bench.py --workload "$w" "${args[@]}" > "$OUT/$n.bench_$w.json" 2> "$log"
       else
         timeout -k 10 600 python bench.py > "$OUT/$n.bench.json" 2> "$log"
       fi ;;
