@@ -32,6 +32,20 @@ def date(y: int, m: int, d: int) -> int:
     return (_dt.date(y, m, d) - EPOCH).days
 
 
+def constant_bits(c) -> int:
+    """A filter constant as the int64 a cubit_filter_node carries: integers as they are; a
+    np.float32 as its 32-bit IEEE pattern (a FLOAT column's constant), any other float as its
+    64-bit pattern (DOUBLE) — the C ABI compares FLOAT / DOUBLE columns with DuckDB's semantics
+    on those patterns."""
+    import numpy as np
+
+    if isinstance(c, np.float32):
+        return int(np.array([c], dtype=np.float32).view(np.uint32)[0])
+    if isinstance(c, (float, np.floating)):
+        return int(np.array([c], dtype=np.float64).view(np.int64)[0])
+    return int(c)
+
+
 def decimal(text: str, scale: int = 2) -> int:
     """DECIMAL(p, scale) physical value (scaled integer), e.g. decimal('0.05') == 5."""
     neg = text.startswith("-")
@@ -56,7 +70,7 @@ class ConstantFilter(TableFilter):
     kind = L.FILTER_CONSTANT
 
     def nodes(self, column):
-        return [(L.FILTER_CONSTANT, _CMP[self.comparison], column, 0, int(self.constant))]
+        return [(L.FILTER_CONSTANT, _CMP[self.comparison], column, 0, constant_bits(self.constant))]
 
 
 @dataclass
@@ -132,7 +146,7 @@ class Cmp(Residual):
     constant: int
 
     def nodes(self):
-        return [(L.FILTER_CONSTANT, _CMP[self.comparison], self.column, 0, int(self.constant))]
+        return [(L.FILTER_CONSTANT, _CMP[self.comparison], self.column, 0, constant_bits(self.constant))]
 
 
 @dataclass

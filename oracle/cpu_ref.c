@@ -52,6 +52,43 @@ static inline int use_inserted(uint64_t start_time, uint64_t tid, uint64_t id) {
     return id < start_time || id == tid;
 }
 
+/* Floating-point comparisons with DuckDB's semantics (src/common/vector_operations/
+ * comparison_operators.cpp:17-88): NaN equals NaN and is greater than every other value; other
+ * values compare as IEEE (so -0.0 == +0.0). LessThan(a, b) = GreaterThan(b, a). */
+static inline int fp_isnan(double x) { return x != x; }
+static inline int fp_eq(double a, double b) { return (fp_isnan(a) && fp_isnan(b)) || a == b; }
+static inline int fp_gt(double a, double b) {
+    if (fp_isnan(b)) return 0;
+    if (fp_isnan(a)) return 1;
+    return a > b;
+}
+static inline int fp_ge(double a, double b) {
+    if (fp_isnan(b)) return fp_isnan(a);
+    if (fp_isnan(a)) return 1;
+    return a >= b;
+}
+static inline double fp_value(int type, int64_t bits) {
+    if (type == OTYPE_FLOAT) {
+        uint32_t u = (uint32_t)bits;
+        float f;
+        memcpy(&f, &u, 4);
+        return (double)f;
+    }
+    double d;
+    memcpy(&d, &bits, 8);
+    return d;
+}
+static inline int cmp_fp(int cmp, double v, double c) {
+    switch (cmp) {
+    case 0: return fp_eq(v, c);
+    case 1: return !fp_eq(v, c);
+    case 2: return fp_gt(c, v);
+    case 3: return fp_ge(c, v);
+    case 4: return fp_gt(v, c);
+    default: return fp_ge(v, c);
+    }
+}
+
 static inline int cmp_op(int cmp, int64_t v, int64_t c) {
     switch (cmp) {
     case OCMP_EQ: return v == c;
@@ -61,6 +98,25 @@ static inline int cmp_op(int cmp, int64_t v, int64_t c) {
     case OCMP_GT: return v > c;
     case OCMP_GE: return v >= c;
     default: return 0;
+    }
+}
+
+/* a comparison of values of column type `type` (FP: bit patterns) */
+static inline int cmp_typed(int type, int cmp, int64_t v, int64_t c) {
+    if (type == OTYPE_FLOAT || type == OTYPE_DOUBLE) return cmp_fp(cmp, fp_value(type, v), fp_value(type, c));
+    return cmp_op(cmp, v, c);
+}
+
+/* the stored value of row r as int64 (FP: its bit pattern, FLOAT zero-extended) */
+static inline int64_t col_value(const ocol *c, uint64_t r) {
+    switch (c->type) {
+    case OTYPE_INT32: return (int64_t)((const int32_t *)c->data)[r];
+    case OTYPE_FLOAT: {
+        uint32_t u;
+        memcpy(&u, (const float *)c->data + r, 4);
+        return (int64_t)u;
+    }
+    default: return ((const int64_t *)c->data)[r];  /* INT64, DOUBLE bits */
     }
 }
 
@@ -76,7 +132,8 @@ static int subtree_end(const ofilter *nodes, int i) {
  * updates the vector references the column data in place (an uncompressed in-memory
  * segment scan is zero-copy) and keeps its physical type. */
 typedef struct {
-    int type;              /* OTYPE_* of data */
+    int type;              /* OTYPE_* of the column */
+    int wide;              /* data is int64[] of values / FP bit patterns (the merged copy) */
     const void *data;      /* first value of the vector */
     const uint8_t *valid;  /* NULL = all valid */
     int64_t vals[VEC];     /* merged copy when the vector has updates (type becomes INT64) */
@@ -99,18 +156,15 @@ static void load_vector(const ocol *c, uint64_t first_row, uint64_t count, const
     } else {
         out->valid = NULL;
     }
+    out->type = c->type;
     if (!has_upd) {
-        out->type = c->type;
-        out->data = c->type == OTYPE_INT32 ? (const void *)((const int32_t *)c->data + first_row)
-                                           : (const void *)((const int64_t *)c->data + first_row);
+        out->wide = 0;
+        out->data = c->type == OTYPE_INT32 || c->type == OTYPE_FLOAT
+                        ? (const void *)((const int32_t *)c->data + first_row)
+                        : (const void *)((const int64_t *)c->data + first_row);
         return;
     }
-    if (c->type == OTYPE_INT32) {
-        const int32_t *src = (const int32_t *)c->data + first_row;
-        for (uint64_t i = 0; i < count; i++) out->vals[i] = src[i];
-    } else {
-        memcpy(out->vals, (const int64_t *)c->data + first_row, count * sizeof(int64_t));
-    }
+    for (uint64_t i = 0; i < count; i++) out->vals[i] = col_value(c, first_row + i);
     if (!out->valid) {
         memset(out->valid_buf, 1, count);
         out->valid = out->valid_buf;
@@ -128,12 +182,17 @@ static void load_vector(const ocol *c, uint64_t first_row, uint64_t count, const
         out->vals[r - first_row] = ok ? c->upd_values[u] : 0;
         out->valid_buf[r - first_row] = (uint8_t)ok;
     }
-    out->type = OTYPE_INT64;
+    out->wide = 1;
     out->data = out->vals;
 }
 
 static inline int64_t vec_value(const vecbuf *v, uint32_t idx) {
-    return v->type == OTYPE_INT32 ? (int64_t)((const int32_t *)v->data)[idx] : ((const int64_t *)v->data)[idx];
+    if (v->wide) return ((const int64_t *)v->data)[idx];
+    switch (v->type) {
+    case OTYPE_INT32: return (int64_t)((const int32_t *)v->data)[idx];
+    case OTYPE_FLOAT: return (int64_t)((const uint32_t *)v->data)[idx];
+    default: return ((const int64_t *)v->data)[idx];
+    }
 }
 static inline int vec_valid(const vecbuf *v, uint32_t idx) { return v->valid ? v->valid[idx] : 1; }
 
@@ -174,6 +233,21 @@ static inline int vec_valid(const vecbuf *v, uint32_t idx) { return v->valid ? v
 
 static uint64_t templated_filter_selection(const vecbuf *v, int cmp, int64_t c, uint32_t *sel, uint64_t approved) {
     uint64_t rc = 0;
+    if (v->type == OTYPE_FLOAT || v->type == OTYPE_DOUBLE) {
+        /* FilterSelectionSwitch<float / double> with DuckDB's floating-point operators */
+        const double pred = fp_value(v->type, c);
+        for (uint64_t a = 0; a < approved; a++) {
+            uint32_t idx = sel[a];
+            int pass = vec_valid(v, idx) && cmp_fp(cmp, fp_value(v->type, vec_value(v, idx)), pred);
+            sel[rc] = idx;
+            rc += (uint64_t)pass;
+        }
+        return rc;
+    }
+    if (v->wide) {
+        TFS_CMP(int64_t)
+        return rc;
+    }
     if (v->type == OTYPE_INT32) {
         /* a constant outside the int32 domain: the comparison is decided by its sign */
         if (c > INT32_MAX || c < INT32_MIN) {
@@ -296,7 +370,7 @@ static uint64_t expr_select(const ofilter *nodes, int i, vecbuf *const *vbufs, c
     for (uint64_t a = 0; a < count; a++) {
         uint32_t idx = sel[a];
         int pass;
-        if (f->kind == OF_CONST) pass = vec_valid(v, idx) && cmp_op(f->cmp, vec_value(v, idx), f->constant);
+        if (f->kind == OF_CONST) pass = vec_valid(v, idx) && cmp_typed(v->type, f->cmp, vec_value(v, idx), f->constant);
         else if (f->kind == OF_IS_NULL) pass = !vec_valid(v, idx);
         else pass = vec_valid(v, idx);
         if (pass) true_sel[tc++] = idx;
@@ -474,7 +548,7 @@ int oracle_fetch(const ocol *c, const omvcc *tx, const int64_t *rowids, uint64_t
     }
     for (uint64_t i = 0; i < n; i++) {
         uint64_t r = (uint64_t)(rowids[i] - row_base);
-        int64_t v = c->type == OTYPE_INT32 ? (int64_t)((const int32_t *)c->data)[r] : ((const int64_t *)c->data)[r];
+        int64_t v = col_value(c, r);
         int valid = row_valid(c, r);
         if (c->n_updates && r <= max_row) {
             for (uint64_t k = first[r]; k < first[r + 1]; k++) {
@@ -547,8 +621,7 @@ void oracle_build_bitvector(const ocol *c, uint64_t n_rows, int cmp, int64_t con
     uint64_t n_words = (n_rows + 63) / 64;
     memset(words, 0, n_words * 8);
     for (uint64_t r = 0; r < n_rows; r++) {
-        int64_t v = c->type == OTYPE_INT32 ? (int64_t)((const int32_t *)c->data)[r] : ((const int64_t *)c->data)[r];
-        if (row_valid(c, r) && cmp_op(cmp, v, constant)) words[r >> 6] |= 1ULL << (r & 63);
+        if (row_valid(c, r) && cmp_typed(c->type, cmp, col_value(c, r), constant)) words[r >> 6] |= 1ULL << (r & 63);
     }
 }
 

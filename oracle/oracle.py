@@ -18,7 +18,7 @@ HERE = Path(__file__).resolve().parent
 LIB = HERE / "lib" / "libcubit_oracle.so"
 
 OMAX_COLS = 16
-OTYPE_INT32, OTYPE_INT64 = 0, 1
+OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE = 0, 1, 2, 3
 OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
 
 
@@ -91,19 +91,31 @@ def lib():
     return _lib
 
 
+def fp_bits(values, dtype) -> np.ndarray:
+    """FLOAT / DOUBLE values as the int64 bit patterns the oracle and the C ABI carry (FLOAT:
+    the 32-bit pattern, zero-extended)."""
+    if np.dtype(dtype) == np.float32:
+        return np.ascontiguousarray(np.asarray(values, dtype=np.float32)).view(np.uint32).astype(np.int64)
+    return np.ascontiguousarray(np.asarray(values, dtype=np.float64)).view(np.int64)
+
+
 class Column:
     """A column as the oracle sees it: base values, optional validity words and a
-    chronological update list (rows, values, version ids[, valid flags: False = SET NULL])."""
+    chronological update list (rows, values, version ids[, valid flags: False = SET NULL]).
+    FLOAT / DOUBLE columns (float32 / float64 data): update values given as floats are carried
+    as their bit patterns (fp_bits)."""
 
     def __init__(self, data: np.ndarray, validity: Optional[np.ndarray] = None, updates=None):
         self.data = np.ascontiguousarray(data)
-        assert self.data.dtype in (np.int32, np.int64)
+        assert self.data.dtype in (np.int32, np.int64, np.float32, np.float64)
         self.validity = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
         self.upd_valid = None
         if updates is None:
             self.upd = None
         else:
             r, v, ver = updates[:3]
+            if self.data.dtype.kind == "f" and np.asarray(v).dtype.kind == "f":
+                v = fp_bits(v, self.data.dtype)
             self.upd = (np.ascontiguousarray(r, dtype=np.int64), np.ascontiguousarray(v, dtype=np.int64),
                         np.ascontiguousarray(ver, dtype=np.uint64))
             if len(updates) > 3 and updates[3] is not None:
@@ -111,7 +123,8 @@ class Column:
 
     def ocol(self) -> OCol:
         c = OCol()
-        c.type = OTYPE_INT32 if self.data.dtype == np.int32 else OTYPE_INT64
+        c.type = {np.dtype(np.int32): OTYPE_INT32, np.dtype(np.int64): OTYPE_INT64, np.dtype(np.float32): OTYPE_FLOAT,
+                  np.dtype(np.float64): OTYPE_DOUBLE}[self.data.dtype]
         c.data = self.data.ctypes.data
         c.validity = self.validity.ctypes.data if self.validity is not None else None
         if self.upd is not None:
