@@ -18,6 +18,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -676,9 +677,11 @@ int cubit_build_bitvector(cubit_ctx* ctx, const void* d_col, int type, const uin
                           int cmp, int64_t constant, uint64_t* d_words) {
     if (!ctx || !d_col || !d_words) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+        return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (cmp < 0 || cmp > 5) return fail(CUBIT_ERR_INVALID, "cmp %d", cmp);
-    HIP_CHECK(launch_compare_bitvector(d_col, type, d_validity, n_rows, cmp, constant, d_words, ctx->stream));
+    HIP_CHECK(launch_compare_bitvector(d_col, type, d_validity, n_rows, cmp, value_key(type, constant), d_words,
+                                       ctx->stream));
     return CUBIT_OK;
 }
 
@@ -1023,7 +1026,8 @@ extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const i
                             const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* d_out) {
     if (!ctx || !d_col || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+        return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     HIP_CHECK(launch_gather(d_col, type, d_rowids, d_count, max_n, row_base, d_out, ctx->stream));
     return CUBIT_OK;
 }
@@ -1346,6 +1350,8 @@ bool storage_of(int type, int& col_type, uint64_t& src_size) {
     case CUBIT_TYPE_INT16: case CUBIT_TYPE_UINT16: col_type = CUBIT_TYPE_INT32, src_size = 2; return true;
     case CUBIT_TYPE_UINT32: col_type = CUBIT_TYPE_INT64, src_size = 4; return true;
     case CUBIT_TYPE_UINT64: col_type = CUBIT_TYPE_INT64, src_size = 8; return true;
+    case CUBIT_TYPE_FLOAT: col_type = CUBIT_TYPE_FLOAT, src_size = 4; return true;
+    case CUBIT_TYPE_DOUBLE: col_type = CUBIT_TYPE_DOUBLE, src_size = 8; return true;
     default: return false;
     }
 }
@@ -1391,8 +1397,9 @@ int widen_column(cubit_table* t, Column& c, int type, const void* data, const ui
 }
 
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64) return widen_column(t, c, type, data, validity, on_device);
-    const uint64_t esz = type == CUBIT_TYPE_INT32 ? 4 : 8;
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+        return widen_column(t, c, type, data, validity, on_device);
+    const uint64_t esz = type_is32(type) ? 4 : 8;  // FLOAT / DOUBLE: the bit patterns as they are
     if (t->n_rows == 0) {  // empty partition: nothing to copy
         c.type = type;
         c.data = on_device ? data : nullptr;
@@ -1445,7 +1452,8 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
     const uint64_t span = (uint64_t)vmax - (uint64_t)vmin;  // no signed overflow
     if (span >= (1ull << 32)) {
         // a wide span (TIMESTAMP microseconds, BIGINT ids) over few distinct values: sort the
-        // valid values on the host instead (only INT64 columns get here)
+        // valid values on the host instead (only INT64 and DOUBLE columns get here: a DOUBLE's
+        // patterns become their keys first)
         std::vector<int64_t> hv(n);
         std::vector<uint64_t> hvalid(validity ? (n + 63) / 64 : 0);
         HIP_CHECK(hipMemcpyAsync(hv.data(), data, n * 8, hipMemcpyDeviceToHost, t->ctx->stream));
@@ -1459,6 +1467,8 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
                 if ((hvalid[i >> 6] >> (i & 63)) & 1) hv[k++] = hv[i];
             hv.resize(k);
         }
+        if (type == CUBIT_TYPE_DOUBLE)
+            for (int64_t& v : hv) v = value_key(type, v);
         distinct = distinct_sorted(hv.data(), hv.size());
         if (distinct.size() > kMaxWideDistinct)
             return fail(CUBIT_ERR_UNSUPPORTED, "%zu distinct values over a span of 2^32 or more; give keys",
@@ -1742,6 +1752,14 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     if (n && !values) return fail(CUBIT_ERR_INVALID, "values is null");
     if (int rc = set_device(t->ctx)) return rc;
     const Column& c = it->second;
+    // a FLOAT / DOUBLE column's keys are given as bit patterns and held as their comparison keys
+    // (-0.0 and +0.0, or two NaNs, become one key)
+    std::vector<int64_t> keyed;
+    if (n && type_is_fp(c.type)) {
+        keyed.resize(n);
+        for (uint32_t k = 0; k < n; ++k) keyed[k] = value_key(c.type, values[k]);
+        values = keyed.data();
+    }
     Index ix;
     ix.encoding = encoding;
     if (t->n_rows == 0) {  // empty partition: an empty index (scans of it launch nothing)
@@ -2010,6 +2028,7 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
         std::stable_sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return rows[x] < rows[y]; });
     Updates u;
     u.n = n;
+    const int type = t->cols.at(col).type;
     for (uint64_t i = 0; valids && i < n; ++i) u.any_null |= valids[i] == 0;
     u.h_rows.reserve(n);
     u.h_values.reserve(n);
@@ -2017,7 +2036,8 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
     for (uint64_t i : order) {
         if (!u.h_rows.empty() && u.h_rows.back() == rows[i]) u.unique_rows = false;
         u.h_rows.push_back(rows[i]);
-        u.h_values.push_back(values[i]);
+        // a FLOAT value is its 32-bit pattern, zero-extended (as the probe hands it back)
+        u.h_values.push_back(type == CUBIT_TYPE_FLOAT ? (int64_t)(uint32_t)values[i] : values[i]);
         u.h_versions.push_back(versions[i]);
         if (u.any_null) u.h_valids.push_back(valids[i] ? 1 : 0);
     }
@@ -2027,13 +2047,12 @@ int store_updates(cubit_table* t, int col, const int64_t* rows, const int64_t* v
         u.distinct_versions.assign(dv.begin(), dv.end());
         std::sort(u.distinct_versions.begin(), u.distinct_versions.end());
     }
-    if (u.any_null) {  // the statistics cover the records that carry a value
+    {  // the statistics cover the records that carry a value (FLOAT / DOUBLE: their keys)
         std::vector<int64_t> vv;
+        vv.reserve(n);
         for (uint64_t i = 0; i < n; ++i)
-            if (u.h_valids[i]) vv.push_back(u.h_values[i]);
+            if (u.valid_at(i)) vv.push_back(value_key(type, u.h_values[i]));
         u.stat_values = distinct_sorted(vv.data(), vv.size());
-    } else {
-        u.stat_values = distinct_sorted(u.h_values.data(), n);
     }
     u.rows = std::make_unique<DevBuf>();
     u.values = std::make_unique<DevBuf>();
@@ -2151,7 +2170,7 @@ int grow_bitvectors(cubit_table* t, uint64_t words) {
 // an owned data buffer of at least `rows` rows holding the column's first n_rows values
 int own_column(cubit_table* t, Column& c, uint64_t rows) {
     if (c.cap_rows >= rows && c.cap_rows) return CUBIT_OK;
-    const uint64_t esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
+    const uint64_t esz = type_is32(c.type) ? 4 : 8;
     auto b = std::make_unique<DevBuf>();
     if (hipMalloc(&b->p, std::max<uint64_t>(rows * esz, 16)) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "column allocation failed");
@@ -2299,7 +2318,7 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
         Column& c = kv.second;
         c.drop_packed();  // the segments do not hold the appended rows
         const uint32_t i = at[col];
-        const uint64_t esz = c.type == CUBIT_TYPE_INT32 ? 4 : 8;
+        const uint64_t esz = type_is32(c.type) ? 4 : 8;
         HIP_CHECK(hipMemcpyAsync(tmp_col.p, data[i], n_new * esz, hipMemcpyHostToDevice, s));
         HIP_CHECK(hipMemcpyAsync(static_cast<char*>(const_cast<void*>(c.data)) + n_old * esz, tmp_col.p, n_new * esz,
                                  hipMemcpyDeviceToDevice, s));
@@ -2456,7 +2475,7 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
     } else {
         std::vector<int64_t> valid_vals;
         for (uint64_t i = 0; i < m; ++i)
-            if (m_valid[i]) valid_vals.push_back(m_vals[i]);
+            if (m_valid[i]) valid_vals.push_back(value_key(c.type, m_vals[i]));
         added = distinct_sorted(valid_vals.data(), valid_vals.size());
     }
     if (c.type == CUBIT_TYPE_INT32 && !added.empty() && (added.front() < INT32_MIN || added.back() > INT32_MAX))
@@ -3116,7 +3135,7 @@ int fit(cubit_table* t, ExprP& e) {
 __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ values,
                                   const uint8_t* __restrict__ valids, const uint64_t* __restrict__ versions, uint64_t n,
                                   uint64_t start_time, uint64_t tid, int pred, int cmp, int64_t c, int64_t c2,
-                                  uint64_t* __restrict__ bv) {
+                                  int type, uint64_t* __restrict__ bv) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t ver = versions[i];
@@ -3133,7 +3152,7 @@ __global__ void patch_leaf_kernel(const int64_t* __restrict__ rows, const int64_
             }
         }
         if (!newest) continue;
-        const int64_t v = values[i];
+        const int64_t v = value_key(type, values[i]);  // the leaf's constants are keys (FLOAT / DOUBLE)
         // a SET NULL record: the row leaves the validity leaf and fails every comparison
         // (UpdateMergeValidity, update_segment.cpp:94-99; NULL never passes a filter)
         const bool ok = !valids || valids[i];
@@ -3191,7 +3210,7 @@ int patch_updates(cubit_table* t, ExprP& e, const cubit_txn* txn, std::map<const
                                static_cast<const int64_t*>(u.rows->p), static_cast<const int64_t*>(u.values->p),
                                u.d_valids(), static_cast<const uint64_t*>(u.versions->p), u.n, txn->start_time,
                                txn->transaction_id, e->leaf.pred, e->leaf.cmp, e->leaf.constant, e->leaf.constant2,
-                               copy);
+                               t->cols.at(e->leaf.column).type, copy);
             HIP_CHECK(hipGetLastError());
             patched[e->leaf.bv] = copy;
         }
@@ -3352,12 +3371,50 @@ double interval_selectivity(cubit_table* t, int col, double lo_c, double hi_c, i
     if ((*rc = ensure_zones(t, {}, {col}))) return 1.0;
     const cubit_table::ColZones& cz = t->col_zones.at(col);
     const uint32_t nz = (uint32_t)cz.fl.size();
+    // FLOAT / DOUBLE: zone bounds and the interval are keys; values are taken uniform in value
+    // (not key) space, so every bound is mapped back to the value it names (NaN, the greatest
+    // value, and ±inf as ±inf; a zone with an infinite span counts as an outlier below)
+    const int type = t->cols.at(col).type;
+    const bool fp = type_is_fp(type);
+    auto value_of = [type](double k) -> double {
+        if (std::isinf(k)) return k;
+        const int64_t key = k >= 9.2e18 ? INT64_MAX : k <= -9.2e18 ? INT64_MIN + 1 : (int64_t)k;
+        const int64_t bits = cubit_fp_value(type, key);
+        double v;
+        if (type == CUBIT_TYPE_FLOAT) {
+            float f;
+            const uint32_t u = (uint32_t)bits;
+            std::memcpy(&f, &u, 4);
+            v = f;
+        } else {
+            std::memcpy(&v, &bits, 8);
+        }
+        return std::isnan(v) ? std::numeric_limits<double>::infinity() : v;
+    };
+    if (fp) {
+        lo_c = value_of(lo_c);
+        hi_c = value_of(hi_c);
+    }
+    auto zone_bounds = [&](uint32_t z, double& lo, double& hi) {
+        if (fp) {
+            lo = value_of((double)cz.mn[z]);
+            hi = value_of((double)cz.mx[z]);
+            if (hi == lo) hi = std::nextafter(hi, std::numeric_limits<double>::infinity());
+        } else {
+            lo = (double)cz.mn[z];
+            hi = (double)cz.mx[z] + 1.0;
+        }
+    };
     // a zone whose value span is far wider than the typical zone's holds a few outliers (one
     // extreme value stretches the uniform assumption over the whole type range): it counts at
     // the other zones' mean fraction instead
     std::vector<double> spans;
-    for (uint32_t z = 0; z < nz; ++z)
-        if (cz.fl[z] & 1) spans.push_back((double)cz.mx[z] - (double)cz.mn[z] + 1.0);
+    for (uint32_t z = 0; z < nz; ++z) {
+        if (!(cz.fl[z] & 1)) continue;
+        double lo, hi;
+        zone_bounds(z, lo, hi);
+        if (std::isfinite(hi - lo)) spans.push_back(hi - lo);
+    }
     double median_span = 0.0;
     if (!spans.empty()) {
         std::nth_element(spans.begin(), spans.begin() + spans.size() / 2, spans.end());
@@ -3367,8 +3424,10 @@ double interval_selectivity(cubit_table* t, int col, double lo_c, double hi_c, i
     for (uint32_t z = 0; z < nz; ++z) {
         const double rows = (double)std::min<uint64_t>(kZoneRows, t->n_rows - (uint64_t)z * kZoneRows);
         if (!(cz.fl[z] & 1)) continue;  // no valid row passes a comparison
-        const double lo = (double)cz.mn[z], hi = (double)cz.mx[z] + 1.0, span = hi - lo;
-        if (median_span > 1.0 && span > 8.0 * median_span) {
+        double lo, hi;
+        zone_bounds(z, lo, hi);
+        const double span = hi - lo;
+        if (!std::isfinite(span) || ((median_span > 1.0 || (fp && median_span > 0.0)) && span > 8.0 * median_span)) {
             outlier_rows += rows;
             continue;
         }
@@ -3563,6 +3622,27 @@ bool cmp_interval(int cmp, int64_t c, double* lo, double* hi) {
     }
 }
 
+// Filter nodes with the constants on FLOAT / DOUBLE columns replaced by their comparison keys
+// (cubit_fp_key): the planner, the zone statistics, the index keys and every kernel compare keys,
+// so DuckDB's floating-point operators (NaN greatest and equal to NaN, -0.0 == +0.0) become integer
+// comparisons. Nodes on other columns are used as given (no copy when there are none).
+struct KeyedNodes {
+    std::vector<cubit_filter_node> buf;
+    const cubit_filter_node* p;
+    KeyedNodes(const cubit_table* t, const cubit_filter_node* nodes, uint32_t n) : p(nodes) {
+        for (uint32_t k = 0; k < n; ++k) {
+            if (nodes[k].kind != CUBIT_FILTER_CONSTANT) continue;
+            auto it = t->cols.find(nodes[k].column);
+            if (it == t->cols.end() || !type_is_fp(it->second.type)) continue;
+            if (buf.empty()) {
+                buf.assign(nodes, nodes + n);
+                p = buf.data();
+            }
+            buf[k].constant = value_key(it->second.type, nodes[k].constant);
+        }
+    }
+};
+
 // Estimated fraction of the partition's rows a filter tree (prefix nodes from i; i ends past the
 // subtree) keeps, on the planner's cost model (interval_selectivity: per-zone min / max, values
 // uniform within a zone, columns independent). An AND folds its constant children on one column
@@ -3641,7 +3721,8 @@ extern "C" int cubit_table_estimate_rows(cubit_table* t, const cubit_filter_node
     if (int rc = set_device(t->ctx)) return rc;
     int rc = CUBIT_OK;
     uint32_t i = 0;
-    const double s = std::min(1.0, std::max(0.0, tree_selectivity(t, nodes, i, &rc)));
+    const KeyedNodes keyed(t, nodes, n_nodes);
+    const double s = std::min(1.0, std::max(0.0, tree_selectivity(t, keyed.p, i, &rc)));
     if (rc) return rc;
     *rows = std::min<uint64_t>(t->n_rows, (uint64_t)std::ceil(s * (double)t->n_rows));
     return CUBIT_OK;
@@ -3670,7 +3751,8 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
     if (n_nodes == 0) {
         e = mk_true();
     } else {
-        Planner p{t, nodes, n_nodes};
+        const KeyedNodes keyed(t, nodes, n_nodes);
+        Planner p{t, keyed.p, n_nodes};
         if (p.subtree_end(0) != (int)n_nodes) return fail(CUBIT_ERR_INVALID, "malformed filter tree");
         e = p.plan(0);
         if (!e) return p.rc ? p.rc : fail(CUBIT_ERR_INVALID, "planning failed");
@@ -4098,8 +4180,10 @@ extern "C" int cubit_table_column_statistics(cubit_table* t, int col, int64_t* v
     // a SET NULL record makes the column nullable (UpdateValidityStatistics,
     // update_segment.cpp:907-918: an update vector with an invalid row sets has_null)
     if (uit != t->upd.end() && uit->second.any_null) any_null = true;
-    if (vmin) *vmin = any_valid ? lo : 0;
-    if (vmax) *vmax = any_valid ? hi : 0;
+    // FLOAT / DOUBLE: the bounds are keys; handed out as the bit patterns of those values
+    const int type = t->cols.at(col).type;
+    if (vmin) *vmin = any_valid ? cubit_fp_value(type, lo) : 0;
+    if (vmax) *vmax = any_valid ? cubit_fp_value(type, hi) : 0;
     if (has_null) *has_null = any_null ? 1 : 0;
     if (has_no_null) *has_no_null = any_valid ? 1 : 0;
     return CUBIT_OK;

@@ -47,6 +47,37 @@ struct EvalProgram {
 
 inline uint32_t prog_nops(const EvalProgram& p, int k) { return (p.nops >> (4 * k)) & 15u; }
 
+// Column value types as the kernels see them: INT32 / INT64 values, or FLOAT / DOUBLE bit patterns
+// (4 / 8 bytes) compared through their order key (cubit_fp_key, include/cubit_gpu.h: NaN one key
+// above +inf, -x → -pattern(x), so -0.0 == +0.0 — DuckDB's floating-point operators,
+// comparison_operators.hpp:100-146). Type codes as in cubit_gpu.h.
+constexpr int kTypeInt32 = 0, kTypeInt64 = 1, kTypeFloat = 8, kTypeDouble = 9;
+__host__ __device__ __forceinline__ bool type_is32(int type) { return type == kTypeInt32 || type == kTypeFloat; }
+__host__ __device__ __forceinline__ bool type_is_fp(int type) { return type == kTypeFloat || type == kTypeDouble; }
+__host__ __device__ __forceinline__ int32_t fp_key32(uint32_t u) {
+    const uint32_t mag = u & 0x7fffffffu;
+    if (mag > 0x7f800000u) return 0x7fc00000;
+    return (u >> 31) ? -(int32_t)mag : (int32_t)mag;
+}
+__host__ __device__ __forceinline__ int64_t fp_key64(uint64_t u) {
+    const uint64_t mag = u & 0x7fffffffffffffffull;
+    if (mag > 0x7ff0000000000000ull) return (int64_t)0x7ff8000000000000ull;
+    return (u >> 63) ? -(int64_t)mag : (int64_t)mag;
+}
+// the comparison key of a value as the ABI carries it (FLOAT: the zero-extended 32-bit pattern)
+__host__ __device__ __forceinline__ int64_t value_key(int type, int64_t v) {
+    if (type == kTypeFloat) return fp_key32((uint32_t)v);
+    if (type == kTypeDouble) return fp_key64((uint64_t)v);
+    return v;
+}
+// kernels templated on the key kind FK (0: the value itself, 1: FLOAT pattern, 2: DOUBLE pattern)
+template <int FK, typename T>
+__host__ __device__ __forceinline__ T key_of(T raw) {
+    if constexpr (FK == 1) return (T)fp_key32((uint32_t)raw);
+    else if constexpr (FK == 2) return (T)fp_key64((uint64_t)raw);
+    else return raw;
+}
+
 inline uint64_t padded_words(uint64_t n_rows) {
     const uint64_t w = (n_rows + 63) / 64;
     return ((w + kPadWords - 1) / kPadWords) * kPadWords;

@@ -1768,7 +1768,7 @@ __device__ __forceinline__ bool cmp_v(CT v, CT c, CT c2) {
     return v >= c && v < c2;
 }
 
-template <typename T, typename CT, int CMP, int M>
+template <typename T, typename CT, int CMP, int M, int FK = 0>
 __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __restrict__ col,
                                                                  const uint64_t* __restrict__ validity,
                                                                  uint64_t n_rows, uint64_t n_words_padded,
@@ -1790,7 +1790,7 @@ __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __rest
             for (int j = 0; j < JB; ++j) {
                 const uint64_t row = (w0 + jb + j) * 64 + lane;
                 ok[j] = row < n_rows;
-                v[j] = ok[j] ? (CT)__builtin_nontemporal_load(col + row) : (CT)0;  // streamed once: nt
+                v[j] = ok[j] ? (CT)key_of<FK>(__builtin_nontemporal_load(col + row)) : (CT)0;  // streamed once: nt
                 if (validity) ok[j] = ok[j] && ((validity[w0 + jb + j] >> lane) & 1ull);
             }
 #pragma unroll
@@ -1821,7 +1821,7 @@ __global__ __launch_bounds__(256) void compare_bitvectors_kernel(const T* __rest
     }
 }
 
-template <typename T, typename CT, int M>
+template <typename T, typename CT, int M, int FK = 0>
 hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64_t n_rows, int cmp,
                                   const MultiKeyArgs& a, hipStream_t stream) {
     const uint64_t nw = padded_words(n_rows);
@@ -1830,7 +1830,7 @@ hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64
     const dim3 grid((unsigned)std::max<uint64_t>(blocks, 1)), block(256);
 #define CUBIT_CMP_CASE(C)                                                                                       \
     case C:                                                                                                     \
-        hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, C, M>), grid, block, 0, stream, col, validity, n_rows, nw, a); \
+        hipLaunchKernelGGL((compare_bitvectors_kernel<T, CT, C, M, FK>), grid, block, 0, stream, col, validity, n_rows, nw, a); \
         break;
     if constexpr (M == 1) {  // a query-time constant: every comparison
         switch (cmp) {
@@ -1867,7 +1867,7 @@ hipError_t launch_compare_multi_t(const T* col, const uint64_t* validity, uint64
 // the candidate values are gathered per set bit (line-granular reads of the column where a
 // line holds a candidate). Comparison semantics are TemplatedFilterSelection's
 // (column_segment.cpp:261-349); NULL rows are never candidates.
-template <typename T, typename CT, int CMP>
+template <typename T, typename CT, int CMP, int FK = 0>
 __global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restrict__ col,
                                                               const uint64_t* __restrict__ validity,
                                                               const uint64_t* __restrict__ lo_bv,
@@ -1904,7 +1904,7 @@ __global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restric
             const T* base = col + (w0 + e) * 64;
             while (cand) {
                 const int b = __builtin_ctzll(cand);
-                const CT v = (CT)base[b];
+                const CT v = (CT)key_of<FK>(base[b]);
                 if (CMP == 2 ? v < c : v == c) hit |= 1ull << b;
                 cand &= cand - 1;
             }
@@ -1921,7 +1921,7 @@ __global__ __launch_bounds__(256) void candidate_check_kernel(const T* __restric
 // conjunction: out = mask ∩ valid ∩ {r : lo <= v[r] <= hi, complemented when neg}, the column
 // read only at the mask's rows (line-granular gathers, as the candidate check). Each thread owns
 // two consecutive words (16-byte loads and stores).
-template <typename T>
+template <typename T, int FK = 0>
 __global__ __launch_bounds__(256) void masked_compare_kernel(const T* __restrict__ col,
                                                              const uint64_t* __restrict__ validity,
                                                              const uint64_t* __restrict__ mask, uint64_t n_words_padded,
@@ -1943,7 +1943,7 @@ __global__ __launch_bounds__(256) void masked_compare_kernel(const T* __restrict
             const T* base = col + (w0 + e) * 64;
             while (cand) {
                 const int b = __builtin_ctzll(cand);
-                const T v = base[b];
+                const T v = key_of<FK>(base[b]);
                 if (((v >= lo) & (v <= hi)) != (neg != 0)) hit |= 1ull << b;
                 cand &= cand - 1;
             }
@@ -1954,16 +1954,16 @@ __global__ __launch_bounds__(256) void masked_compare_kernel(const T* __restrict
     }
 }
 
-template <typename T, typename CT>
+template <typename T, typename CT, int FK = 0>
 hipError_t launch_candidate_t(const T* col, const uint64_t* validity, const uint64_t* lo_bv, const uint64_t* hi_bv,
                               uint64_t n_rows, int cmp, CT c, uint64_t* out, hipStream_t stream) {
     const uint64_t nw = padded_words(n_rows);
     const dim3 grid((unsigned)std::min<uint64_t>((nw / 2 + 255) / 256, 8192)), block(256);
     if (cmp == 2)
-        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 2>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
+        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 2, FK>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
                            n_rows, nw, c, out);
     else if (cmp == 0)
-        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 0>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
+        hipLaunchKernelGGL((candidate_check_kernel<T, CT, 0, FK>), grid, block, 0, stream, col, validity, lo_bv, hi_bv,
                            n_rows, nw, c, out);
     else
         return hipErrorInvalidValue;
@@ -1982,6 +1982,15 @@ bool keys_fit32(const MultiKeyArgs& a, int cmp) {
 template <int M>
 hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int cmp,
                             const MultiKeyArgs& a, hipStream_t stream) {
+    // FLOAT / DOUBLE: the patterns' keys (FLOAT keys are int32, so are the planner's keys for it)
+    if (type == kTypeFloat)
+        return keys_fit32(a, cmp) ? launch_compare_multi_t<int32_t, int32_t, M, 1>(static_cast<const int32_t*>(col),
+                                                                                   validity, n_rows, cmp, a, stream)
+                                  : launch_compare_multi_t<int32_t, int64_t, M, 1>(static_cast<const int32_t*>(col),
+                                                                                   validity, n_rows, cmp, a, stream);
+    if (type == kTypeDouble)
+        return launch_compare_multi_t<int64_t, int64_t, M, 2>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
+                                                              stream);
     if (type == 0 && keys_fit32(a, cmp))
         return launch_compare_multi_t<int32_t, int32_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
                                                            stream);
@@ -1997,7 +2006,7 @@ hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity,
 // min / max / any-valid of a column (the statistics an index build needs; the reference
 // keeps them per segment as BaseStatistics, used by CheckZonemap, row_group.cpp:361-371).
 // out[0] = min, out[1] = max (pre-set to INT64_MAX / INT64_MIN), out[2] = valid rows.
-template <typename T>
+template <typename T, int FK = 0>
 __global__ __launch_bounds__(256) void column_minmax_kernel(const T* __restrict__ col,
                                                             const uint64_t* __restrict__ validity, uint64_t n,
                                                             int64_t* __restrict__ out) {
@@ -2006,7 +2015,7 @@ __global__ __launch_bounds__(256) void column_minmax_kernel(const T* __restrict_
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) continue;
-        const int64_t v = (int64_t)col[i];
+        const int64_t v = (int64_t)key_of<FK>(col[i]);
         mn = v < mn ? v : mn;
         mx = v > mx ? v : mx;
         ++cnt;
@@ -2027,7 +2036,7 @@ __global__ __launch_bounds__(256) void column_minmax_kernel(const T* __restrict_
 
 // presence bitmap of the valid values: bit (v - vmin) of `bits`. Narrow ranges (≤ 2^16
 // values) collect in LDS first so the few global words are OR-ed once per workgroup.
-template <typename T, bool LDS>
+template <typename T, bool LDS, int FK = 0>
 __global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col, const uint64_t* __restrict__ validity,
                                                        uint64_t n, int64_t vmin, uint64_t range,
                                                        uint64_t* __restrict__ bits) {
@@ -2040,7 +2049,7 @@ __global__ __launch_bounds__(256) void presence_kernel(const T* __restrict__ col
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) continue;
-        const uint64_t off = (uint64_t)((int64_t)col[i] - vmin);
+        const uint64_t off = (uint64_t)((int64_t)key_of<FK>(col[i]) - vmin);
         const uint64_t bit = 1ull << (off & 63);
         if (LDS) {
             if (!(s_bits[off >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&s_bits[off >> 6]), bit);
@@ -2828,7 +2837,7 @@ __global__ __launch_bounds__(256) void zone_class_kernel(const uint64_t* __restr
 // Per-zone statistics of a raw column (the segment statistics CheckZonemap consults,
 // numeric_stats.cpp:157-228): min / max over the zone's valid rows and whether any / every row
 // is valid. One workgroup per zone; consecutive threads read consecutive 4-row chunks.
-template <typename T>
+template <typename T, int FK = 0>
 __global__ __launch_bounds__(256) void column_zone_stats_kernel(const T* __restrict__ col,
                                                                 const uint64_t* __restrict__ validity, uint64_t n_rows,
                                                                 int64_t* __restrict__ mn, int64_t* __restrict__ mx,
@@ -2854,18 +2863,20 @@ __global__ __launch_bounds__(256) void column_zone_stats_kernel(const T* __restr
             int64_t x[4];
             if (sizeof(T) == 4) {
                 const bp_u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const bp_u32x4*>(col + b));
-                x[0] = (int32_t)q.x, x[1] = (int32_t)q.y, x[2] = (int32_t)q.z, x[3] = (int32_t)q.w;
+                x[0] = key_of<FK>((int32_t)q.x), x[1] = key_of<FK>((int32_t)q.y), x[2] = key_of<FK>((int32_t)q.z),
+                x[3] = key_of<FK>((int32_t)q.w);
             } else {
                 const u64x2 q0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(col + b));
                 const u64x2 q1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(col + b) + 1);
-                x[0] = (int64_t)q0.x, x[1] = (int64_t)q0.y, x[2] = (int64_t)q1.x, x[3] = (int64_t)q1.y;
+                x[0] = key_of<FK>((int64_t)q0.x), x[1] = key_of<FK>((int64_t)q0.y), x[2] = key_of<FK>((int64_t)q1.x),
+                x[3] = key_of<FK>((int64_t)q1.y);
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if ((vb >> j) & 1u) take(x[j]);
         } else {
             for (uint64_t r = b; r < r1; ++r)
-                if ((vb >> (r - b)) & 1u) take((int64_t)col[r]);
+                if ((vb >> (r - b)) & 1u) take((int64_t)key_of<FK>(col[r]));
         }
     }
     s_lo[t] = lo;
@@ -3009,8 +3020,8 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                 if (j < nb) {
                     const uint64_t row = wd[j] * 64 + lane;
                     if (row < n_rows)
-                        colv[j] = type == 0 ? (int64_t)static_cast<const int32_t*>(col)[row]
-                                            : static_cast<const int64_t*>(col)[row];
+                        colv[j] = value_key(type, type_is32(type) ? (int64_t)static_cast<const int32_t*>(col)[row]
+                                                                  : static_cast<const int64_t*>(col)[row]);
                     if (validity) vw[j] = validity[wd[j]];
                 }
             }
@@ -3027,7 +3038,8 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                 const int o_a = __shfl(ok_c, (int)(q & 63), 64), o_b = __shfl(ok_n, (int)(q & 63), 64);
                 const bool has_rec = lane < cnt;
                 const int64_t rrow = q < 64 ? r_a : r_b;
-                const int64_t nv = q < 64 ? v_a : v_b;
+                const int64_t nv = q < 64 ? v_a : v_b;  // as stored (FLOAT / DOUBLE: the bit pattern)
+                const int64_t nk = value_key(type, nv);  // as compared (colv holds keys too)
                 const bool nvalid = (q < 64 ? o_a : o_b) != 0;
                 const uint32_t pos = has_rec ? (uint32_t)(rrow & 63) : 0;
                 const int64_t ov = __shfl(colv[j], (int)pos, 64);  // the row's old value
@@ -3042,7 +3054,7 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                 }
                 const uint64_t vword = (old_vword & ~rec_bits) | new_bits;
                 if (has_rec) {
-                    if (type == 0) static_cast<int32_t*>(col)[rrow] = nvalid ? (int32_t)nv : 0;
+                    if (type_is32(type)) static_cast<int32_t*>(col)[rrow] = nvalid ? (int32_t)nv : 0;
                     else static_cast<int64_t*>(col)[rrow] = nvalid ? nv : 0;
                 }
                 if (validity && lane == 0) validity[word] = vword;
@@ -3050,7 +3062,7 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                 // the popcount of the record rows below it), else its old value
                 const uint64_t row = word * 64 + lane;
                 const bool mine = (rec_bits >> lane) & 1ull;
-                const int64_t from_rec = __shfl(nv, (int)__popcll(rec_bits & ((1ull << lane) - 1ull)), 64);
+                const int64_t from_rec = __shfl(nk, (int)__popcll(rec_bits & ((1ull << lane) - 1ull)), 64);
                 const bool present = row < n_rows && ((vword >> lane) & 1ull);
                 const int64_t v = present ? (mine ? from_rec : colv[j]) : 0;
                 for (int x = 0; x < 2; ++x) {
@@ -3066,13 +3078,13 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                             ra = n;
                             rb = n;
                             if (ovalid && nvalid) {
-                                const int64_t lo = ov < nv ? ov : nv, hi = ov < nv ? nv : ov;
+                                const int64_t lo = ov < nk ? ov : nk, hi = ov < nk ? nk : ov;
                                 ra = upper_key(keys, n, lo);
                                 rb = upper_key(keys, n, hi);
                             } else if (ovalid) {
                                 ra = upper_key(keys, n, ov);
                             } else if (nvalid) {
-                                ra = upper_key(keys, n, nv);
+                                ra = upper_key(keys, n, nk);
                             }
                         };
                         uint32_t a = n, b = 0;
@@ -3109,7 +3121,7 @@ __global__ __launch_bounds__(256) void merge_words_kernel(const int64_t* __restr
                             if (ix.encoding == 1) return (k > 0 && ix.keys[k - 1] == val) ? (int32_t)k - 1 : -1;
                             return (k == 0 || k == n) ? -1 : (int32_t)k - 1;
                         };
-                        const int32_t ko = has_rec ? which(ovalid, ov) : -1, kn = has_rec ? which(nvalid, nv) : -1;
+                        const int32_t ko = has_rec ? which(ovalid, ov) : -1, kn = has_rec ? which(nvalid, nk) : -1;
                         for (uint32_t jj = 0; jj < cnt; ++jj) {
                             for (int side = 0; side < 2; ++side) {
                                 const int32_t k = __shfl(side ? kn : ko, (int)jj, 64);
@@ -3340,6 +3352,15 @@ hipError_t launch_compare_bitvector(const void* col, int type, const uint64_t* v
 hipError_t launch_candidate_check(const void* col, int type, const uint64_t* validity, const uint64_t* lo_bv,
                                   const uint64_t* hi_bv, uint64_t n_rows, int cmp, int64_t constant,
                                   uint64_t* out_words, hipStream_t stream) {
+    if (type == kTypeFloat)
+        return constant >= INT32_MIN && constant <= INT32_MAX
+                   ? launch_candidate_t<int32_t, int32_t, 1>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv,
+                                                             n_rows, cmp, (int32_t)constant, out_words, stream)
+                   : launch_candidate_t<int32_t, int64_t, 1>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv,
+                                                             n_rows, cmp, constant, out_words, stream);
+    if (type == kTypeDouble)
+        return launch_candidate_t<int64_t, int64_t, 2>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
+                                                       cmp, constant, out_words, stream);
     if (type == 0 && constant >= INT32_MIN && constant <= INT32_MAX)
         return launch_candidate_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                     cmp, (int32_t)constant, out_words, stream);
@@ -3370,7 +3391,13 @@ hipError_t launch_compare_bitvectors(const void* col, int type, const uint64_t* 
 hipError_t launch_column_minmax(const void* col, int type, const uint64_t* validity, uint64_t n_rows, int64_t* out3,
                                 hipStream_t stream) {
     const dim3 grid(grid_for(n_rows, 2048)), block(256);
-    if (type == 0)
+    if (type == kTypeFloat)
+        hipLaunchKernelGGL((column_minmax_kernel<int32_t, 1>), grid, block, 0, stream, static_cast<const int32_t*>(col),
+                           validity, n_rows, out3);
+    else if (type == kTypeDouble)
+        hipLaunchKernelGGL((column_minmax_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, n_rows, out3);
+    else if (type == 0)
         hipLaunchKernelGGL(column_minmax_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
                            validity, n_rows, out3);
     else
@@ -3383,15 +3410,21 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
                            uint64_t range, uint64_t* bits, hipStream_t stream) {
     const dim3 grid(grid_for(n_rows, 2048)), block(256);
     const bool lds = range <= 65536;
-#define CUBIT_PRESENCE(T, L)                                                                                   \
-    hipLaunchKernelGGL((presence_kernel<T, L>), grid, block, 0, stream, static_cast<const T*>(col), validity, \
+#define CUBIT_PRESENCE(T, L, FK)                                                                                   \
+    hipLaunchKernelGGL((presence_kernel<T, L, FK>), grid, block, 0, stream, static_cast<const T*>(col), validity, \
                        n_rows, vmin, range, bits)
-    if (type == 0) {
-        if (lds) CUBIT_PRESENCE(int32_t, true);
-        else CUBIT_PRESENCE(int32_t, false);
+    if (type == kTypeFloat) {  // a FLOAT column's keys span less than 2^32 (a DOUBLE's are sorted on the host)
+        if (lds) CUBIT_PRESENCE(int32_t, true, 1);
+        else CUBIT_PRESENCE(int32_t, false, 1);
+    } else if (type == kTypeDouble) {
+        if (lds) CUBIT_PRESENCE(int64_t, true, 2);
+        else CUBIT_PRESENCE(int64_t, false, 2);
+    } else if (type == 0) {
+        if (lds) CUBIT_PRESENCE(int32_t, true, 0);
+        else CUBIT_PRESENCE(int32_t, false, 0);
     } else {
-        if (lds) CUBIT_PRESENCE(int64_t, true);
-        else CUBIT_PRESENCE(int64_t, false);
+        if (lds) CUBIT_PRESENCE(int64_t, true, 0);
+        else CUBIT_PRESENCE(int64_t, false, 0);
     }
 #undef CUBIT_PRESENCE
     return hipGetLastError();
@@ -3476,7 +3509,11 @@ hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hip
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream) {
     const dim3 grid(grid_for(max_n, 8192)), block(256);
-    if (type == 0)
+    // the values as stored: a FLOAT pattern zero-extended, a DOUBLE pattern as it is
+    if (type == kTypeFloat)
+        hipLaunchKernelGGL(gather_kernel<uint32_t>, grid, block, 0, stream, static_cast<const uint32_t*>(col), rowids,
+                           d_count, max_n, row_base, out);
+    else if (type == 0)
         hipLaunchKernelGGL(gather_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col), rowids,
                            d_count, max_n, row_base, out);
     else
@@ -3489,7 +3526,10 @@ hipError_t launch_gather_valid(const void* col, int type, const uint64_t* validi
                                const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* out,
                                uint64_t* out_valid, hipStream_t stream) {
     const dim3 grid(grid_for(max_n, 8192)), block(256);
-    if (type == 0)
+    if (type == kTypeFloat)
+        hipLaunchKernelGGL(gather_valid_kernel<uint32_t>, grid, block, 0, stream, static_cast<const uint32_t*>(col),
+                           validity, rowids, d_count, max_n, row_base, out, out_valid);
+    else if (type == 0)
         hipLaunchKernelGGL(gather_valid_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
                            validity, rowids, d_count, max_n, row_base, out, out_valid);
     else
@@ -3602,11 +3642,18 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
     const uint64_t nw = padded_words(n_rows);
     const CmpRange r = cmp_range(cmp, constant, 0);
     const dim3 grid(grid_for(nw / 2)), block(256);
-    if (type == 0) {
+    if (type_is32(type)) {
         int32_t lo32, hi32;
         r.clamp32(lo32, hi32);
-        hipLaunchKernelGGL(masked_compare_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
-                           validity, mask, nw, lo32, hi32, r.neg, out);
+        if (type == kTypeFloat)
+            hipLaunchKernelGGL((masked_compare_kernel<int32_t, 1>), grid, block, 0, stream,
+                               static_cast<const int32_t*>(col), validity, mask, nw, lo32, hi32, r.neg, out);
+        else
+            hipLaunchKernelGGL(masked_compare_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
+                               validity, mask, nw, lo32, hi32, r.neg, out);
+    } else if (type == kTypeDouble) {
+        hipLaunchKernelGGL((masked_compare_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, mask, nw, r.lo, r.hi, r.neg, out);
     } else {
         hipLaunchKernelGGL(masked_compare_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, mask, nw, r.lo, r.hi, r.neg, out);
@@ -3674,7 +3721,13 @@ hipError_t launch_zone_classes(const uint64_t* bv, uint64_t n_rows, uint32_t z0,
 hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* validity, uint64_t n_rows, uint32_t nz,
                                     int64_t* mn, int64_t* mx, uint8_t* fl, hipStream_t stream) {
     if (nz == 0) return hipSuccess;
-    if (type == 0)
+    if (type == kTypeFloat)
+        hipLaunchKernelGGL((column_zone_stats_kernel<int32_t, 1>), dim3(nz), dim3(256), 0, stream,
+                           static_cast<const int32_t*>(col), validity, n_rows, mn, mx, fl);
+    else if (type == kTypeDouble)
+        hipLaunchKernelGGL((column_zone_stats_kernel<int64_t, 2>), dim3(nz), dim3(256), 0, stream,
+                           static_cast<const int64_t*>(col), validity, n_rows, mn, mx, fl);
+    else if (type == 0)
         hipLaunchKernelGGL(column_zone_stats_kernel<int32_t>, dim3(nz), dim3(256), 0, stream,
                            static_cast<const int32_t*>(col), validity, n_rows, mn, mx, fl);
     else

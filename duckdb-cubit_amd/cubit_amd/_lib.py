@@ -25,6 +25,21 @@ TYPE_INT8, TYPE_INT16, TYPE_UINT8, TYPE_UINT16, TYPE_UINT32, TYPE_UINT64 = 2, 3,
 SEGMENT_TYPES = {"int8": TYPE_INT8, "int16": TYPE_INT16, "int32": TYPE_INT32, "int64": TYPE_INT64,
                  "uint8": TYPE_UINT8, "uint16": TYPE_UINT16, "uint32": TYPE_UINT32, "uint64": TYPE_UINT64,
                  "bool": TYPE_INT8}
+# FLOAT / DOUBLE columns hold IEEE bit patterns; constants, keys, update values and probed values
+# cross the ABI as those patterns in an int64 (FLOAT: the 32-bit pattern, zero-extended)
+TYPE_FLOAT, TYPE_DOUBLE = 8, 9
+COLUMN_TYPES = dict(SEGMENT_TYPES, float32=TYPE_FLOAT, float64=TYPE_DOUBLE)
+
+
+def fp_bits(values, type_: int):
+    """Values of a FLOAT / DOUBLE column as the int64 bit patterns the ABI carries; other types'
+    values as int64."""
+    import numpy as _np
+    if type_ == TYPE_FLOAT:
+        return _np.ascontiguousarray(_np.asarray(values, dtype=_np.float32)).view(_np.uint32).astype(_np.int64)
+    if type_ == TYPE_DOUBLE:
+        return _np.ascontiguousarray(_np.asarray(values, dtype=_np.float64)).view(_np.int64)
+    return _np.ascontiguousarray(_np.asarray(values, dtype=_np.int64))
 CMP_EQ, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE = range(6)
 FILTER_CONSTANT, FILTER_IS_NULL, FILTER_IS_NOT_NULL, FILTER_OR, FILTER_AND = range(5)
 INDEX_RANGE, INDEX_EQUALITY, INDEX_BINS = 0, 1, 2

@@ -176,11 +176,12 @@ class CubitTable:
 
     def add_column(self, col: int, data: np.ndarray, validity: Optional[np.ndarray] = None) -> None:
         """Register a column of any integral dtype: int32 / int64 as they are, the narrower and
-        unsigned ones widened by the library into an INT32 / INT64 column (uint64 below 2^63)."""
+        unsigned ones widened by the library into an INT32 / INT64 column (uint64 below 2^63);
+        float32 / float64 as a FLOAT / DOUBLE column (DuckDB's floating-point comparisons)."""
         data = np.ascontiguousarray(data)
-        if data.dtype.name not in L.SEGMENT_TYPES:
+        if data.dtype.name not in L.COLUMN_TYPES:
             raise TypeError(f"unsupported dtype {data.dtype}")
-        t = L.SEGMENT_TYPES[data.dtype.name]
+        t = L.COLUMN_TYPES[data.dtype.name]
         assert data.shape[0] == self.n_rows
         vptr = None
         if validity is not None:
@@ -214,7 +215,8 @@ class CubitTable:
 
     def download_column(self, col: int) -> np.ndarray:
         ptr, typ = self.column_data(col)
-        out = np.empty(self.n_rows, dtype=np.int32 if typ == L.TYPE_INT32 else np.int64)
+        dt = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64}.get(typ, np.int64)
+        out = np.empty(self.n_rows, dtype=dt)
         if self.n_rows:
             L.check(self.lib.cubit_memcpy_d2h(self.ctx.handle, out.ctypes.data, C.c_void_p(ptr), out.nbytes))
         return out
@@ -225,8 +227,11 @@ class CubitTable:
         self.types[col] = type_
 
     def build_index(self, col: int, encoding: int = L.INDEX_RANGE, keys: Optional[Sequence[int]] = None) -> None:
-        if keys:
-            k = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+        if keys is not None and len(keys):
+            # FLOAT / DOUBLE columns: keys given as floats cross as their bit patterns
+            typ = self.types.get(col)
+            is_fp = typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(keys).dtype.kind == "f"
+            k = L.fp_bits(keys, typ) if is_fp else np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
             L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, k.ctypes.data, len(k)))
         else:
             L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, None, 0))
@@ -260,6 +265,9 @@ class CubitTable:
         """Update records (row, value, version), chronological. valid (bool per record, optional):
         False = the record sets the row NULL (cubit_table_set_updates_nullable)."""
         rows = np.ascontiguousarray(rows, dtype=np.int64)
+        typ = self.types.get(col)
+        if typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(values).dtype.kind == "f":
+            values = L.fp_bits(values, typ)  # FLOAT / DOUBLE values cross as their bit patterns
         values = np.ascontiguousarray(values, dtype=np.int64)
         versions = np.ascontiguousarray(versions, dtype=np.uint64)
         if valid is None:
@@ -282,7 +290,8 @@ class CubitTable:
         keep = []
         for c in cols:
             a = np.ascontiguousarray(columns[c])
-            want = np.int32 if self.types.get(c) == L.TYPE_INT32 else np.int64
+            want = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64}.get(
+                self.types.get(c), np.int64)
             if a.dtype != want or len(a) != n_new:
                 raise ValueError(f"column {c}: {len(a)} values of {a.dtype}, want {n_new} of {np.dtype(want)}")
             keep.append(a)

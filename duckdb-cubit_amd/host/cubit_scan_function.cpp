@@ -426,10 +426,18 @@ void PlanWidths(PartScan& P, const std::vector<column_t>& column_ids, const std:
             lo = P.part.row_base;
             hi = P.part.row_base + (int64_t)P.part.n_rows - 1;
         } else {
-            int hn = 0, hv = 0;
+            int hn = 0, hv = 0, type = 0;
+            const void* data = nullptr;
             check(cubit_table_column_statistics(P.part.table, (int)col, &lo, &hi, &hn, &hv),
                   "cubit_table_column_statistics");
+            check(cubit_table_column_data(P.part.table, (int)col, &data, &type), "cubit_table_column_data");
             P.nullable[e] = hn != 0;
+            // FLOAT: the 32-bit patterns (zero-extended) cross as 4 bytes; DOUBLE: the 8-byte patterns
+            if (type == CUBIT_TYPE_DOUBLE) continue;
+            if (type == CUBIT_TYPE_FLOAT) {
+                lo = 0;
+                hi = 0xffffffffll;
+            }
             if (P.nullable[e]) {
                 lo = std::min<int64_t>(lo, 0);
                 hi = std::max<int64_t>(hi, 0);
@@ -968,12 +976,16 @@ bool CubitScanStatistics(const FunctionData* bind_data, column_t column_id, Colu
     out = ColumnStatistics{};
     for (const CubitPartition& part : bind.parts) {
         int64_t mn = 0, mx = 0;
-        int hn = 0, hv = 0;
+        int hn = 0, hv = 0, type = 0;
+        const void* data = nullptr;
         check(cubit_table_column_statistics(part.table, (int)column_id, &mn, &mx, &hn, &hv),
               "cubit_table_column_statistics");
+        check(cubit_table_column_data(part.table, (int)column_id, &data, &type), "cubit_table_column_data");
         if (hv) {
-            out.min = out.has_no_null ? std::min(out.min, mn) : mn;
-            out.max = out.has_no_null ? std::max(out.max, mx) : mx;
+            // FLOAT / DOUBLE bounds are bit patterns: ordered by their comparison keys
+            auto less = [type](int64_t a, int64_t b) { return cubit_fp_key(type, a) < cubit_fp_key(type, b); };
+            out.min = out.has_no_null ? std::min(out.min, mn, less) : mn;
+            out.max = out.has_no_null ? std::max(out.max, mx, less) : mx;
             out.has_no_null = true;
         }
         out.has_null = out.has_null || hn != 0;

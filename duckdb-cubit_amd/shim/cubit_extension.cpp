@@ -229,10 +229,12 @@ static void Check(int rc) {
 
 // ------------------------------------------------------------------ filters
 
-// Physical types whose values the GPU compares exactly as int64: the signed integers up to
-// 64 bits (DATE, TIME, TIMESTAMP*, DECIMAL(≤18) included), BOOLEAN and the unsigned integers
-// up to 32 bits. UBIGINT, HUGEINT, UHUGEINT, FLOAT, DOUBLE and VARCHAR stay on seq_scan.
-static bool IntegerPhysical(PhysicalType t) {
+// Physical types whose values the GPU compares exactly, carried as int64: the signed integers up
+// to 64 bits (DATE, TIME, TIMESTAMP*, DECIMAL(≤18) included), BOOLEAN, the unsigned integers up to
+// 32 bits, and FLOAT / DOUBLE as their bit patterns (the library compares them with DuckDB's
+// floating-point operators, include/cubit_gpu.h). UBIGINT, HUGEINT, UHUGEINT and VARCHAR stay on
+// seq_scan.
+static bool GpuPhysical(PhysicalType t) {
     switch (t) {
     case PhysicalType::BOOL:
     case PhysicalType::INT8:
@@ -242,22 +244,47 @@ static bool IntegerPhysical(PhysicalType t) {
     case PhysicalType::UINT8:
     case PhysicalType::UINT16:
     case PhysicalType::UINT32:
+    case PhysicalType::FLOAT:
+    case PhysicalType::DOUBLE:
         return true;
     default:
         return false;
     }
 }
 
-// uploaded as CUBIT_TYPE_INT64 (else CUBIT_TYPE_INT32)
+// uploaded from 8-byte values (INT64, UINT32 widened, DOUBLE patterns; else from 4-byte ones)
 static bool WidePhysical(PhysicalType t) {
-    return t == PhysicalType::INT64 || t == PhysicalType::UINT32;
+    return t == PhysicalType::INT64 || t == PhysicalType::UINT32 || t == PhysicalType::DOUBLE;
+}
+
+// the CUBIT_TYPE_* a column is registered as
+static int UploadType(PhysicalType t) {
+    switch (t) {
+    case PhysicalType::FLOAT:
+        return CUBIT_TYPE_FLOAT;
+    case PhysicalType::DOUBLE:
+        return CUBIT_TYPE_DOUBLE;
+    default:
+        return WidePhysical(t) ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32;
+    }
+}
+
+static uint32_t FloatBits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+static int64_t DoubleBits(double d) {
+    int64_t b;
+    memcpy(&b, &d, 8);
+    return b;
 }
 
 static bool Supported(const TableFilter &f) {
     switch (f.filter_type) {
     case TableFilterType::CONSTANT_COMPARISON: {
         auto &c = f.Cast<ConstantFilter>();
-        if (!IntegerPhysical(c.constant.type().InternalType())) {
+        if (!GpuPhysical(c.constant.type().InternalType())) {
             return false;
         }
         switch (c.comparison_type) {
@@ -311,6 +338,10 @@ static int64_t PhysicalAsInt64(Vector &v, idx_t i) {
         return FlatVector::GetData<int16_t>(v)[i];
     case PhysicalType::INT32:
         return FlatVector::GetData<int32_t>(v)[i];
+    case PhysicalType::FLOAT:
+        return FloatBits(FlatVector::GetData<float>(v)[i]);  // the pattern, zero-extended
+    case PhysicalType::DOUBLE:
+        return DoubleBits(FlatVector::GetData<double>(v)[i]);
     default:
         return FlatVector::GetData<int64_t>(v)[i];
     }
@@ -332,6 +363,10 @@ static int64_t ConstantAsInt64(const Value &v) {
         return v.GetValueUnsafe<int16_t>();
     case PhysicalType::INT32:
         return v.GetValueUnsafe<int32_t>();  // DATE days, INTEGER, DECIMAL(≤9)
+    case PhysicalType::FLOAT:
+        return FloatBits(v.GetValueUnsafe<float>());
+    case PhysicalType::DOUBLE:
+        return DoubleBits(v.GetValueUnsafe<double>());
     default:
         return v.GetValueUnsafe<int64_t>();  // BIGINT, DECIMAL(10..18) scaled
     }
@@ -584,6 +619,14 @@ static void CopyOut(const int64_t *src, Vector &dst, idx_t n) {
         }
         break;
     }
+    case PhysicalType::FLOAT: {  // the 32-bit patterns back into the floats (DOUBLE: the 8-byte copy below)
+        auto d = FlatVector::GetData<float>(dst);
+        for (idx_t i = 0; i < n; i++) {
+            const uint32_t u = (uint32_t)src[i];
+            memcpy(d + i, &u, 4);
+        }
+        break;
+    }
     default:
         memcpy(FlatVector::GetData<int64_t>(dst), src, n * sizeof(int64_t));
         break;
@@ -693,8 +736,20 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
     const auto &type = bind.table.GetColumn(LogicalIndex(column_id)).GetType();
     auto stats = BaseStatistics::CreateEmpty(type);
     if (has_no_null) {
-        NumericStats::SetMin(stats, Value::Numeric(type, lo));  // DECIMAL: lo is the storage value
-        NumericStats::SetMax(stats, Value::Numeric(type, hi));
+        const auto phys = type.InternalType();
+        if (phys == PhysicalType::FLOAT || phys == PhysicalType::DOUBLE) {  // bit patterns
+            float f[2];
+            double d[2];
+            const uint32_t u[2] = {(uint32_t)lo, (uint32_t)hi};
+            memcpy(f, u, sizeof(f));
+            memcpy(&d[0], &lo, 8);
+            memcpy(&d[1], &hi, 8);
+            NumericStats::SetMin(stats, phys == PhysicalType::FLOAT ? Value::FLOAT(f[0]) : Value::DOUBLE(d[0]));
+            NumericStats::SetMax(stats, phys == PhysicalType::FLOAT ? Value::FLOAT(f[1]) : Value::DOUBLE(d[1]));
+        } else {
+            NumericStats::SetMin(stats, Value::Numeric(type, lo));  // DECIMAL: lo is the storage value
+            NumericStats::SetMax(stats, Value::Numeric(type, hi));
+        }
         stats.SetHasNoNull();
     }
     if (has_null) {
@@ -1171,7 +1226,7 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
                 if (!wide) {
                     narrow.assign(snap.values[c].begin() + b, snap.values[c].begin() + e);
                 }
-                Check(cubit_table_add_column(t, (int)col, wide ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32,
+                Check(cubit_table_add_column(t, (int)col, UploadType(attached.columns[col]),
                                              wide ? (const void *)(snap.values[c].data() + b) : (const void *)narrow.data(),
                                              valid, 0));
             }
@@ -1387,8 +1442,12 @@ static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string
                 StringUtil::Trim(lit);
                 ix.keys.push_back(ConstantAsInt64(Value(lit).DefaultCastAs(def.GetType())));
             }
-            std::sort(ix.keys.begin(), ix.keys.end());
-            ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end()), ix.keys.end());
+            // ascending in the column's order (FLOAT / DOUBLE patterns by their comparison keys)
+            const int type = UploadType(def.GetType().InternalType());
+            auto key = [type](int64_t v) { return cubit_fp_key(type, v); };
+            std::sort(ix.keys.begin(), ix.keys.end(), [&](int64_t a, int64_t b) { return key(a) < key(b); });
+            ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end(), [&](int64_t a, int64_t b) { return key(a) == key(b); }),
+                          ix.keys.end());
         }
         if (ix.encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) {
             throw InvalidInputException("cubit_attach: bins on %s need at least two edges", name);
@@ -1435,8 +1494,8 @@ static void CubitAttachImpl(ClientContext &context, const string &table_name, co
             StringUtil::Trim(name);
             const auto &def = duck.GetColumn(name);
             const auto phys = def.GetType().InternalType();
-            if (!IntegerPhysical(phys)) {
-                throw InvalidInputException("cubit_attach: column %s is not integer-backed", name);
+            if (!GpuPhysical(phys)) {
+                throw InvalidInputException("cubit_attach: column %s is not integer-, FLOAT- or DOUBLE-backed", name);
             }
             attached.columns[def.StorageOid()] = phys;
             attached.column_order.push_back(def.StorageOid());

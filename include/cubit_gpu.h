@@ -52,6 +52,38 @@ extern "C" {
 #define CUBIT_TYPE_UINT16 5
 #define CUBIT_TYPE_UINT32 6
 #define CUBIT_TYPE_UINT64 7
+/* FLOAT / DOUBLE (PhysicalType::FLOAT / DOUBLE): the column holds the IEEE bit patterns as DuckDB's
+ * vectors do, and every value crossing the ABI — filter constants, index keys, update values,
+ * statistics, probed values — is a bit pattern carried in an int64 (FLOAT: the 32-bit pattern,
+ * zero-extended). Comparisons follow DuckDB's floating-point operators
+ * (src/common/vector_operations/comparison_operators.cpp:17-88, src/include/duckdb/common/
+ * operator/comparison_operators.hpp:100-146): NaN equals NaN and is greater than every other value,
+ * -0.0 equals +0.0. The library compares through cubit_fp_key below, an order-preserving map of the
+ * patterns onto signed integers under which those operators are plain integer comparisons. */
+#define CUBIT_TYPE_FLOAT 8
+#define CUBIT_TYPE_DOUBLE 9
+
+/* The comparison key of a FLOAT / DOUBLE bit pattern (any other type: the value itself): every
+ * NaN → one key above +inf's, -x → -(pattern of x) (so -0.0 and +0.0 share key 0), +x → its pattern.
+ * cubit_fp_value is its inverse on keys (a NaN key → the positive quiet NaN, key 0 → +0.0). */
+static inline int64_t cubit_fp_key(int type, int64_t bits) {
+    if (type == CUBIT_TYPE_FLOAT) {
+        const uint32_t u = (uint32_t)bits, mag = u & 0x7fffffffu;
+        if (mag > 0x7f800000u) return 0x7fc00000;
+        return (u >> 31) ? -(int64_t)mag : (int64_t)mag;
+    }
+    if (type == CUBIT_TYPE_DOUBLE) {
+        const uint64_t u = (uint64_t)bits, mag = u & 0x7fffffffffffffffull;
+        if (mag > 0x7ff0000000000000ull) return (int64_t)0x7ff8000000000000ull;
+        return (u >> 63) ? -(int64_t)mag : (int64_t)mag;
+    }
+    return bits;
+}
+static inline int64_t cubit_fp_value(int type, int64_t key) {
+    if (type == CUBIT_TYPE_FLOAT) return key < 0 ? (int64_t)(0x80000000u | (uint32_t)(-key)) : key;
+    if (type == CUBIT_TYPE_DOUBLE) return key < 0 ? (int64_t)(0x8000000000000000ull | (uint64_t)(-key)) : key;
+    return key;
+}
 
 /* ---- comparison (ExpressionType COMPARE_* used by ConstantFilter,
  *      src/planner/filter/constant_filter.cpp) */

@@ -12,7 +12,9 @@ ROOT = Path(__file__).resolve().parent.parent
 def declared(header):
     text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(cubit_\w+)\s*\(", text, flags=re.M))
+    # header-only helpers (static inline) are not library symbols
+    inline = set(re.findall(r"^static\s+inline\b[\w\s\*]*?\b(cubit_\w+)\s*\(", text, flags=re.M))
+    return set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(cubit_\w+)\s*\(", text, flags=re.M)) - inline
 
 
 def test_every_declared_symbol_is_exported():

@@ -411,6 +411,46 @@ def test_window_transfer_compaction_round_trips(ctx):
     t.close()
 
 
+@pytest.mark.parametrize("tasks", [1, 4])
+def test_float_and_double_columns_through_table_function(ctx, tasks):
+    """FLOAT / DOUBLE filter and projection columns (DuckDB's floating-point comparisons: NaN
+    greatest and equal to NaN, -0.0 == +0.0): the filter on a DOUBLE column and on a FLOAT one
+    equals the oracle's scan, and every projected row hands back the stored bit pattern (FLOAT
+    crossing as 4 bytes, DOUBLE as 8; -0.0 and NaN payloads intact) with its NULL-ness."""
+    from cubit_amd.datagen import validity_from_mask
+
+    n = 900_001
+    rng = np.random.default_rng(41)
+    special = [0.0, -0.0, np.inf, -np.inf, np.nan, 1.5, -1.5]
+    d = (rng.standard_normal(n) * 100).astype(np.float64)
+    d[rng.integers(0, n, 5000)] = np.array(special)[rng.integers(0, len(special), 5000)]
+    d[7] = np.array([0xFFF8000000000123], dtype=np.uint64).view(np.float64)[0]  # a negative NaN with payload
+    f = (rng.standard_normal(n) * 10).astype(np.float32)
+    f[rng.integers(0, n, 5000)] = np.array(special, dtype=np.float32)[rng.integers(0, len(special), 5000)]
+    fvalid = rng.random(n) > 0.03
+    t = CubitTable(ctx, n)
+    t.add_column(0, d)
+    t.add_column(1, f, validity_from_mask(fvalid))
+    t.build_index(1, L.INDEX_RANGE, np.array([-10.0, -1.0, 0.0, 1.0, 10.0], dtype=np.float32))
+    cols = [O.Column(d), O.Column(f, validity_from_mask(fvalid))]
+    for fs in [F.TableFilterSet({0: F.ConstantFilter(">=", 150.0)}),
+               F.TableFilterSet({0: F.ConstantFilter("=", np.nan)}),
+               F.TableFilterSet({0: F.ConjunctionAndFilter([F.ConstantFilter(">", -5.0), F.ConstantFilter("<=", 5.0)]),
+                                 1: F.ConstantFilter("!=", np.float32(-0.0))}),
+               F.TableFilterSet({1: F.ConjunctionOrFilter([F.ConstantFilter("<", np.float32(-9.5)),
+                                                           F.ConstantFilter("=", np.float32(0.0))])})]:
+        keep = O.table_scan(cols, F.serialize(fs), n)
+        fn = CubitScanFunction(t, [ROW_ID, 0, 1], [0, 1, 2], fs)
+        chunks = drain(fn, tasks, validity=True)
+        fn.close()
+        assert np.array_equal(ordered(chunks, 0), keep)
+        assert np.array_equal(ordered(chunks, 1), O.fetch(cols[0], keep))
+        fv, fok = O.fetch(cols[1], keep, with_valid=True)
+        assert np.array_equal(ordered(chunks, 2), fv)
+        assert np.array_equal(ordered(chunks, 5), fok)
+    t.close()
+
+
 def test_compaction_overflow_falls_back_to_8_byte_values(ctx, monkeypatch):
     """The device checks the compaction bound as it narrows: with every compacted column's offset
     moved one above its minimum (CUBIT_SCAN_TEST_SHIFT_OFFSET), the groups (staged) or the
