@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
@@ -1081,8 +1082,32 @@ struct DevBuf {
     }
 };
 
+// A VARCHAR column's dictionary: its distinct strings in DuckDB's string order
+// (string_type.hpp:143-206: the bytes as unsigned — std::string_view's order — then the length,
+// a prefix before its extensions), string `code` = bytes[offs[code], offs[code + 1]).
+struct DictData {
+    std::vector<char> bytes;
+    std::vector<uint64_t> offs{0};
+    uint64_t size() const { return offs.size() - 1; }
+    std::string_view at(uint64_t code) const {
+        return std::string_view(bytes.data() + offs[code], offs[code + 1] - offs[code]);
+    }
+    // the first code whose string is >= s (size() when none), and whether it is s
+    uint64_t lower_bound(std::string_view s, bool* present) const {
+        uint64_t lo = 0, hi = size();
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (at(mid) < s) lo = mid + 1;
+            else hi = mid;
+        }
+        *present = lo < size() && at(lo) == s;
+        return lo;
+    }
+};
+
 struct Column {
     int type = 0;
+    std::shared_ptr<const DictData> dict;  // VARCHAR: the dictionary its codes index
     const void* data = nullptr;        // device
     const uint64_t* validity = nullptr;  // device, padded to the table's cap_words (null = no NULLs)
     uint64_t cap_rows = 0;  // rows the owned data buffer holds (0 = caller-owned device data)
@@ -1352,6 +1377,7 @@ bool storage_of(int type, int& col_type, uint64_t& src_size) {
     case CUBIT_TYPE_UINT64: col_type = CUBIT_TYPE_INT64, src_size = 8; return true;
     case CUBIT_TYPE_FLOAT: col_type = CUBIT_TYPE_FLOAT, src_size = 4; return true;
     case CUBIT_TYPE_DOUBLE: col_type = CUBIT_TYPE_DOUBLE, src_size = 8; return true;
+    case CUBIT_TYPE_VARCHAR: col_type = CUBIT_TYPE_VARCHAR, src_size = 4; return true;  // codes
     default: return false;
     }
 }
@@ -1397,7 +1423,7 @@ int widen_column(cubit_table* t, Column& c, int type, const void* data, const ui
 }
 
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && type != CUBIT_TYPE_VARCHAR && !type_is_fp(type))
         return widen_column(t, c, type, data, validity, on_device);
     const uint64_t esz = type_is32(type) ? 4 : 8;  // FLOAT / DOUBLE: the bit patterns as they are
     if (t->n_rows == 0) {  // empty partition: nothing to copy
@@ -1435,7 +1461,10 @@ constexpr size_t kMaxWideDistinct = 1 << 16;
 // below 2^32, else by sorting the valid values on the host.
 int value_stats(cubit_table* t, const void* data, int type, const uint64_t* validity, uint64_t n,
                 std::vector<int64_t>& distinct, bool want_distinct, int64_t& vmin, int64_t& vmax, bool& any) {
-    const Column c{type, data, validity};
+    Column c;
+    c.type = type;
+    c.data = data;
+    c.validity = validity;
     DevBuf stats;
     if (hipMalloc(&stats.p, 3 * sizeof(int64_t)) != hipSuccess) return fail(CUBIT_ERR_OOM, "stats allocation failed");
     int64_t h[3] = {INT64_MAX, INT64_MIN, 0};
@@ -1550,6 +1579,8 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     int col_type = 0;
     uint64_t src_size = 0;
     if (!storage_of(type, col_type, src_size)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (type == CUBIT_TYPE_VARCHAR)
+        return fail(CUBIT_ERR_INVALID, "a VARCHAR column is registered with its dictionary (cubit_table_add_dict_column)");
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (int rc = set_device(t->ctx)) return rc;
     Column c;
@@ -1560,6 +1591,121 @@ extern "C" int cubit_table_add_column(cubit_table* t, int col, int type, const v
     t->bins.erase(col);
     return CUBIT_OK;
 }
+
+// ------------------------------------------------------------------ VARCHAR dictionaries
+
+struct cubit_dict {
+    std::shared_ptr<const DictData> d;
+};
+
+extern "C" int cubit_dict_create(const char* bytes, const uint64_t* offsets, uint64_t n, cubit_dict** out) {
+    if (!out || (n && (!offsets || (!bytes && offsets[n] > offsets[0])))) return fail(CUBIT_ERR_INVALID, "null argument");
+    std::vector<std::string_view> v;
+    v.reserve(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) return fail(CUBIT_ERR_INVALID, "offsets descend at string %llu", (unsigned long long)i);
+        v.emplace_back(bytes + offsets[i], offsets[i + 1] - offsets[i]);
+    }
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    if (v.size() > (uint64_t)INT32_MAX) return fail(CUBIT_ERR_UNSUPPORTED, "%zu distinct strings exceed 2^31 - 1", v.size());
+    auto d = std::make_shared<DictData>();
+    uint64_t total = 0;
+    for (auto sv : v) total += sv.size();
+    d->bytes.reserve(total);
+    d->offs.reserve(v.size() + 1);
+    for (auto sv : v) {
+        d->bytes.insert(d->bytes.end(), sv.begin(), sv.end());
+        d->offs.push_back(d->bytes.size());
+    }
+    *out = new cubit_dict{std::move(d)};
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_dict_destroy(cubit_dict* d) {
+    delete d;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_dict_size(const cubit_dict* d, uint64_t* n) {
+    if (!d || !n) return fail(CUBIT_ERR_INVALID, "null argument");
+    *n = d->d->size();
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_dict_entry(const cubit_dict* d, uint64_t code, const char** data, uint64_t* size) {
+    if (!d || !data || !size) return fail(CUBIT_ERR_INVALID, "null argument");
+    if (code >= d->d->size()) return fail(CUBIT_ERR_INVALID, "code %llu past the dictionary's %llu strings",
+                                          (unsigned long long)code, (unsigned long long)d->d->size());
+    const std::string_view sv = d->d->at(code);
+    *data = sv.data();
+    *size = sv.size();
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_dict_encode(const cubit_dict* d, const char* bytes, const uint64_t* offsets, uint64_t n,
+                                 const uint64_t* validity, int32_t* codes) {
+    if (!d || (n && (!offsets || !codes))) return fail(CUBIT_ERR_INVALID, "null argument");
+    for (uint64_t i = 0; i < n; ++i) {
+        if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) {
+            codes[i] = 0;
+            continue;
+        }
+        if (offsets[i + 1] < offsets[i]) return fail(CUBIT_ERR_INVALID, "offsets descend at string %llu", (unsigned long long)i);
+        bool present = false;
+        const uint64_t c = d->d->lower_bound(std::string_view(bytes + offsets[i], offsets[i + 1] - offsets[i]), &present);
+        if (!present) return fail(CUBIT_ERR_UNSUPPORTED, "string %llu is not in the dictionary", (unsigned long long)i);
+        codes[i] = (int32_t)c;
+    }
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_dict_lookup(const cubit_dict* d, const char* data, uint64_t size, uint64_t* lower_bound,
+                                 int* present) {
+    if (!d || !lower_bound || (size && !data)) return fail(CUBIT_ERR_INVALID, "null argument");
+    bool p = false;
+    *lower_bound = d->d->lower_bound(std::string_view(data ? data : "", size), &p);
+    if (present) *present = p ? 1 : 0;
+    return CUBIT_OK;
+}
+
+extern "C" int cubit_table_add_dict_column(cubit_table* t, int col, cubit_dict* d, const int32_t* codes,
+                                           const uint64_t* validity, int on_device) {
+    if (!t || !d || (!codes && t->n_rows)) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (int rc = set_device(t->ctx)) return rc;
+    Column c;
+    if (int rc = copy_column(t, c, CUBIT_TYPE_VARCHAR, codes, validity, on_device)) return rc;
+    c.dict = d->d;
+    if (t->n_rows) {  // every valid code names a dictionary string
+        std::vector<int64_t> unused;
+        int64_t vmin = 0, vmax = 0;
+        bool any = false;
+        if (int rc = value_stats(t, c.data, CUBIT_TYPE_VARCHAR, c.validity, t->n_rows, unused, false, vmin, vmax, any))
+            return rc;
+        if (any && (vmin < 0 || (uint64_t)vmax >= c.dict->size()))
+            return fail(CUBIT_ERR_INVALID, "code %lld outside the dictionary's %llu strings",
+                        (long long)(vmin < 0 ? vmin : vmax), (unsigned long long)c.dict->size());
+    }
+    t->cols[col] = std::move(c);
+    drop_patches(t, col);
+    t->idx.erase(col);
+    t->bins.erase(col);
+    return CUBIT_OK;
+}
+
+namespace {
+// codes handed to a VARCHAR column (updates, appends): each valid one must name a dictionary string
+int check_codes(const Column& c, const int64_t* v, const uint8_t* valid, uint64_t n) {
+    if (c.type != CUBIT_TYPE_VARCHAR) return CUBIT_OK;
+    for (uint64_t i = 0; i < n; ++i)
+        if ((!valid || valid[i]) && (v[i] < 0 || (uint64_t)v[i] >= c.dict->size()))
+            return fail(CUBIT_ERR_INVALID, "code %lld outside the dictionary's %llu strings", (long long)v[i],
+                        (unsigned long long)c.dict->size());
+    return CUBIT_OK;
+}
+}  // namespace
 
 // The segments' T (a CUBIT_TYPE_* code): its byte size and signedness, the column type its
 // values widen to and the BpGroup::tnorm that carries T's arithmetic there.
@@ -1758,6 +1904,19 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     if (n && type_is_fp(c.type)) {
         keyed.resize(n);
         for (uint32_t k = 0; k < n; ++k) keyed[k] = value_key(c.type, values[k]);
+        values = keyed.data();
+    }
+    // a VARCHAR column's keys are given as addresses of cubit_strings and held as the code bound
+    // each names (the first code whose string is >= the key: exact for every key of RANGE and BINS,
+    // and an EQUALITY key absent from the dictionary becomes a bitvector of its neighbour's code)
+    if (n && c.type == CUBIT_TYPE_VARCHAR) {
+        keyed.resize(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            const cubit_string* str = reinterpret_cast<const cubit_string*>((intptr_t)values[k]);
+            if (!str || (str->size && !str->data)) return fail(CUBIT_ERR_INVALID, "VARCHAR key %u is not a cubit_string", k);
+            bool present = false;
+            keyed[k] = (int64_t)c.dict->lower_bound(std::string_view(str->data ? str->data : "", str->size), &present);
+        }
         values = keyed.data();
     }
     Index ix;
@@ -2085,6 +2244,7 @@ extern "C" int cubit_table_set_updates(cubit_table* t, int col, const int64_t* r
     if (int rc = set_device(t->ctx)) return rc;
     for (uint64_t i = 0; i < n; ++i)
         if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
+    if (int rc = check_codes(t->cols.at(col), values, nullptr, n)) return rc;
     return store_updates(t, col, rows, values, versions, n);
 }
 
@@ -2118,6 +2278,7 @@ extern "C" int cubit_table_set_updates_nullable(cubit_table* t, int col, const i
         if (rows[i] < 0 || (uint64_t)rows[i] >= t->n_rows) return fail(CUBIT_ERR_INVALID, "update row out of range");
         any_null |= valid && !valid[i];
     }
+    if (int rc = check_codes(cit->second, values, valid, n)) return rc;
     if (any_null)
         if (int rc = ensure_validity(t, cit->second)) return rc;
     return store_updates(t, col, rows, values, versions, n, any_null ? valid : nullptr);
@@ -2291,6 +2452,14 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
         if (!t->cols.count(cols[i])) return fail(CUBIT_ERR_INVALID, "column %d not registered", cols[i]);
         if (!data[i]) return fail(CUBIT_ERR_INVALID, "column %d: null data", cols[i]);
         if (!at.emplace(cols[i], i).second) return fail(CUBIT_ERR_INVALID, "column %d given twice", cols[i]);
+        const Column& c = t->cols.at(cols[i]);
+        if (c.type == CUBIT_TYPE_VARCHAR) {  // the appended codes name dictionary strings (NULL rows: any)
+            const int32_t* codes = static_cast<const int32_t*>(data[i]);
+            const uint64_t* vw = validity ? validity[i] : nullptr;
+            for (uint64_t r = 0; r < n_new; ++r)
+                if ((!vw || ((vw[r >> 6] >> (r & 63)) & 1ull)) && (codes[r] < 0 || (uint64_t)codes[r] >= c.dict->size()))
+                    return fail(CUBIT_ERR_INVALID, "column %d: appended code %d outside the dictionary", cols[i], codes[r]);
+        }
     }
     if (int rc = set_device(t->ctx)) return rc;
     hipStream_t s = t->ctx->stream;
@@ -3629,16 +3798,40 @@ bool cmp_interval(int cmp, int64_t c, double* lo, double* hi) {
 struct KeyedNodes {
     std::vector<cubit_filter_node> buf;
     const cubit_filter_node* p;
+    int rc = CUBIT_OK;
     KeyedNodes(const cubit_table* t, const cubit_filter_node* nodes, uint32_t n) : p(nodes) {
         for (uint32_t k = 0; k < n; ++k) {
             if (nodes[k].kind != CUBIT_FILTER_CONSTANT) continue;
             auto it = t->cols.find(nodes[k].column);
-            if (it == t->cols.end() || !type_is_fp(it->second.type)) continue;
+            if (it == t->cols.end() || (!type_is_fp(it->second.type) && it->second.type != CUBIT_TYPE_VARCHAR)) continue;
             if (buf.empty()) {
                 buf.assign(nodes, nodes + n);
                 p = buf.data();
             }
-            buf[k].constant = value_key(it->second.type, nodes[k].constant);
+            if (it->second.type != CUBIT_TYPE_VARCHAR) {
+                buf[k].constant = value_key(it->second.type, nodes[k].constant);
+                continue;
+            }
+            // a string constant → a comparison of codes with the same rows: lb = the first code whose
+            // string is >= s; s absent: = matches nothing (code -1), != every valid row, <= is < lb,
+            // > is >= lb
+            const cubit_string* str = reinterpret_cast<const cubit_string*>((intptr_t)nodes[k].constant);
+            if (!str || (str->size && !str->data)) {
+                rc = fail(CUBIT_ERR_INVALID, "filter node %u: a VARCHAR constant must be a cubit_string", k);
+                return;
+            }
+            bool present = false;
+            const int64_t lb =
+                (int64_t)it->second.dict->lower_bound(std::string_view(str->data ? str->data : "", str->size), &present);
+            int cmp = nodes[k].cmp;
+            int64_t c = lb;
+            if (!present) {
+                if (cmp == CUBIT_CMP_EQ || cmp == CUBIT_CMP_NE) c = -1;
+                else if (cmp == CUBIT_CMP_LE) cmp = CUBIT_CMP_LT;
+                else if (cmp == CUBIT_CMP_GT) cmp = CUBIT_CMP_GE;
+            }
+            buf[k].cmp = cmp;
+            buf[k].constant = c;
         }
     }
 };
@@ -3722,6 +3915,7 @@ extern "C" int cubit_table_estimate_rows(cubit_table* t, const cubit_filter_node
     int rc = CUBIT_OK;
     uint32_t i = 0;
     const KeyedNodes keyed(t, nodes, n_nodes);
+    if (keyed.rc) return keyed.rc;
     const double s = std::min(1.0, std::max(0.0, tree_selectivity(t, keyed.p, i, &rc)));
     if (rc) return rc;
     *rows = std::min<uint64_t>(t->n_rows, (uint64_t)std::ceil(s * (double)t->n_rows));
@@ -3752,6 +3946,7 @@ int plan_program(cubit_table* t, const cubit_filter_node* nodes, uint32_t n_node
         e = mk_true();
     } else {
         const KeyedNodes keyed(t, nodes, n_nodes);
+        if (keyed.rc) return keyed.rc;
         Planner p{t, keyed.p, n_nodes};
         if (p.subtree_end(0) != (int)n_nodes) return fail(CUBIT_ERR_INVALID, "malformed filter tree");
         e = p.plan(0);

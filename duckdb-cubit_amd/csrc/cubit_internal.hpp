@@ -51,8 +51,12 @@ inline uint32_t prog_nops(const EvalProgram& p, int k) { return (p.nops >> (4 * 
 // (4 / 8 bytes) compared through their order key (cubit_fp_key, include/cubit_gpu.h: NaN one key
 // above +inf, -x → -pattern(x), so -0.0 == +0.0 — DuckDB's floating-point operators,
 // comparison_operators.hpp:100-146). Type codes as in cubit_gpu.h.
-constexpr int kTypeInt32 = 0, kTypeInt64 = 1, kTypeFloat = 8, kTypeDouble = 9;
-__host__ __device__ __forceinline__ bool type_is32(int type) { return type == kTypeInt32 || type == kTypeFloat; }
+// VARCHAR columns hold int32 codes of an order-preserving dictionary (cubit_dict): compared as
+// INT32 values, the codes order as the strings do.
+constexpr int kTypeInt32 = 0, kTypeInt64 = 1, kTypeFloat = 8, kTypeDouble = 9, kTypeVarchar = 10;
+__host__ __device__ __forceinline__ bool type_is32(int type) {
+    return type == kTypeInt32 || type == kTypeFloat || type == kTypeVarchar;
+}
 __host__ __device__ __forceinline__ bool type_is_fp(int type) { return type == kTypeFloat || type == kTypeDouble; }
 __host__ __device__ __forceinline__ int32_t fp_key32(uint32_t u) {
     const uint32_t mag = u & 0x7fffffffu;

@@ -1991,10 +1991,10 @@ hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity,
     if (type == kTypeDouble)
         return launch_compare_multi_t<int64_t, int64_t, M, 2>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
                                                               stream);
-    if (type == 0 && keys_fit32(a, cmp))
+    if (type_is32(type) && keys_fit32(a, cmp))
         return launch_compare_multi_t<int32_t, int32_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
                                                            stream);
-    if (type == 0)
+    if (type_is32(type))
         return launch_compare_multi_t<int32_t, int64_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
                                                            stream);
     return launch_compare_multi_t<int64_t, int64_t, M>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
@@ -3361,10 +3361,10 @@ hipError_t launch_candidate_check(const void* col, int type, const uint64_t* val
     if (type == kTypeDouble)
         return launch_candidate_t<int64_t, int64_t, 2>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                        cmp, constant, out_words, stream);
-    if (type == 0 && constant >= INT32_MIN && constant <= INT32_MAX)
+    if (type_is32(type) && constant >= INT32_MIN && constant <= INT32_MAX)
         return launch_candidate_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                     cmp, (int32_t)constant, out_words, stream);
-    if (type == 0)
+    if (type_is32(type))
         return launch_candidate_t<int32_t, int64_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                     cmp, constant, out_words, stream);
     return launch_candidate_t<int64_t, int64_t>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows, cmp,
@@ -3397,7 +3397,7 @@ hipError_t launch_column_minmax(const void* col, int type, const uint64_t* valid
     else if (type == kTypeDouble)
         hipLaunchKernelGGL((column_minmax_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, n_rows, out3);
-    else if (type == 0)
+    else if (type_is32(type))
         hipLaunchKernelGGL(column_minmax_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
                            validity, n_rows, out3);
     else
@@ -3419,7 +3419,7 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
     } else if (type == kTypeDouble) {
         if (lds) CUBIT_PRESENCE(int64_t, true, 2);
         else CUBIT_PRESENCE(int64_t, false, 2);
-    } else if (type == 0) {
+    } else if (type_is32(type)) {
         if (lds) CUBIT_PRESENCE(int32_t, true, 0);
         else CUBIT_PRESENCE(int32_t, false, 0);
     } else {
@@ -3513,7 +3513,7 @@ hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const
     if (type == kTypeFloat)
         hipLaunchKernelGGL(gather_kernel<uint32_t>, grid, block, 0, stream, static_cast<const uint32_t*>(col), rowids,
                            d_count, max_n, row_base, out);
-    else if (type == 0)
+    else if (type_is32(type))
         hipLaunchKernelGGL(gather_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col), rowids,
                            d_count, max_n, row_base, out);
     else
@@ -3529,7 +3529,7 @@ hipError_t launch_gather_valid(const void* col, int type, const uint64_t* validi
     if (type == kTypeFloat)
         hipLaunchKernelGGL(gather_valid_kernel<uint32_t>, grid, block, 0, stream, static_cast<const uint32_t*>(col),
                            validity, rowids, d_count, max_n, row_base, out, out_valid);
-    else if (type == 0)
+    else if (type_is32(type))
         hipLaunchKernelGGL(gather_valid_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
                            validity, rowids, d_count, max_n, row_base, out, out_valid);
     else
@@ -3727,7 +3727,7 @@ hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* v
     else if (type == kTypeDouble)
         hipLaunchKernelGGL((column_zone_stats_kernel<int64_t, 2>), dim3(nz), dim3(256), 0, stream,
                            static_cast<const int64_t*>(col), validity, n_rows, mn, mx, fl);
-    else if (type == 0)
+    else if (type_is32(type))
         hipLaunchKernelGGL(column_zone_stats_kernel<int32_t>, dim3(nz), dim3(256), 0, stream,
                            static_cast<const int32_t*>(col), validity, n_rows, mn, mx, fl);
     else

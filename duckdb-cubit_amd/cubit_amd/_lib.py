@@ -28,6 +28,9 @@ SEGMENT_TYPES = {"int8": TYPE_INT8, "int16": TYPE_INT16, "int32": TYPE_INT32, "i
 # FLOAT / DOUBLE columns hold IEEE bit patterns; constants, keys, update values and probed values
 # cross the ABI as those patterns in an int64 (FLOAT: the 32-bit pattern, zero-extended)
 TYPE_FLOAT, TYPE_DOUBLE = 8, 9
+# VARCHAR columns hold int32 codes of an order-preserving dictionary (cubit_dict); their filter
+# constants and index keys are addresses of cubit_string structs (filters.string_ref)
+TYPE_VARCHAR = 10
 COLUMN_TYPES = dict(SEGMENT_TYPES, float32=TYPE_FLOAT, float64=TYPE_DOUBLE)
 
 
@@ -122,6 +125,13 @@ GPU_SIGNATURES = {
     "cubit_copy_stream_wait_event": (C.c_int, [_P, _P, _P]),
     "cubit_copy_event_destroy": (C.c_int, [_P, _P]),
     "cubit_build_bitvector": (C.c_int, [_P, _P, C.c_int, _P, _U64, C.c_int, _I64, _P]),
+    "cubit_dict_create": (C.c_int, [_P, _P, _U64, C.POINTER(_P)]),
+    "cubit_dict_destroy": (C.c_int, [_P]),
+    "cubit_dict_size": (C.c_int, [_P, C.POINTER(_U64)]),
+    "cubit_dict_entry": (C.c_int, [_P, _U64, C.POINTER(_P), C.POINTER(_U64)]),
+    "cubit_dict_encode": (C.c_int, [_P, _P, _P, _U64, _P, _P]),
+    "cubit_dict_lookup": (C.c_int, [_P, _P, _U64, C.POINTER(_U64), C.POINTER(C.c_int)]),
+    "cubit_table_add_dict_column": (C.c_int, [_P, C.c_int, _P, _P, _P, C.c_int]),
     "cubit_bitvector_eval": (
         C.c_int,
         [_P, C.POINTER(_P), _U32, _U32, C.POINTER(_I32), _U32, _U64, _I64, _P, _U64, _P, _P, _U32],

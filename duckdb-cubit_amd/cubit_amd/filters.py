@@ -15,6 +15,7 @@ library (cubit_filter_node) and by the CPU oracle (ofilter).
 """
 from __future__ import annotations
 
+import ctypes as C
 import datetime as _dt
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -32,13 +33,44 @@ def date(y: int, m: int, d: int) -> int:
     return (_dt.date(y, m, d) - EPOCH).days
 
 
+class _CString(C.Structure):
+    """cubit_string / the oracle's ostring: {const char *data; uint64_t size}."""
+
+    _fields_ = [("data", C.c_void_p), ("size", C.c_uint64)]
+
+
+_STRINGS = {}  # bytes -> (buffer, _CString): kept for the life of the process
+_STRING_AT = {}  # address of a _CString -> bytes
+
+
+def string_ref(b) -> int:
+    """The address of a persistent {data, size} struct holding `b` (str is UTF-8 encoded): how a
+    VARCHAR constant, index key or (oracle) update value crosses the ABI."""
+    if isinstance(b, str):
+        b = b.encode()
+    b = bytes(b)
+    if b not in _STRINGS:
+        buf = C.create_string_buffer(b, max(len(b), 1))
+        cs = _CString(C.cast(buf, C.c_void_p).value, len(b))
+        _STRINGS[b] = (buf, cs)
+        _STRING_AT[C.addressof(cs)] = b
+    return C.addressof(_STRINGS[b][1])
+
+
+def string_at(addr: int) -> bytes:
+    """The bytes of a struct made by string_ref."""
+    return _STRING_AT[int(addr)]
+
+
 def constant_bits(c) -> int:
     """A filter constant as the int64 a cubit_filter_node carries: integers as they are; a
     np.float32 as its 32-bit IEEE pattern (a FLOAT column's constant), any other float as its
     64-bit pattern (DOUBLE) — the C ABI compares FLOAT / DOUBLE columns with DuckDB's semantics
-    on those patterns."""
+    on those patterns; str / bytes as the address of a cubit_string (a VARCHAR column's constant)."""
     import numpy as np
 
+    if isinstance(c, (str, bytes)):
+        return string_ref(c)
     if isinstance(c, np.float32):
         return int(np.array([c], dtype=np.float32).view(np.uint32)[0])
     if isinstance(c, (float, np.floating)):

@@ -159,6 +159,72 @@ def padded_words(n_rows: int) -> int:
     return int(L.gpu_lib().cubit_padded_words(n_rows))
 
 
+def pack_strings(values):
+    """A list of str / bytes / None as (bytes buffer, uint64 offsets[n + 1], valid bool[n]) — the
+    layout cubit_dict_create / cubit_dict_encode take (None: a NULL row, an empty slot)."""
+    parts = [b"" if v is None else (v.encode() if isinstance(v, str) else bytes(v)) for v in values]
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    if parts:
+        offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8).copy()
+    valid = np.array([v is not None for v in values], dtype=bool)
+    return buf, offs, valid
+
+
+class Dictionary:
+    """cubit_dict: a VARCHAR column's order-preserving dictionary (the distinct strings in DuckDB's
+    order; code = rank)."""
+
+    def __init__(self, strings, lib=None):
+        self.lib = lib or L.gpu_lib()
+        buf, offs, valid = pack_strings([s for s in strings if s is not None])
+        h = C.c_void_p()
+        L.check(self.lib.cubit_dict_create(buf.ctypes.data, offs.ctypes.data, len(offs) - 1, C.byref(h)))
+        self.handle = h
+
+    def __len__(self):
+        n = C.c_uint64()
+        L.check(self.lib.cubit_dict_size(self.handle, C.byref(n)))
+        return int(n.value)
+
+    def entry(self, code: int) -> bytes:
+        p, n = C.c_void_p(), C.c_uint64()
+        L.check(self.lib.cubit_dict_entry(self.handle, int(code), C.byref(p), C.byref(n)))
+        return C.string_at(p.value, n.value) if n.value else b""
+
+    def entries(self):
+        return [self.entry(i) for i in range(len(self))]
+
+    def encode(self, values) -> Tuple[np.ndarray, np.ndarray]:
+        """(int32 codes, bool valid) of a list of str / bytes / None."""
+        from cubit_amd.datagen import validity_from_mask
+
+        buf, offs, valid = pack_strings(values)
+        codes = np.zeros(max(len(values), 1), dtype=np.int32)
+        vw = validity_from_mask(valid)
+        L.check(self.lib.cubit_dict_encode(self.handle, buf.ctypes.data, offs.ctypes.data, len(values),
+                                           vw.ctypes.data, codes.ctypes.data))
+        return codes[: len(values)], valid
+
+    def lookup(self, s):
+        b = s.encode() if isinstance(s, str) else bytes(s)
+        buf = C.create_string_buffer(b, max(len(b), 1))
+        lb, present = C.c_uint64(), C.c_int()
+        L.check(self.lib.cubit_dict_lookup(self.handle, buf, len(b), C.byref(lb), C.byref(present)))
+        return int(lb.value), bool(present.value)
+
+    def close(self):
+        if self.handle:
+            self.lib.cubit_dict_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class CubitTable:
     """A row-range partition [row_base, row_base + n_rows) resident on one device."""
 
@@ -207,6 +273,21 @@ class CubitTable:
         self.types[col] = L.TYPE_INT32 if typ in (L.TYPE_INT8, L.TYPE_INT16, L.TYPE_UINT8, L.TYPE_UINT16,
                                                   L.TYPE_INT32) else L.TYPE_INT64
 
+    def add_string_column(self, col: int, values, dictionary: Optional[Dictionary] = None) -> Dictionary:
+        """Register a VARCHAR column from a list of str / bytes / None (NULL): encoded against
+        `dictionary` (default: one built from the values) and held as int32 codes."""
+        from cubit_amd.datagen import validity_from_mask
+
+        d = dictionary or Dictionary(values, self.lib)
+        codes, valid = d.encode(values)
+        assert len(codes) == self.n_rows
+        vw = validity_from_mask(valid) if not valid.all() else None
+        L.check(self.lib.cubit_table_add_dict_column(self.handle, col, d.handle, codes.ctypes.data,
+                                                     vw.ctypes.data if vw is not None else None, 0))
+        self.types[col] = L.TYPE_VARCHAR
+        self._keep.append(d)
+        return d
+
     def column_data(self, col: int):
         """(device pointer, CUBIT type) of a registered column's values."""
         ptr, typ = C.c_void_p(), C.c_int()
@@ -230,8 +311,13 @@ class CubitTable:
         if keys is not None and len(keys):
             # FLOAT / DOUBLE columns: keys given as floats cross as their bit patterns
             typ = self.types.get(col)
-            is_fp = typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(keys).dtype.kind == "f"
-            k = L.fp_bits(keys, typ) if is_fp else np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+            if typ == L.TYPE_VARCHAR:  # string keys cross as addresses of cubit_strings
+                from cubit_amd.filters import string_ref
+
+                k = np.array([string_ref(x) for x in keys], dtype=np.int64)
+            else:
+                is_fp = typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(keys).dtype.kind == "f"
+                k = L.fp_bits(keys, typ) if is_fp else np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
             L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, k.ctypes.data, len(k)))
         else:
             L.check(self.lib.cubit_table_build_index(self.handle, col, encoding, None, 0))
@@ -290,8 +376,8 @@ class CubitTable:
         keep = []
         for c in cols:
             a = np.ascontiguousarray(columns[c])
-            want = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64}.get(
-                self.types.get(c), np.int64)
+            want = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64,
+                    L.TYPE_VARCHAR: np.int32}.get(self.types.get(c), np.int64)
             if a.dtype != want or len(a) != n_new:
                 raise ValueError(f"column {c}: {len(a)} values of {a.dtype}, want {n_new} of {np.dtype(want)}")
             keep.append(a)

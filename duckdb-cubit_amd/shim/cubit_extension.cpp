@@ -31,6 +31,8 @@
 //   TableFilterSet / ConstantFilter / Conjunction* / Is[Not]NullFilter
 //                                                  planner/table_filter.hpp:20-101, planner/filter/*.hpp
 //   DuckTransaction::{start_time, transaction_id}  transaction/duck_transaction.hpp:23-38
+#include <deque>
+
 #include "duckdb.hpp"
 #include "duckdb/catalog/catalog_entry/duck_table_entry.hpp"
 #include "duckdb/catalog/catalog_entry/table_catalog_entry.hpp"
@@ -80,6 +82,7 @@ struct CubitIndexSpec {
     column_t column;
     int encoding;  // CUBIT_INDEX_RANGE / _EQUALITY / _BINS
     vector<int64_t> keys;
+    vector<string> str_keys;  // a VARCHAR column's keys (sorted, distinct)
 };
 
 // One GPU partition per attached table: the device context, the cubit_table, which storage
@@ -124,12 +127,18 @@ struct CubitPartitionSet {
     std::shared_ptr<CubitContexts> contexts;
     vector<cubit_table *> parts;
     vector<uint64_t> part_base;  // first row id of each partition
+    // per VARCHAR column: the order-preserving dictionary every partition's codes index (one per
+    // table, so codes are global); the chunks decode codes with it
+    unordered_map<column_t, cubit_dict *> dicts;
     // a scan's init_global — the only part of a scan that reads the tables; its chunks come from
     // its own buffers — holds it shared; a sync's in-place appends and deletes hold it exclusive
     std::shared_mutex rw;
     ~CubitPartitionSet() {
         for (auto t : parts) {
             cubit_table_destroy(t);
+        }
+        for (auto &kv : dicts) {
+            cubit_dict_destroy(kv.second);
         }
     }
 };
@@ -232,8 +241,9 @@ static void Check(int rc) {
 // Physical types whose values the GPU compares exactly, carried as int64: the signed integers up
 // to 64 bits (DATE, TIME, TIMESTAMP*, DECIMAL(≤18) included), BOOLEAN, the unsigned integers up to
 // 32 bits, and FLOAT / DOUBLE as their bit patterns (the library compares them with DuckDB's
-// floating-point operators, include/cubit_gpu.h). UBIGINT, HUGEINT, UHUGEINT and VARCHAR stay on
-// seq_scan.
+// floating-point operators, include/cubit_gpu.h), and VARCHAR as int32 codes of the table's
+// order-preserving dictionary (constants cross as cubit_strings). UBIGINT, HUGEINT and UHUGEINT stay
+// on seq_scan.
 static bool GpuPhysical(PhysicalType t) {
     switch (t) {
     case PhysicalType::BOOL:
@@ -246,6 +256,7 @@ static bool GpuPhysical(PhysicalType t) {
     case PhysicalType::UINT32:
     case PhysicalType::FLOAT:
     case PhysicalType::DOUBLE:
+    case PhysicalType::VARCHAR:  // as codes of an order-preserving dictionary (cubit_dict)
         return true;
     default:
         return false;
@@ -374,7 +385,10 @@ static int64_t ConstantAsInt64(const Value &v) {
 
 // prefix-order cubit_filter_node tree of one column's TableFilter (kinds are numbered like
 // TableFilterType, comparisons like the CUBIT_CMP_* of ExpressionType::COMPARE_*)
-static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node> &out) {
+// A VARCHAR constant crosses as the address of a cubit_string over the Value's own bytes (the
+// TableFilterSet outlives the scan's init_global, which plans it); `strings` holds the structs.
+static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node> &out,
+                 std::deque<cubit_string> &strings) {
     cubit_filter_node n {};
     n.column = column;
     switch (f.filter_type) {
@@ -401,7 +415,13 @@ static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node>
             n.cmp = CUBIT_CMP_GE;
             break;
         }
-        n.constant = ConstantAsInt64(c.constant);
+        if (c.constant.type().InternalType() == PhysicalType::VARCHAR) {
+            const string &str = StringValue::Get(c.constant);
+            strings.push_back(cubit_string {str.data(), str.size()});
+            n.constant = (int64_t)(intptr_t)&strings.back();
+        } else {
+            n.constant = ConstantAsInt64(c.constant);
+        }
         out.push_back(n);
         return;
     }
@@ -422,7 +442,7 @@ static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node>
         n.n_children = (int32_t)children.size();
         out.push_back(n);
         for (auto &ch : children) {
-            Emit(*ch, column, out);
+            Emit(*ch, column, out, strings);
         }
         return;
     }
@@ -460,6 +480,8 @@ struct CubitGlobalState : public GlobalTableFunctionState {
     std::shared_ptr<CubitPartitionSet> set;  // released after the scan (member order)
     idx_t max_threads = 1;
     vector<LogicalType> out_types;  // output chunk column types, in output order
+    vector<cubit_dict *> out_dicts;  // a VARCHAR output column's dictionary (held by `set`), else null
+    std::deque<cubit_string> strings;  // the VARCHAR constants of the pushed filters
     // set when the scan runs as seq_scan (the partition was not current at init_global)
     unique_ptr<GlobalTableFunctionState> seq_global;
 };
@@ -513,12 +535,13 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
         g->seq_global = bind.seq.init_global(context, seq_input);
         return std::move(g);
     }
+    auto g = make_uniq<CubitGlobalState>();
     vector<cubit_filter_node> nodes;
     if (input.filters && !input.filters->filters.empty()) {
         // the TableFilterSet is an AND over columns; its keys index column_ids
         nodes.push_back(cubit_filter_node {CUBIT_FILTER_AND, 0, 0, (int32_t)input.filters->filters.size(), 0});
         for (auto &kv : input.filters->filters) {
-            Emit(*kv.second, (int32_t)input.column_ids[kv.first], nodes);
+            Emit(*kv.second, (int32_t)input.column_ids[kv.first], nodes, g->strings);
         }
     }
     auto &tx = DuckTransaction::Get(context, bind.table.catalog);
@@ -528,7 +551,6 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
         cols.push_back(c == COLUMN_IDENTIFIER_ROW_ID ? CUBIT_COLUMN_ROW_ID : (uint64_t)c);
     }
     vector<uint64_t> proj(input.projection_ids.begin(), input.projection_ids.end());
-    auto g = make_uniq<CubitGlobalState>();
     g->set = set;
     auto &parts = set->parts;
     if (cubit_scan_init_global_multi(parts.data(), (uint32_t)parts.size(), cols.data(), (uint32_t)cols.size(),
@@ -547,6 +569,8 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
         g->out_types.push_back(c == COLUMN_IDENTIFIER_ROW_ID
                                    ? LogicalType(LogicalType::ROW_TYPE)
                                    : bind.table.GetColumn(LogicalIndex(c)).GetType());
+        auto d = set->dicts.find(c);
+        g->out_dicts.push_back(c != COLUMN_IDENTIFIER_ROW_ID && d != set->dicts.end() ? d->second : nullptr);
     }
     return std::move(g);
 }
@@ -583,9 +607,24 @@ static void Narrow(const int64_t *src, Vector &dst, idx_t n) {
     }
 }
 
-// int64 staging → the column's physical type (DATE/INTEGER narrow, BIGINT/DECIMAL copy)
-static void CopyOut(const int64_t *src, Vector &dst, idx_t n) {
+// int64 staging → the column's physical type (DATE/INTEGER narrow, BIGINT/DECIMAL copy; VARCHAR
+// codes → the dictionary's strings, copied into the vector's string heap; a NULL row's code is 0
+// and its slot is left as the validity mask says)
+static void CopyOut(const int64_t *src, Vector &dst, idx_t n, const uint64_t *valid, cubit_dict *dict) {
     switch (dst.GetType().InternalType()) {
+    case PhysicalType::VARCHAR: {
+        auto d = FlatVector::GetData<string_t>(dst);
+        for (idx_t i = 0; i < n; i++) {
+            const char *p = nullptr;
+            uint64_t len = 0;
+            if (!((valid[i >> 6] >> (i & 63)) & 1) || !dict || cubit_dict_entry(dict, (uint64_t)src[i], &p, &len) != CUBIT_OK) {
+                d[i] = string_t();
+                continue;
+            }
+            d[i] = StringVector::AddString(dst, p, len);
+        }
+        break;
+    }
     case PhysicalType::BOOL:
         Narrow<bool>(src, dst, n);
         break;
@@ -667,7 +706,7 @@ static void CubitScanFunc(ClientContext &context, TableFunctionInput &data, Data
         throw InternalException("cubit_scan: %s", cubit_scan_last_error());
     }
     for (idx_t c = 0; c < output.ColumnCount(); c++) {
-        CopyOut(l.ptrs[c], output.data[c], n);
+        CopyOut(l.ptrs[c], output.data[c], n, l.vptrs[c], g.out_dicts[c]);
         CopyValidity(l.vptrs[c], output.data[c], n);
     }
     output.SetCardinality(n);  // 0 rows = finished (PhysicalTableScan::GetData)
@@ -734,6 +773,9 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
         return nullptr;
     }
     const auto &type = bind.table.GetColumn(LogicalIndex(column_id)).GetType();
+    if (type.InternalType() == PhysicalType::VARCHAR) {
+        return nullptr;  // the partition's statistics are dictionary codes, not strings
+    }
     auto stats = BaseStatistics::CreateEmpty(type);
     if (has_no_null) {
         const auto phys = type.InternalType();
@@ -977,6 +1019,7 @@ struct CubitSnapshot {
     uint64_t rows = 0;   // first … first+rows-1
     vector<vector<int64_t>> values;
     vector<vector<uint64_t>> validity;
+    vector<vector<string>> strings;  // a VARCHAR column's values (its `values` stay 0)
     vector<bool> present;
 };
 
@@ -1005,7 +1048,12 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
     snap.rows = 0;
     snap.values.assign(cols.size(), {});
     snap.validity.assign(cols.size(), {});
+    snap.strings.assign(cols.size(), {});
     snap.present.clear();
+    vector<bool> is_str(cols.size());
+    for (idx_t c = 0; c < cols.size(); c++) {
+        is_str[c] = entry.GetColumn(LogicalIndex(cols[c])).GetType().InternalType() == PhysicalType::VARCHAR;
+    }
     while (auto chunk = res->Fetch()) {
         chunk->Flatten();
         auto ids = FlatVector::GetData<int64_t>(chunk->data[0]);
@@ -1017,6 +1065,9 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
                 for (idx_t c = 0; c < cols.size(); c++) {
                     snap.values[c].resize(snap.rows, 0);
                     snap.validity[c].resize((snap.rows + 63) / 64, 0);
+                    if (is_str[c]) {
+                        snap.strings[c].resize(snap.rows);
+                    }
                 }
             }
             snap.present[r] = true;
@@ -1026,7 +1077,11 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
                     continue;
                 }
                 snap.validity[c][r >> 6] |= 1ull << (r & 63);
-                snap.values[c][r] = PhysicalAsInt64(vec, i);
+                if (is_str[c]) {
+                    snap.strings[c][r] = FlatVector::GetData<string_t>(vec)[i].GetString();
+                } else {
+                    snap.values[c][r] = PhysicalAsInt64(vec, i);
+                }
             }
         }
     }
@@ -1036,8 +1091,62 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
         for (idx_t c = 0; c < cols.size(); c++) {
             snap.values[c].resize(snap.rows, 0);
             snap.validity[c].resize((snap.rows + 63) / 64, 0);
+            if (is_str[c]) {
+                snap.strings[c].resize(snap.rows);
+            }
         }
     }
+}
+
+// Strings as the bytes + offsets layout cubit_dict_create / cubit_dict_encode read (string i =
+// bytes[offsets[i], offsets[i+1]); an invalid row contributes an empty slot)
+static void PackStrings(const vector<string> &strs, vector<char> &bytes, vector<uint64_t> &offsets) {
+    bytes.clear();
+    offsets.assign(1, 0);
+    for (auto &x : strs) {
+        bytes.insert(bytes.end(), x.begin(), x.end());
+        offsets.push_back(bytes.size());
+    }
+}
+
+// A VARCHAR column of a snapshot as its table-wide dictionary (its valid strings) and every row's
+// code (NULL rows: 0); the caller owns the dictionary.
+static cubit_dict *EncodeStrings(const vector<string> &strs, const vector<uint64_t> &validity, vector<int32_t> &codes) {
+    vector<string> valid_strs;
+    for (idx_t r = 0; r < strs.size(); r++) {
+        if ((validity[r >> 6] >> (r & 63)) & 1) {
+            valid_strs.push_back(strs[r]);
+        }
+    }
+    vector<char> bytes;
+    vector<uint64_t> offsets;
+    PackStrings(valid_strs, bytes, offsets);
+    cubit_dict *d = nullptr;
+    Check(cubit_dict_create(bytes.data(), offsets.data(), valid_strs.size(), &d));
+    PackStrings(strs, bytes, offsets);
+    codes.assign(strs.size(), 0);
+    const int rc = cubit_dict_encode(d, bytes.data(), offsets.data(), strs.size(), validity.data(), codes.data());
+    if (rc != CUBIT_OK) {
+        cubit_dict_destroy(d);
+        Check(rc);
+    }
+    return d;
+}
+
+// Whether every valid string of a snapshot column is in `d` (an in-place append keeps the
+// dictionary; a new string makes the sync rebuild with a new one)
+static bool StringsInDict(cubit_dict *d, const vector<string> &strs, const vector<uint64_t> &validity) {
+    for (idx_t r = 0; r < strs.size(); r++) {
+        if (!((validity[r >> 6] >> (r & 63)) & 1)) {
+            continue;
+        }
+        uint64_t lb = 0;
+        int present = 0;
+        if (cubit_dict_lookup(d, strs[r].data(), strs[r].size(), &lb, &present) != CUBIT_OK || !present) {
+            return false;
+        }
+    }
+    return true;
 }
 
 // Every distinct value when the column has at most this many (l_discount 11, l_quantity 50);
@@ -1203,8 +1312,18 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
     const uint64_t rg = 122880, units = (snap.rows + rg - 1) / rg;
     const uint64_t n_parts = std::max<uint64_t>(1, std::min<uint64_t>(ctxs.size(), units));
     vector<bool> few(attached.column_order.size());
+    vector<vector<int32_t>> codes(attached.column_order.size());  // VARCHAR columns: every row's code
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
-        few[c] = FewDistinct(snap.values[c], snap.validity[c]);
+        const column_t col = attached.column_order[c];
+        if (attached.columns[col] == PhysicalType::VARCHAR) {
+            cubit_dict *d = EncodeStrings(snap.strings[c], snap.validity[c], codes[c]);
+            set->dicts[col] = d;  // the set owns it from here (its destructor frees it)
+            uint64_t size = 0;
+            cubit_dict_size(d, &size);
+            few[c] = size <= kDefaultDistinctIndexMax;
+        } else {
+            few[c] = FewDistinct(snap.values[c], snap.validity[c]);
+        }
     }
     for (uint64_t p = 0; p < n_parts; p++) {
         const uint64_t b = std::min(snap.rows, units * p / n_parts * rg);
@@ -1216,11 +1335,15 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
         for (idx_t c = 0; c < attached.column_order.size(); c++) {
             const column_t col = attached.column_order[c];
             const uint64_t *valid = snap.validity[c].data() + b / 64;
+            if (attached.columns[col] == PhysicalType::VARCHAR) {
+                Check(cubit_table_add_dict_column(t, (int)col, set->dicts[col], codes[c].data() + b, valid, 0));
+            }
             const bool from_segments =
-                entry && n_parts == 1 &&
+                attached.columns[col] != PhysicalType::VARCHAR && entry && n_parts == 1 &&
                 AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
                 SampleMatches(ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
-            if (!from_segments) {  // (re-)registering replaces a column taken from segments
+            if (!from_segments && attached.columns[col] != PhysicalType::VARCHAR) {
+                // (re-)registering replaces a column taken from segments
                 const bool wide = WidePhysical(attached.columns[col]);
                 vector<int32_t> narrow;
                 if (!wide) {
@@ -1233,7 +1356,15 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
             bool named = false;
             for (auto &ix : attached.indexes) {
                 if (ix.column == col) {
-                    Check(cubit_table_build_index(t, (int)col, ix.encoding, ix.keys.data(), (uint32_t)ix.keys.size()));
+                    vector<cubit_string> strs;  // a VARCHAR column's keys as cubit_strings
+                    vector<int64_t> addrs;
+                    strs.reserve(ix.str_keys.size());
+                    for (auto &k : ix.str_keys) {
+                        strs.push_back(cubit_string {k.data(), k.size()});
+                        addrs.push_back((int64_t)(intptr_t)&strs.back());
+                    }
+                    const auto &keys = ix.str_keys.empty() ? ix.keys : addrs;
+                    Check(cubit_table_build_index(t, (int)col, ix.encoding, keys.data(), (uint32_t)keys.size()));
                     named = true;
                 }
             }
@@ -1339,6 +1470,12 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
         if (snap.rows == 0 && entry.GetStorage().GetTotalRows() < gpu_rows) {
             rebuild = true;  // fewer rows than the partition: renumbered by a vacuum
         }
+        for (idx_t c = 0; c < attached.column_order.size() && !rebuild; c++) {
+            auto d = cur->dicts.find(attached.column_order[c]);
+            if (d != cur->dicts.end() && !StringsInDict(d->second, snap.strings[c], snap.validity[c])) {
+                rebuild = true;  // an appended string the dictionary lacks: a new dictionary
+            }
+        }
     }
     if (rebuild || !cur) {
         ReadRows(con, table_name, entry, attached.column_order, 0, total_rows, snap);
@@ -1371,7 +1508,15 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
         for (idx_t c = 0; c < attached.column_order.size(); c++) {
             const column_t col = attached.column_order[c];
             cols.push_back((int)col);
-            if (WidePhysical(attached.columns[col])) {
+            if (attached.columns[col] == PhysicalType::VARCHAR) {  // codes in the kept dictionary
+                vector<char> bytes;
+                vector<uint64_t> offsets;
+                PackStrings(snap.strings[c], bytes, offsets);
+                narrow.emplace_back(snap.rows, 0);
+                Check(cubit_dict_encode(cur->dicts.at(col), bytes.data(), offsets.data(), snap.rows,
+                                        snap.validity[c].data(), narrow.back().data()));
+                data.push_back(narrow.back().data());
+            } else if (WidePhysical(attached.columns[col])) {
                 data.push_back(snap.values[c].data());
             } else {
                 narrow.emplace_back(snap.values[c].begin(), snap.values[c].end());
@@ -1437,7 +1582,14 @@ static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string
         } else {
             throw InvalidInputException("cubit_attach: unknown index encoding '%s'", enc);
         }
-        if (colon != string::npos) {
+        if (colon != string::npos && def.GetType().InternalType() == PhysicalType::VARCHAR) {
+            for (auto lit : StringUtil::Split(rest.substr(colon + 1), ',')) {
+                StringUtil::Trim(lit);
+                ix.str_keys.push_back(lit);  // byte order = DuckDB's string order (string_type.hpp:176-206)
+            }
+            std::sort(ix.str_keys.begin(), ix.str_keys.end());
+            ix.str_keys.erase(std::unique(ix.str_keys.begin(), ix.str_keys.end()), ix.str_keys.end());
+        } else if (colon != string::npos) {
             for (auto lit : StringUtil::Split(rest.substr(colon + 1), ',')) {
                 StringUtil::Trim(lit);
                 ix.keys.push_back(ConstantAsInt64(Value(lit).DefaultCastAs(def.GetType())));
@@ -1449,7 +1601,7 @@ static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string
             ix.keys.erase(std::unique(ix.keys.begin(), ix.keys.end(), [&](int64_t a, int64_t b) { return key(a) == key(b); }),
                           ix.keys.end());
         }
-        if (ix.encoding == CUBIT_INDEX_BINS && ix.keys.size() < 2) {
+        if (ix.encoding == CUBIT_INDEX_BINS && ix.keys.size() + ix.str_keys.size() < 2) {
             throw InvalidInputException("cubit_attach: bins on %s need at least two edges", name);
         }
         out.push_back(std::move(ix));

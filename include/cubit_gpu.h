@@ -62,6 +62,15 @@ extern "C" {
  * patterns onto signed integers under which those operators are plain integer comparisons. */
 #define CUBIT_TYPE_FLOAT 8
 #define CUBIT_TYPE_DOUBLE 9
+/* VARCHAR (PhysicalType::VARCHAR, string_t): the column holds int32 codes of an order-preserving
+ * dictionary (cubit_dict: the distinct strings sorted as DuckDB compares them —
+ * src/include/duckdb/common/types/string_type.hpp:143-206: the bytes as unsigned, then the length),
+ * so a code comparison is the string comparison and every index, zonemap and kernel works on the
+ * codes. A CONSTANT filter node on a VARCHAR column carries the ADDRESS of a cubit_string in
+ * `constant` (the planner maps it to a code bound; strings absent from the dictionary included);
+ * index keys (cubit_table_build_index `values`) likewise. Update values, appended values, probed
+ * values and statistics are codes. */
+#define CUBIT_TYPE_VARCHAR 10
 
 /* The comparison key of a FLOAT / DOUBLE bit pattern (any other type: the value itself): every
  * NaN → one key above +inf's, -x → -(pattern of x) (so -0.0 and +0.0 share key 0), +x → its pattern.
@@ -141,6 +150,13 @@ static inline int64_t cubit_fp_value(int type, int64_t key) {
 
 typedef struct cubit_ctx cubit_ctx;
 typedef struct cubit_table cubit_table;
+typedef struct cubit_dict cubit_dict;
+
+/* a string constant or key of a VARCHAR column (string_t's data and size) */
+typedef struct {
+    const char *data;
+    uint64_t size;
+} cubit_string;
 
 /* One node of a predicate tree in prefix order. A TableFilterSet (per-column AND,
  * table_filter.hpp:67-101) is an AND root whose children each reference one column; a
@@ -331,6 +347,31 @@ int cubit_table_column_data(cubit_table *t, int col, const void **data, int *typ
  * INT64 values (cubit_table_column_data reports the type held). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
+/* ---- VARCHAR dictionaries. A dictionary is built once per table (every partition of a table
+ * encodes its rows against the same one, so codes are global) from any list of strings: n strings,
+ * string i = bytes[offsets[i], offsets[i+1]) — duplicates and order do not matter; it keeps the
+ * distinct ones sorted in DuckDB's string order (at most 2^31 - 1). Immutable once built: a table
+ * that gains a string its dictionary lacks is re-registered with a new one (cubit_dict_encode
+ * says so). cubit_dict_destroy drops the caller's reference; columns registered with the
+ * dictionary hold their own until they go. Host-only: no context, no device memory. */
+int cubit_dict_create(const char *bytes, const uint64_t *offsets, uint64_t n, cubit_dict **out);
+int cubit_dict_destroy(cubit_dict *d);
+int cubit_dict_size(const cubit_dict *d, uint64_t *n);
+/* the string of a code (pointers into the dictionary, valid while it lives) */
+int cubit_dict_entry(const cubit_dict *d, uint64_t code, const char **data, uint64_t *size);
+/* codes[i] = the code of string i (layout as cubit_dict_create); a row whose validity bit is 0
+ * (validity may be NULL) gets code 0 and its string is not read. CUBIT_ERR_UNSUPPORTED when a
+ * valid string is not in the dictionary (codes are then unspecified). */
+int cubit_dict_encode(const cubit_dict *d, const char *bytes, const uint64_t *offsets, uint64_t n,
+                      const uint64_t *validity, int32_t *codes);
+/* *lower_bound = the first code whose string is >= s (the size when none), *present = s is in it */
+int cubit_dict_lookup(const cubit_dict *d, const char *data, uint64_t size, uint64_t *lower_bound, int *present);
+/* Register a VARCHAR column: codes (host, or device with on_device = 1 as cubit_table_add_column)
+ * of the table's rows against `d`, validity as for cubit_table_add_column. Every valid code must
+ * lie in [0, size of d) (CUBIT_ERR_INVALID otherwise). The column holds a reference to d. */
+int cubit_table_add_dict_column(cubit_table *t, int col, cubit_dict *d, const int32_t *codes, const uint64_t *validity,
+                                int on_device);
+
 /* The values of a caller-owned column changed: drop what the table derived from them. */
 int cubit_table_column_changed(cubit_table *t, int col);
 /* Register a column given as DuckDB BITPACKING segments (K5; the reference's persistent

@@ -101,8 +101,30 @@ static inline int cmp_op(int cmp, int64_t v, int64_t c) {
     }
 }
 
-/* a comparison of values of column type `type` (FP: bit patterns) */
+/* string_t comparisons (src/include/duckdb/common/types/string_type.hpp:143-206, Equals /
+ * GreaterThan): the bytes compared as unsigned (the byte-swapped prefix, then memcmp), a string
+ * that is a prefix of the other is the smaller one */
+static inline int str_order(const ostring *a, const ostring *b) {
+    const uint64_t m = a->size < b->size ? a->size : b->size;
+    const int r = m ? memcmp(a->data, b->data, m) : 0;
+    if (r) return r < 0 ? -1 : 1;
+    return a->size < b->size ? -1 : a->size > b->size ? 1 : 0;
+}
+static inline int cmp_str(int cmp, int64_t v, int64_t c) {
+    const int o = str_order((const ostring *)(intptr_t)v, (const ostring *)(intptr_t)c);
+    switch (cmp) {
+    case OCMP_EQ: return o == 0;
+    case OCMP_NE: return o != 0;
+    case OCMP_LT: return o < 0;
+    case OCMP_LE: return o <= 0;
+    case OCMP_GT: return o > 0;
+    default: return o >= 0;
+    }
+}
+
+/* a comparison of values of column type `type` (FP: bit patterns; VARCHAR: ostring addresses) */
 static inline int cmp_typed(int type, int cmp, int64_t v, int64_t c) {
+    if (type == OTYPE_VARCHAR) return cmp_str(cmp, v, c);
     if (type == OTYPE_FLOAT || type == OTYPE_DOUBLE) return cmp_fp(cmp, fp_value(type, v), fp_value(type, c));
     return cmp_op(cmp, v, c);
 }
@@ -111,6 +133,7 @@ static inline int cmp_typed(int type, int cmp, int64_t v, int64_t c) {
 static inline int64_t col_value(const ocol *c, uint64_t r) {
     switch (c->type) {
     case OTYPE_INT32: return (int64_t)((const int32_t *)c->data)[r];
+    case OTYPE_VARCHAR: return (int64_t)(intptr_t)((const ostring *)c->data + r);
     case OTYPE_FLOAT: {
         uint32_t u;
         memcpy(&u, (const float *)c->data + r, 4);
@@ -161,7 +184,8 @@ static void load_vector(const ocol *c, uint64_t first_row, uint64_t count, const
         out->wide = 0;
         out->data = c->type == OTYPE_INT32 || c->type == OTYPE_FLOAT
                         ? (const void *)((const int32_t *)c->data + first_row)
-                        : (const void *)((const int64_t *)c->data + first_row);
+                        : c->type == OTYPE_VARCHAR ? (const void *)((const ostring *)c->data + first_row)
+                                                   : (const void *)((const int64_t *)c->data + first_row);
         return;
     }
     for (uint64_t i = 0; i < count; i++) out->vals[i] = col_value(c, first_row + i);
@@ -191,6 +215,7 @@ static inline int64_t vec_value(const vecbuf *v, uint32_t idx) {
     switch (v->type) {
     case OTYPE_INT32: return (int64_t)((const int32_t *)v->data)[idx];
     case OTYPE_FLOAT: return (int64_t)((const uint32_t *)v->data)[idx];
+    case OTYPE_VARCHAR: return (int64_t)(intptr_t)((const ostring *)v->data + idx);
     default: return ((const int64_t *)v->data)[idx];
     }
 }
@@ -233,6 +258,16 @@ static inline int vec_valid(const vecbuf *v, uint32_t idx) { return v->valid ? v
 
 static uint64_t templated_filter_selection(const vecbuf *v, int cmp, int64_t c, uint32_t *sel, uint64_t approved) {
     uint64_t rc = 0;
+    if (v->type == OTYPE_VARCHAR) {
+        /* FilterSelectionSwitch<string_t> (column_segment.cpp:278-349) */
+        for (uint64_t a = 0; a < approved; a++) {
+            uint32_t idx = sel[a];
+            int pass = vec_valid(v, idx) && cmp_str(cmp, vec_value(v, idx), c);
+            sel[rc] = idx;
+            rc += (uint64_t)pass;
+        }
+        return rc;
+    }
     if (v->type == OTYPE_FLOAT || v->type == OTYPE_DOUBLE) {
         /* FilterSelectionSwitch<float / double> with DuckDB's floating-point operators */
         const double pred = fp_value(v->type, c);

@@ -11,7 +11,13 @@ extern "C" {
 
 /* FLOAT / DOUBLE: `data` holds the IEEE values; constants, update values and fetched values
  * carry their bit patterns (FLOAT: the 32-bit pattern, zero-extended) */
-enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3 };
+/* VARCHAR: `data` is an array of ostring; constants, update values and fetched values carry the
+ * address of an ostring (string_t comparisons: unsigned bytes, then length — string_type.hpp:143-206) */
+enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3, OTYPE_VARCHAR = 4 };
+typedef struct {
+    const char *data;
+    uint64_t size;
+} ostring;
 /* ExpressionType comparisons used by ConstantFilter (table_filter.hpp / constant_filter.cpp) */
 enum { OCMP_EQ = 0, OCMP_NE = 1, OCMP_LT = 2, OCMP_LE = 3, OCMP_GT = 4, OCMP_GE = 5 };
 /* TableFilterType (src/include/duckdb/planner/table_filter.hpp:20-27) */

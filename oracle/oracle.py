@@ -18,7 +18,7 @@ HERE = Path(__file__).resolve().parent
 LIB = HERE / "lib" / "libcubit_oracle.so"
 
 OMAX_COLS = 16
-OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE = 0, 1, 2, 3
+OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE, OTYPE_VARCHAR = 0, 1, 2, 3, 4
 OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
 
 
@@ -132,6 +132,64 @@ class Column:
             c.upd_rows, c.upd_values, c.upd_version = (a.ctypes.data for a in self.upd)
             c.upd_valid = self.upd_valid.ctypes.data if self.upd_valid is not None else None
         return c
+
+
+class OString(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("size", C.c_uint64)]
+
+
+class StringColumn(Column):
+    """A VARCHAR column as the oracle sees it: an ostring per row (string_t: data + size), NULL
+    rows from None. Update values are strings too (carried as addresses, filters.string_ref);
+    fetch hands back addresses — decode() turns them into bytes."""
+
+    def __init__(self, values, updates=None):
+        from cubit_amd.datagen import validity_from_mask
+        from cubit_amd.filters import string_ref
+
+        self.values = [None if v is None else (v.encode() if isinstance(v, str) else bytes(v)) for v in values]
+        n = len(self.values)
+        self._bufs = [C.create_string_buffer(v or b"", max(len(v or b""), 1)) for v in self.values]
+        self.arr = (OString * max(n, 1))()
+        for i, (v, b) in enumerate(zip(self.values, self._bufs)):
+            self.arr[i] = OString(C.cast(b, C.c_void_p).value, len(v or b""))
+        valid = np.array([v is not None for v in self.values], dtype=bool)
+        self.validity = None if valid.all() else validity_from_mask(valid)
+        self.data = np.zeros(0, dtype=np.int8)  # unused (the ostrings are in self.arr)
+        self.upd = None
+        self.upd_valid = None
+        if updates is not None:
+            r, v, ver = updates[:3]
+            vals = np.array([0 if x is None else string_ref(x) for x in v], dtype=np.int64)
+            self.upd = (np.ascontiguousarray(r, dtype=np.int64), vals, np.ascontiguousarray(ver, dtype=np.uint64))
+            ok = updates[3] if len(updates) > 3 and updates[3] is not None else np.array([x is not None for x in v])
+            self.upd_valid = np.ascontiguousarray(ok, dtype=np.uint8)
+
+    def ocol(self) -> OCol:
+        c = OCol()
+        c.type = OTYPE_VARCHAR
+        c.data = C.addressof(self.arr)
+        c.validity = self.validity.ctypes.data if self.validity is not None else None
+        if self.upd is not None:
+            c.n_updates = len(self.upd[0])
+            c.upd_rows, c.upd_values, c.upd_version = (a.ctypes.data for a in self.upd)
+            c.upd_valid = self.upd_valid.ctypes.data
+        return c
+
+    def decode(self, addrs, valid=None):
+        """Fetched values (ostring addresses) → bytes (None where not valid)."""
+        from cubit_amd.filters import string_at
+
+        base, size = C.addressof(self.arr), C.sizeof(OString)
+        out = []
+        for i, a in enumerate(np.asarray(addrs, dtype=np.int64).tolist()):
+            if valid is not None and not valid[i]:
+                out.append(None)
+            elif base <= a < base + size * len(self.values):
+                out.append(self.values[(a - base) // size])
+            else:
+                out.append(string_at(a))
+        return out
 
 
 class Mvcc:
