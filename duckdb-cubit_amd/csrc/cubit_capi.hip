@@ -678,7 +678,7 @@ int cubit_build_bitvector(cubit_ctx* ctx, const void* d_col, int type, const uin
                           int cmp, int64_t constant, uint64_t* d_words) {
     if (!ctx || !d_col || !d_words) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_keyed(type))
         return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (cmp < 0 || cmp > 5) return fail(CUBIT_ERR_INVALID, "cmp %d", cmp);
     HIP_CHECK(launch_compare_bitvector(d_col, type, d_validity, n_rows, cmp, value_key(type, constant), d_words,
@@ -1027,7 +1027,7 @@ extern "C" int cubit_gather(cubit_ctx* ctx, const void* d_col, int type, const i
                             const uint64_t* d_count, uint64_t max_n, int64_t row_base, int64_t* d_out) {
     if (!ctx || !d_col || !d_rowids || !d_count || !d_out) return fail(CUBIT_ERR_INVALID, "null argument");
     CUBIT_LOCK(ctx);
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_fp(type))
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && !type_is_keyed(type))
         return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     HIP_CHECK(launch_gather(d_col, type, d_rowids, d_count, max_n, row_base, d_out, ctx->stream));
     return CUBIT_OK;
@@ -1374,7 +1374,7 @@ bool storage_of(int type, int& col_type, uint64_t& src_size) {
     case CUBIT_TYPE_INT8: case CUBIT_TYPE_UINT8: col_type = CUBIT_TYPE_INT32, src_size = 1; return true;
     case CUBIT_TYPE_INT16: case CUBIT_TYPE_UINT16: col_type = CUBIT_TYPE_INT32, src_size = 2; return true;
     case CUBIT_TYPE_UINT32: col_type = CUBIT_TYPE_INT64, src_size = 4; return true;
-    case CUBIT_TYPE_UINT64: col_type = CUBIT_TYPE_INT64, src_size = 8; return true;
+    case CUBIT_TYPE_UINT64: col_type = CUBIT_TYPE_UINT64, src_size = 8; return true;  // the bits, keyed
     case CUBIT_TYPE_FLOAT: col_type = CUBIT_TYPE_FLOAT, src_size = 4; return true;
     case CUBIT_TYPE_DOUBLE: col_type = CUBIT_TYPE_DOUBLE, src_size = 8; return true;
     case CUBIT_TYPE_VARCHAR: col_type = CUBIT_TYPE_VARCHAR, src_size = 4; return true;  // codes
@@ -1383,7 +1383,7 @@ bool storage_of(int type, int& col_type, uint64_t& src_size) {
 }
 
 // A column of a narrower or unsigned type code: its values (host or device) widened on the
-// device into an owned INT32 / INT64 column; UINT64 values must stay below 2^63.
+// device into an owned INT32 / INT64 column (UINT64 columns are held as their bits, keyed).
 int widen_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
     int col_type = 0;
     uint64_t ssz = 0;
@@ -1410,20 +1410,11 @@ int widen_column(cubit_table* t, Column& c, int type, const void* data, const ui
         if (int rc = copy_validity(t, c, validity, on_device)) return rc;
     }
     HIP_CHECK(hipStreamSynchronize(s));
-    if (type == CUBIT_TYPE_UINT64) {
-        std::vector<int64_t> unused;
-        int64_t vmin = 0, vmax = 0;
-        bool any = false;
-        if (int rc = value_stats(t, c.data, CUBIT_TYPE_INT64, c.validity, t->n_rows, unused, false, vmin, vmax, any))
-            return rc;
-        if (any && vmin < 0)
-            return fail(CUBIT_ERR_UNSUPPORTED, "UINT64 column holds a value of 2^63 or more (an INT64 column cannot hold it)");
-    }
     return CUBIT_OK;
 }
 
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
-    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && type != CUBIT_TYPE_VARCHAR && !type_is_fp(type))
+    if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && type != CUBIT_TYPE_VARCHAR && !type_is_keyed(type))
         return widen_column(t, c, type, data, validity, on_device);
     const uint64_t esz = type_is32(type) ? 4 : 8;  // FLOAT / DOUBLE: the bit patterns as they are
     if (t->n_rows == 0) {  // empty partition: nothing to copy
@@ -1496,7 +1487,7 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
                 if ((hvalid[i >> 6] >> (i & 63)) & 1) hv[k++] = hv[i];
             hv.resize(k);
         }
-        if (type == CUBIT_TYPE_DOUBLE)
+        if (type == CUBIT_TYPE_DOUBLE || type == CUBIT_TYPE_UINT64)
             for (int64_t& v : hv) v = value_key(type, v);
         distinct = distinct_sorted(hv.data(), hv.size());
         if (distinct.size() > kMaxWideDistinct)
@@ -1724,7 +1715,7 @@ bool seg_type_of(int type, SegType& st) {
     case CUBIT_TYPE_UINT8: st = {1, false, CUBIT_TYPE_INT32, 8}; return true;
     case CUBIT_TYPE_UINT16: st = {2, false, CUBIT_TYPE_INT32, 16}; return true;
     case CUBIT_TYPE_UINT32: st = {4, false, CUBIT_TYPE_INT64, 32}; return true;
-    case CUBIT_TYPE_UINT64: st = {8, false, CUBIT_TYPE_INT64, 0}; return true;
+    case CUBIT_TYPE_UINT64: st = {8, false, CUBIT_TYPE_UINT64, 0}; return true;
     default: return false;
     }
 }
@@ -1869,17 +1860,6 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
         if (int rc = copy_validity(t, c, validity, 0)) return rc;
         HIP_CHECK(hipStreamSynchronize(s));
     }
-    if (type == CUBIT_TYPE_UINT64) {
-        // held as INT64: every valid value must stay below 2^63, i.e. read as a non-negative INT64
-        std::vector<int64_t> unused;
-        int64_t vmin = 0, vmax = 0;
-        bool any = false;
-        if (int rc = value_stats(t, c.data, CUBIT_TYPE_INT64, c.validity, t->n_rows, unused, false, vmin, vmax, any))
-            return rc;
-        if (any && vmin < 0)
-            return fail(CUBIT_ERR_UNSUPPORTED, "UINT64 column %d holds a value of 2^63 or more (an INT64 column cannot hold it)",
-                        col);
-    }
     t->cols[col] = std::move(c);
     drop_patches(t, col);
     t->idx.erase(col);
@@ -1901,7 +1881,7 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
     // a FLOAT / DOUBLE column's keys are given as bit patterns and held as their comparison keys
     // (-0.0 and +0.0, or two NaNs, become one key)
     std::vector<int64_t> keyed;
-    if (n && type_is_fp(c.type)) {
+    if (n && type_is_keyed(c.type)) {
         keyed.resize(n);
         for (uint32_t k = 0; k < n; ++k) keyed[k] = value_key(c.type, values[k]);
         values = keyed.data();
@@ -2774,7 +2754,8 @@ struct PendingK0 {
 int compute_k0(cubit_table* t, const PendingK0& k) {
     const Column& cl = t->cols.at(k.col);
     hipError_t e;
-    if (cl.bp_n_groups && t->use_packed) {
+    // (UBIGINT segments: the packed compare orders values as signed; such columns compare unpacked)
+    if (cl.bp_n_groups && t->use_packed && cl.type != CUBIT_TYPE_UINT64) {
         // straight from the BITPACKING segments: w/8 bytes per row instead of sizeof(T)
         e = hipMemsetAsync(k.bv, 0, t->nwp * 8, t->ctx->stream);
         if (e == hipSuccess)
@@ -3050,9 +3031,9 @@ struct Planner {
                 case CUBIT_CMP_GT: if (v == INT64_MAX) bd.empty = true; else lower(v + 1); break;
                 case CUBIT_CMP_LT: upper(v); break;
                 case CUBIT_CMP_LE: if (v != INT64_MAX) upper(v + 1); break;
-                case CUBIT_CMP_EQ:
+                case CUBIT_CMP_EQ:  // [v, v + 1); v = INT64_MAX: [v, ∞) is {v} (a UBIGINT 2^64 - 1's key)
                     lower(v);
-                    if (v == INT64_MAX) bd.empty = true; else upper(v + 1);
+                    if (v != INT64_MAX) upper(v + 1);
                     break;
                 default: break;
                 }
@@ -3803,7 +3784,7 @@ struct KeyedNodes {
         for (uint32_t k = 0; k < n; ++k) {
             if (nodes[k].kind != CUBIT_FILTER_CONSTANT) continue;
             auto it = t->cols.find(nodes[k].column);
-            if (it == t->cols.end() || (!type_is_fp(it->second.type) && it->second.type != CUBIT_TYPE_VARCHAR)) continue;
+            if (it == t->cols.end() || (!type_is_keyed(it->second.type) && it->second.type != CUBIT_TYPE_VARCHAR)) continue;
             if (buf.empty()) {
                 buf.assign(nodes, nodes + n);
                 p = buf.data();

@@ -53,11 +53,15 @@ inline uint32_t prog_nops(const EvalProgram& p, int k) { return (p.nops >> (4 * 
 // comparison_operators.hpp:100-146). Type codes as in cubit_gpu.h.
 // VARCHAR columns hold int32 codes of an order-preserving dictionary (cubit_dict): compared as
 // INT32 values, the codes order as the strings do.
-constexpr int kTypeInt32 = 0, kTypeInt64 = 1, kTypeFloat = 8, kTypeDouble = 9, kTypeVarchar = 10;
+// UBIGINT (UINT64) columns hold the unsigned values' bits, compared through the key v ^ 2^63 (the
+// unsigned order as a signed one).
+constexpr int kTypeInt32 = 0, kTypeInt64 = 1, kTypeUInt64 = 7, kTypeFloat = 8, kTypeDouble = 9, kTypeVarchar = 10;
 __host__ __device__ __forceinline__ bool type_is32(int type) {
     return type == kTypeInt32 || type == kTypeFloat || type == kTypeVarchar;
 }
 __host__ __device__ __forceinline__ bool type_is_fp(int type) { return type == kTypeFloat || type == kTypeDouble; }
+// values compared through a key other than themselves (FLOAT, DOUBLE, UBIGINT)
+__host__ __device__ __forceinline__ bool type_is_keyed(int type) { return type_is_fp(type) || type == kTypeUInt64; }
 __host__ __device__ __forceinline__ int32_t fp_key32(uint32_t u) {
     const uint32_t mag = u & 0x7fffffffu;
     if (mag > 0x7f800000u) return 0x7fc00000;
@@ -72,13 +76,16 @@ __host__ __device__ __forceinline__ int64_t fp_key64(uint64_t u) {
 __host__ __device__ __forceinline__ int64_t value_key(int type, int64_t v) {
     if (type == kTypeFloat) return fp_key32((uint32_t)v);
     if (type == kTypeDouble) return fp_key64((uint64_t)v);
+    if (type == kTypeUInt64) return (int64_t)((uint64_t)v ^ 0x8000000000000000ull);
     return v;
 }
-// kernels templated on the key kind FK (0: the value itself, 1: FLOAT pattern, 2: DOUBLE pattern)
+// kernels templated on the key kind FK (0: the value itself, 1: FLOAT pattern, 2: DOUBLE pattern,
+// 3: UBIGINT bits)
 template <int FK, typename T>
 __host__ __device__ __forceinline__ T key_of(T raw) {
     if constexpr (FK == 1) return (T)fp_key32((uint32_t)raw);
     else if constexpr (FK == 2) return (T)fp_key64((uint64_t)raw);
+    else if constexpr (FK == 3) return (T)((uint64_t)raw ^ 0x8000000000000000ull);
     else return raw;
 }
 

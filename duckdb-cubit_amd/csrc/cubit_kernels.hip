@@ -1991,6 +1991,9 @@ hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity,
     if (type == kTypeDouble)
         return launch_compare_multi_t<int64_t, int64_t, M, 2>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
                                                               stream);
+    if (type == kTypeUInt64)
+        return launch_compare_multi_t<int64_t, int64_t, M, 3>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
+                                                              stream);
     if (type_is32(type) && keys_fit32(a, cmp))
         return launch_compare_multi_t<int32_t, int32_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
                                                            stream);
@@ -3361,6 +3364,9 @@ hipError_t launch_candidate_check(const void* col, int type, const uint64_t* val
     if (type == kTypeDouble)
         return launch_candidate_t<int64_t, int64_t, 2>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                        cmp, constant, out_words, stream);
+    if (type == kTypeUInt64)
+        return launch_candidate_t<int64_t, int64_t, 3>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
+                                                       cmp, constant, out_words, stream);
     if (type_is32(type) && constant >= INT32_MIN && constant <= INT32_MAX)
         return launch_candidate_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                     cmp, (int32_t)constant, out_words, stream);
@@ -3397,6 +3403,9 @@ hipError_t launch_column_minmax(const void* col, int type, const uint64_t* valid
     else if (type == kTypeDouble)
         hipLaunchKernelGGL((column_minmax_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, n_rows, out3);
+    else if (type == kTypeUInt64)
+        hipLaunchKernelGGL((column_minmax_kernel<int64_t, 3>), grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, n_rows, out3);
     else if (type_is32(type))
         hipLaunchKernelGGL(column_minmax_kernel<int32_t>, grid, block, 0, stream, static_cast<const int32_t*>(col),
                            validity, n_rows, out3);
@@ -3419,6 +3428,9 @@ hipError_t launch_presence(const void* col, int type, const uint64_t* validity, 
     } else if (type == kTypeDouble) {
         if (lds) CUBIT_PRESENCE(int64_t, true, 2);
         else CUBIT_PRESENCE(int64_t, false, 2);
+    } else if (type == kTypeUInt64) {
+        if (lds) CUBIT_PRESENCE(int64_t, true, 3);
+        else CUBIT_PRESENCE(int64_t, false, 3);
     } else if (type_is32(type)) {
         if (lds) CUBIT_PRESENCE(int32_t, true, 0);
         else CUBIT_PRESENCE(int32_t, false, 0);
@@ -3654,6 +3666,9 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
     } else if (type == kTypeDouble) {
         hipLaunchKernelGGL((masked_compare_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, mask, nw, r.lo, r.hi, r.neg, out);
+    } else if (type == kTypeUInt64) {
+        hipLaunchKernelGGL((masked_compare_kernel<int64_t, 3>), grid, block, 0, stream, static_cast<const int64_t*>(col),
+                           validity, mask, nw, r.lo, r.hi, r.neg, out);
     } else {
         hipLaunchKernelGGL(masked_compare_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, mask, nw, r.lo, r.hi, r.neg, out);
@@ -3726,6 +3741,9 @@ hipError_t launch_column_zone_stats(const void* col, int type, const uint64_t* v
                            static_cast<const int32_t*>(col), validity, n_rows, mn, mx, fl);
     else if (type == kTypeDouble)
         hipLaunchKernelGGL((column_zone_stats_kernel<int64_t, 2>), dim3(nz), dim3(256), 0, stream,
+                           static_cast<const int64_t*>(col), validity, n_rows, mn, mx, fl);
+    else if (type == kTypeUInt64)
+        hipLaunchKernelGGL((column_zone_stats_kernel<int64_t, 3>), dim3(nz), dim3(256), 0, stream,
                            static_cast<const int64_t*>(col), validity, n_rows, mn, mx, fl);
     else if (type_is32(type))
         hipLaunchKernelGGL(column_zone_stats_kernel<int32_t>, dim3(nz), dim3(256), 0, stream,

@@ -75,7 +75,8 @@ def constant_bits(c) -> int:
         return int(np.array([c], dtype=np.float32).view(np.uint32)[0])
     if isinstance(c, (float, np.floating)):
         return int(np.array([c], dtype=np.float64).view(np.int64)[0])
-    return int(c)
+    c = int(c)
+    return c - (1 << 64) if c >= 1 << 63 else c  # a UBIGINT constant past 2^63: its bits as an int64
 
 
 def decimal(text: str, scale: int = 2) -> int:

@@ -270,8 +270,7 @@ class CubitTable:
         L.check(self.lib.cubit_table_add_bitpacked_column(self.handle, col, typ, data.ctypes.data, data.nbytes,
                                                           so.ctypes.data, sr.ctypes.data, len(so),
                                                           vw.ctypes.data if vw is not None else None))
-        self.types[col] = L.TYPE_INT32 if typ in (L.TYPE_INT8, L.TYPE_INT16, L.TYPE_UINT8, L.TYPE_UINT16,
-                                                  L.TYPE_INT32) else L.TYPE_INT64
+        self.types[col] = self.column_data(col)[1]
 
     def add_string_column(self, col: int, values, dictionary: Optional[Dictionary] = None) -> Dictionary:
         """Register a VARCHAR column from a list of str / bytes / None (NULL): encoded against
@@ -296,7 +295,8 @@ class CubitTable:
 
     def download_column(self, col: int) -> np.ndarray:
         ptr, typ = self.column_data(col)
-        dt = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64}.get(typ, np.int64)
+        dt = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64, L.TYPE_UINT64: np.uint64,
+              L.TYPE_VARCHAR: np.int32}.get(typ, np.int64)
         out = np.empty(self.n_rows, dtype=dt)
         if self.n_rows:
             L.check(self.lib.cubit_memcpy_d2h(self.ctx.handle, out.ctypes.data, C.c_void_p(ptr), out.nbytes))
@@ -315,6 +315,8 @@ class CubitTable:
                 from cubit_amd.filters import string_ref
 
                 k = np.array([string_ref(x) for x in keys], dtype=np.int64)
+            elif typ == L.TYPE_UINT64:  # UBIGINT keys as their bits
+                k = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64)).view(np.int64)
             else:
                 is_fp = typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(keys).dtype.kind == "f"
                 k = L.fp_bits(keys, typ) if is_fp else np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
@@ -354,6 +356,8 @@ class CubitTable:
         typ = self.types.get(col)
         if typ in (L.TYPE_FLOAT, L.TYPE_DOUBLE) and np.asarray(values).dtype.kind == "f":
             values = L.fp_bits(values, typ)  # FLOAT / DOUBLE values cross as their bit patterns
+        if np.asarray(values).dtype == np.uint64:
+            values = np.ascontiguousarray(values).view(np.int64)  # UBIGINT values as their bits
         values = np.ascontiguousarray(values, dtype=np.int64)
         versions = np.ascontiguousarray(versions, dtype=np.uint64)
         if valid is None:
@@ -377,7 +381,7 @@ class CubitTable:
         for c in cols:
             a = np.ascontiguousarray(columns[c])
             want = {L.TYPE_INT32: np.int32, L.TYPE_FLOAT: np.float32, L.TYPE_DOUBLE: np.float64,
-                    L.TYPE_VARCHAR: np.int32}.get(self.types.get(c), np.int64)
+                    L.TYPE_VARCHAR: np.int32, L.TYPE_UINT64: np.uint64}.get(self.types.get(c), np.int64)
             if a.dtype != want or len(a) != n_new:
                 raise ValueError(f"column {c}: {len(a)} values of {a.dtype}, want {n_new} of {np.dtype(want)}")
             keep.append(a)

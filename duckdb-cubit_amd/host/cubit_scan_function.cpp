@@ -438,7 +438,9 @@ void PlanWidths(PartScan& P, const std::vector<column_t>& column_ids, const std:
                 lo = 0;
                 hi = 0xffffffffll;
             }
-            if (P.nullable[e]) {
+            if (P.nullable[e] && type == CUBIT_TYPE_UINT64) {
+                lo = 0;  // bits of unsigned bounds: 0 is below every value, and the span stays unsigned
+            } else if (P.nullable[e]) {
                 lo = std::min<int64_t>(lo, 0);
                 hi = std::max<int64_t>(hi, 0);
             }

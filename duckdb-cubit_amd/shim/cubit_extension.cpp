@@ -241,9 +241,9 @@ static void Check(int rc) {
 // Physical types whose values the GPU compares exactly, carried as int64: the signed integers up
 // to 64 bits (DATE, TIME, TIMESTAMP*, DECIMAL(≤18) included), BOOLEAN, the unsigned integers up to
 // 32 bits, and FLOAT / DOUBLE as their bit patterns (the library compares them with DuckDB's
-// floating-point operators, include/cubit_gpu.h), and VARCHAR as int32 codes of the table's
-// order-preserving dictionary (constants cross as cubit_strings). UBIGINT, HUGEINT and UHUGEINT stay
-// on seq_scan.
+// floating-point operators, include/cubit_gpu.h), UBIGINT as its bits (compared unsigned), and
+// VARCHAR as int32 codes of the table's order-preserving dictionary (constants cross as
+// cubit_strings). HUGEINT and UHUGEINT stay on seq_scan.
 static bool GpuPhysical(PhysicalType t) {
     switch (t) {
     case PhysicalType::BOOL:
@@ -254,6 +254,7 @@ static bool GpuPhysical(PhysicalType t) {
     case PhysicalType::UINT8:
     case PhysicalType::UINT16:
     case PhysicalType::UINT32:
+    case PhysicalType::UINT64:   // the bits, compared unsigned
     case PhysicalType::FLOAT:
     case PhysicalType::DOUBLE:
     case PhysicalType::VARCHAR:  // as codes of an order-preserving dictionary (cubit_dict)
@@ -265,7 +266,8 @@ static bool GpuPhysical(PhysicalType t) {
 
 // uploaded from 8-byte values (INT64, UINT32 widened, DOUBLE patterns; else from 4-byte ones)
 static bool WidePhysical(PhysicalType t) {
-    return t == PhysicalType::INT64 || t == PhysicalType::UINT32 || t == PhysicalType::DOUBLE;
+    return t == PhysicalType::INT64 || t == PhysicalType::UINT32 || t == PhysicalType::UINT64 ||
+           t == PhysicalType::DOUBLE;
 }
 
 // the CUBIT_TYPE_* a column is registered as
@@ -275,6 +277,8 @@ static int UploadType(PhysicalType t) {
         return CUBIT_TYPE_FLOAT;
     case PhysicalType::DOUBLE:
         return CUBIT_TYPE_DOUBLE;
+    case PhysicalType::UINT64:
+        return CUBIT_TYPE_UINT64;
     default:
         return WidePhysical(t) ? CUBIT_TYPE_INT64 : CUBIT_TYPE_INT32;
     }
@@ -378,6 +382,8 @@ static int64_t ConstantAsInt64(const Value &v) {
         return FloatBits(v.GetValueUnsafe<float>());
     case PhysicalType::DOUBLE:
         return DoubleBits(v.GetValueUnsafe<double>());
+    case PhysicalType::UINT64:
+        return (int64_t)v.GetValueUnsafe<uint64_t>();  // the bits
     default:
         return v.GetValueUnsafe<int64_t>();  // BIGINT, DECIMAL(10..18) scaled
     }
@@ -788,6 +794,9 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
             memcpy(&d[1], &hi, 8);
             NumericStats::SetMin(stats, phys == PhysicalType::FLOAT ? Value::FLOAT(f[0]) : Value::DOUBLE(d[0]));
             NumericStats::SetMax(stats, phys == PhysicalType::FLOAT ? Value::FLOAT(f[1]) : Value::DOUBLE(d[1]));
+        } else if (phys == PhysicalType::UINT64) {
+            NumericStats::SetMin(stats, Value::UBIGINT((uint64_t)lo));
+            NumericStats::SetMax(stats, Value::UBIGINT((uint64_t)hi));
         } else {
             NumericStats::SetMin(stats, Value::Numeric(type, lo));  // DECIMAL: lo is the storage value
             NumericStats::SetMax(stats, Value::Numeric(type, hi));
@@ -1187,6 +1196,8 @@ static int SegmentType(PhysicalType t) {
         return CUBIT_TYPE_UINT16;
     case PhysicalType::UINT32:
         return CUBIT_TYPE_UINT32;
+    case PhysicalType::UINT64:
+        return CUBIT_TYPE_UINT64;
     default:
         return -1;
     }

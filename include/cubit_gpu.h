@@ -42,8 +42,10 @@ extern "C" {
  *      values; the narrower and unsigned codes name the T of BITPACKING segments
  *      (cubit_table_add_bitpacked_column; bitpacking.cpp:953-977 GetFunction: BOOL and INT8
  *      as int8_t, …, UINT64 and LIST offsets as uint64_t), unpacked into an INT32 column
- *      (INT8, INT16, UINT8, UINT16) or an INT64 column (UINT32, and UINT64 whose every valid
- *      value is below 2^63). */
+ *      (INT8, INT16, UINT8, UINT16) or an INT64 column (UINT32). A UINT64 (UBIGINT) column
+ *      holds the unsigned values' 64 bits and compares them unsigned, through the key
+ *      v ^ 2^63 (cubit_fp_key): its constants, keys, update values, statistics and probed values
+ *      are those bits in an int64. */
 #define CUBIT_TYPE_INT32 0
 #define CUBIT_TYPE_INT64 1
 #define CUBIT_TYPE_INT8 2
@@ -72,10 +74,12 @@ extern "C" {
  * values and statistics are codes. */
 #define CUBIT_TYPE_VARCHAR 10
 
-/* The comparison key of a FLOAT / DOUBLE bit pattern (any other type: the value itself): every
+/* The comparison key of a FLOAT / DOUBLE bit pattern or UINT64 value (any other type: the value
+ * itself): UINT64 → v ^ 2^63; FLOAT / DOUBLE: every
  * NaN → one key above +inf's, -x → -(pattern of x) (so -0.0 and +0.0 share key 0), +x → its pattern.
  * cubit_fp_value is its inverse on keys (a NaN key → the positive quiet NaN, key 0 → +0.0). */
 static inline int64_t cubit_fp_key(int type, int64_t bits) {
+    if (type == CUBIT_TYPE_UINT64) return (int64_t)((uint64_t)bits ^ 0x8000000000000000ull);  /* unsigned order */
     if (type == CUBIT_TYPE_FLOAT) {
         const uint32_t u = (uint32_t)bits, mag = u & 0x7fffffffu;
         if (mag > 0x7f800000u) return 0x7fc00000;
@@ -89,6 +93,7 @@ static inline int64_t cubit_fp_key(int type, int64_t bits) {
     return bits;
 }
 static inline int64_t cubit_fp_value(int type, int64_t key) {
+    if (type == CUBIT_TYPE_UINT64) return (int64_t)((uint64_t)key ^ 0x8000000000000000ull);
     if (type == CUBIT_TYPE_FLOAT) return key < 0 ? (int64_t)(0x80000000u | (uint32_t)(-key)) : key;
     if (type == CUBIT_TYPE_DOUBLE) return key < 0 ? (int64_t)(0x8000000000000000ull | (uint64_t)(-key)) : key;
     return key;
@@ -342,9 +347,10 @@ int cubit_table_column_data(cubit_table *t, int col, const void **data, int *typ
  * Index bitvectors are not rebuilt by it (rebuild with cubit_table_build_index). `type` may be
  * any CUBIT_TYPE_* code: an 8- / 16-bit or unsigned column is widened on the device into an
  * owned INT32 / INT64 column (even from on_device data) — TINYINT … UINTEGER vectors as DuckDB
- * holds them — and a UINT64 column with a valid value of 2^63 or
- * more is refused (CUBIT_ERR_UNSUPPORTED). Appends, updates and probes then use the INT32 /
- * INT64 values (cubit_table_column_data reports the type held). */
+ * holds them; a UINT64 (UBIGINT), FLOAT or DOUBLE column keeps its values' bits and compares them
+ * through its key (see the type codes); a VARCHAR column is registered with its dictionary
+ * (cubit_table_add_dict_column). Appends, updates and probes then use the stored values
+ * (cubit_table_column_data reports the type held). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
                            int on_device);
 /* ---- VARCHAR dictionaries. A dictionary is built once per table (every partition of a table
@@ -382,8 +388,8 @@ int cubit_table_column_changed(cubit_table *t, int col);
  * (CONSTANT, CONSTANT_DELTA, FOR, DELTA_FOR) into the column; NULLs come from `validity`
  * (host words; DuckDB keeps them in a separate validity segment). `type` is the segments' T,
  * any CUBIT_TYPE_* (header fields of T's size, T's wrap-around arithmetic); the column holds
- * the values widened to INT32 or INT64 (see the type codes). A UINT64 column with a valid value
- * of 2^63 or more is refused (CUBIT_ERR_UNSUPPORTED) after the unpack. Malformed segments are
+ * the values widened to INT32 or INT64, or (UINT64) as their 64 bits, compared unsigned (see the
+ * type codes). Malformed segments are
  * refused before anything is launched. With timing on, the unpack kernel is a timed launch
  * (cubit_last_kernel_ms). */
 int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,

@@ -125,6 +125,17 @@ static inline int cmp_str(int cmp, int64_t v, int64_t c) {
 /* a comparison of values of column type `type` (FP: bit patterns; VARCHAR: ostring addresses) */
 static inline int cmp_typed(int type, int cmp, int64_t v, int64_t c) {
     if (type == OTYPE_VARCHAR) return cmp_str(cmp, v, c);
+    if (type == OTYPE_UINT64) {
+        const uint64_t a = (uint64_t)v, b = (uint64_t)c;
+        switch (cmp) {
+        case OCMP_EQ: return a == b;
+        case OCMP_NE: return a != b;
+        case OCMP_LT: return a < b;
+        case OCMP_LE: return a <= b;
+        case OCMP_GT: return a > b;
+        default: return a >= b;
+        }
+    }
     if (type == OTYPE_FLOAT || type == OTYPE_DOUBLE) return cmp_fp(cmp, fp_value(type, v), fp_value(type, c));
     return cmp_op(cmp, v, c);
 }
@@ -277,6 +288,10 @@ static uint64_t templated_filter_selection(const vecbuf *v, int cmp, int64_t c, 
             sel[rc] = idx;
             rc += (uint64_t)pass;
         }
+        return rc;
+    }
+    if (v->type == OTYPE_UINT64) {  /* FilterSelectionSwitch<uint64_t>: unsigned compares */
+        TFS_CMP(uint64_t)
         return rc;
     }
     if (v->wide) {

@@ -13,7 +13,8 @@ extern "C" {
  * carry their bit patterns (FLOAT: the 32-bit pattern, zero-extended) */
 /* VARCHAR: `data` is an array of ostring; constants, update values and fetched values carry the
  * address of an ostring (string_t comparisons: unsigned bytes, then length — string_type.hpp:143-206) */
-enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3, OTYPE_VARCHAR = 4 };
+/* UINT64 (UBIGINT): the values' bits in `data`, constants and values as those bits, compared unsigned */
+enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3, OTYPE_VARCHAR = 4, OTYPE_UINT64 = 5 };
 typedef struct {
     const char *data;
     uint64_t size;

@@ -18,7 +18,7 @@ HERE = Path(__file__).resolve().parent
 LIB = HERE / "lib" / "libcubit_oracle.so"
 
 OMAX_COLS = 16
-OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE, OTYPE_VARCHAR = 0, 1, 2, 3, 4
+OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE, OTYPE_VARCHAR, OTYPE_UINT64 = 0, 1, 2, 3, 4, 5
 OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
 
 
@@ -107,7 +107,7 @@ class Column:
 
     def __init__(self, data: np.ndarray, validity: Optional[np.ndarray] = None, updates=None):
         self.data = np.ascontiguousarray(data)
-        assert self.data.dtype in (np.int32, np.int64, np.float32, np.float64)
+        assert self.data.dtype in (np.int32, np.int64, np.float32, np.float64, np.uint64)
         self.validity = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
         self.upd_valid = None
         if updates is None:
@@ -116,6 +116,8 @@ class Column:
             r, v, ver = updates[:3]
             if self.data.dtype.kind == "f" and np.asarray(v).dtype.kind == "f":
                 v = fp_bits(v, self.data.dtype)
+            if np.asarray(v).dtype == np.uint64:  # UBIGINT values as their bits
+                v = np.ascontiguousarray(v, dtype=np.uint64).view(np.int64)
             self.upd = (np.ascontiguousarray(r, dtype=np.int64), np.ascontiguousarray(v, dtype=np.int64),
                         np.ascontiguousarray(ver, dtype=np.uint64))
             if len(updates) > 3 and updates[3] is not None:
@@ -124,7 +126,7 @@ class Column:
     def ocol(self) -> OCol:
         c = OCol()
         c.type = {np.dtype(np.int32): OTYPE_INT32, np.dtype(np.int64): OTYPE_INT64, np.dtype(np.float32): OTYPE_FLOAT,
-                  np.dtype(np.float64): OTYPE_DOUBLE}[self.data.dtype]
+                  np.dtype(np.float64): OTYPE_DOUBLE, np.dtype(np.uint64): OTYPE_UINT64}[self.data.dtype]
         c.data = self.data.ctypes.data
         c.validity = self.validity.ctypes.data if self.validity is not None else None
         if self.upd is not None:

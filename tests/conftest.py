@@ -16,7 +16,8 @@ def _ensure_built():
     need = [PKG / "lib" / "libcubit_datagen.so", PKG / "lib" / "libcubitgpu.so", ROOT / "oracle" / "lib" / "libcubit_oracle.so"]
     if not all(p.exists() for p in need):
         subprocess.run(["make", "-s", "-C", str(PKG), "-j8"], check=True)
-        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+    # the oracle (one gcc line, test infrastructure) is kept current with its sources every session
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
 
 
 _ensure_built()

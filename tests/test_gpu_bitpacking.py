@@ -294,15 +294,17 @@ def test_every_type_unpacks_and_filters(ctx, dtype, mode):
     the 4-byte alignment for 1- and 2-byte T, T's wrap-around arithmetic in descending
     DELTA_FOR / CONSTANT_DELTA groups) unpack into the INT32 / INT64 column to the oracle's
     values, and the filter straight from the segments equals the oracle's scan of them, for
-    every comparison. UBIGINT values of 2^63 and more are refused loudly."""
-    below = np.dtype(dtype) == np.uint64
-    v, valid, c = typed_case(dtype, mode, below_2_63=below)
+    every comparison. UBIGINT keeps its 64 bits over the whole range (values past 2^63
+    included) and compares them unsigned, as the oracle's FilterSelectionSwitch<uint64_t>."""
+    ubig = np.dtype(dtype) == np.uint64
+    v, valid, c = typed_case(dtype, mode)
     n = len(v)
     t, vw = packed_table(ctx, c, dtype, n, valid, row_base=7)
     got = t.download_column(0)
-    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else np.int64)
-    assert np.array_equal(got[valid], v[valid].astype(np.int64)), (np.dtype(dtype).name, mode)
-    wide = v.astype(np.int64)
+    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else
+                         np.uint64 if ubig else np.int64)
+    assert np.array_equal(got[valid], v[valid].astype(got.dtype)), (np.dtype(dtype).name, mode)
+    wide = v if ubig else v.astype(np.int64)
     oc = O.Column(wide, vw)
     rng = np.random.default_rng(11)
     picks = [int(x) for x in rng.choice(wide[valid], 4)] + [int(wide[valid].min()), int(wide[valid].max())]
@@ -316,14 +318,6 @@ def test_every_type_unpacks_and_filters(ctx, dtype, mode):
         t.use_packed_filter(False)
         assert np.array_equal(t.scan(fs), ref), (np.dtype(dtype).name, mode, cmp, k)
     t.close()
-    if below:
-        v2, valid2, c2 = typed_case(dtype, mode)  # the full UBIGINT range
-        if (v2[valid2] >= np.uint64(2 ** 63)).any():
-            t2 = CubitTable(ctx, len(v2))
-            with pytest.raises(Exception, match="2\\^63"):
-                t2.add_bitpacked_column(0, c2.data, c2.seg_off, c2.seg_count, dtype,
-                                        validity=validity_from_mask(valid2))
-            t2.close()
 
 
 @pytest.mark.parametrize("mode", FORCED)
@@ -331,19 +325,14 @@ def test_every_type_unpacks_and_filters(ctx, dtype, mode):
 def test_bitwidths_reference_case_on_gpu(ctx, bits, mode):
     """bitpacking_bitwidths.test_slow through K5: each table's unpacked column has the
     reference's distinct-value counts (bits or bits - 1 values, 2,048 rows each), and an
-    equality scan straight from the segments finds each value's 2,048 rows. UBIGINT's 2^63 is
-    beyond an INT64 column: that table is refused."""
+    equality scan (straight from the segments where the type allows) finds each value's 2,048
+    rows — UBIGINT's 2^63 included, read back and compared unsigned."""
     for name, v in bitwidth_tables(bits).items():
         c = O.bp_compress(v, None, mode)
         t = CubitTable(ctx, len(v))
-        if v.dtype == np.uint64 and int(v.max()) >= 2 ** 63:
-            with pytest.raises(Exception, match="2\\^63"):
-                t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, v.dtype)
-            t.close()
-            continue
         t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, v.dtype)
         got = t.download_column(0)
-        assert np.array_equal(got, v.astype(np.int64)), (name, mode)
+        assert np.array_equal(got, v.astype(got.dtype)), (name, mode)
         vals, counts = np.unique(got, return_counts=True)
         assert len(vals) == (bits - 1 if name == "test_signed_pos" else bits) and set(counts.tolist()) == {2048}
         t.use_packed_filter(True)
@@ -387,13 +376,22 @@ def test_nulls_reference_case_on_gpu(ctx, mode):
 
 
 def test_delta_full_range_reference_case_on_gpu(ctx):
-    """bitpacking_delta.test_slow's UBIGINT column (0 and 2^64 - 1) is refused by K5 with a
-    message naming the bound, not read back wrong."""
+    """bitpacking_delta.test_slow's UBIGINT column (0 and 2^64 - 1 alternating) through K5: read
+    back bit-exact, and the unsigned comparisons split it as the reference's SUM / COUNT see it —
+    2^64 - 1 is the greatest value, not -1."""
     v = np.where(np.arange(100_000) % 2 == 0, np.uint64(0), np.uint64(2 ** 64 - 1)).astype(np.uint64)
     c = O.bp_compress(v, None, "for")
     t = CubitTable(ctx, len(v))
-    with pytest.raises(Exception, match="2\\^63"):
-        t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, np.uint64)
+    t.add_bitpacked_column(0, c.data, c.seg_off, c.seg_count, np.uint64)
+    assert np.array_equal(t.download_column(0), v)
+    for cmp, k, want in ((">", 0, 50_000), ("=", 2 ** 64 - 1, 50_000), ("<", 2 ** 63, 50_000), (">=", 0, 100_000),
+                         ("<=", 2 ** 64 - 2, 50_000)):
+        rows = t.scan(F.TableFilterSet({0: F.ConstantFilter(cmp, k)}))
+        assert len(rows) == want, (cmp, k)
+        assert np.array_equal(rows, O.table_scan([O.Column(v)], F.serialize(F.TableFilterSet(
+            {0: F.ConstantFilter(cmp, k)})), len(v)))
+    lo, hi, _, _ = t.column_statistics(0)
+    assert (lo & (2 ** 64 - 1), hi & (2 ** 64 - 1)) == (0, 2 ** 64 - 1)
     t.close()
 
 
@@ -421,24 +419,27 @@ def test_plain_columns_of_every_type(ctx, dtype):
     """cubit_table_add_column with a narrower or unsigned type code (TINYINT … UBIGINT vectors
     as DuckDB holds them) widens the values on the device into an INT32 / INT64 column; index
     scans, unindexed comparisons and the probe then equal numpy on the widened values. UBIGINT
-    values of 2^63 and more are refused."""
+    keeps its 64 bits over the whole range and compares them unsigned (the probe hands the bits
+    back as int64)."""
     rng = np.random.default_rng(abs(hash(np.dtype(dtype).name)) % 2 ** 32)
     n = 300_007
+    ubig = np.dtype(dtype) == np.uint64
     if dtype is np.bool_:
         v = rng.random(n) < 0.3
     else:
         info = np.iinfo(dtype)
-        hi = min(int(info.max), 2 ** 63 - 1)
-        v = rng.integers(info.min, hi, n, dtype=dtype, endpoint=True)
+        v = rng.integers(info.min, info.max, n, dtype=dtype, endpoint=True)
         v[:1000] = info.min
-    wide = v.astype(np.int64)
+    wide = v if ubig else v.astype(np.int64)  # UBIGINT: numpy's unsigned order is the reference's
     valid = rng.random(n) > 0.1
     t = CubitTable(ctx, n, row_base=9)
     t.add_column(0, v, validity=validity_from_mask(valid))
     got = t.download_column(0)
-    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else np.int64)
+    assert got.dtype == (np.int32 if np.dtype(dtype).itemsize <= 2 or dtype is np.int32 else
+                         np.uint64 if ubig else np.int64)
     assert np.array_equal(got[valid], wide[valid])
-    assert np.array_equal(probe_all(ctx, t, 0, n, row_base=9)[valid], wide[valid])
+    probed = probe_all(ctx, t, 0, n, row_base=9)
+    assert np.array_equal((probed.view(np.uint64) if ubig else probed)[valid], wide[valid])
     k = int(np.median(wide[valid]))
     for cmp, mask in (("<", wide < k), (">=", wide >= k), ("=", wide == int(wide[valid][0]))):
         kk = int(wide[valid][0]) if cmp == "=" else k
@@ -450,13 +451,17 @@ def test_plain_columns_of_every_type(ctx, dtype):
         fs = F.TableFilterSet({0: F.ConstantFilter("=", int(wide[valid][1]))})
         ref = np.flatnonzero((wide == int(wide[valid][1])) & valid).astype(np.int64) + 9
         assert np.array_equal(t.scan(fs), ref)
+    if ubig:  # a range index with keys across 2^63: leaves, the candidate check and the statistics
+        keys = [2 ** 62, 2 ** 63 - 1, 2 ** 63, 2 ** 63 + 2 ** 61, 2 ** 64 - 5]
+        t.build_index(0, L.INDEX_RANGE, keys)
+        for kk in keys + [2 ** 63 + 12345, 3, 2 ** 64 - 1]:
+            for cmp, op in (("<", np.less), (">=", np.greater_equal), ("=", np.equal)):
+                fs = F.TableFilterSet({0: F.ConstantFilter(cmp, kk)})
+                ref = np.flatnonzero(op(wide, np.uint64(kk)) & valid).astype(np.int64) + 9
+                assert np.array_equal(t.scan(fs), ref), (cmp, kk)
+        lo, hi, _, _ = t.column_statistics(0)
+        assert (lo & (2 ** 64 - 1), hi & (2 ** 64 - 1)) == (int(wide[valid].min()), int(wide[valid].max()))
     t.close()
-    if np.dtype(dtype) == np.uint64:
-        big = np.full(1000, 2 ** 63, np.uint64)
-        t2 = CubitTable(ctx, len(big))
-        with pytest.raises(Exception, match="2\\^63"):
-            t2.add_column(0, big)
-        t2.close()
 
 
 @pytest.mark.parametrize("mode", ["auto", "for", "delta_for", "constant_delta"])

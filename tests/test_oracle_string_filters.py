@@ -77,3 +77,21 @@ def test_fetch_returns_strings_with_updates():
     assert col.decode(got, ok) == [b"new", None, b"", vals[4]]
     fs = F.TableFilterSet({0: F.ConstantFilter("=", b"new")})
     assert 3 in O.table_scan([col], F.serialize(fs), 500, tx=tx).tolist()
+
+
+def test_ubigint_compares_unsigned():
+    """FilterSelectionSwitch<uint64_t> on the oracle: values past 2^63 are the largest (numpy's
+    unsigned order), NULL rows never pass."""
+    rng = np.random.default_rng(5)
+    edges = np.array([0, 1, 2 ** 63 - 1, 2 ** 63, 2 ** 64 - 1], dtype=np.uint64)
+    v = np.concatenate([edges, rng.integers(0, 2 ** 64 - 1, 3000, dtype=np.uint64, endpoint=True)])
+    valid = rng.random(len(v)) > 0.1
+    from cubit_amd.datagen import validity_from_mask
+
+    col = O.Column(v, validity_from_mask(valid))
+    for c in [int(x) for x in edges] + [int(v[9])]:
+        for op, f in [("=", np.equal), ("!=", np.not_equal), ("<", np.less), ("<=", np.less_equal),
+                      (">", np.greater), (">=", np.greater_equal)]:
+            fs = F.TableFilterSet({0: F.ConstantFilter(op, c)})
+            want = np.flatnonzero(f(v, np.uint64(c)) & valid)
+            assert np.array_equal(O.table_scan([col], F.serialize(fs), len(v)), want), (op, c)
