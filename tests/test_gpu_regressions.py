@@ -231,3 +231,27 @@ def test_exact_index_over_a_wide_span(ctx):
         if step == 0:
             t.append({0: extra}, {0: validity_from_mask(ev)})
     t.close()
+
+
+def test_equality_at_int64_max_on_a_binned_column(ctx):
+    """Round 6: an AND over a column with a BINS index folds its constants into one half-open
+    interval; `v = INT64_MAX` has no representable end, and was folded to FALSE. It is [INT64_MAX,
+    ∞) = {INT64_MAX} (UBIGINT's 2^64 - 1 has that key). Every comparison at both ends of int64
+    against numpy, with and without the bins."""
+    n = 200_003
+    rng = np.random.default_rng(3)
+    v = rng.integers(-1000, 1000, n).astype(np.int64)
+    v[::7] = np.iinfo(np.int64).max
+    v[::11] = np.iinfo(np.int64).min
+    for bins in (False, True):
+        t = CubitTable(ctx, n)
+        t.add_column(0, v)
+        t.build_index(0, L.INDEX_RANGE)
+        if bins:
+            t.build_index(0, L.INDEX_BINS, [-(2 ** 63), -10, 0, 10, 2 ** 63 - 1])
+        for c in (2 ** 63 - 1, -(2 ** 63), 0):
+            for cmp, op in (("=", np.equal), ("<", np.less), ("<=", np.less_equal), (">", np.greater),
+                            (">=", np.greater_equal), ("!=", np.not_equal)):
+                fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
+                assert np.array_equal(t.scan(fs), np.flatnonzero(op(v, c))), (bins, cmp, c)
+        t.close()
