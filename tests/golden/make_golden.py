@@ -377,7 +377,14 @@ def main():
         "test/sql/delete/test_segment_deletes.test", "test/sql/transactions/test_multi_transaction_append.test",
         "test/sql/transactions/test_multi_version_large.test", "test/sql/transactions/test_null_version.test",
         "test/sql/transactions/test_transaction_local_data.test")}
-    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "mvcc_scripts": mvcc, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
+    # VARCHAR update chains under concurrent transactions (replayed on dictionary codes,
+    # tests/sql_replay.py encode_strings)
+    smvcc = {Path(rel).stem: sqllogic_script(rel) for rel in (
+        "test/sql/update/test_string_update.test", "test/sql/update/test_string_update_null.test",
+        "test/sql/update/test_string_update_rollback.test", "test/sql/update/test_string_update_rollback_null.test",
+        "test/sql/update/test_string_update_many_strings.test", "test/sql/update/test_repeated_string_update.test",
+        "test/sql/update/test_update_same_string_value.test")}
+    (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "mvcc_scripts": mvcc, "string_mvcc_scripts": smvcc, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,

@@ -538,6 +538,14 @@ def answer(q: Query, f: Frame, nulls_first: bool, filtered: bool = False):
     sel, where, order = split_query(q.sql)
     if where and not filtered:
         f = frame_take(f, parse_cond(where)(f)[0])
+    m = re.match(r"DISTINCT (\w+)$", sel, re.I)
+    if m:  # SELECT DISTINCT col [ORDER BY col]: each value once, NULL first or last
+        v, ok = f[m.group(1).lower()]
+        vals = sorted(set(v[ok].tolist()))
+        out = [[x] for x in vals]
+        if (~ok).any():
+            out = [[None]] + out if nulls_first else out + [[None]]
+        return out
     if sel == "*":
         if order:
             col = q.columns[int(order) - 1] if order.isdigit() else order.lower()
@@ -569,6 +577,32 @@ def answer(q: Query, f: Frame, nulls_first: bool, filtered: bool = False):
 
 def cases(golden, group: str):
     return golden["cases"][group]
+
+
+_LITERAL = re.compile(r"'((?:[^']|'')*)'")
+
+
+def encode_strings(case: dict):
+    """A VARCHAR script as an integer one: every string the script names — its literals and the
+    strings of its expected rows — sorted as DuckDB orders strings (string_t: the bytes, then the
+    length: Python's bytes order) and replaced by its rank. The ranks order as the strings do, so
+    comparisons, ORDER BY and DISTINCT replay on them unchanged, and they are the codes of a
+    cubit_dict built from the same strings. Returns (the coded case, the strings by code)."""
+    strings = set()
+    for step in case["script"]:
+        strings.update(m.group(1).replace("''", "'").encode() for m in _LITERAL.finditer(step["sql"]))
+        for row in step.get("rows", []):
+            strings.update(v.encode() for v in row if isinstance(v, str))
+    words = sorted(strings)
+    code = {w: i for i, w in enumerate(words)}
+    steps = []
+    for step in case["script"]:
+        st = dict(step)
+        st["sql"] = _LITERAL.sub(lambda m: str(code[m.group(1).replace("''", "'").encode()]), step["sql"])
+        if "rows" in st:
+            st["rows"] = [[code[v.encode()] if isinstance(v, str) else v for v in row] for row in step["rows"]]
+        steps.append(st)
+    return {**case, "script": steps}, words
 
 
 def queries(case: dict):
