@@ -305,3 +305,21 @@ def test_updates_merges_and_appends(ctx, dt, index):
             fs = F.TableFilterSet({0: F.ConstantFilter(cmp, c)})
             txn, tx = tx_other
             assert np.array_equal(t.scan(fs, txn=txn), oracle_rows([acol], fs, len(allv), tx)), (cmp, c)
+
+
+@pytest.mark.parametrize("index", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_nan_ordering_counts_on_gpu(ctx, dt, index):
+    """nan_ordering.test's filtered counts (f > 0: 4, f < 0: 3 over 10,008 rows with two NaNs,
+    ±inf and a NULL) through cubit_table_scan's count, with and without an index."""
+    from test_oracle_float_filters import ORDERING, ordering_column
+
+    vals, valid = ordering_column(dt)
+    t = CubitTable(ctx, len(vals))
+    t.add_column(0, vals, validity_from_mask(valid))
+    if index is not None:
+        t.build_index(0, index)
+    for c in ORDERING["counts"]:
+        fs = F.TableFilterSet({0: F.ConstantFilter(OPS[c["cmp"]], dt(float(c["constant"])))})
+        assert t.count(fs) == c["count"], c["sql"]
+    t.close()

@@ -80,3 +80,42 @@ def test_signed_zero_and_nan_payloads(dt):
     assert rows("<=", pos_nan) == set(range(n))
     assert rows(">", pos_nan) == set()
     assert rows(">=", neg_nan) == {6, 7}
+
+
+ORDERING = json.loads((Path(__file__).resolve().parent / "golden" / "float_filter_cases.json").read_text())["ordering"]
+
+
+def ordering_column(dt):
+    """nan_ordering.test's table: the values and the NULL mask."""
+    special = {"nan": math.nan, "infinity": math.inf, "inf": math.inf, "-infinity": -math.inf, "-inf": -math.inf}
+    vals, valid = [], []
+    for v, k in ORDERING["inserted"]:
+        vals += [dt(0.0) if v == "null" else dt(special.get(v, v) if v in special else float(v))] * k
+        valid += [v != "null"] * k
+    return np.array(vals, dtype=dt), np.array(valid)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_nan_ordering_counts_and_order(dt):
+    """nan_ordering.test: COUNT(*) WHERE f > 0 = 4 and WHERE f < 0 = 3 over its 10,008 rows (two
+    NaNs, ±inf, NULL), on the oracle; and the total order its ORDER BY prints (-inf < -1 < 1 < inf <
+    nan, NULL first) is the order of the C ABI's comparison keys (cubit_fp_key, restated here as
+    numpy: every NaN → one key above +inf, -x → -pattern(x))."""
+    from cubit_amd.datagen import validity_from_mask
+
+    vals, valid = ordering_column(dt)
+    col = O.Column(vals, validity_from_mask(valid))
+    for c in ORDERING["counts"]:
+        fs = F.TableFilterSet({0: F.ConstantFilter(OPS[c["cmp"]], dt(float(c["constant"])))})
+        assert len(O.table_scan([col], F.serialize(fs), len(vals))) == c["count"], c["sql"]
+    first6 = vals[:6][valid[:6]]
+    bits = O.fp_bits(first6, dt).astype(np.uint64) if dt == np.float32 else O.fp_bits(first6, dt).view(np.uint64)
+    width = 32 if dt == np.float32 else 64
+    sign = bits >> np.uint64(width - 1)
+    mag = bits & np.uint64((1 << (width - 1)) - 1)
+    nan = mag > np.uint64(0x7F800000 if dt == np.float32 else 0x7FF0000000000000)
+    nan_key = 0x7FC00000 if dt == np.float32 else 0x7FF8000000000000
+    key = np.where(nan, nan_key, np.where(sign == 1, -mag.astype(np.int64), mag.astype(np.int64)))
+    order = ["NULL"] + [printed(float(x)) for x in first6[np.argsort(key, kind="stable")]]
+    want = [x if x in ("NULL", "nan", "inf", "-inf") else f"{float(x):g}" for x in ORDERING["order_by_f"]]
+    assert order == want
