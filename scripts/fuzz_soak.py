@@ -4,7 +4,9 @@ a larger size and for a fixed wall-clock budget, with fresh seeds — random pus
 TableFilterSets and residual AND/OR trees over range / equality / edge-keyed range + bins /
 unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
 updates from a writer; each scan under a random decode kernel (AUTO, pair-claimed, run-claimed,
-look-back). Every result is compared with the oracle; every third filter also runs through the
+look-back); every third table holds the typed columns instead (DOUBLE / FLOAT with NaN and ±0,
+VARCHAR dictionary codes, full-range UBIGINT: tests/test_gpu_typed_fuzz.py). Every result is
+compared with the oracle; every third filter also runs through the
 table function (random projection with the row id, 1-4 pipeline tasks, staged or per-window
 copies): row ids, values and NULL-ness against the oracle's scan and fetch. Prints one summary
 line.
@@ -29,6 +31,7 @@ from cubit_amd.scan_function import ROW_ID, CubitScanFunction  # noqa: E402
 from cubit_amd.table import Context, CubitTable  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from test_gpu_planner_fuzz import TXN_START, rand_const_filter, rand_residual  # noqa: E402
+from test_gpu_typed_fuzz import typed_round  # noqa: E402
 
 
 def table_function_check(t, rng, fs, residual, txn, ref, ocols, row_base, tx, label):
@@ -159,7 +162,10 @@ def main():
     rounds = checks = 0
     seed = seed0
     while time.perf_counter() < t_end:
-        checks += round_(ctx, seed, n, with_updates=bool(rounds % 2))
+        if rounds % 3 == 2:  # FLOAT / DOUBLE / VARCHAR / UBIGINT columns (tests/test_gpu_typed_fuzz.py)
+            checks += typed_round(ctx, seed, n, with_updates=bool(rounds % 2), n_cases=30)
+        else:
+            checks += round_(ctx, seed, n, with_updates=bool(rounds % 2))
         rounds += 1
         seed += 1
         print(f"round {rounds}: {checks} scans match the oracle", flush=True)
