@@ -101,7 +101,9 @@ def round_(ctx, seed, n, with_updates):
                 t.use_packed_filter(bool(rng.random() < 0.5))
             else:
                 t.add_column(c, typed, vw)
-            d = typed.astype(np.int32 if dt.itemsize <= 2 or dt == np.int32 else np.int64)
+            # the oracle's view of the column: UBIGINT stays unsigned (its constants cross as bits, so
+            # a negative constant is a value past 2^63 on both sides); the others as held (INT32 / INT64)
+            d = typed if dt == np.uint64 else typed.astype(np.int32 if dt.itemsize <= 2 or dt == np.int32 else np.int64)
         else:
             t.add_column(c, d, vw)
         data.append((d, vw))
