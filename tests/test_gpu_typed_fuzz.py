@@ -201,3 +201,74 @@ def table_function_check(t, rng, fs, residual, txn, ref, ocols, d, row_base, tx,
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_typed_random_filters_match_oracle(ctx, seed):
     assert typed_round(ctx, 7000 + seed, 300_007, with_updates=bool(seed % 2)) == 24
+
+
+@pytest.mark.parametrize("tasks", [1, 3])
+def test_typed_columns_over_partitions(tasks):
+    """A table of DOUBLE, VARCHAR (one dictionary, codes global) and UBIGINT columns held as three
+    partitions on three contexts, scanned through one table-function cursor
+    (cubit_scan_init_global_multi): rows and values equal the whole-table oracle; the statistics
+    callback merges the partitions' bounds in each type's order (DOUBLE by its comparison key —
+    a negative maximum is not the largest pattern — and UBIGINT unsigned)."""
+    from cubit_amd import scan_function as S
+
+    rng = np.random.default_rng(77)
+    n, world = 700_003, 3
+    dbl = (rng.standard_normal(n) * 100 - 400).astype(np.float64)  # mostly negative: bit order ≠ value order
+    dbl[rng.integers(0, n, 50)] = math.nan
+    ub = rng.integers(0, 2 ** 64 - 1, n, dtype=np.uint64, endpoint=True)
+    words = [b"", b"a", b"ab", b"b", b"\x80", b"zz"]
+    strs = [words[i] for i in rng.integers(0, len(words), n)]
+    d = Dictionary(words)
+    codes, _ = d.encode(strs)
+    ctxs = [Context(0) for _ in range(world)]
+    cuts = [0, 250_000, 480_000, n]
+    tables = []
+    for r in range(world):
+        b, e = cuts[r], cuts[r + 1]
+        t = CubitTable(ctxs[r], e - b, row_base=b)
+        t.add_column(0, dbl[b:e])
+        seg = np.ascontiguousarray(codes[b:e])
+        L.check(t.lib.cubit_table_add_dict_column(t.handle, 1, d.handle, seg.ctypes.data, None, 0))
+        t.types[1] = L.TYPE_VARCHAR
+        t.add_column(2, ub[b:e])
+        t.build_index(1, L.INDEX_EQUALITY)
+        tables.append(t)
+    lo, hi, hn, hv = S.statistics(tables, 0)
+    finite = dbl[~np.isnan(dbl)]
+    assert np.array([lo]).view(np.float64)[0] == finite.min() and math.isnan(np.array([hi]).view(np.float64)[0])
+    lo, hi, _, _ = S.statistics(tables, 2)
+    assert (lo & (2 ** 64 - 1), hi & (2 ** 64 - 1)) == (int(ub.min()), int(ub.max()))
+    ocols = [O.Column(dbl), O.StringColumn(strs), O.Column(ub)]
+    for fs in [F.TableFilterSet({0: F.ConstantFilter(">", -350.0), 1: F.ConstantFilter("<=", b"ab")}),
+               F.TableFilterSet({2: F.ConstantFilter(">=", 2 ** 63), 1: F.ConstantFilter("!=", b"b")}),
+               F.TableFilterSet({0: F.ConstantFilter("=", math.nan)})]:
+        ref = O.table_scan(ocols, F.serialize(fs), n)
+        fn = S.CubitScanFunction(tables, [0, 1, 2, ROW_ID], [3, 0, 1, 2], fs)
+        parts, lock = [], threading.Lock()
+
+        def task():
+            local = fn.init_local()
+            while True:
+                vals = fn.function(local)
+                if len(vals[0]) == 0:
+                    return
+                with lock:
+                    parts.append(vals)
+
+        th = [threading.Thread(target=task) for _ in range(tasks)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        fn.close()
+        ids = np.concatenate([p[0] for p in parts])
+        o = np.argsort(ids, kind="stable")
+        assert np.array_equal(ids[o], ref)
+        assert np.array_equal(np.concatenate([p[1] for p in parts])[o], O.fp_bits(dbl[ref], np.float64))
+        assert [d.entry(c) for c in np.concatenate([p[2] for p in parts])[o]] == [strs[i] for i in ref]
+        assert np.array_equal(np.concatenate([p[3] for p in parts])[o].view(np.uint64), ub[ref])
+    for t in tables:
+        t.close()
+    for c in ctxs:
+        c.close()
