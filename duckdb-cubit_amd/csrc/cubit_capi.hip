@@ -1108,6 +1108,11 @@ struct DictData {
 struct Column {
     int type = 0;
     std::shared_ptr<const DictData> dict;  // VARCHAR: the dictionary its codes index
+    // FLOAT / DOUBLE: `data` holds the comparison keys (an INT32 / INT64 column to every compare
+    // kernel, key_type) and `raw` the bit patterns as registered (probes, downloads), both owned and
+    // kept in step by appends and merges; raw = data for every other type
+    const void* raw = nullptr;
+    std::unique_ptr<DevBuf> raw_buf;
     const void* data = nullptr;        // device
     const uint64_t* validity = nullptr;  // device, padded to the table's cap_words (null = no NULLs)
     uint64_t cap_rows = 0;  // rows the owned data buffer holds (0 = caller-owned device data)
@@ -1129,6 +1134,10 @@ struct Column {
         bp_n_groups = 0;
     }
 };
+
+// the type and values the compare kernels read for a column, and the values its probes read
+int ktype(const Column& c) { return key_type(c.type); }
+const void* raw_of(const Column& c) { return type_is_fp(c.type) ? c.raw : c.data; }
 
 struct Index {
     int encoding = CUBIT_INDEX_RANGE;
@@ -1413,7 +1422,34 @@ int widen_column(cubit_table* t, Column& c, int type, const void* data, const ui
     return CUBIT_OK;
 }
 
+// A FLOAT / DOUBLE column: the patterns copied into an owned buffer (from host or device memory) and
+// their keys computed beside them into `data`.
+int fp_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
+    const uint64_t esz = type_is32(type) ? 4 : 8;
+    hipStream_t s = t->ctx->stream;
+    c.type = type;
+    c.raw_buf = std::make_unique<DevBuf>();
+    auto keys = std::make_unique<DevBuf>();
+    if (hipMalloc(&c.raw_buf->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess ||
+        hipMalloc(&keys->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "column allocation failed");
+    if (t->n_rows)
+        HIP_CHECK(hipMemcpyAsync(c.raw_buf->p, data, t->n_rows * esz, on_device ? hipMemcpyDeviceToDevice
+                                                                                : hipMemcpyHostToDevice, s));
+    HIP_CHECK(launch_fp_keys(c.raw_buf->p, type, t->n_rows, keys->p, s));
+    c.raw = c.raw_buf->p;
+    c.data = keys->p;
+    c.cap_rows = t->n_rows;
+    c.owned.push_back(std::move(keys));
+    if (validity) {
+        if (int rc = copy_validity(t, c, validity, on_device)) return rc;
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    return CUBIT_OK;
+}
+
 int copy_column(cubit_table* t, Column& c, int type, const void* data, const uint64_t* validity, int on_device) {
+    if (type_is_fp(type)) return fp_column(t, c, type, data, validity, on_device);
     if (type != CUBIT_TYPE_INT32 && type != CUBIT_TYPE_INT64 && type != CUBIT_TYPE_VARCHAR && !type_is_keyed(type))
         return widen_column(t, c, type, data, validity, on_device);
     const uint64_t esz = type_is32(type) ? 4 : 8;  // FLOAT / DOUBLE: the bit patterns as they are
@@ -1487,7 +1523,7 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
                 if ((hvalid[i >> 6] >> (i & 63)) & 1) hv[k++] = hv[i];
             hv.resize(k);
         }
-        if (type == CUBIT_TYPE_DOUBLE || type == CUBIT_TYPE_UINT64)
+        if (type == CUBIT_TYPE_UINT64)  // (a DOUBLE column's `data` already holds keys)
             for (int64_t& v : hv) v = value_key(type, v);
         distinct = distinct_sorted(hv.data(), hv.size());
         if (distinct.size() > kMaxWideDistinct)
@@ -1512,7 +1548,7 @@ int value_stats(cubit_table* t, const void* data, int type, const uint64_t* vali
 
 int column_stats(cubit_table* t, const Column& c, std::vector<int64_t>& distinct, bool want_distinct,
                  int64_t& vmin, int64_t& vmax, bool& any) {
-    return value_stats(t, c.data, c.type, c.validity, t->n_rows, distinct, want_distinct, vmin, vmax, any);
+    return value_stats(t, c.data, ktype(c), c.validity, t->n_rows, distinct, want_distinct, vmin, vmax, any);
 }
 
 }  // namespace
@@ -1947,7 +1983,7 @@ extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, co
             ix.owned.push_back(std::move(b));
             ix.bytes += t->cap_words * 8;
         }
-        HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
+        HIP_CHECK(launch_compare_bitvectors(c.data, ktype(c), c.validity, t->n_rows, cmp, mk, t->ctx->stream));
     }
     HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
     drop_patches(t, col);
@@ -2327,6 +2363,16 @@ int own_column(cubit_table* t, Column& c, uint64_t rows) {
     c.data = b->p;
     c.cap_rows = rows;
     c.owned.push_back(std::move(b));
+    if (type_is_fp(c.type)) {  // the patterns grow beside the keys
+        auto r = std::make_unique<DevBuf>();
+        if (hipMalloc(&r->p, std::max<uint64_t>(rows * esz, 16)) != hipSuccess)
+            return fail(CUBIT_ERR_OOM, "column allocation failed");
+        if (t->n_rows)
+            HIP_CHECK(hipMemcpyAsync(r->p, c.raw, t->n_rows * esz, hipMemcpyDeviceToDevice, t->ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
+        c.raw_buf = std::move(r);
+        c.raw = c.raw_buf->p;
+    }
     return CUBIT_OK;
 }
 
@@ -2371,7 +2417,7 @@ int maintain_exact_keys(cubit_table* t, int col, Index& ix, const std::vector<in
             ++mk.m;
             fresh.emplace_back(missing[k], std::move(b));
         }
-        HIP_CHECK(launch_compare_bitvectors(c.data, c.type, c.validity, t->n_rows, cmp, mk, t->ctx->stream));
+        HIP_CHECK(launch_compare_bitvectors(c.data, ktype(c), c.validity, t->n_rows, cmp, mk, t->ctx->stream));
     }
     HIP_CHECK(hipStreamSynchronize(t->ctx->stream));
     // merge into the sorted key list (keys, bvs and owned stay parallel)
@@ -2469,6 +2515,11 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
         const uint32_t i = at[col];
         const uint64_t esz = type_is32(c.type) ? 4 : 8;
         HIP_CHECK(hipMemcpyAsync(tmp_col.p, data[i], n_new * esz, hipMemcpyHostToDevice, s));
+        if (type_is_fp(c.type)) {  // the patterns appended as given, the slice keyed in place for the rest
+            HIP_CHECK(hipMemcpyAsync(static_cast<char*>(const_cast<void*>(c.raw)) + n_old * esz, tmp_col.p,
+                                     n_new * esz, hipMemcpyDeviceToDevice, s));
+            HIP_CHECK(launch_fp_keys(tmp_col.p, c.type, n_new, tmp_col.p, s));
+        }
         HIP_CHECK(hipMemcpyAsync(static_cast<char*>(const_cast<void*>(c.data)) + n_old * esz, tmp_col.p, n_new * esz,
                                  hipMemcpyDeviceToDevice, s));
         const uint64_t* slice_valid = nullptr;
@@ -2502,11 +2553,11 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
         std::vector<int64_t> added;
         int64_t smin = 0, smax = 0;
         bool sany = false;
-        int rc = value_stats(t, tmp_col.p, c.type, slice_valid, n_new, added, want_distinct, smin, smax, sany);
+        int rc = value_stats(t, tmp_col.p, ktype(c), slice_valid, n_new, added, want_distinct, smin, smax, sany);
         if (rc == CUBIT_ERR_UNSUPPORTED && want_distinct) {  // too wide a span for a presence bitmap
             ixs[0]->exact_all = false;
             want_distinct = false;
-            rc = value_stats(t, tmp_col.p, c.type, slice_valid, n_new, added, false, smin, smax, sany);
+            rc = value_stats(t, tmp_col.p, ktype(c), slice_valid, n_new, added, false, smin, smax, sany);
         }
         if (rc) return rc;
         for (Index* ix : ixs) {
@@ -2530,7 +2581,7 @@ extern "C" int cubit_table_append(cubit_table* t, uint64_t n_new, const int* col
                     mk.out[mk.m] = static_cast<uint64_t*>(tmp_bits.p) + (uint64_t)mk.m * slice_words;
                     ++mk.m;
                 }
-                HIP_CHECK(launch_compare_bitvectors(tmp_col.p, c.type, slice_valid, n_new, cmp, mk, s));
+                HIP_CHECK(launch_compare_bitvectors(tmp_col.p, ktype(c), slice_valid, n_new, cmp, mk, s));
                 for (uint32_t m = 0; m < mk.m; ++m)
                     HIP_CHECK(launch_splice_bits(ix->bvs[k0 + m], mk.out[m], n_old, n_new, s));
             }
@@ -2672,8 +2723,19 @@ extern "C" int cubit_table_merge_updates(cubit_table* t, int col, uint64_t horiz
         mi[x].encoding = ix->encoding == CUBIT_INDEX_RANGE ? 0 : ix->encoding == CUBIT_INDEX_EQUALITY ? 1 : 2;
     }
     // every 64-row word holding merged rows, rewritten by one wave (rows ascend, each once)
-    HIP_CHECK(launch_merge_words(rows_p, vals_p, valid_p, m, t->n_rows, const_cast<void*>(c.data), c.type,
+    // FLOAT / DOUBLE: the merge compares and writes keys (the key column is what the indexes were built
+    // from); the patterns are scattered into the pattern column beside it
+    DevBuf d_keys_of;
+    const int64_t* merge_vals = vals_p;
+    if (type_is_fp(c.type)) {
+        if (hipMalloc(&d_keys_of.p, m * 8) != hipSuccess) return fail(CUBIT_ERR_OOM, "merge key allocation failed");
+        HIP_CHECK(launch_value_keys(vals_p, m, c.type, static_cast<int64_t*>(d_keys_of.p), s));
+        merge_vals = static_cast<const int64_t*>(d_keys_of.p);
+    }
+    HIP_CHECK(launch_merge_words(rows_p, merge_vals, valid_p, m, t->n_rows, const_cast<void*>(c.data), ktype(c),
                                  const_cast<uint64_t*>(c.validity), mi[0], mi[1], s));
+    if (type_is_fp(c.type))
+        HIP_CHECK(launch_scatter_raw(rows_p, vals_p, valid_p, m, c.type, const_cast<void*>(c.raw), s));
     HIP_CHECK(hipStreamSynchronize(s));
     // statistics and exact keys for the merged values (a merged NULL leaves the index bounds:
     // they only have to contain the valid values)
@@ -2764,7 +2826,7 @@ int compute_k0(cubit_table* t, const PendingK0& k) {
                                          cl.validity, k.cmp, k.c, 0, k.bv, t->ctx->stream, cl.bp_simple_width);
         t->last_packed++;
     } else {
-        e = launch_compare_bitvector(cl.data, cl.type, cl.validity, t->n_rows, k.cmp, k.c, k.bv, t->ctx->stream);
+        e = launch_compare_bitvector(cl.data, ktype(cl), cl.validity, t->n_rows, k.cmp, k.c, k.bv, t->ctx->stream);
     }
     if (e != hipSuccess) return fail(CUBIT_ERR_HIP, "compare kernel: %s", hipGetErrorString(e));
     return CUBIT_OK;
@@ -2851,7 +2913,7 @@ struct Planner {
         if ((rc = scratch_bv(t, &bv))) return nullptr;
         const uint64_t* lo_bv = has_lo ? ix.bvs[hi_it - 1 - ix.keys.begin()] : nullptr;
         const uint64_t* hi_bv = has_hi ? ix.bvs[hi_it - ix.keys.begin()] : nullptr;
-        hipError_t e = launch_candidate_check(cl.data, cl.type, cl.validity, lo_bv, hi_bv, t->n_rows, cmp, c, bv,
+        hipError_t e = launch_candidate_check(cl.data, ktype(cl), cl.validity, lo_bv, hi_bv, t->n_rows, cmp, c, bv,
                                               t->ctx->stream);
         if (e != hipSuccess) {
             rc = fail(CUBIT_ERR_HIP, "candidate check kernel: %s", hipGetErrorString(e));
@@ -3229,7 +3291,7 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
     for (const auto& kv : narrow) {
         const PendingK0& k = kv.second;
         const Column& cl = t->cols.at(k.col);
-        HIP_CHECK(launch_masked_compare(cl.data, cl.type, cl.validity, mask, t->n_rows, k.cmp, k.c, k.bv, ctx->stream));
+        HIP_CHECK(launch_masked_compare(cl.data, ktype(cl), cl.validity, mask, t->n_rows, k.cmp, k.c, k.bv, ctx->stream));
         mask = k.bv;
         t->last_narrowed++;
         t->last_narrow_cols.push_back(k.col);
@@ -3441,7 +3503,7 @@ int ensure_zones(cubit_table* t, const std::vector<const uint64_t*>& bvs, const 
     for (size_t i = 0; i < todo_c.size(); ++i) {
         const Column& c = t->cols.at(todo_c[i]);
         uint8_t* p = dev + cbase + i * per_col;
-        HIP_CHECK(launch_column_zone_stats(c.data, c.type, c.validity, t->n_rows, nz, reinterpret_cast<int64_t*>(p),
+        HIP_CHECK(launch_column_zone_stats(c.data, ktype(c), c.validity, t->n_rows, nz, reinterpret_cast<int64_t*>(p),
                                            reinterpret_cast<int64_t*>(p + 8ull * nz), p + 16ull * nz, s));
     }
     std::vector<uint8_t> host(cbase + todo_c.size() * per_col);
@@ -4484,10 +4546,10 @@ int probe_impl(cubit_table* t, int col, const cubit_txn* txn, const int64_t* d_r
     if (int rc = set_device(t->ctx)) return rc;
     const Column& c = it->second;
     if (d_valid)
-        HIP_CHECK(launch_gather_valid(c.data, c.type, c.validity, d_rowids, d_count, max_n, t->row_base, d_out, d_valid,
+        HIP_CHECK(launch_gather_valid(raw_of(c), c.type, c.validity, d_rowids, d_count, max_n, t->row_base, d_out, d_valid,
                                       t->ctx->stream));
     else
-        HIP_CHECK(launch_gather(c.data, c.type, d_rowids, d_count, max_n, t->row_base, d_out, t->ctx->stream));
+        HIP_CHECK(launch_gather(raw_of(c), c.type, d_rowids, d_count, max_n, t->row_base, d_out, t->ctx->stream));
     auto uit = t->upd.find(col);
     if (txn && uit != t->upd.end() && uit->second.any_visible(txn)) {
         const Updates& u = uit->second;
@@ -4532,7 +4594,7 @@ extern "C" int cubit_table_column_data(cubit_table* t, int col, const void** dat
     CUBIT_LOCK(t->ctx);
     auto it = t->cols.find(col);
     if (it == t->cols.end()) return fail(CUBIT_ERR_INVALID, "column %d not registered", col);
-    *data = it->second.data;
+    *data = raw_of(it->second);  // FLOAT / DOUBLE: the patterns (the keys are internal)
     if (type) *type = it->second.type;
     return CUBIT_OK;
 }

@@ -60,6 +60,11 @@ __host__ __device__ __forceinline__ bool type_is32(int type) {
     return type == kTypeInt32 || type == kTypeFloat || type == kTypeVarchar;
 }
 __host__ __device__ __forceinline__ bool type_is_fp(int type) { return type == kTypeFloat || type == kTypeDouble; }
+// the type a table's compare kernels see for a column: FLOAT / DOUBLE columns keep their keys as an
+// INT32 / INT64 column beside the patterns
+__host__ __device__ __forceinline__ int key_type(int type) {
+    return type == kTypeFloat ? kTypeInt32 : type == kTypeDouble ? kTypeInt64 : type;
+}
 // values compared through a key other than themselves (FLOAT, DOUBLE, UBIGINT)
 __host__ __device__ __forceinline__ bool type_is_keyed(int type) { return type_is_fp(type) || type == kTypeUInt64; }
 __host__ __device__ __forceinline__ int32_t fp_key32(uint32_t u) {
@@ -235,6 +240,12 @@ hipError_t launch_narrow_unsigned(const int64_t* in, const uint64_t* d_count, ui
 hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hipStream_t stream);
 hipError_t launch_narrow_i32(const int64_t* in, const uint64_t* d_count, uint64_t max_n, int64_t offset, int32_t* out,
                              hipStream_t stream, uint32_t* overflow = nullptr);
+// FLOAT / DOUBLE columns: keys[i] = the comparison key of pattern raw[i] (the column the compare
+// kernels read); out[i] = value_key(type, v[i]); raw[rows[i]] = v[i] (0 where valids[i] = 0)
+hipError_t launch_fp_keys(const void* raw, int type, uint64_t n, void* keys, hipStream_t stream);
+hipError_t launch_value_keys(const int64_t* v, uint64_t n, int type, int64_t* out, hipStream_t stream);
+hipError_t launch_scatter_raw(const int64_t* rows, const int64_t* v, const uint8_t* valids, uint64_t m, int type,
+                              void* raw, hipStream_t stream);
 hipError_t launch_gather(const void* col, int type, const int64_t* rowids, const uint64_t* d_count, uint64_t max_n,
                          int64_t row_base, int64_t* out, hipStream_t stream);
 // the probe with NULL-ness: values (0 at NULL rows) and out_valid bit i = row rowids[i] valid

@@ -2689,6 +2689,52 @@ __global__ __launch_bounds__(256) void widen_kernel(const S* __restrict__ in, ui
     }
 }
 
+// ------------------------------------------------------------------ FLOAT / DOUBLE keys
+
+// A FLOAT / DOUBLE column is held twice: its bit patterns (probes) and their comparison keys
+// (key_of<FK>), which every compare kernel reads as a plain INT32 / INT64 column — the per-value key
+// in the compare loop made K0 instruction-bound (FLOAT 0.71 ms vs INT32 0.39 ms at 600 M rows).
+// One streaming pass, 16-byte loads and stores.
+template <int FK, typename T>
+__global__ __launch_bounds__(256) void fp_keys_kernel(const T* __restrict__ raw, uint64_t n, T* __restrict__ keys) {
+    constexpr int PER = 16 / sizeof(T);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * PER;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * PER; i < n; i += stride) {
+        if (i + PER <= n && (reinterpret_cast<uintptr_t>(raw + i) % 16) == 0 && (reinterpret_cast<uintptr_t>(keys + i) % 16) == 0) {
+            u64x2 q = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(raw + i));
+            T v[PER];
+            __builtin_memcpy(v, &q, 16);
+#pragma unroll
+            for (int k = 0; k < PER; ++k) v[k] = key_of<FK>(v[k]);
+            __builtin_memcpy(&q, v, 16);
+            *reinterpret_cast<u64x2*>(keys + i) = q;
+        } else {
+            for (uint64_t k = i; k < n && k < i + PER; ++k) keys[k] = key_of<FK>(raw[k]);
+        }
+    }
+}
+
+// out[i] = value_key(type, v[i]): update values (bit patterns) as the keys a merge compares and
+// writes into the key column
+__global__ __launch_bounds__(256) void value_keys_kernel(const int64_t* __restrict__ v, uint64_t n, int type,
+                                                         int64_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = value_key(type, v[i]);
+}
+
+// raw[rows[i]] = the merged record's bit pattern (0 for a NULL record): the pattern column beside the
+// keys a merge rewrote
+__global__ __launch_bounds__(256) void scatter_raw_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ v,
+                                                          const uint8_t* __restrict__ valids, uint64_t m, int is32,
+                                                          void* __restrict__ raw) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const int64_t x = (!valids || valids[i]) ? v[i] : 0;
+        if (is32) static_cast<int32_t*>(raw)[rows[i]] = (int32_t)x;
+        else static_cast<int64_t*>(raw)[rows[i]] = x;
+    }
+}
+
 // ------------------------------------------------------------------ K3: probe
 
 template <typename T>
@@ -3515,6 +3561,33 @@ hipError_t launch_widen(const void* in, int src_type, uint64_t n, void* out, hip
     default:
         return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_fp_keys(const void* raw, int type, uint64_t n, void* keys, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (type == kTypeFloat)
+        hipLaunchKernelGGL((fp_keys_kernel<1, int32_t>), dim3(grid_for((n + 3) / 4)), dim3(256), 0, stream,
+                           static_cast<const int32_t*>(raw), n, static_cast<int32_t*>(keys));
+    else if (type == kTypeDouble)
+        hipLaunchKernelGGL((fp_keys_kernel<2, int64_t>), dim3(grid_for((n + 1) / 2)), dim3(256), 0, stream,
+                           static_cast<const int64_t*>(raw), n, static_cast<int64_t*>(keys));
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_value_keys(const int64_t* v, uint64_t n, int type, int64_t* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(value_keys_kernel, dim3(grid_for(n)), dim3(256), 0, stream, v, n, type, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_raw(const int64_t* rows, const int64_t* v, const uint8_t* valids, uint64_t m, int type,
+                              void* raw, hipStream_t stream) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_raw_kernel, dim3(grid_for(m)), dim3(256), 0, stream, rows, v, valids, m,
+                       type_is32(type) ? 1 : 0, raw);
     return hipGetLastError();
 }
 
