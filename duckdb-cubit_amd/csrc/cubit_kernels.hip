@@ -1991,9 +1991,17 @@ hipError_t launch_compare_m(const void* col, int type, const uint64_t* validity,
     if (type == kTypeDouble)
         return launch_compare_multi_t<int64_t, int64_t, M, 2>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
                                                               stream);
-    if (type == kTypeUInt64)
-        return launch_compare_multi_t<int64_t, int64_t, M, 3>(static_cast<const int64_t*>(col), validity, n_rows, cmp, a,
-                                                              stream);
+    if (type == kTypeUInt64) {
+        // the keys v ^ 2^63 order as the raw values do unsigned: un-key the constants once and
+        // compare the 64 bits unsigned (no per-value XOR in the loop)
+        MultiKeyArgs u = a;
+        for (int k = 0; k < kMultiKeys; ++k) {
+            u.c[k] = (int64_t)((uint64_t)u.c[k] ^ 0x8000000000000000ull);
+            u.c2[k] = (int64_t)((uint64_t)u.c2[k] ^ 0x8000000000000000ull);
+        }
+        return launch_compare_multi_t<uint64_t, uint64_t, M>(static_cast<const uint64_t*>(col), validity, n_rows, cmp, u,
+                                                             stream);
+    }
     if (type_is32(type) && keys_fit32(a, cmp))
         return launch_compare_multi_t<int32_t, int32_t, M>(static_cast<const int32_t*>(col), validity, n_rows, cmp, a,
                                                            stream);
@@ -3410,9 +3418,9 @@ hipError_t launch_candidate_check(const void* col, int type, const uint64_t* val
     if (type == kTypeDouble)
         return launch_candidate_t<int64_t, int64_t, 2>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                        cmp, constant, out_words, stream);
-    if (type == kTypeUInt64)
-        return launch_candidate_t<int64_t, int64_t, 3>(static_cast<const int64_t*>(col), validity, lo_bv, hi_bv, n_rows,
-                                                       cmp, constant, out_words, stream);
+    if (type == kTypeUInt64)  // unsigned compare against the un-keyed constant
+        return launch_candidate_t<uint64_t, uint64_t>(static_cast<const uint64_t*>(col), validity, lo_bv, hi_bv, n_rows,
+                                                      cmp, (uint64_t)constant ^ 0x8000000000000000ull, out_words, stream);
     if (type_is32(type) && constant >= INT32_MIN && constant <= INT32_MAX)
         return launch_candidate_t<int32_t, int32_t>(static_cast<const int32_t*>(col), validity, lo_bv, hi_bv, n_rows,
                                                     cmp, (int32_t)constant, out_words, stream);
@@ -3740,8 +3748,9 @@ hipError_t launch_masked_compare(const void* col, int type, const uint64_t* vali
         hipLaunchKernelGGL((masked_compare_kernel<int64_t, 2>), grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, mask, nw, r.lo, r.hi, r.neg, out);
     } else if (type == kTypeUInt64) {
-        hipLaunchKernelGGL((masked_compare_kernel<int64_t, 3>), grid, block, 0, stream, static_cast<const int64_t*>(col),
-                           validity, mask, nw, r.lo, r.hi, r.neg, out);
+        hipLaunchKernelGGL(masked_compare_kernel<uint64_t>, grid, block, 0, stream, static_cast<const uint64_t*>(col),
+                           validity, mask, nw, (uint64_t)r.lo ^ 0x8000000000000000ull,
+                           (uint64_t)r.hi ^ 0x8000000000000000ull, r.neg, out);
     } else {
         hipLaunchKernelGGL(masked_compare_kernel<int64_t>, grid, block, 0, stream, static_cast<const int64_t*>(col),
                            validity, mask, nw, r.lo, r.hi, r.neg, out);
