@@ -31,6 +31,9 @@ TYPE_FLOAT, TYPE_DOUBLE = 8, 9
 # VARCHAR columns hold int32 codes of an order-preserving dictionary (cubit_dict); their filter
 # constants and index keys are addresses of cubit_string structs (filters.string_ref)
 TYPE_VARCHAR = 10
+# HUGEINT / UHUGEINT columns are dictionary columns over the values' 16-byte order keys
+# (cubit_key128 / filters.key128): the type codes name the key encoding
+TYPE_INT128, TYPE_UINT128 = 11, 12
 COLUMN_TYPES = dict(SEGMENT_TYPES, float32=TYPE_FLOAT, float64=TYPE_DOUBLE)
 
 

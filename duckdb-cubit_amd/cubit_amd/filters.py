@@ -62,6 +62,25 @@ def string_at(addr: int) -> bytes:
     return _STRING_AT[int(addr)]
 
 
+def key128(v: int, signed: bool = True) -> bytes:
+    """A HUGEINT (signed) / UHUGEINT value's 16-byte order key, as cubit_key128 writes it: the
+    128 bits big-endian, HUGEINT's sign bit flipped — unsigned byte order = the values' order. A
+    HUGEINT / UHUGEINT column's constants and index keys are these keys (as str / bytes constants)."""
+    v = int(v)
+    if signed:
+        assert -(1 << 127) <= v < (1 << 127), v
+        v += 1 << 127
+    else:
+        assert 0 <= v < (1 << 128), v
+    return v.to_bytes(16, "big")
+
+
+def value128(key: bytes, signed: bool = True) -> int:
+    """cubit_value128: the value of a 16-byte order key."""
+    v = int.from_bytes(bytes(key), "big")
+    return v - (1 << 127) if signed else v
+
+
 def constant_bits(c) -> int:
     """A filter constant as the int64 a cubit_filter_node carries: integers as they are; a
     np.float32 as its 32-bit IEEE pattern (a FLOAT column's constant), any other float as its

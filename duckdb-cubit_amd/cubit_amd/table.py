@@ -238,6 +238,7 @@ class CubitTable:
         self.handle = h
         ctx._tables.add(self)
         self.types: Dict[int, int] = {}
+        self.huge: Dict[int, bool] = {}  # HUGEINT (True) / UHUGEINT (False) dictionary columns
         self._keep = []
 
     def add_column(self, col: int, data: np.ndarray, validity: Optional[np.ndarray] = None) -> None:
@@ -287,6 +288,19 @@ class CubitTable:
         self._keep.append(d)
         return d
 
+    def add_huge_column(self, col: int, values, signed: bool = True,
+                        dictionary: Optional[Dictionary] = None) -> Dictionary:
+        """Register a HUGEINT (signed) / UHUGEINT column from a list of Python ints / None (NULL):
+        a dictionary column over the values' 16-byte order keys (filters.key128), its codes the
+        values' ranks. Constants and index keys on it are key128(...) bytes; probed codes map back
+        through dictionary.entry + filters.value128."""
+        from cubit_amd.filters import key128
+
+        keys = [None if v is None else key128(v, signed) for v in values]
+        d = self.add_string_column(col, keys, dictionary)
+        self.huge[col] = signed  # a dictionary column (types: VARCHAR) whose keys are 128-bit values
+        return d
+
     def column_data(self, col: int):
         """(device pointer, CUBIT type) of a registered column's values."""
         ptr, typ = C.c_void_p(), C.c_int()
@@ -312,8 +326,10 @@ class CubitTable:
             # FLOAT / DOUBLE columns: keys given as floats cross as their bit patterns
             typ = self.types.get(col)
             if typ == L.TYPE_VARCHAR:  # string keys cross as addresses of cubit_strings
-                from cubit_amd.filters import string_ref
+                from cubit_amd.filters import key128, string_ref
 
+                if col in self.huge:  # HUGEINT / UHUGEINT keys given as ints: their order keys
+                    keys = [key128(x, self.huge[col]) for x in keys]
                 k = np.array([string_ref(x) for x in keys], dtype=np.int64)
             elif typ == L.TYPE_UINT64:  # UBIGINT keys as their bits
                 k = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64)).view(np.int64)

@@ -127,8 +127,9 @@ struct CubitPartitionSet {
     std::shared_ptr<CubitContexts> contexts;
     vector<cubit_table *> parts;
     vector<uint64_t> part_base;  // first row id of each partition
-    // per VARCHAR column: the order-preserving dictionary every partition's codes index (one per
-    // table, so codes are global); the chunks decode codes with it
+    // per dictionary column (VARCHAR; HUGEINT / UHUGEINT over their order keys): the
+    // order-preserving dictionary every partition's codes index (one per table, so codes are
+    // global); the chunks decode codes with it
     unordered_map<column_t, cubit_dict *> dicts;
     // a scan's init_global — the only part of a scan that reads the tables; its chunks come from
     // its own buffers — holds it shared; a sync's in-place appends and deletes hold it exclusive
@@ -243,7 +244,8 @@ static void Check(int rc) {
 // 32 bits, and FLOAT / DOUBLE as their bit patterns (the library compares them with DuckDB's
 // floating-point operators, include/cubit_gpu.h), UBIGINT as its bits (compared unsigned), and
 // VARCHAR as int32 codes of the table's order-preserving dictionary (constants cross as
-// cubit_strings). HUGEINT and UHUGEINT stay on seq_scan.
+// cubit_strings), and HUGEINT / UHUGEINT as codes of a dictionary over their 16-byte order keys
+// (cubit_key128: the codes are the values' ranks; constants cross as cubit_strings over keys).
 static bool GpuPhysical(PhysicalType t) {
     switch (t) {
     case PhysicalType::BOOL:
@@ -258,10 +260,33 @@ static bool GpuPhysical(PhysicalType t) {
     case PhysicalType::FLOAT:
     case PhysicalType::DOUBLE:
     case PhysicalType::VARCHAR:  // as codes of an order-preserving dictionary (cubit_dict)
+    case PhysicalType::INT128:   // as codes of a dictionary over the values' order keys
+    case PhysicalType::UINT128:
         return true;
     default:
         return false;
     }
+}
+
+// a column held as dictionary codes: VARCHAR (the strings), HUGEINT / UHUGEINT (their order keys)
+static bool DictPhysical(PhysicalType t) {
+    return t == PhysicalType::VARCHAR || t == PhysicalType::INT128 || t == PhysicalType::UINT128;
+}
+
+// a HUGEINT / UHUGEINT value as its 16-byte order key (cubit_key128), in a string for the
+// dictionary's bytes + offsets layout
+static string Key128(PhysicalType t, uint64_t lower, uint64_t upper) {
+    unsigned char k[16];
+    cubit_key128(t == PhysicalType::INT128 ? CUBIT_TYPE_INT128 : CUBIT_TYPE_UINT128, lower, upper, k);
+    return string((const char *)k, 16);
+}
+static string Key128(const Value &v) {
+    if (v.type().InternalType() == PhysicalType::INT128) {
+        const auto h = v.GetValueUnsafe<hugeint_t>();
+        return Key128(PhysicalType::INT128, h.lower, (uint64_t)h.upper);
+    }
+    const auto u = v.GetValueUnsafe<uhugeint_t>();
+    return Key128(PhysicalType::UINT128, u.lower, u.upper);
 }
 
 // uploaded from 8-byte values (INT64, UINT32 widened, DOUBLE patterns; else from 4-byte ones)
@@ -392,9 +417,13 @@ static int64_t ConstantAsInt64(const Value &v) {
 // prefix-order cubit_filter_node tree of one column's TableFilter (kinds are numbered like
 // TableFilterType, comparisons like the CUBIT_CMP_* of ExpressionType::COMPARE_*)
 // A VARCHAR constant crosses as the address of a cubit_string over the Value's own bytes (the
-// TableFilterSet outlives the scan's init_global, which plans it); `strings` holds the structs.
-static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node> &out,
-                 std::deque<cubit_string> &strings) {
+// TableFilterSet outlives the scan's init_global, which plans it), a HUGEINT / UHUGEINT constant
+// as one over its order key; the arena holds the structs and keys.
+struct ConstantArena {
+    std::deque<cubit_string> strings;
+    std::deque<string> keys;
+};
+static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node> &out, ConstantArena &arena) {
     cubit_filter_node n {};
     n.column = column;
     switch (f.filter_type) {
@@ -421,10 +450,15 @@ static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node>
             n.cmp = CUBIT_CMP_GE;
             break;
         }
-        if (c.constant.type().InternalType() == PhysicalType::VARCHAR) {
+        const auto phys = c.constant.type().InternalType();
+        if (phys == PhysicalType::VARCHAR) {
             const string &str = StringValue::Get(c.constant);
-            strings.push_back(cubit_string {str.data(), str.size()});
-            n.constant = (int64_t)(intptr_t)&strings.back();
+            arena.strings.push_back(cubit_string {str.data(), str.size()});
+            n.constant = (int64_t)(intptr_t)&arena.strings.back();
+        } else if (phys == PhysicalType::INT128 || phys == PhysicalType::UINT128) {
+            arena.keys.push_back(Key128(c.constant));
+            arena.strings.push_back(cubit_string {arena.keys.back().data(), 16});
+            n.constant = (int64_t)(intptr_t)&arena.strings.back();
         } else {
             n.constant = ConstantAsInt64(c.constant);
         }
@@ -448,7 +482,7 @@ static void Emit(const TableFilter &f, int32_t column, vector<cubit_filter_node>
         n.n_children = (int32_t)children.size();
         out.push_back(n);
         for (auto &ch : children) {
-            Emit(*ch, column, out, strings);
+            Emit(*ch, column, out, arena);
         }
         return;
     }
@@ -486,8 +520,8 @@ struct CubitGlobalState : public GlobalTableFunctionState {
     std::shared_ptr<CubitPartitionSet> set;  // released after the scan (member order)
     idx_t max_threads = 1;
     vector<LogicalType> out_types;  // output chunk column types, in output order
-    vector<cubit_dict *> out_dicts;  // a VARCHAR output column's dictionary (held by `set`), else null
-    std::deque<cubit_string> strings;  // the VARCHAR constants of the pushed filters
+    vector<cubit_dict *> out_dicts;  // a dictionary output column's dictionary (held by `set`), else null
+    ConstantArena constants;  // the VARCHAR / HUGEINT / UHUGEINT constants of the pushed filters
     // set when the scan runs as seq_scan (the partition was not current at init_global)
     unique_ptr<GlobalTableFunctionState> seq_global;
 };
@@ -547,7 +581,7 @@ static unique_ptr<GlobalTableFunctionState> CubitInitGlobal(ClientContext &conte
         // the TableFilterSet is an AND over columns; its keys index column_ids
         nodes.push_back(cubit_filter_node {CUBIT_FILTER_AND, 0, 0, (int32_t)input.filters->filters.size(), 0});
         for (auto &kv : input.filters->filters) {
-            Emit(*kv.second, (int32_t)input.column_ids[kv.first], nodes, g->strings);
+            Emit(*kv.second, (int32_t)input.column_ids[kv.first], nodes, g->constants);
         }
     }
     auto &tx = DuckTransaction::Get(context, bind.table.catalog);
@@ -628,6 +662,25 @@ static void CopyOut(const int64_t *src, Vector &dst, idx_t n, const uint64_t *va
                 continue;
             }
             d[i] = StringVector::AddString(dst, p, len);
+        }
+        break;
+    }
+    case PhysicalType::INT128:
+    case PhysicalType::UINT128: {  // codes → order keys → the 128-bit values
+        const bool is_signed = dst.GetType().InternalType() == PhysicalType::INT128;
+        for (idx_t i = 0; i < n; i++) {
+            const char *p = nullptr;
+            uint64_t len = 0, lower = 0, upper = 0;
+            if (((valid[i >> 6] >> (i & 63)) & 1) && dict && cubit_dict_entry(dict, (uint64_t)src[i], &p, &len) == CUBIT_OK &&
+                len == 16) {
+                cubit_value128(is_signed ? CUBIT_TYPE_INT128 : CUBIT_TYPE_UINT128, (const unsigned char *)p, &lower,
+                               &upper);
+            }
+            if (is_signed) {
+                FlatVector::GetData<hugeint_t>(dst)[i] = hugeint_t((int64_t)upper, lower);
+            } else {
+                FlatVector::GetData<uhugeint_t>(dst)[i] = uhugeint_t(upper, lower);
+            }
         }
         break;
     }
@@ -785,7 +838,27 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
     auto stats = BaseStatistics::CreateEmpty(type);
     if (has_no_null) {
         const auto phys = type.InternalType();
-        if (phys == PhysicalType::FLOAT || phys == PhysicalType::DOUBLE) {  // bit patterns
+        if (phys == PhysicalType::INT128 || phys == PhysicalType::UINT128) {
+            // the codes' min / max are the values' (codes are ranks): their entries, decoded
+            auto d = set->dicts.find(column_id);
+            const char *p[2] = {nullptr, nullptr};
+            uint64_t len[2] = {0, 0}, lower[2], upper[2];
+            if (d == set->dicts.end() || cubit_dict_entry(d->second, (uint64_t)lo, &p[0], &len[0]) != CUBIT_OK ||
+                cubit_dict_entry(d->second, (uint64_t)hi, &p[1], &len[1]) != CUBIT_OK || len[0] != 16 || len[1] != 16) {
+                return nullptr;
+            }
+            const int kt = phys == PhysicalType::INT128 ? CUBIT_TYPE_INT128 : CUBIT_TYPE_UINT128;
+            for (int k = 0; k < 2; k++) {
+                cubit_value128(kt, (const unsigned char *)p[k], &lower[k], &upper[k]);
+            }
+            if (phys == PhysicalType::INT128) {
+                NumericStats::SetMin(stats, Value::HUGEINT(hugeint_t((int64_t)upper[0], lower[0])));
+                NumericStats::SetMax(stats, Value::HUGEINT(hugeint_t((int64_t)upper[1], lower[1])));
+            } else {
+                NumericStats::SetMin(stats, Value::UHUGEINT(uhugeint_t(upper[0], lower[0])));
+                NumericStats::SetMax(stats, Value::UHUGEINT(uhugeint_t(upper[1], lower[1])));
+            }
+        } else if (phys == PhysicalType::FLOAT || phys == PhysicalType::DOUBLE) {  // bit patterns
             float f[2];
             double d[2];
             const uint32_t u[2] = {(uint32_t)lo, (uint32_t)hi};
@@ -1028,7 +1101,7 @@ struct CubitSnapshot {
     uint64_t rows = 0;   // first … first+rows-1
     vector<vector<int64_t>> values;
     vector<vector<uint64_t>> validity;
-    vector<vector<string>> strings;  // a VARCHAR column's values (its `values` stay 0)
+    vector<vector<string>> strings;  // a dictionary column's values: strings, 128-bit order keys (`values` stay 0)
     vector<bool> present;
 };
 
@@ -1061,7 +1134,7 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
     snap.present.clear();
     vector<bool> is_str(cols.size());
     for (idx_t c = 0; c < cols.size(); c++) {
-        is_str[c] = entry.GetColumn(LogicalIndex(cols[c])).GetType().InternalType() == PhysicalType::VARCHAR;
+        is_str[c] = DictPhysical(entry.GetColumn(LogicalIndex(cols[c])).GetType().InternalType());
     }
     while (auto chunk = res->Fetch()) {
         chunk->Flatten();
@@ -1086,7 +1159,14 @@ static void ReadRows(Connection &con, const string &table_name, DuckTableEntry &
                     continue;
                 }
                 snap.validity[c][r >> 6] |= 1ull << (r & 63);
-                if (is_str[c]) {
+                const auto phys = vec.GetType().InternalType();
+                if (phys == PhysicalType::INT128) {
+                    const auto h = FlatVector::GetData<hugeint_t>(vec)[i];
+                    snap.strings[c][r] = Key128(phys, h.lower, (uint64_t)h.upper);
+                } else if (phys == PhysicalType::UINT128) {
+                    const auto u = FlatVector::GetData<uhugeint_t>(vec)[i];
+                    snap.strings[c][r] = Key128(phys, u.lower, u.upper);
+                } else if (is_str[c]) {
                     snap.strings[c][r] = FlatVector::GetData<string_t>(vec)[i].GetString();
                 } else {
                     snap.values[c][r] = PhysicalAsInt64(vec, i);
@@ -1323,10 +1403,10 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
     const uint64_t rg = 122880, units = (snap.rows + rg - 1) / rg;
     const uint64_t n_parts = std::max<uint64_t>(1, std::min<uint64_t>(ctxs.size(), units));
     vector<bool> few(attached.column_order.size());
-    vector<vector<int32_t>> codes(attached.column_order.size());  // VARCHAR columns: every row's code
+    vector<vector<int32_t>> codes(attached.column_order.size());  // dictionary columns: every row's code
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
         const column_t col = attached.column_order[c];
-        if (attached.columns[col] == PhysicalType::VARCHAR) {
+        if (DictPhysical(attached.columns[col])) {
             cubit_dict *d = EncodeStrings(snap.strings[c], snap.validity[c], codes[c]);
             set->dicts[col] = d;  // the set owns it from here (its destructor frees it)
             uint64_t size = 0;
@@ -1346,14 +1426,14 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
         for (idx_t c = 0; c < attached.column_order.size(); c++) {
             const column_t col = attached.column_order[c];
             const uint64_t *valid = snap.validity[c].data() + b / 64;
-            if (attached.columns[col] == PhysicalType::VARCHAR) {
+            if (DictPhysical(attached.columns[col])) {
                 Check(cubit_table_add_dict_column(t, (int)col, set->dicts[col], codes[c].data() + b, valid, 0));
             }
             const bool from_segments =
-                attached.columns[col] != PhysicalType::VARCHAR && entry && n_parts == 1 &&
+                !DictPhysical(attached.columns[col]) && entry && n_parts == 1 &&
                 AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
                 SampleMatches(ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
-            if (!from_segments && attached.columns[col] != PhysicalType::VARCHAR) {
+            if (!from_segments && !DictPhysical(attached.columns[col])) {
                 // (re-)registering replaces a column taken from segments
                 const bool wide = WidePhysical(attached.columns[col]);
                 vector<int32_t> narrow;
@@ -1367,7 +1447,7 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
             bool named = false;
             for (auto &ix : attached.indexes) {
                 if (ix.column == col) {
-                    vector<cubit_string> strs;  // a VARCHAR column's keys as cubit_strings
+                    vector<cubit_string> strs;  // a dictionary column's keys as cubit_strings
                     vector<int64_t> addrs;
                     strs.reserve(ix.str_keys.size());
                     for (auto &k : ix.str_keys) {
@@ -1519,7 +1599,7 @@ static void SyncPartition(ClientContext &context, DuckTableEntry &entry, CubitAt
         for (idx_t c = 0; c < attached.column_order.size(); c++) {
             const column_t col = attached.column_order[c];
             cols.push_back((int)col);
-            if (attached.columns[col] == PhysicalType::VARCHAR) {  // codes in the kept dictionary
+            if (DictPhysical(attached.columns[col])) {  // codes in the kept dictionary
                 vector<char> bytes;
                 vector<uint64_t> offsets;
                 PackStrings(snap.strings[c], bytes, offsets);
@@ -1593,10 +1673,14 @@ static vector<CubitIndexSpec> ParseIndexSpec(DuckTableEntry &entry, const string
         } else {
             throw InvalidInputException("cubit_attach: unknown index encoding '%s'", enc);
         }
-        if (colon != string::npos && def.GetType().InternalType() == PhysicalType::VARCHAR) {
+        const auto phys = def.GetType().InternalType();
+        if (colon != string::npos && DictPhysical(phys)) {
             for (auto lit : StringUtil::Split(rest.substr(colon + 1), ',')) {
                 StringUtil::Trim(lit);
-                ix.str_keys.push_back(lit);  // byte order = DuckDB's string order (string_type.hpp:176-206)
+                // byte order = DuckDB's string order (string_type.hpp:176-206); HUGEINT / UHUGEINT
+                // literals as their order keys (byte order = the values' order)
+                ix.str_keys.push_back(phys == PhysicalType::VARCHAR ? lit
+                                                                    : Key128(Value(lit).DefaultCastAs(def.GetType())));
             }
             std::sort(ix.str_keys.begin(), ix.str_keys.end());
             ix.str_keys.erase(std::unique(ix.str_keys.begin(), ix.str_keys.end()), ix.str_keys.end());

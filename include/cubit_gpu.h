@@ -73,6 +73,33 @@ extern "C" {
  * index keys (cubit_table_build_index `values`) likewise. Update values, appended values, probed
  * values and statistics are codes. */
 #define CUBIT_TYPE_VARCHAR 10
+/* HUGEINT / UHUGEINT (PhysicalType::INT128 / UINT128: hugeint_t / uhugeint_t, {lower, upper}) have
+ * no column storage of their own: such a column is a dictionary column (cubit_table_add_dict_column)
+ * over its values' 16-byte ORDER KEYS (cubit_key128: the 128 bits big-endian, HUGEINT's sign bit
+ * flipped), whose unsigned byte order — the dictionary's order — is the values' order (hugeint_t's
+ * and uhugeint_t's comparison operators). Its codes are the values' ranks, so every index, zonemap
+ * and kernel works on them as on a VARCHAR column's; filter constants and index keys cross as
+ * cubit_strings over their keys, probed codes map back through cubit_dict_entry + cubit_value128.
+ * The type codes name the key encoding only (a column of more than 2^31 - 1 distinct values does
+ * not fit the INT32 codes and stays on the caller's CPU path). */
+#define CUBIT_TYPE_INT128 11
+#define CUBIT_TYPE_UINT128 12
+static inline void cubit_key128(int type, uint64_t lower, uint64_t upper, unsigned char key[16]) {
+    if (type == CUBIT_TYPE_INT128) upper ^= 0x8000000000000000ull; /* signed order as unsigned bytes */
+    for (int i = 0; i < 8; i++) {
+        key[i] = (unsigned char)(upper >> (56 - 8 * i));
+        key[8 + i] = (unsigned char)(lower >> (56 - 8 * i));
+    }
+}
+static inline void cubit_value128(int type, const unsigned char key[16], uint64_t *lower, uint64_t *upper) {
+    uint64_t hi = 0, lo = 0;
+    for (int i = 0; i < 8; i++) {
+        hi = (hi << 8) | key[i];
+        lo = (lo << 8) | key[8 + i];
+    }
+    *lower = lo;
+    *upper = type == CUBIT_TYPE_INT128 ? hi ^ 0x8000000000000000ull : hi;
+}
 
 /* The comparison key of a FLOAT / DOUBLE bit pattern or UINT64 value (any other type: the value
  * itself): UINT64 → v ^ 2^63; FLOAT / DOUBLE: every

@@ -122,9 +122,38 @@ static inline int cmp_str(int cmp, int64_t v, int64_t c) {
     }
 }
 
-/* a comparison of values of column type `type` (FP: bit patterns; VARCHAR: ostring addresses) */
+/* hugeint_t / uhugeint_t comparisons (hugeint.cpp / uhugeint.cpp operators: upper, then lower
+ * unsigned) as the compiler's 128-bit integers */
+static inline int cmp_huge(int type, int cmp, int64_t v, int64_t c) {
+    const ohuge *a = (const ohuge *)(intptr_t)v, *b = (const ohuge *)(intptr_t)c;
+    int o;
+    if (type == OTYPE_INT128) {
+        const __int128 x = (__int128)(((unsigned __int128)a->upper << 64) | a->lower);
+        const __int128 y = (__int128)(((unsigned __int128)b->upper << 64) | b->lower);
+        o = x < y ? -1 : x > y;
+    } else {
+        const unsigned __int128 x = ((unsigned __int128)a->upper << 64) | a->lower;
+        const unsigned __int128 y = ((unsigned __int128)b->upper << 64) | b->lower;
+        o = x < y ? -1 : x > y;
+    }
+    switch (cmp) {
+    case OCMP_EQ: return o == 0;
+    case OCMP_NE: return o != 0;
+    case OCMP_LT: return o < 0;
+    case OCMP_LE: return o <= 0;
+    case OCMP_GT: return o > 0;
+    default: return o >= 0;
+    }
+}
+static inline int is_addr_type(int type) {
+    return type == OTYPE_VARCHAR || type == OTYPE_INT128 || type == OTYPE_UINT128;
+}
+
+/* a comparison of values of column type `type` (FP: bit patterns; VARCHAR / INT128 / UINT128:
+ * ostring / ohuge addresses) */
 static inline int cmp_typed(int type, int cmp, int64_t v, int64_t c) {
     if (type == OTYPE_VARCHAR) return cmp_str(cmp, v, c);
+    if (type == OTYPE_INT128 || type == OTYPE_UINT128) return cmp_huge(type, cmp, v, c);
     if (type == OTYPE_UINT64) {
         const uint64_t a = (uint64_t)v, b = (uint64_t)c;
         switch (cmp) {
@@ -145,6 +174,8 @@ static inline int64_t col_value(const ocol *c, uint64_t r) {
     switch (c->type) {
     case OTYPE_INT32: return (int64_t)((const int32_t *)c->data)[r];
     case OTYPE_VARCHAR: return (int64_t)(intptr_t)((const ostring *)c->data + r);
+    case OTYPE_INT128:
+    case OTYPE_UINT128: return (int64_t)(intptr_t)((const ohuge *)c->data + r);
     case OTYPE_FLOAT: {
         uint32_t u;
         memcpy(&u, (const float *)c->data + r, 4);
@@ -196,7 +227,9 @@ static void load_vector(const ocol *c, uint64_t first_row, uint64_t count, const
         out->data = c->type == OTYPE_INT32 || c->type == OTYPE_FLOAT
                         ? (const void *)((const int32_t *)c->data + first_row)
                         : c->type == OTYPE_VARCHAR ? (const void *)((const ostring *)c->data + first_row)
-                                                   : (const void *)((const int64_t *)c->data + first_row);
+                        : c->type == OTYPE_INT128 || c->type == OTYPE_UINT128
+                            ? (const void *)((const ohuge *)c->data + first_row)
+                            : (const void *)((const int64_t *)c->data + first_row);
         return;
     }
     for (uint64_t i = 0; i < count; i++) out->vals[i] = col_value(c, first_row + i);
@@ -227,6 +260,8 @@ static inline int64_t vec_value(const vecbuf *v, uint32_t idx) {
     case OTYPE_INT32: return (int64_t)((const int32_t *)v->data)[idx];
     case OTYPE_FLOAT: return (int64_t)((const uint32_t *)v->data)[idx];
     case OTYPE_VARCHAR: return (int64_t)(intptr_t)((const ostring *)v->data + idx);
+    case OTYPE_INT128:
+    case OTYPE_UINT128: return (int64_t)(intptr_t)((const ohuge *)v->data + idx);
     default: return ((const int64_t *)v->data)[idx];
     }
 }
@@ -269,11 +304,11 @@ static inline int vec_valid(const vecbuf *v, uint32_t idx) { return v->valid ? v
 
 static uint64_t templated_filter_selection(const vecbuf *v, int cmp, int64_t c, uint32_t *sel, uint64_t approved) {
     uint64_t rc = 0;
-    if (v->type == OTYPE_VARCHAR) {
-        /* FilterSelectionSwitch<string_t> (column_segment.cpp:278-349) */
+    if (is_addr_type(v->type)) {
+        /* FilterSelectionSwitch<string_t / hugeint_t / uhugeint_t> (column_segment.cpp:278-349) */
         for (uint64_t a = 0; a < approved; a++) {
             uint32_t idx = sel[a];
-            int pass = vec_valid(v, idx) && cmp_str(cmp, vec_value(v, idx), c);
+            int pass = vec_valid(v, idx) && cmp_typed(v->type, cmp, vec_value(v, idx), c);
             sel[rc] = idx;
             rc += (uint64_t)pass;
         }

@@ -14,11 +14,19 @@ extern "C" {
 /* VARCHAR: `data` is an array of ostring; constants, update values and fetched values carry the
  * address of an ostring (string_t comparisons: unsigned bytes, then length — string_type.hpp:143-206) */
 /* UINT64 (UBIGINT): the values' bits in `data`, constants and values as those bits, compared unsigned */
-enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3, OTYPE_VARCHAR = 4, OTYPE_UINT64 = 5 };
+/* INT128 / UINT128 (HUGEINT / UHUGEINT): `data` is an array of ohuge (hugeint_t / uhugeint_t:
+ * lower, upper — hugeint.hpp, uhugeint.hpp); constants, update values and fetched values carry the
+ * address of an ohuge; compared as 128-bit integers, signed / unsigned */
+enum { OTYPE_INT32 = 0, OTYPE_INT64 = 1, OTYPE_FLOAT = 2, OTYPE_DOUBLE = 3, OTYPE_VARCHAR = 4, OTYPE_UINT64 = 5,
+       OTYPE_INT128 = 6, OTYPE_UINT128 = 7 };
 typedef struct {
     const char *data;
     uint64_t size;
 } ostring;
+typedef struct {
+    uint64_t lower;
+    uint64_t upper; /* int64_t for HUGEINT */
+} ohuge;
 /* ExpressionType comparisons used by ConstantFilter (table_filter.hpp / constant_filter.cpp) */
 enum { OCMP_EQ = 0, OCMP_NE = 1, OCMP_LT = 2, OCMP_LE = 3, OCMP_GT = 4, OCMP_GE = 5 };
 /* TableFilterType (src/include/duckdb/planner/table_filter.hpp:20-27) */

@@ -19,6 +19,7 @@ LIB = HERE / "lib" / "libcubit_oracle.so"
 
 OMAX_COLS = 16
 OTYPE_INT32, OTYPE_INT64, OTYPE_FLOAT, OTYPE_DOUBLE, OTYPE_VARCHAR, OTYPE_UINT64 = 0, 1, 2, 3, 4, 5
+OTYPE_INT128, OTYPE_UINT128 = 6, 7
 OB_AND, OB_OR, OB_ANDNOT, OB_NOT = -1, -2, -3, -4
 
 
@@ -191,6 +192,82 @@ class StringColumn(Column):
                 out.append(self.values[(a - base) // size])
             else:
                 out.append(string_at(a))
+        return out
+
+
+class OHuge(C.Structure):
+    """hugeint_t / uhugeint_t: {lower, upper} (hugeint.hpp)."""
+
+    _fields_ = [("lower", C.c_uint64), ("upper", C.c_uint64)]
+
+
+_HUGES = {}  # int -> OHuge, kept for the life of the process
+_HUGE_AT = {}  # address -> int
+
+
+def huge_ref(v: int) -> int:
+    """The address of a persistent ohuge holding the 128-bit integer v (negative: two's
+    complement): how a HUGEINT / UHUGEINT constant or update value reaches the oracle."""
+    v = int(v)
+    if v not in _HUGES:
+        u = v & ((1 << 128) - 1)
+        h = OHuge(u & (2 ** 64 - 1), u >> 64)
+        _HUGES[v] = h
+        _HUGE_AT[C.addressof(h)] = v
+    return C.addressof(_HUGES[v])
+
+
+class HugeColumn(Column):
+    """A HUGEINT (signed=True) / UHUGEINT column as the oracle sees it: an ohuge per row from
+    Python ints, NULL rows from None; update values are ints (or None) carried as ohuge
+    addresses; fetch hands back addresses — decode() turns them into ints."""
+
+    def __init__(self, values, signed=True, updates=None):
+        from cubit_amd.datagen import validity_from_mask
+
+        self.signed = signed
+        self.values = [None if v is None else int(v) for v in values]
+        lo, hi = (-(1 << 127), (1 << 127) - 1) if signed else (0, (1 << 128) - 1)
+        assert all(v is None or lo <= v <= hi for v in self.values)
+        n = len(self.values)
+        self.arr = (OHuge * max(n, 1))()
+        for i, v in enumerate(self.values):
+            u = (v or 0) & ((1 << 128) - 1)
+            self.arr[i] = OHuge(u & (2 ** 64 - 1), u >> 64)
+        valid = np.array([v is not None for v in self.values], dtype=bool)
+        self.validity = None if valid.all() else validity_from_mask(valid)
+        self.data = np.zeros(0, dtype=np.int8)  # unused (the ohuges are in self.arr)
+        self.upd = None
+        self.upd_valid = None
+        if updates is not None:
+            r, v, ver = updates[:3]
+            vals = np.array([0 if x is None else huge_ref(x) for x in v], dtype=np.int64)
+            self.upd = (np.ascontiguousarray(r, dtype=np.int64), vals, np.ascontiguousarray(ver, dtype=np.uint64))
+            ok = updates[3] if len(updates) > 3 and updates[3] is not None else np.array([x is not None for x in v])
+            self.upd_valid = np.ascontiguousarray(ok, dtype=np.uint8)
+
+    def ocol(self) -> OCol:
+        c = OCol()
+        c.type = OTYPE_INT128 if self.signed else OTYPE_UINT128
+        c.data = C.addressof(self.arr)
+        c.validity = self.validity.ctypes.data if self.validity is not None else None
+        if self.upd is not None:
+            c.n_updates = len(self.upd[0])
+            c.upd_rows, c.upd_values, c.upd_version = (a.ctypes.data for a in self.upd)
+            c.upd_valid = self.upd_valid.ctypes.data
+        return c
+
+    def decode(self, addrs, valid=None):
+        """Fetched values (ohuge addresses) → ints (None where not valid)."""
+        base, size = C.addressof(self.arr), C.sizeof(OHuge)
+        out = []
+        for i, a in enumerate(np.asarray(addrs, dtype=np.int64).tolist()):
+            if valid is not None and not valid[i]:
+                out.append(None)
+            elif base <= a < base + size * len(self.values):
+                out.append(self.values[(a - base) // size])
+            else:
+                out.append(_HUGE_AT[a])
         return out
 
 
