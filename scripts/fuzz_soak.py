@@ -5,7 +5,8 @@ TableFilterSets and residual AND/OR trees over range / equality / edge-keyed ran
 unindexed columns with NULLs, deletes visible to a snapshot and, in every other round,
 updates from a writer; each scan under a random decode kernel (AUTO, pair-claimed, run-claimed,
 look-back); every third table holds the typed columns instead (DOUBLE / FLOAT with NaN and ±0,
-VARCHAR dictionary codes, full-range UBIGINT: tests/test_gpu_typed_fuzz.py). Every result is
+VARCHAR dictionary codes, full-range UBIGINT, HUGEINT over 16-byte order keys:
+tests/test_gpu_typed_fuzz.py). Every result is
 compared with the oracle; every third filter also runs through the
 table function (random projection with the row id, 1-4 pipeline tasks, staged or per-window
 copies): row ids, values and NULL-ness against the oracle's scan and fetch. Prints one summary
@@ -164,7 +165,7 @@ def main():
     rounds = checks = 0
     seed = seed0
     while time.perf_counter() < t_end:
-        if rounds % 3 == 2:  # FLOAT / DOUBLE / VARCHAR / UBIGINT columns (tests/test_gpu_typed_fuzz.py)
+        if rounds % 3 == 2:  # FLOAT / DOUBLE / VARCHAR / UBIGINT / HUGEINT columns (tests/test_gpu_typed_fuzz.py)
             checks += typed_round(ctx, seed, n, with_updates=bool(rounds % 2), n_cases=30)
         else:
             checks += round_(ctx, seed, n, with_updates=bool(rounds % 2))

@@ -1,12 +1,15 @@
 """Random filters over the typed columns (round 6) vs the oracle: a DOUBLE and a FLOAT column
 holding NaN / ±0 / ±inf / subnormals, a VARCHAR column (dictionary codes; strings with the empty
-string, NUL and high bytes, constants present and absent) and a full-range UBIGINT column, each with
+string, NUL and high bytes, constants present and absent), a full-range UBIGINT column and a HUGEINT
+column (codes of a dictionary over 16-byte order keys; values across the sign, 2^64 and the bounds,
+constants present and absent; the oracle compares the 128-bit values themselves), each with
 NULLs and a random index (none, every-value range, equality, range edges + bins); random pushed
 TableFilterSets and residual AND/OR trees over them under three snapshots (committed / writer /
 reader deletes, and in every other round update records of each type, SET NULL included); every
 scan against the oracle's restatement (FilterSelectionSwitch<float / double / string_t /
-uint64_t>), every third one also through the table function (row ids, values as stored — FLOAT /
-DOUBLE patterns, UBIGINT bits, VARCHAR codes decoded — and NULL-ness against the oracle's fetch).
+uint64_t / hugeint_t>), every third one also through the table function (row ids, values as stored —
+FLOAT / DOUBLE patterns, UBIGINT bits, VARCHAR and HUGEINT codes decoded — and NULL-ness against the
+oracle's fetch).
 scripts/fuzz_soak.py runs typed_round at a larger size for a wall-clock budget."""
 import math
 import threading
@@ -20,12 +23,14 @@ from cubit_amd.datagen import validity_from_mask
 from cubit_amd.scan_function import ROW_ID, CubitScanFunction
 from cubit_amd.table import Context, CubitTable, Dictionary
 from oracle import oracle as O
+from test_oracle_huge_filters import oracle_filters
 
 pytestmark = pytest.mark.gpu
 
 TXN_START = 4611686018427388000
 CMPS = ["=", "!=", "<", "<=", ">", ">="]
-KINDS = ["double", "float", "varchar", "ubigint"]
+KINDS = ["double", "float", "varchar", "ubigint", "hugeint"]
+HUGE = {4: True}  # column 4: HUGEINT (signed)
 
 
 @pytest.fixture(scope="module")
@@ -45,16 +50,22 @@ def pools(rng):
         [bytes(rng.integers(0, 256, rng.integers(1, 6)).tolist()) for _ in range(10)]
     ub = np.concatenate([np.array([0, 1, 2 ** 63 - 1, 2 ** 63, 2 ** 64 - 1], dtype=np.uint64),
                          rng.integers(0, 2 ** 64 - 1, 15, dtype=np.uint64, endpoint=True)])
+    hi = (1 << 127) - 1
+    hg = sorted({-hi - 1, -hi, -(2 ** 64), -1, 0, 1, 2 ** 63, 2 ** 64, hi - 1, hi} |
+                {int(rng.integers(-2 ** 62, 2 ** 62)) << int(rng.integers(0, 64)) for _ in range(10)})
     consts = {"double": list(dbl) + [3.25, -math.inf],
               "float": list(flt) + [np.float32(3.25)],
               "varchar": strs + [b"a\x01", b"zzz", b"\xff\xff\xff", b"m"],
-              "ubigint": [int(x) for x in ub] + [2 ** 63 + 7, 12345]}
-    return {"double": dbl, "float": flt, "varchar": strs, "ubigint": ub}, consts
+              "ubigint": [int(x) for x in ub] + [2 ** 63 + 7, 12345],
+              "hugeint": hg + [2 ** 64 + 1, -(2 ** 64) - 1, 7, hi - 2]}
+    return {"double": dbl, "float": flt, "varchar": strs, "ubigint": ub, "hugeint": hg}, consts
 
 
 def const_of(kind, c):
     """A constant as the filter classes take it: FLOAT as np.float32, DOUBLE as float, VARCHAR bytes,
-    UBIGINT int."""
+    UBIGINT int, HUGEINT its order key."""
+    if kind == "hugeint":
+        return F.key128(c, True)
     if kind == "float":
         return np.float32(c)
     if kind == "double":
@@ -77,7 +88,7 @@ def rand_residual(rng, consts, depth=0):
     if depth < 2 and rng.random() < 0.5:
         kids = [rand_residual(rng, consts, depth + 1) for _ in range(rng.integers(2, 4))]
         return F.And(*kids) if rng.random() < 0.5 else F.Or(*kids)
-    c = int(rng.integers(0, 4))
+    c = int(rng.integers(0, len(KINDS)))
     if rng.random() < 0.1:
         return F.IsNull(c)
     cs = consts[KINDS[c]]
@@ -90,7 +101,7 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
     pool, consts = pools(rng)
     row_base = int(rng.integers(0, 1 << 40))
     t = CubitTable(ctx, n, row_base=row_base)
-    valid = [rng.random(n) > 0.08 for _ in range(4)]
+    valid = [rng.random(n) > 0.08 for _ in range(len(KINDS))]
     vw = [validity_from_mask(v) for v in valid]
     dbl = pool["double"][rng.integers(0, len(pool["double"]), n)]
     flt = pool["float"][rng.integers(0, len(pool["float"]), n)]
@@ -101,6 +112,9 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
     d = Dictionary(pool["varchar"])
     t.add_string_column(2, strs, d)
     t.add_column(3, ub, vw[3])
+    hg = [pool["hugeint"][i] if ok else None for i, ok in zip(rng.integers(0, len(pool["hugeint"]), n), valid[4])]
+    dh = Dictionary([F.key128(v, True) for v in pool["hugeint"]])
+    t.add_huge_column(4, hg, True, dh)
     for c, kind in enumerate(KINDS):
         choice = rng.integers(0, 4)
         if choice == 1:
@@ -108,7 +122,7 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
         elif choice == 2:
             t.build_index(c, L.INDEX_EQUALITY)
         elif choice == 3:
-            picks = (pool[kind][rng.integers(0, len(pool[kind]), 4)].tolist() if kind != "varchar"
+            picks = (pool[kind][rng.integers(0, len(pool[kind]), 4)].tolist() if kind not in ("varchar", "hugeint")
                      else [pool[kind][i] for i in rng.integers(0, len(pool[kind]), 4)])
             # distinct (-0.0 and +0.0 are one key), ascending, NaN left out
             keys = sorted({k for k in picks if not (isinstance(k, float) and math.isnan(k))})
@@ -120,22 +134,25 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
     writer = TXN_START + 5
     upd = {}
     code = {s: i for i, s in enumerate(d.entries())}
+    hcode = {v: i for i, v in enumerate(pool["hugeint"])}  # the pool is sorted: its ranks are the codes
     if with_updates:
         for c, kind in enumerate(KINDS):
             rows = np.sort(rng.choice(n, size=n // 100, replace=False)).astype(np.int64)
             ok = rng.random(len(rows)) > 0.15
             vers = np.where(rng.random(len(rows)) < 0.5, np.uint64(3), np.uint64(writer)).astype(np.uint64)
             pick = rng.integers(0, len(pool[kind]), len(rows))
-            if kind == "varchar":
+            if kind in ("varchar", "hugeint"):
                 vals = [pool[kind][i] for i in pick]
-                t.set_updates(c, rows, np.array([code[s] for s in vals], np.int64), vers, ok)
+                cm = code if kind == "varchar" else hcode
+                t.set_updates(c, rows, np.array([cm[s] for s in vals], np.int64), vers, ok)
                 upd[c] = (rows, [s if k else None for s, k in zip(vals, ok)], vers, ok)
             else:
                 vals = pool[kind][pick]
                 t.set_updates(c, rows, vals, vers, ok)
                 upd[c] = (rows, vals, vers, ok)
     ocols = [O.Column(dbl, vw[0], updates=upd.get(0)), O.Column(flt, vw[1], updates=upd.get(1)),
-             O.StringColumn(strs, updates=upd.get(2)), O.Column(ub, vw[3], updates=upd.get(3))]
+             O.StringColumn(strs, updates=upd.get(2)), O.Column(ub, vw[3], updates=upd.get(3)),
+             O.HugeColumn(hg, signed=True, updates=upd.get(4))]
     del_rows = np.sort(rng.choice(n, size=n // 20, replace=False)).astype(np.int64)
     del_ids = np.where(rng.random(len(del_rows)) < 0.5, np.uint64(4), np.uint64(writer)).astype(np.uint64)
     t.set_deletes(del_rows, del_ids)
@@ -144,17 +161,17 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
     views = [(2, writer), (2, TXN_START + 6), (10, TXN_START + 7)]
     checks = 0
     for i in range(n_cases):
-        cols = rng.choice(4, size=rng.integers(0, 4), replace=False)
+        cols = rng.choice(len(KINDS), size=rng.integers(0, len(KINDS)), replace=False)
         fs = F.TableFilterSet({int(c): rand_filter(rng, KINDS[c], consts) for c in cols})
         residual = rand_residual(rng, consts) if rng.random() < 0.4 else None
         start, tid = views[i % 3]
         tx = O.Mvcc(start, tid, deleted=deleted)
-        ref = O.table_scan(ocols, F.serialize(fs, residual), n, row_base=row_base, tx=tx)
+        ref = O.table_scan(ocols, F.serialize(*oracle_filters(fs, residual, HUGE)), n, row_base=row_base, tx=tx)
         got = np.sort(t.scan(fs, residual, txn=L.Txn(start, tid), ordered=bool(i % 2)))
         if not np.array_equal(got, ref):
             raise AssertionError(f"typed seed {seed} case {i}: {len(got)} vs {len(ref)} rows; {fs} {residual}")
         if i % 3 == 0:
-            table_function_check(t, rng, fs, residual, L.Txn(start, tid), ref, ocols, d, row_base, tx,
+            table_function_check(t, rng, fs, residual, L.Txn(start, tid), ref, ocols, (d, dh), row_base, tx,
                                  f"typed seed {seed} case {i}")
         checks += 1
     t.close()
@@ -162,8 +179,8 @@ def typed_round(ctx, seed, n, with_updates, n_cases=24):
 
 
 def table_function_check(t, rng, fs, residual, txn, ref, ocols, d, row_base, tx, label):
-    keep = [int(c) for c in rng.permutation(4)[: int(rng.integers(1, 5))]]
-    fn = CubitScanFunction(t, [0, 1, 2, 3, ROW_ID], [4] + keep, fs, residual, txn=txn)
+    keep = [int(c) for c in rng.permutation(len(KINDS))[: int(rng.integers(1, len(KINDS) + 1))]]
+    fn = CubitScanFunction(t, list(range(len(KINDS))) + [ROW_ID], [len(KINDS)] + keep, fs, residual, txn=txn)
     parts, lock = [], threading.Lock()
 
     def task():
@@ -193,7 +210,10 @@ def table_function_check(t, rng, fs, residual, txn, ref, ocols, d, row_base, tx,
         rv, rvalid = O.fetch(ocols[c], ref, row_base=row_base, tx=tx, with_valid=True)
         assert np.array_equal(valid, rvalid), (label, c)
         if c == 2:  # VARCHAR: codes against the oracle's strings
-            assert [d.entry(v) if ok else None for v, ok in zip(vals, valid)] == ocols[2].decode(rv, rvalid), label
+            assert [d[0].entry(v) if ok else None for v, ok in zip(vals, valid)] == ocols[2].decode(rv, rvalid), label
+        elif c == 4:  # HUGEINT: codes against the oracle's 128-bit values
+            assert [F.value128(d[1].entry(v)) if ok else None for v, ok in zip(vals, valid)] == \
+                ocols[4].decode(rv, rvalid), label
         else:
             assert np.array_equal(vals[valid], rv[rvalid]), (label, c)
 

@@ -52,6 +52,30 @@ def huge_filter(op, v):
     return F.ConstantFilter(op, O.huge_ref(v))
 
 
+def oracle_filters(fs, residual, huge):
+    """A filter set + residual written for the GPU (constants on HUGEINT / UHUGEINT columns as their
+    order keys, filters.key128) restated for the oracle (those constants as ohuge addresses);
+    huge = {column: signed}."""
+    def tf(f, signed):
+        if isinstance(f, F.ConstantFilter):
+            return F.ConstantFilter(f.comparison, O.huge_ref(F.value128(f.constant, signed)))
+        if isinstance(f, (F.ConjunctionAndFilter, F.ConjunctionOrFilter)):
+            return type(f)([tf(c, signed) for c in f.child_filters])
+        return f
+
+    def rf(r):
+        if isinstance(r, F.Cmp) and r.column in huge:
+            return F.Cmp(r.column, r.comparison, O.huge_ref(F.value128(r.constant, huge[r.column])))
+        if isinstance(r, (F.And, F.Or)):
+            return type(r)(*[rf(c) for c in r.children])
+        return r
+
+    out = F.TableFilterSet()
+    for c, f in fs.filters.items():
+        out.filters[c] = tf(f, huge[c]) if c in huge else f
+    return out, (None if residual is None else rf(residual))
+
+
 def answer(case, q, rows, cols):
     """The query's result lines from the rows its pushed filter kept (as sqllogictest prints them)."""
     h = case["columns"].index("h")
