@@ -832,10 +832,33 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
         return nullptr;
     }
     const auto &type = bind.table.GetColumn(LogicalIndex(column_id)).GetType();
-    if (type.InternalType() == PhysicalType::VARCHAR) {
-        return nullptr;  // the partition's statistics are dictionary codes, not strings
-    }
     auto stats = BaseStatistics::CreateEmpty(type);
+    if (type.InternalType() == PhysicalType::VARCHAR) {
+        // the codes' min / max are ranks: their dictionary entries are the column's min / max
+        // strings (StringStats keeps their prefixes). Length and unicode are not tracked here:
+        // left unknown / possible, as conservative statistics must be.
+        auto d = set->dicts.find(column_id);
+        if (d == set->dicts.end()) {
+            return nullptr;
+        }
+        if (has_no_null) {
+            for (int64_t code : {lo, hi}) {
+                const char *p = nullptr;
+                uint64_t len = 0;
+                if (cubit_dict_entry(d->second, (uint64_t)code, &p, &len) != CUBIT_OK) {
+                    return nullptr;
+                }
+                StringStats::Update(stats, string_t(p, (uint32_t)len));
+            }
+            StringStats::ResetMaxStringLength(stats);
+            StringStats::SetContainsUnicode(stats);
+            stats.SetHasNoNull();
+        }
+        if (has_null) {
+            stats.SetHasNull();
+        }
+        return stats.ToUnique();
+    }
     if (has_no_null) {
         const auto phys = type.InternalType();
         if (phys == PhysicalType::INT128 || phys == PhysicalType::UINT128) {
