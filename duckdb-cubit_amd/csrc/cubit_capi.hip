@@ -1088,6 +1088,7 @@ struct DevBuf {
 struct DictData {
     std::vector<char> bytes;
     std::vector<uint64_t> offs{0};
+    uint64_t fingerprint = 0;  // FNV-1a over the entries and their lengths: an index file names its dictionary
     uint64_t size() const { return offs.size() - 1; }
     std::string_view at(uint64_t code) const {
         return std::string_view(bytes.data() + offs[code], offs[code + 1] - offs[code]);
@@ -1645,6 +1646,13 @@ extern "C" int cubit_dict_create(const char* bytes, const uint64_t* offsets, uin
         d->bytes.insert(d->bytes.end(), sv.begin(), sv.end());
         d->offs.push_back(d->bytes.size());
     }
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t b) { h = (h ^ b) * 1099511628211ull; };
+    for (auto sv : v) {
+        mix(sv.size());
+        for (char c : sv) mix((unsigned char)c);
+    }
+    d->fingerprint = h;
     *out = new cubit_dict{std::move(d)};
     return CUBIT_OK;
 }
@@ -2029,6 +2037,16 @@ struct IndexFileHeader {
     uint64_t n_bv;
 };
 static_assert(sizeof(IndexFileHeader) == 72, "stable on-disk header");
+// version 2 appends what the keys and leaves are relative to: the column's type (keys of FLOAT /
+// DOUBLE are comparison keys, of VARCHAR / HUGEINT codes) and, for a dictionary column, its
+// dictionary's fingerprint — codes of another dictionary would name other strings. A version-1
+// file (no tail) loads onto a column that is not a dictionary column.
+struct IndexFileTail {
+    int32_t col_type;
+    uint32_t reserved;
+    uint64_t dict_fingerprint;
+};
+static_assert(sizeof(IndexFileTail) == 16, "stable on-disk tail");
 
 }  // namespace
 
@@ -2050,7 +2068,9 @@ extern "C" int cubit_table_save_index(cubit_table* t, int col, int encoding, con
     if (!f) return fail(CUBIT_ERR_INVALID, "cannot open %s for writing", path);
     IndexFileHeader h{};
     std::memcpy(h.magic, kIndexMagic, 8);
-    h.version = 1;
+    h.version = 2;
+    const Column& sc = t->cols.at(col);
+    const IndexFileTail tail{sc.type, 0u, sc.dict ? sc.dict->fingerprint : 0ull};
     h.encoding = (uint32_t)ix->encoding;
     h.n_rows = t->n_rows;
     h.nwp = t->nwp;
@@ -2060,7 +2080,7 @@ extern "C" int cubit_table_save_index(cubit_table* t, int col, int encoding, con
     h.vmax = ix->vmax;
     h.n_keys = ix->keys.size();
     h.n_bv = ix->bvs.size();
-    bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1 &&
+    bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1 && std::fwrite(&tail, sizeof(tail), 1, f) == 1 &&
               (h.n_keys == 0 || std::fwrite(ix->keys.data(), 8, h.n_keys, f) == h.n_keys);
     std::vector<uint64_t> host(ok ? t->nwp : 0);
     for (size_t k = 0; ok && k < ix->bvs.size(); ++k) {
@@ -2086,8 +2106,19 @@ extern "C" int cubit_table_load_index(cubit_table* t, int col, const char* path)
         return fail(CUBIT_ERR_INVALID, "%s: %s", path, why);
     };
     IndexFileHeader h{};
-    if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, kIndexMagic, 8) != 0 || h.version != 1)
+    if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, kIndexMagic, 8) != 0 ||
+        (h.version != 1 && h.version != 2))
         return bad("not a cubit index file");
+    const Column& lc = t->cols.at(col);
+    if (h.version == 2) {
+        IndexFileTail tail{};
+        if (std::fread(&tail, sizeof(tail), 1, f) != 1) return bad("truncated header");
+        if (tail.col_type != lc.type) return bad("index was built on a column of another type");
+        if (tail.dict_fingerprint != (lc.dict ? lc.dict->fingerprint : 0ull))
+            return bad("index was built against another dictionary");
+    } else if (lc.dict) {
+        return bad("a version-1 index file does not name its dictionary");
+    }
     if (h.n_rows != t->n_rows || h.nwp != t->nwp) return bad("index was built for a partition of another size");
     if (h.encoding > CUBIT_INDEX_BINS) return bad("unknown encoding");
     const uint64_t want_bv = h.encoding == CUBIT_INDEX_BINS ? (h.n_keys ? h.n_keys - 1 : 0) : h.n_keys;

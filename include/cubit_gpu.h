@@ -457,7 +457,10 @@ int cubit_table_index_info(cubit_table *t, int col, uint32_t *n_bitvectors, uint
  * bound_index.hpp:117-118): write a column's RANGE / EQUALITY / BINS index (keys,
  * statistics, bitvectors) to one file, and load it back into a partition of the same size
  * (it replaces that encoding's index on the column). The file does not carry the column
- * data: load it only beside the column it was built from. */
+ * data: load it only beside the column it was built from. It names the column's type and, for a
+ * dictionary column (VARCHAR, HUGEINT / UHUGEINT), its dictionary (a fingerprint of the entries):
+ * a load onto a column of another type or against another dictionary is refused
+ * (CUBIT_ERR_INVALID). */
 int cubit_table_save_index(cubit_table *t, int col, int encoding, const char *path);
 int cubit_table_load_index(cubit_table *t, int col, const char *path);
 

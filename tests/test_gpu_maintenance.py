@@ -52,10 +52,16 @@ def rand_filter_set(rng, n_cols):
 def read_index(path):
     b = open(path, "rb").read()
     magic, ver, enc, n_rows, nwp, exact, empty, vmin, vmax, n_keys, n_bv = struct.unpack("<8sIIQQIIqqQQ", b[:72])
-    assert magic == b"CUBITIX1"
-    keys = np.frombuffer(b[72:72 + 8 * n_keys], dtype=np.int64)
-    bvs = np.frombuffer(b[72 + 8 * n_keys:], dtype=np.uint64).reshape(n_bv, nwp)
-    return dict(enc=enc, n_rows=n_rows, nwp=nwp, exact=exact, empty=empty, vmin=vmin, vmax=vmax, keys=keys, bvs=bvs)
+    assert magic == b"CUBITIX1" and ver in (1, 2)
+    h = 72
+    col_type, fingerprint = None, None
+    if ver == 2:  # the tail: column type, dictionary fingerprint
+        col_type, _, fingerprint = struct.unpack("<iIQ", b[72:88])
+        h = 88
+    keys = np.frombuffer(b[h:h + 8 * n_keys], dtype=np.int64)
+    bvs = np.frombuffer(b[h + 8 * n_keys:], dtype=np.uint64).reshape(n_bv, nwp)
+    return dict(enc=enc, n_rows=n_rows, nwp=nwp, exact=exact, empty=empty, vmin=vmin, vmax=vmax, keys=keys, bvs=bvs,
+                col_type=col_type, fingerprint=fingerprint)
 
 
 def bits(mask, nwp):

@@ -246,3 +246,35 @@ def test_string_column_through_table_function(ctx, tasks):
         assert np.array_equal(ok, wok)
         assert [d.entry(c) if o else None for c, o in zip(codes, ok)] == col.decode(want, wok)
     t.close()
+
+
+def test_index_files_name_their_dictionary(ctx, tmp_path):
+    """A saved index on a dictionary column loads beside the same dictionary (scans equal the
+    built index's) and is refused against another dictionary or onto a column of another type:
+    its codes would name other strings."""
+    rng = np.random.default_rng(41)
+    n = 100_003
+    vals, pool = random_strings(rng, n)
+    d = Dictionary(pool)
+    t = CubitTable(ctx, n)
+    t.add_string_column(0, vals, d)
+    t.build_index(0, L.INDEX_EQUALITY)
+    path = tmp_path / "eq.cix"
+    t.save_index(0, L.INDEX_EQUALITY, path)
+    fs = F.TableFilterSet({0: F.ConstantFilter("=", pool[4])})
+    want = t.scan(fs)
+    u = CubitTable(ctx, n)
+    u.add_string_column(0, vals, d)
+    u.load_index(0, path)
+    assert u.index_info(0)[0] == t.index_info(0)[0]
+    assert np.array_equal(u.scan(fs), want)
+    other = CubitTable(ctx, n)
+    other.add_string_column(0, vals, Dictionary(pool + [b"not in the first one"]))
+    with pytest.raises(L.CubitError):
+        other.load_index(0, path)
+    ints = CubitTable(ctx, n)
+    ints.add_column(0, np.zeros(n, dtype=np.int32))
+    with pytest.raises(L.CubitError):
+        ints.load_index(0, path)
+    for x in (t, u, other, ints):
+        x.close()
