@@ -2959,6 +2959,45 @@ struct Planner {
         return mk_leaf(l);
     }
 
+    // lo <= v < hi (either side open) on a column whose equality index holds every distinct
+    // value (exact_all): the union of the keys' bitvectors inside, or the valid rows minus the
+    // union of those outside — the fewer leaves; nullptr when both exceed 16.
+    ExprP eq_interval(int col, const IndexView& ix, int64_t lo, int64_t hi, bool has_lo, bool has_hi) {
+        const size_t b = has_lo ? (size_t)(std::lower_bound(ix.keys.begin(), ix.keys.end(), lo) - ix.keys.begin()) : 0;
+        const size_t e = has_hi ? (size_t)(std::lower_bound(ix.keys.begin(), ix.keys.end(), hi) - ix.keys.begin())
+                                : ix.keys.size();
+        auto leaf = [&](size_t k) {
+            Leaf l;
+            l.bv = ix.bvs[k];
+            l.column = col;
+            l.cmp = CUBIT_CMP_EQ;
+            l.constant = ix.keys[k];
+            l.zsrc = kZoneBits;
+            return mk_leaf(l);
+        };
+        const size_t inside = e > b ? e - b : 0, outside = ix.keys.size() - inside;
+        if (inside <= 16 && inside <= outside + 1) {
+            ExprP acc = mk_false();
+            for (size_t k = b; k < e; ++k) acc = mk_bin(Expr::OR, acc, leaf(k));
+            return acc;
+        }
+        if (outside > 16) return nullptr;
+        ExprP out = mk_false();
+        for (size_t k = 0; k < ix.keys.size(); ++k)
+            if (k < b || k >= e) out = mk_bin(Expr::OR, out, leaf(k));
+        return mk_bin(Expr::ANDNOT, nn(col), out);
+    }
+
+    // the column's equality index when it holds every distinct value (an interval over it is a
+    // union of its bitvectors), else null
+    const Index* exact_equality(int col) const {
+        auto it = t->idx.find(col);
+        return it != t->idx.end() && it->second.encoding == CUBIT_INDEX_EQUALITY && it->second.exact_all &&
+                       !it->second.empty
+                   ? &it->second
+                   : nullptr;
+    }
+
     ExprP eq_leaf(int col, const IndexView& ix, int64_t c, bool& exact) {
         exact = true;
         auto it = std::lower_bound(ix.keys.begin(), ix.keys.end(), c);
@@ -3026,27 +3065,18 @@ struct Planner {
                     ExprP e = eq_leaf(col, ix, c, exact);
                     if (exact) return mk_bin(Expr::ANDNOT, nn(col), e);
                 } else if (ix.exact_all) {
-                    // union of the equality bitvectors in range; wide ranges go to K0
-                    std::vector<size_t> sel;
-                    for (size_t k = 0; k < ix.keys.size(); ++k) {
-                        const int64_t v = ix.keys[k];
-                        const bool in = cmp == CUBIT_CMP_LT ? v < c : cmp == CUBIT_CMP_LE ? v <= c
-                                        : cmp == CUBIT_CMP_GT ? v > c : v >= c;
-                        if (in) sel.push_back(k);
-                    }
-                    if (sel.size() <= 16) {
-                        ExprP acc = mk_false();
-                        for (size_t k : sel) {
-                            Leaf l;
-                            l.bv = ix.bvs[k];
-                            l.column = col;
-                            l.cmp = CUBIT_CMP_EQ;
-                            l.constant = ix.keys[k];
-                            l.zsrc = kZoneBits;
-                            acc = mk_bin(Expr::OR, acc, mk_leaf(l));
-                        }
-                        return acc;
-                    }
+                    // the equality bitvectors in range, or the valid rows outside the others
+                    // (whichever reads fewer); wide ranges both ways go to K0
+                    const bool has_lo = cmp == CUBIT_CMP_GT || cmp == CUBIT_CMP_GE;
+                    int64_t lo = 0, hi = 0;
+                    bool empty = false;
+                    if (cmp == CUBIT_CMP_GE) lo = c;
+                    else if (cmp == CUBIT_CMP_GT) empty = c == INT64_MAX, lo = empty ? c : c + 1;
+                    else if (cmp == CUBIT_CMP_LT) hi = c;
+                    else if (c == INT64_MAX) return nn(col);
+                    else hi = c + 1;
+                    if (empty) return mk_false();
+                    if (ExprP e = eq_interval(col, ix, lo, hi, has_lo, !has_lo)) return e;
                 }
             }
         }
@@ -3114,7 +3144,7 @@ struct Planner {
             kids.push_back(j);
             const cubit_filter_node& c = nodes[j];
             if (c.kind == CUBIT_FILTER_CONSTANT && c.n_children == 0 && c.cmp != CUBIT_CMP_NE && c.cmp >= 0 &&
-                c.cmp <= 5 && t->bins.count(c.column)) {
+                c.cmp <= 5 && (t->bins.count(c.column) || exact_equality(c.column))) {
                 Bounds& bd = by_col[c.column];
                 const int64_t v = c.constant;
                 auto lower = [&](int64_t x) { bd.lo = bd.has_lo ? std::max(bd.lo, x) : x; bd.has_lo = true; };
@@ -3139,7 +3169,14 @@ struct Planner {
         for (auto& [col, bd] : by_col) {
             ExprP e;
             if (bd.empty || (bd.has_lo && bd.has_hi && bd.hi <= bd.lo)) e = mk_false();
-            else e = interval_from_bins(col, bd.lo, bd.hi, bd.has_lo, bd.has_hi);
+            else if (t->bins.count(col)) e = interval_from_bins(col, bd.lo, bd.hi, bd.has_lo, bd.has_hi);
+            if (!e && !rc && bd.members.size() > 1) {
+                // two or more bounds on an every-value equality index: one union for the interval
+                if (const Index* eq = exact_equality(col)) {
+                    const IndexView v = view_of(t, col, *eq);  // exact only while every updated value is a key
+                    if (v.exact_all && !v.empty) e = eq_interval(col, v, bd.lo, bd.hi, bd.has_lo, bd.has_hi);
+                }
+            }
             if (rc) return nullptr;
             if (!e) continue;
             for (uint32_t m : bd.members) done[m] = 1;

@@ -278,3 +278,46 @@ def test_index_files_name_their_dictionary(ctx, tmp_path):
         ints.load_index(0, path)
     for x in (t, u, other, ints):
         x.close()
+
+
+def test_equality_index_plans_intervals_as_one_union(ctx):
+    """On an every-value equality index, bounds on one column fold into one interval read as the
+    union of the keys inside it, or the valid rows minus the union of those outside — the fewer
+    bitvectors (l_shipmode's seven modes: [RAIL, SHIP) reads 2, not 4 + 5) — with NULLs, and
+    after update records (a value that is not a key makes the index inexact: K0 then)."""
+    rng = np.random.default_rng(43)
+    n = 300_007
+    modes = [b"AIR", b"FOB", b"MAIL", b"RAIL", b"REG AIR", b"SHIP", b"TRUCK"]
+    vals = [None if rng.random() < 0.05 else modes[i] for i in rng.integers(0, 7, n)]
+    d = Dictionary(modes + [b"ZZZ"])  # one entry no row holds: an update may bring it in
+    t = CubitTable(ctx, n)
+    t.add_string_column(0, vals, d)
+    t.build_index(0, L.INDEX_EQUALITY)
+    col = O.StringColumn(vals)
+    cases = [
+        ([(">=", b"RAIL"), ("<", b"SHIP")], 2),            # inside: RAIL, REG AIR
+        ([(">", b"AIR"), ("<=", b"TRUCK")], 1),            # outside: AIR (valid rows minus it)
+        ([(">=", b"B"), ("<", b"S")], 3),                  # absent bounds: FOB, MAIL, RAIL... as codes
+        ([(">=", b"MAIL")], 3),                            # one bound: outside AIR, FOB, (ZZZ absent)
+        ([("<", b"MAIL"), (">", b"AIR"), ("<=", b"FOB")], 1),
+        ([(">", b"TRUCK")], 0),
+    ]
+    for terms, max_leaves in cases:
+        flt = F.ConjunctionAndFilter([F.ConstantFilter(op, c) for op, c in terms]) if len(terms) > 1 else \
+            F.ConstantFilter(*terms[0])
+        fs = F.TableFilterSet({0: flt})
+        want = O.table_scan([col], F.serialize(fs), n)
+        assert np.array_equal(t.scan(fs), want), terms
+        leaves, _ = t.last_plan()
+        assert leaves <= max_leaves + 1, (terms, leaves)  # + the validity leaf
+    # an update to a code no row held before: the index stops being every-value, plans fall back
+    rows = np.array([5, 17, 900], dtype=np.int64)
+    t.set_updates(0, rows, np.array([7, 3, 7], dtype=np.int64), np.array([1, 1, 1], dtype=np.uint64))
+    ucol = O.StringColumn(vals, updates=(rows, [b"ZZZ", b"RAIL", b"ZZZ"], np.array([1, 1, 1], dtype=np.uint64)))
+    txn, tx = L.Txn(5, TXN_START + 1), O.Mvcc(5, TXN_START + 1)
+    for terms, _ in cases:
+        flt = F.ConjunctionAndFilter([F.ConstantFilter(op, c) for op, c in terms]) if len(terms) > 1 else \
+            F.ConstantFilter(*terms[0])
+        fs = F.TableFilterSet({0: flt})
+        assert np.array_equal(t.scan(fs, txn=txn), O.table_scan([ucol], F.serialize(fs), n, 0, tx)), terms
+    t.close()
