@@ -874,13 +874,17 @@ static unique_ptr<BaseStatistics> CubitStatistics(ClientContext &context, const 
             for (int k = 0; k < 2; k++) {
                 cubit_value128(kt, (const unsigned char *)p[k], &lower[k], &upper[k]);
             }
-            if (phys == PhysicalType::INT128) {
-                NumericStats::SetMin(stats, Value::HUGEINT(hugeint_t((int64_t)upper[0], lower[0])));
-                NumericStats::SetMax(stats, Value::HUGEINT(hugeint_t((int64_t)upper[1], lower[1])));
-            } else {
-                NumericStats::SetMin(stats, Value::UHUGEINT(uhugeint_t(upper[0], lower[0])));
-                NumericStats::SetMax(stats, Value::UHUGEINT(uhugeint_t(upper[1], lower[1])));
-            }
+            // as the column's logical type: HUGEINT, UHUGEINT, DECIMAL(19..38) or UUID storage values
+            auto value_of = [&](int k) {
+                const hugeint_t h((int64_t)upper[k], lower[k]);
+                if (phys == PhysicalType::UINT128) return Value::UHUGEINT(uhugeint_t(upper[k], lower[k]));
+                if (type.id() == LogicalTypeId::DECIMAL)
+                    return Value::DECIMAL(h, DecimalType::GetWidth(type), DecimalType::GetScale(type));
+                if (type.id() == LogicalTypeId::UUID) return Value::UUID(h);
+                return Value::HUGEINT(h);
+            };
+            NumericStats::SetMin(stats, value_of(0));
+            NumericStats::SetMax(stats, value_of(1));
         } else if (phys == PhysicalType::FLOAT || phys == PhysicalType::DOUBLE) {  // bit patterns
             float f[2];
             double d[2];
