@@ -374,8 +374,10 @@ int cubit_table_column_data(cubit_table *t, int col, const void **data, int *typ
  * Index bitvectors are not rebuilt by it (rebuild with cubit_table_build_index). `type` may be
  * any CUBIT_TYPE_* code: an 8- / 16-bit or unsigned column is widened on the device into an
  * owned INT32 / INT64 column (even from on_device data) — TINYINT … UINTEGER vectors as DuckDB
- * holds them; a UINT64 (UBIGINT), FLOAT or DOUBLE column keeps its values' bits and compares them
- * through its key (see the type codes); a VARCHAR column is registered with its dictionary
+ * holds them; a UINT64 (UBIGINT) column keeps its values' bits and compares them unsigned; a FLOAT
+ * or DOUBLE column is copied into the table (even from on_device data) as its bit patterns plus
+ * their comparison keys (see the type codes) — widened and FP copies are the table's own, so a
+ * later change to the caller's buffer is not seen: register the column again; a VARCHAR column is registered with its dictionary
  * (cubit_table_add_dict_column). Appends, updates and probes then use the stored values
  * (cubit_table_column_data reports the type held). */
 int cubit_table_add_column(cubit_table *t, int col, int type, const void *data, const uint64_t *validity,
