@@ -3241,8 +3241,40 @@ int materialize(cubit_table* t, const ExprP& e, uint64_t** out) {
 }
 
 bool fits(const ExprP& e);
+int fit(cubit_table* t, ExprP& e);
 double literal_selectivity(cubit_table* t, const Leaf& l, bool neg, int* rc);
 double conj_selectivity(cubit_table* t, const Emitter::Lits& lits, int* rc);
+
+// top-level conjuncts of e (a & ~leaf contributes the complemented leaf as a conjunct)
+void conj_parts(const ExprP& e, std::vector<ExprP>& out) {
+    if (e->kind == Expr::AND) {
+        conj_parts(e->a, out);
+        conj_parts(e->b, out);
+    } else if (e->kind == Expr::ANDNOT && e->b->kind == Expr::LEAF) {
+        conj_parts(e->a, out);
+        out.push_back(mk_leaf(e->b->leaf, !e->b->neg));
+    } else if (e->kind != Expr::CONST_TRUE) {
+        out.push_back(e);
+    }
+}
+void leaves_of(const ExprP& e, std::vector<const uint64_t*>& out) {
+    if (e->kind == Expr::LEAF) out.push_back(e->leaf.bv);
+    else if (e->a) {
+        leaves_of(e->a, out);
+        if (e->b) leaves_of(e->b, out);
+    }
+}
+// estimated fraction of rows a subtree keeps, from its literals' estimates
+double expr_selectivity(cubit_table* t, const ExprP& e, int* rc) {
+    switch (e->kind) {
+    case Expr::LEAF: return literal_selectivity(t, e->leaf, e->neg, rc);
+    case Expr::AND: return expr_selectivity(t, e->a, rc) * expr_selectivity(t, e->b, rc);
+    case Expr::OR: return std::min(1.0, expr_selectivity(t, e->a, rc) + expr_selectivity(t, e->b, rc));
+    case Expr::ANDNOT: return expr_selectivity(t, e->a, rc) * (1.0 - expr_selectivity(t, e->b, rc));
+    case Expr::CONST_TRUE: return 1.0;
+    default: return 0.0;
+    }
+}
 
 // Selection narrowing of K0 leaves (RowGroup::TemplatedScan's filter loop, row_group.cpp:537-550:
 // each filter column after the first is read only at the rows the earlier ones kept). When the
@@ -3256,7 +3288,10 @@ double conj_selectivity(cubit_table* t, const Emitter::Lits& lits, int* rc);
 // version), the reference's AdaptiveFilter ordering its filters by observed cost
 // (adaptive_filter.cpp:21-88) made up front: when the mask is estimated to keep more than one
 // row in 32, the K0 leaves are built in full (gathering most lines costs more than reading the
-// column in order). No count is read back: planning never waits for the device. allow = false
+// column in order). The other conjuncts need not be literals: a union of equality bitvectors (an
+// interval on an every-value equality index) or any subtree joins the mask, its selectivity
+// estimated from its literals (OR: their sum, AND: their product). No count is read back:
+// planning never waits for the device. allow = false
 // (visible MVCC updates, whose patches need whole leaves) builds every leaf in full. Every
 // pending leaf is built on return; t->last_narrow_cols lists the K0 columns in build order.
 int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool allow) {
@@ -3282,8 +3317,15 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
         return std::any_of(pending.begin(), pending.end(), [&](const PendingK0& k) { return k.bv == bv; });
     };
     if (pending.empty()) return CUBIT_OK;
-    Emitter::Lits lits;
-    if (!allow || t->n_rows == 0 || e->kind == Expr::LEAF || !Emitter::conj_leaves(e, lits)) return compute_rest();
+    if (!allow || t->n_rows == 0 || e->kind == Expr::LEAF) return compute_rest();
+    std::vector<ExprP> parts;
+    conj_parts(e, parts);
+    Emitter::Lits lits;  // the literal conjuncts
+    std::vector<ExprP> others;  // the other conjuncts (unions, subtrees)
+    for (const ExprP& p : parts) {
+        if (p->kind == Expr::LEAF) lits.push_back({p->leaf, p->neg});
+        else others.push_back(p);
+    }
     std::vector<const uint64_t*> narrow_bvs;
     Emitter::Lits rest;
     for (const auto& lit : lits) {
@@ -3293,13 +3335,18 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
         else
             rest.push_back(lit);
     }
+    std::vector<const uint64_t*> other_bvs;
+    for (const ExprP& p : others) leaves_of(p, other_bvs);
     for (const auto& lit : rest)  // a narrowed leaf must not also be read whole
         if (std::find(narrow_bvs.begin(), narrow_bvs.end(), lit.first.bv) != narrow_bvs.end()) return compute_rest();
+    for (const uint64_t* bv : other_bvs)
+        if (std::find(narrow_bvs.begin(), narrow_bvs.end(), bv) != narrow_bvs.end()) return compute_rest();
     if (narrow_bvs.empty()) return compute_rest();
-    // selectivity estimates: the mask of the other literals (independent columns: the
-    // product), each K0 comparison
+    // selectivity estimates: the mask of the other conjuncts (independent columns: the
+    // product; literals on one column as one interval), each K0 comparison
     int rc = CUBIT_OK;
-    const double rest_sel = conj_selectivity(t, rest, &rc);
+    double rest_sel = conj_selectivity(t, rest, &rc);
+    for (const ExprP& p : others) rest_sel *= expr_selectivity(t, p, &rc);
     if (rc) return rc;
     std::vector<std::pair<double, PendingK0>> narrow;
     for (const uint64_t* bv : narrow_bvs) {
@@ -3317,23 +3364,28 @@ int narrow_k0(cubit_table* t, ExprP& e, std::vector<PendingK0>& pending, bool al
         return x.first != y.first ? x.first < y.first
                                   : (x.second.col != y.second.col ? x.second.col < y.second.col : x.second.c < y.second.c);
     });
-    for (const auto& lit : rest) {  // complemented K0 leaves of the other literals: in full
+    std::vector<const uint64_t*> rest_bvs = other_bvs;  // K0 leaves inside the other conjuncts: in full
+    for (const auto& lit : rest) rest_bvs.push_back(lit.first.bv);
+    for (const uint64_t* bv : rest_bvs) {
         PendingK0 k;
-        if (take(lit.first.bv, &k)) {
+        if (take(bv, &k)) {
             if (int rc2 = compute_k0(t, k)) return rc2;
             t->last_narrow_cols.push_back(k.col);
         }
     }
-    const double mask_sel = rest.empty() ? narrow.front().first : rest_sel;
+    const bool has_rest = !rest.empty() || !others.empty();
+    const double mask_sel = has_rest ? rest_sel : narrow.front().first;
     uint64_t* mask = nullptr;
     cubit_ctx* ctx = t->ctx;
-    if (!rest.empty()) {
+    if (has_rest) {
         ExprP r = mk_true();
         for (const auto& lit : rest) r = mk_bin(Expr::AND, r, mk_leaf(lit.first, lit.second));
-        if (!fits(r) || mask_sel * 32 > 1.0) {
+        for (const ExprP& p : others) r = mk_bin(Expr::AND, r, p);
+        if (mask_sel * 32 > 1.0) {
             for (const auto& kv : narrow) pending.push_back(kv.second);
             return compute_rest();
         }
+        if (int rc2 = fit(t, r)) return rc2;  // a mask of more leaves than one pass: split
         if (int rc2 = materialize(t, r, &mask)) return rc2;
     } else {
         const PendingK0 first = narrow.front().second;

@@ -116,7 +116,7 @@ def test_mask_density_decides(ctx):
     assert len(ref) == 0
     res = F.And(F.And(F.Cmp(0, ">=", 10), F.Cmp(0, "<", 20)), F.And(F.Cmp(3, "=", 7), F.Cmp(2, ">=", 0)))
     _, narrowed = check(t, oc, None, res)
-    assert narrowed >= 1  # (the ranges on the equality-indexed column are unindexed too)
+    assert narrowed >= 1  # column 2 through the mask of [10, 20) (a union of the equality index's leaves) and 3 = 7
     # an OR keeps the comparison whole (no conjunction to narrow by)
     res = F.Or(F.Cmp(0, "=", 3), F.Cmp(1, "<", 0))
     _, narrowed = check(t, oc, None, res)
