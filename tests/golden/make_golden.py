@@ -119,6 +119,19 @@ def main():
             {"after": "con1 COMMIT", "expect": {"con1": 2, "con2": 1}},
         ],
     }
+    # test/optimizer/pushdown/timestamp_to_date_pushdown.test: t1(ts TIMESTAMP, i INT) as runs of
+    # (timestamp, i from generate_series(lo, hi)); `ts::date == d` is pushed to the scan as the
+    # TIMESTAMP range [d 00:00, d + 1 day) (the file checks the plan keeps a SEQ_SCAN filter and no
+    # FILTER above it); each count(*) with its optional bound on i
+    tsd = {
+        "source": "test/optimizer/pushdown/timestamp_to_date_pushdown.test:14-75",
+        "runs": [["2024-05-01 00:00:00", 1, 2000], ["2024-05-02 00:00:00", 1, 1000],
+                 ["2024-05-02 00:22:00", 1, 1000], ["2024-05-03 00:00:00", 1, 2000]],
+        "queries": [{"date": "2024-05-02", "i": [">", 1000], "count": 0},
+                    {"date": "2024-05-02", "i": ["<=", 500], "count": 1000},
+                    {"date": "2024-05-01", "i": ["<=", 500], "count": 500},
+                    {"date": "2024-05-03", "i": None, "count": 2000}],
+    }
     # test/optimizer/pushdown/table_or_pushdown.test: integers(a, b) = (1,1) … (5,5); the
     # integer queries' expected rows (a values). The trees use the repo's residual syntax:
     # ["or"|"and", children…] / [column, cmp, constant], column 0 = a, 1 = b.
@@ -385,6 +398,7 @@ def main():
         "test/sql/update/test_string_update_many_strings.test", "test/sql/update/test_repeated_string_update.test",
         "test/sql/update/test_update_same_string_value.test")}
     (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "mvcc_scripts": mvcc, "string_mvcc_scripts": smvcc, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
+                                                          "timestamp_date_pushdown": tsd,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,

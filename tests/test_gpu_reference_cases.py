@@ -10,8 +10,8 @@ from cubit_amd.scan_function import ROW_ID, CubitScanFunction
 from cubit_amd.table import Context, CubitTable
 from test_oracle_tpch import (art_appended_cases, art_scan_cases, block_boundary_states, filter_cache_filters, filter_cache_table,
                               filter_pushdown_tables, many_updaters_reads, multi_version_views,
-                              obsolete_filter_columns, obsolete_filter_sets, residual_from_json, update_case_views,
-                              zonemap_table)
+                              obsolete_filter_columns, obsolete_filter_sets, residual_from_json, timestamp_filter_sets,
+                              timestamp_table, update_case_views, zonemap_table)
 
 pytestmark = pytest.mark.gpu
 
@@ -37,6 +37,23 @@ def test_zonemap_segment(ctx, golden, encoding):
         rows = t.scan(F.TableFilterSet({0: F.ConstantFilter("=", int(k))}))
         got = int(data[rows].astype(np.int64).sum()) if len(rows) else None
         assert got == want, k
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_timestamp_date_pushdown(ctx, golden, encoding):
+    """timestamp_to_date_pushdown.test: a TIMESTAMP column (int64 microseconds) filtered by the
+    day range DuckDB pushes for ts::date = d, beside a bound on i; the file's counts, with the
+    timestamp column unindexed, range- or equality-indexed."""
+    c = golden["cases"]["timestamp_date_pushdown"]
+    ts, i, us = timestamp_table(c)
+    t = CubitTable(ctx, len(ts))
+    t.add_column(0, ts)
+    t.add_column(1, i)
+    if encoding is not None:
+        t.build_index(0, encoding)
+    for fs, want in timestamp_filter_sets(c, us):
+        assert len(t.scan(fs)) == want and t.count(fs) == want
+    t.close()
 
 
 def test_interleaved_versions(ctx, golden):

@@ -149,6 +149,39 @@ def test_zonemap_segment_reference_case(golden):
         assert got == want
 
 
+def timestamp_table(c):
+    """t1(ts TIMESTAMP as int64 microseconds since the epoch, i INTEGER) from the case's runs."""
+    from datetime import datetime, timezone
+
+    def us(text):
+        return int(datetime.fromisoformat(text).replace(tzinfo=timezone.utc).timestamp()) * 1_000_000
+
+    ts = np.concatenate([np.full(hi - lo + 1, us(t), dtype=np.int64) for t, lo, hi in c["runs"]])
+    i = np.concatenate([np.arange(lo, hi + 1, dtype=np.int32) for _, lo, hi in c["runs"]])
+    return ts, i, us
+
+
+def timestamp_filter_sets(c, us):
+    """Each query's pushed filters: ts in [d 00:00, d + 1 day), and the bound on i."""
+    out = []
+    for q in c["queries"]:
+        lo = us(q["date"] + " 00:00:00")
+        f = {0: F.ConjunctionAndFilter([F.ConstantFilter(">=", lo), F.ConstantFilter("<", lo + 86_400_000_000)])}
+        if q["i"]:
+            f[1] = F.ConstantFilter(q["i"][0], q["i"][1])
+        out.append((F.TableFilterSet(f), q["count"]))
+    return out
+
+
+def test_timestamp_date_pushdown_reference_case(golden):
+    """test/optimizer/pushdown/timestamp_to_date_pushdown.test: ts::date = d pushed as a TIMESTAMP
+    range, beside a bound on i: the file's counts."""
+    c = golden["cases"]["timestamp_date_pushdown"]
+    ts, i, us = timestamp_table(c)
+    for fs, want in timestamp_filter_sets(c, us):
+        assert len(O.table_scan([O.Column(ts), O.Column(i)], F.serialize(fs), len(ts))) == want
+
+
 def test_interleaved_versions_reference_case(golden):
     """test/sql/transactions/test_interleaved_versions.test:66-120 (deletes by two txns)."""
     data = np.array([1, 2], dtype=np.int32)
