@@ -1911,6 +1911,90 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     return CUBIT_OK;
 }
 
+// DuckDB RLE segments → device column. Each segment (rle.cpp RLECompressState::FlushSegment,
+// :190-205: 8-byte header = offset of the uint16 run lengths, the run values as T from byte 8,
+// the lengths after them) is walked on the host: run lengths are read until they cover the
+// segment's rows (RLEScanState, :248-277 — zero-length runs, which a run of exactly 65,535 rows
+// leaves behind, included), each value widened to the column's type as the BITPACKING path does.
+// Only the runs cross to the device, and rle_expand_kernel writes the column.
+extern "C" int cubit_table_add_rle_column(cubit_table* t, int col, int type, const uint8_t* bytes, uint64_t n_bytes,
+                                          const uint64_t* seg_offsets, const uint64_t* seg_rows, uint32_t n_segments,
+                                          const uint64_t* validity) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    SegType st;
+    if (!seg_type_of(type, st)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (n_segments && (!bytes || !seg_offsets || !seg_rows)) return fail(CUBIT_ERR_INVALID, "null argument");
+    const uint64_t tsz = st.tsz;
+    const bool wide = st.col_type != CUBIT_TYPE_INT32;
+    std::vector<int64_t> vals;
+    std::vector<uint64_t> ends;
+    uint64_t row = 0;
+    for (uint32_t sg = 0; sg < n_segments; ++sg) {
+        const uint64_t base = seg_offsets[sg];
+        if (base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
+        uint64_t off;
+        std::memcpy(&off, bytes + base, 8);
+        if (off < 8 || off > n_bytes - base) return fail(CUBIT_ERR_INVALID, "segment %u: bad run-length offset", sg);
+        uint64_t covered = 0;
+        for (uint64_t k = 0; covered < seg_rows[sg]; ++k) {
+            if (8 + (k + 1) * tsz > off || off + 2 * (k + 1) > n_bytes - base)
+                return fail(CUBIT_ERR_INVALID, "segment %u: runs cover %llu of %llu rows", sg, (unsigned long long)covered,
+                            (unsigned long long)seg_rows[sg]);
+            uint16_t len;
+            std::memcpy(&len, bytes + base + off + 2 * k, 2);
+            uint64_t raw = 0;  // T's bits, zero-extended, then widened as T
+            std::memcpy(&raw, bytes + base + 8 + k * tsz, tsz);
+            int64_t v = (int64_t)raw;
+            if (st.sgn && tsz < 8) v = (int64_t)(raw << (64 - 8 * tsz)) >> (64 - 8 * tsz);
+            covered += len;
+            if (covered > seg_rows[sg]) return fail(CUBIT_ERR_INVALID, "segment %u: runs overrun its rows", sg);
+            vals.push_back(v);
+            ends.push_back(row + covered);
+        }
+        row += seg_rows[sg];
+    }
+    if (row != t->n_rows)
+        return fail(CUBIT_ERR_INVALID, "segments hold %llu rows, partition has %llu", (unsigned long long)row,
+                    (unsigned long long)t->n_rows);
+    if (int rc = set_device(t->ctx)) return rc;
+    hipStream_t s = t->ctx->stream;
+    const uint64_t esz = wide ? 8 : 4;
+    std::vector<int32_t> narrow;
+    if (!wide) narrow.assign(vals.begin(), vals.end());
+    DevBuf d_vals, d_ends;
+    auto out = std::make_unique<DevBuf>();
+    if (hipMalloc(&d_vals.p, std::max<uint64_t>(vals.size() * esz, 16)) != hipSuccess ||
+        hipMalloc(&d_ends.p, std::max<uint64_t>(ends.size() * 8, 16)) != hipSuccess ||
+        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "RLE column allocation failed");
+    if (!vals.empty()) {
+        HIP_CHECK(hipMemcpyAsync(d_vals.p, wide ? (const void*)vals.data() : (const void*)narrow.data(),
+                                 vals.size() * esz, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_ends.p, ends.data(), ends.size() * 8, hipMemcpyHostToDevice, s));
+    }
+    hipEvent_t e0, e1;
+    if (int rc = timing_events(t->ctx, e0, e1)) return rc;
+    HIP_CHECK(launch_rle_expand(d_vals.p, static_cast<const uint64_t*>(d_ends.p), ends.size(), t->n_rows, wide ? 1 : 0,
+                                out->p, s, e0, e1));
+    HIP_CHECK(hipStreamSynchronize(s));
+    Column c;
+    c.type = st.col_type;
+    c.data = out->p;
+    c.cap_rows = t->n_rows;
+    c.owned.push_back(std::move(out));
+    if (validity) {
+        if (int rc = copy_validity(t, c, validity, 0)) return rc;
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    t->cols[col] = std::move(c);
+    drop_patches(t, col);
+    t->idx.erase(col);
+    t->bins.erase(col);
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_table_build_index(cubit_table* t, int col, int encoding, const int64_t* values, uint32_t n) {
     if (!t) return fail(CUBIT_ERR_INVALID, "null table");
     CUBIT_LOCK(t->ctx);

@@ -3702,6 +3702,73 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ RLE expand
+// DuckDB RLE segments (src/storage/compression/rle.cpp) expanded into a plain column. The host
+// has parsed every segment into runs — the run values (already widened to the column's type) and
+// each run's end row (exclusive, cumulative over the partition; zero-length runs, which the
+// reference writes after a run of exactly 65,535 rows, repeat the previous end). A workgroup owns
+// one 2,048-row tile: one lane finds the first run ending past the tile's start, the tile's runs
+// (at most 2,048 non-empty ones, plus empty ones between them) are staged in LDS a window at a
+// time, and every lane finds its rows' runs by binary search in LDS; the stores are coalesced.
+template <typename T>
+__global__ __launch_bounds__(256) void rle_expand_kernel(const T* __restrict__ vals, const uint64_t* __restrict__ ends,
+                                                         uint64_t n_runs, uint64_t n_rows, T* __restrict__ out) {
+    constexpr int TILE = 2048, WIN = 2048;
+    __shared__ uint64_t s_end[WIN];
+    __shared__ T s_val[WIN];
+    __shared__ uint64_t s_first;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    if (t0 >= n_rows) return;
+    const uint64_t t1 = t0 + TILE < n_rows ? t0 + TILE : n_rows;
+    if (threadIdx.x == 0) {  // first run whose end > t0
+        uint64_t lo = 0, hi = n_runs;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (ends[mid] > t0) hi = mid;
+            else lo = mid + 1;
+        }
+        s_first = lo;
+    }
+    __syncthreads();
+    uint64_t first = s_first;
+    uint64_t row = t0;  // rows [t0, row) are written
+    while (row < t1 && first < n_runs) {
+        const uint64_t cnt = n_runs - first < (uint64_t)WIN ? n_runs - first : (uint64_t)WIN;
+        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            s_end[i] = ends[first + i];
+            s_val[i] = vals[first + i];
+        }
+        __syncthreads();
+        const uint64_t covered = s_end[cnt - 1] < t1 ? s_end[cnt - 1] : t1;  // rows this window holds
+        for (uint64_t r = row + threadIdx.x; r < covered; r += blockDim.x) {
+            uint32_t lo = 0, hi = (uint32_t)cnt - 1;  // first staged run with end > r
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) / 2;
+                if (s_end[mid] > r) hi = mid;
+                else lo = mid + 1;
+            }
+            out[r] = s_val[lo];
+        }
+        row = covered;
+        first += cnt;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_rle_expand(const void* vals, const uint64_t* ends, uint64_t n_runs, uint64_t n_rows, int type,
+                             void* out, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+    if (n_rows == 0) return hipSuccess;
+    const uint64_t tiles = (n_rows + 2047) / 2048;
+    if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+    if (type == 0)
+        hipExtLaunchKernelGGL(rle_expand_kernel<int32_t>, dim3((unsigned)tiles), dim3(256), 0, stream, start, stop, 0,
+                              static_cast<const int32_t*>(vals), ends, n_runs, n_rows, static_cast<int32_t*>(out));
+    else
+        hipExtLaunchKernelGGL(rle_expand_kernel<int64_t>, dim3((unsigned)tiles), dim3(256), 0, stream, start, stop, 0,
+                              static_cast<const int64_t*>(vals), ends, n_runs, n_rows, static_cast<int64_t*>(out));
+    return hipGetLastError();
+}
+
 // A comparison (CUBIT_CMP_* or kCmpBetween) as the inclusive range [lo, hi] of passing values,
 // complemented when neg (!=); empty: lo > hi. clamp32 narrows it to INT32 values.
 struct CmpRange {

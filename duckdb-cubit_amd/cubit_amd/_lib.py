@@ -149,6 +149,7 @@ GPU_SIGNATURES = {
     "cubit_table_info": (C.c_int, [_P, C.POINTER(_U64), C.POINTER(_I64), C.POINTER(_P)]),
     "cubit_table_add_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _P, C.c_int]),
     "cubit_table_add_bitpacked_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _U64, _P, _P, _U32, _P]),
+    "cubit_table_add_rle_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _U64, _P, _P, _U32, _P]),
     "cubit_table_build_index": (C.c_int, [_P, C.c_int, C.c_int, _P, _U32]),
     "cubit_table_index_info": (C.c_int, [_P, C.c_int, C.POINTER(_U32), C.POINTER(_U64)]),
     "cubit_table_set_deletes": (C.c_int, [_P, _P, _P, _U64]),

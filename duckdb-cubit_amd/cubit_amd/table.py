@@ -273,6 +273,21 @@ class CubitTable:
                                                           vw.ctypes.data if vw is not None else None))
         self.types[col] = self.column_data(col)[1]
 
+    def add_rle_column(self, col: int, data: np.ndarray, seg_offsets: np.ndarray, seg_rows: np.ndarray,
+                       dtype, validity: Optional[np.ndarray] = None) -> None:
+        """A column given as DuckDB RLE segment images (uint8 bytes, per-segment byte offsets and
+        row counts); the runs are read on the host and expanded on the GPU. `dtype` and the column
+        held as for add_bitpacked_column."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        so = np.ascontiguousarray(seg_offsets, dtype=np.uint64)
+        sr = np.ascontiguousarray(seg_rows, dtype=np.uint64)
+        vw = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
+        typ = L.SEGMENT_TYPES[np.dtype(dtype).name]
+        L.check(self.lib.cubit_table_add_rle_column(self.handle, col, typ, data.ctypes.data if data.size else None,
+                                                    data.nbytes, so.ctypes.data, sr.ctypes.data, len(so),
+                                                    vw.ctypes.data if vw is not None else None))
+        self.types[col] = self.column_data(col)[1]
+
     def add_string_column(self, col: int, values, dictionary: Optional[Dictionary] = None) -> Dictionary:
         """Register a VARCHAR column from a list of str / bytes / None (NULL): encoded against
         `dictionary` (default: one built from the values) and held as int32 codes."""

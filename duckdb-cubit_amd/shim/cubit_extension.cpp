@@ -1320,10 +1320,13 @@ static int SegmentType(PhysicalType t) {
 // "[c]" is the values, "[c, 0]" the validity, segment_start an absolute row) and are read from
 // the row-data block manager (TableIOManager::GetBlockManagerForRowData, table_io_manager.hpp:30;
 // BlockManager::RegisterBlock, block_manager.hpp:83; BufferManager::Pin, buffer_manager.hpp:41)
-// at their block offset. A segment's first 8 bytes are the end of its metadata, i.e. its size
-// (BitpackingCompressState::FlushSegment). Deleted rows stay in the segments (visibility is the
+// at their block offset. A BITPACKING segment's first 8 bytes are the end of its metadata, i.e.
+// its size (BitpackingCompressState::FlushSegment); an RLE segment's are the offset of its run
+// lengths, which end it (RLECompressState::FlushSegment, rle.cpp:190-205). A column whose
+// segments are all BITPACKING or all RLE is taken from them; mixed codecs (or CONSTANT
+// segments) use the snapshot's values. Deleted rows stay in the segments (visibility is the
 // partition's delete list); updates make has_updates true and keep this path off.
-static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalType ptype, uint64_t n_rows,
+static bool AttachSegmentColumn(DuckTableEntry &entry, column_t col, PhysicalType ptype, uint64_t n_rows,
                                   cubit_table *t, const uint64_t *validity) {
     const int seg_type = SegmentType(ptype);
     if (seg_type < 0 || n_rows == 0) {
@@ -1332,6 +1335,7 @@ static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalT
     auto &storage = entry.GetStorage();
     const string path = "[" + to_string(col) + "]";
     const string bitpacking = CompressionTypeToString(CompressionType::COMPRESSION_BITPACKING);
+    const string rle = CompressionTypeToString(CompressionType::COMPRESSION_RLE);
     vector<ColumnSegmentInfo> segs;
     for (auto &info : storage.GetColumnSegmentInfo()) {
         if (info.column_id == col && info.column_path == path) {
@@ -1341,9 +1345,14 @@ static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalT
     std::sort(segs.begin(), segs.end(), [](const ColumnSegmentInfo &a, const ColumnSegmentInfo &b) {
         return a.segment_start < b.segment_start;
     });
+    // every segment of one codec: BITPACKING (unpacked on the GPU) or RLE (runs expanded on the GPU)
+    const string codec = segs.empty() ? bitpacking : segs[0].compression_type;
+    if (codec != bitpacking && codec != rle) {
+        return false;
+    }
     uint64_t next = 0;
     for (auto &sg : segs) {
-        if (!sg.persistent || sg.has_updates || sg.compression_type != bitpacking || sg.segment_start != next) {
+        if (!sg.persistent || sg.has_updates || sg.compression_type != codec || sg.segment_start != next) {
             return false;
         }
         next += sg.segment_count;
@@ -1358,10 +1367,23 @@ static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalT
         auto handle = block_manager.RegisterBlock(sg.block_id);
         auto pin = block_manager.buffer_manager.Pin(handle);
         const_data_ptr_t p = pin.Ptr() + sg.block_offset;
+        const uint64_t room = block_manager.GetBlockSize() - sg.block_offset;
         uint64_t size = 0;
-        memcpy(&size, p, sizeof(size));
-        if (size < 8 || sg.block_offset + size > block_manager.GetBlockSize()) {
-            return false;  // not a BITPACKING segment header
+        memcpy(&size, p, sizeof(size));  // BITPACKING: the segment's size; RLE: where its run lengths start
+        if (size < 8 || size > room) {
+            return false;  // not a segment header
+        }
+        if (codec == rle) {  // the run lengths end the segment: read them until they cover its rows
+            uint64_t covered = 0, k = 0;
+            while (covered < sg.segment_count) {
+                if (size + 2 * (k + 1) > room) {
+                    return false;
+                }
+                uint16_t len;
+                memcpy(&len, p + size + 2 * k++, 2);
+                covered += len;
+            }
+            size += 2 * k;
         }
         const uint64_t at = (bytes.size() + 7) / 8 * 8;
         bytes.resize(at + size, 0);
@@ -1369,8 +1391,9 @@ static bool AttachBitpackedColumn(DuckTableEntry &entry, column_t col, PhysicalT
         offsets.push_back(at);
         rows.push_back(sg.segment_count);
     }
-    return cubit_table_add_bitpacked_column(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(),
-                                            rows.data(), (uint32_t)segs.size(), validity) == CUBIT_OK;
+    auto add = codec == rle ? cubit_table_add_rle_column : cubit_table_add_bitpacked_column;
+    return add(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(), rows.data(), (uint32_t)segs.size(),
+               validity) == CUBIT_OK;
 }
 
 // The column as registered against the snapshot's values on a sample (the valid rows of a
@@ -1419,7 +1442,7 @@ static bool SampleMatches(cubit_ctx *ctx, cubit_table *t, column_t col, const ve
 // contiguous range per context (boundaries on row groups of 122,880 rows = 1,920 bitvector words,
 // so every partition's validity words are the snapshot's own), partition i on the contexts' i-th.
 // With `entry` and one partition, a column held in persistent BITPACKING segments is registered
-// from them (AttachBitpackedColumn). Every partition gets the same indexes (the
+// from them (AttachSegmentColumn). Every partition gets the same indexes (the
 // every-distinct-value default decided over the whole snapshot). The set is not visible to scans
 // until the caller swaps it in.
 static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached, const CubitSnapshot &snap,
@@ -1458,7 +1481,7 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
             }
             const bool from_segments =
                 !DictPhysical(attached.columns[col]) && entry && n_parts == 1 &&
-                AttachBitpackedColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
+                AttachSegmentColumn(*entry, col, attached.columns[col], snap.rows, t, valid) &&
                 SampleMatches(ctxs[p], t, col, snap.values[c], snap.validity[c], snap.rows);
             if (!from_segments && !DictPhysical(attached.columns[col])) {
                 // (re-)registering replaces a column taken from segments

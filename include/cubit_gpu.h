@@ -424,6 +424,19 @@ int cubit_table_column_changed(cubit_table *t, int col);
 int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
                                      const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
                                      const uint64_t *validity);
+/* Register a column given as DuckDB RLE segments (src/storage/compression/rle.cpp, the
+ * reference's run-length codec for numeric columns): segment i at seg_offsets[i] with seg_rows[i]
+ * rows, each as RLECompressState::FlushSegment writes it (8-byte header = offset of the uint16
+ * run lengths, the run values as T from byte 8, the lengths after them; runs of at most 65,535
+ * rows, zero-length runs allowed); the segments cover the partition in row order. The host reads
+ * the runs (a segment whose runs do not cover its rows is refused before anything is launched),
+ * only the runs cross to the device, and the GPU expands them into the column. `type` and the
+ * column held are as for cubit_table_add_bitpacked_column; NULLs come from `validity` (a NULL
+ * row's run value is whatever run it fell in, as in the reference). With timing on, the expand
+ * kernel is a timed launch. */
+int cubit_table_add_rle_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
+                               const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
+                               const uint64_t *validity);
 /* A column registered with cubit_table_add_bitpacked_column keeps its segments on the device:
  * a constant comparison the index cannot answer (K0) then unpacks and compares in one pass over
  * the packed bytes (w/8 bytes per row — the reference's ColumnSegment::Scan →

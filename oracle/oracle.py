@@ -441,3 +441,86 @@ def bp_group_modes(col: BitpackedColumn):
     k = lib().oracle_bp_group_modes(col.data.ctypes.data, col.seg_off.ctypes.data, col.seg_count.ctypes.data,
                                     len(col.seg_off), m.ctypes.data, cap)
     return [BP_MODE_NAMES.get(int(x), "invalid") for x in m[:k]]
+
+
+# ------------------------------------------------------------------ RLE segments (rle.cpp)
+RLE_MAX_COUNT = 65535  # NumericLimits<rle_count_t>::Maximum(), rle_count_t = uint16_t (rle.cpp:13)
+
+
+def rle_compress(values, valid=None, block_size: int = 262144, row_group: int = 122880):
+    """DuckDB's RLE compressor restated (src/storage/compression/rle.cpp): one RLECompressState per
+    row group (a column checkpoint), RLEState::Update (:45-78) — a NULL row only lengthens the
+    current run (leading NULLs join the first valid value's run), a run reaching 65,535 rows is
+    written and the next entry starts at 0, so a run of a multiple of 65,535 rows leaves a
+    zero-length entry behind; NULL-only runs carry NullValue<T> (numeric_limits<T>::min) —
+    WriteValue (:166-188: a segment holds at most (block_size - 8) / (sizeof(T) + 2) entries) and
+    FlushSegment (:190-205: the run lengths moved next to the values at AlignValue(8 + n·sizeof(T)),
+    that offset in the 8-byte header). Returns (bytes uint8, segment offsets, segment row counts),
+    segments 8-aligned and back to back."""
+    v = np.ascontiguousarray(values)
+    dt = v.dtype
+    assert dt.kind in "iu", dt
+    n = len(v)
+    ok = np.ones(n, bool) if valid is None else np.asarray(valid, bool)
+    null_value = np.iinfo(dt).min
+    max_entries = (block_size - 8) // (dt.itemsize + 2)
+    segs = []
+    for g0 in range(0, n, row_group):
+        gv, gok = v[g0:g0 + row_group], ok[g0:g0 + row_group]
+        m = len(gv)
+        entries = []  # (value, count) in write order
+        first = int(np.argmax(gok)) if gok.any() else m
+        for _ in range(first // RLE_MAX_COUNT):  # leading NULLs reaching the limit: written as NullValue
+            entries.append((null_value, RLE_MAX_COUNT))
+        lead = first % RLE_MAX_COUNT
+        if first == m:
+            entries.append((null_value, lead))  # Finalize flushes the NULL-only run, even when empty
+        else:
+            # the value each row's run carries: the last valid value at or before it
+            idx = np.where(gok, np.arange(m), 0)
+            np.maximum.accumulate(idx, out=idx)
+            filled = gv[idx[first:]]
+            starts = np.flatnonzero(np.concatenate([[True], filled[1:] != filled[:-1]]))
+            lens = np.diff(np.concatenate([starts, [len(filled)]]))
+            lens[0] += lead
+            for s0, L in zip(starts.tolist(), lens.tolist()):
+                val = filled[s0]
+                entries += [(val, RLE_MAX_COUNT)] * (L // RLE_MAX_COUNT)
+                entries.append((val, L % RLE_MAX_COUNT))  # 0 after a multiple of the limit
+        for c0 in range(0, len(entries), max_entries):
+            chunk = entries[c0:c0 + max_entries]
+            k = len(chunk)
+            off = (8 + dt.itemsize * k + 7) // 8 * 8
+            seg = bytearray(off + 2 * k)
+            seg[:8] = int(off).to_bytes(8, "little")
+            seg[8:8 + dt.itemsize * k] = np.array([e[0] for e in chunk], dtype=dt.newbyteorder("<")).tobytes()
+            seg[off:] = np.array([e[1] for e in chunk], dtype="<u2").tobytes()
+            segs.append((bytes(seg), sum(e[1] for e in chunk)))
+    offs, data = [], bytearray()
+    for seg, _ in segs:
+        data += bytes((-len(data)) % 8)
+        offs.append(len(data))
+        data += seg
+    return (np.frombuffer(bytes(data) or b"\0", dtype=np.uint8).copy(), np.array(offs, np.uint64),
+            np.array([r for _, r in segs], np.uint64))
+
+
+def rle_decode(data, seg_offsets, seg_rows, dtype) -> np.ndarray:
+    """RLEScanState restated (rle.cpp:248-277, RLEScanPartial :335-380): from each segment's
+    header offset, run lengths are read until they cover the segment's rows, each run's value
+    repeated; the values as T."""
+    dt = np.dtype(dtype)
+    b = np.asarray(data, np.uint8).tobytes()
+    out = []
+    for o, rows in zip(np.asarray(seg_offsets).tolist(), np.asarray(seg_rows).tolist()):
+        off = int.from_bytes(b[o:o + 8], "little")
+        vals, lens, covered, k = [], [], 0, 0
+        while covered < rows:
+            L = int.from_bytes(b[o + off + 2 * k:o + off + 2 * k + 2], "little")
+            vals.append(np.frombuffer(b, dtype=dt.newbyteorder("<"), count=1, offset=o + 8 + k * dt.itemsize)[0])
+            lens.append(L)
+            covered += L
+            k += 1
+        assert covered == rows
+        out.append(np.repeat(np.array(vals, dtype=dt), lens))
+    return np.concatenate(out) if out else np.zeros(0, dt)
