@@ -1963,10 +1963,12 @@ extern "C" int cubit_table_add_rle_column(cubit_table* t, int col, int type, con
     const uint64_t esz = wide ? 8 : 4;
     std::vector<int32_t> narrow;
     if (!wide) narrow.assign(vals.begin(), vals.end());
-    DevBuf d_vals, d_ends;
+    DevBuf d_vals, d_ends, d_tiles;
     auto out = std::make_unique<DevBuf>();
+    const uint64_t n_tiles = (t->n_rows + 2047) / 2048;
     if (hipMalloc(&d_vals.p, std::max<uint64_t>(vals.size() * esz, 16)) != hipSuccess ||
         hipMalloc(&d_ends.p, std::max<uint64_t>(ends.size() * 8, 16)) != hipSuccess ||
+        hipMalloc(&d_tiles.p, (n_tiles + 1) * 8) != hipSuccess ||
         hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess)
         return fail(CUBIT_ERR_OOM, "RLE column allocation failed");
     if (!vals.empty()) {
@@ -1977,7 +1979,7 @@ extern "C" int cubit_table_add_rle_column(cubit_table* t, int col, int type, con
     hipEvent_t e0, e1;
     if (int rc = timing_events(t->ctx, e0, e1)) return rc;
     HIP_CHECK(launch_rle_expand(d_vals.p, static_cast<const uint64_t*>(d_ends.p), ends.size(), t->n_rows, wide ? 1 : 0,
-                                out->p, s, e0, e1));
+                                static_cast<uint64_t*>(d_tiles.p), out->p, s, e0, e1));
     HIP_CHECK(hipStreamSynchronize(s));
     Column c;
     c.type = st.col_type;

@@ -225,9 +225,10 @@ struct BpGroup {
 hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
                             hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // DuckDB RLE segments parsed into runs (values of the column's type, cumulative exclusive run
-// ends) expanded into the column (type 0: INT32, else INT64)
+// ends) expanded into the column (type 0: INT32, else INT64); tile_first: scratch of
+// (n_rows + 2047) / 2048 + 1 words
 hipError_t launch_rle_expand(const void* vals, const uint64_t* ends, uint64_t n_runs, uint64_t n_rows, int type,
-                             void* out, hipStream_t stream, hipEvent_t start, hipEvent_t stop);
+                             uint64_t* tile_first, void* out, hipStream_t stream, hipEvent_t start, hipEvent_t stop);
 // K5 + K0 fused: {valid rows whose value cmp constant} straight from the BITPACKING groups
 // (cmp = CUBIT_CMP_* or kCmpBetween); out must be zero (words shared by two groups are OR-ed)
 // simple_width > 0: every group is FOR of ≤ 32 bits, CONSTANT or CONSTANT_DELTA, and the widest

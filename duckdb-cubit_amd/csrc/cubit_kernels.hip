@@ -3706,66 +3706,137 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
 // DuckDB RLE segments (src/storage/compression/rle.cpp) expanded into a plain column. The host
 // has parsed every segment into runs — the run values (already widened to the column's type) and
 // each run's end row (exclusive, cumulative over the partition; zero-length runs, which the
-// reference writes after a run of exactly 65,535 rows, repeat the previous end). A workgroup owns
-// one 2,048-row tile: one lane finds the first run ending past the tile's start, the tile's runs
-// (at most 2,048 non-empty ones, plus empty ones between them) are staged in LDS a window at a
-// time, and every lane finds its rows' runs by binary search in LDS; the stores are coalesced.
+// reference writes after a run of exactly 65,535 rows, repeat the previous end). Workgroups take
+// 2,048-row tiles in turn; a tile's runs, from its first row's through its last row's, are known
+// beforehand (rle_tile_first_kernel, a lane per tile). A tile inside one run or across one
+// boundary is filled straight from those two runs; otherwise its runs are staged in LDS and each
+// lane finds the run of its first of 8 consecutive rows by binary search and walks on from it.
+// Every lane writes its 8 rows as 16-byte stores.
+// tile_first[b] = the first run ending past row 2,048·b (b = 0 … tiles; n_runs past the end): one
+// lane per tile, so the dependent loads of the searches overlap across the whole grid
+__global__ __launch_bounds__(256) void rle_tile_first_kernel(const uint64_t* __restrict__ ends, uint64_t n_runs,
+                                                             uint64_t n_tiles, uint64_t* __restrict__ tile_first) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > n_tiles) return;
+    const uint64_t r = b * 2048;
+    uint64_t lo = 0, hi = n_runs;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (ends[mid] > r) hi = mid;
+        else lo = mid + 1;
+    }
+    tile_first[b] = lo;
+}
+
+template <typename T, int PER>
+__device__ __forceinline__ void rle_store(T* __restrict__ out, uint64_t r0, uint64_t t1, const T (&v)[PER]) {
+    if (r0 + PER <= t1) {  // 32 / 64 contiguous bytes per lane, 16-byte stores
+        using V = __attribute__((ext_vector_type(4))) uint32_t;
+        V* o = reinterpret_cast<V*>(out + r0);
+#pragma unroll
+        for (int q = 0; q < (int)(PER * sizeof(T) / 16); ++q) {
+            V w;
+            __builtin_memcpy(&w, reinterpret_cast<const char*>(v) + 16 * q, 16);
+            o[q] = w;
+        }
+    } else {
+        for (int k = 0; k < PER && r0 + k < t1; ++k) out[r0 + k] = v[k];
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rle_expand_kernel(const T* __restrict__ vals, const uint64_t* __restrict__ ends,
-                                                         uint64_t n_runs, uint64_t n_rows, T* __restrict__ out) {
-    constexpr int TILE = 2048, WIN = 2048;
+                                                         const uint64_t* __restrict__ tile_first, uint64_t n_runs,
+                                                         uint64_t n_rows, T* __restrict__ out) {
+    constexpr int TILE = 2048, PER = 8, WIN = 2064;  // a tile holds at most 2,048 non-empty runs (+ one empty)
     __shared__ uint64_t s_end[WIN];
     __shared__ T s_val[WIN];
-    __shared__ uint64_t s_first;
-    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-    if (t0 >= n_rows) return;
-    const uint64_t t1 = t0 + TILE < n_rows ? t0 + TILE : n_rows;
-    if (threadIdx.x == 0) {  // first run whose end > t0
-        uint64_t lo = 0, hi = n_runs;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) / 2;
-            if (ends[mid] > t0) hi = mid;
-            else lo = mid + 1;
+    const uint64_t n_tiles = (n_rows + TILE - 1) / TILE;
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // tile-uniform control flow
+        const uint64_t t0 = tile * TILE;
+        const uint64_t t1 = t0 + TILE < n_rows ? t0 + TILE : n_rows;
+        const uint64_t r0 = t0 + (uint64_t)threadIdx.x * PER;
+        // the tile's runs: from the first ending past t0 through the first ending past t1 (one
+        // more than needed when a run ends at t1 exactly), within the partition's runs
+        const uint64_t first = tile_first[tile];
+        const uint64_t stop = tile_first[tile + 1] < n_runs ? tile_first[tile + 1] + 1 : n_runs;
+        const uint64_t cnt = stop - first;
+        T v[PER];
+        if (cnt <= 2) {  // inside one run or across one boundary (long runs): no staging
+            const uint64_t e0 = ends[first];
+            const T a = vals[first], b = cnt == 2 ? vals[first + 1] : a;
+#pragma unroll
+            for (int k = 0; k < PER; ++k) v[k] = r0 + k < e0 ? a : b;
+            if (r0 < t1) rle_store<T, PER>(out, r0, t1, v);
+            continue;
         }
-        s_first = lo;
-    }
-    __syncthreads();
-    uint64_t first = s_first;
-    uint64_t row = t0;  // rows [t0, row) are written
-    while (row < t1 && first < n_runs) {
-        const uint64_t cnt = n_runs - first < (uint64_t)WIN ? n_runs - first : (uint64_t)WIN;
-        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-            s_end[i] = ends[first + i];
-            s_val[i] = vals[first + i];
-        }
-        __syncthreads();
-        const uint64_t covered = s_end[cnt - 1] < t1 ? s_end[cnt - 1] : t1;  // rows this window holds
-        for (uint64_t r = row + threadIdx.x; r < covered; r += blockDim.x) {
-            uint32_t lo = 0, hi = (uint32_t)cnt - 1;  // first staged run with end > r
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) / 2;
-                if (s_end[mid] > r) hi = mid;
-                else lo = mid + 1;
+        if (cnt <= (uint64_t)WIN) {
+            // the tile's runs in LDS; each lane expands 8 consecutive rows: one search, then a walk
+            for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+                s_end[i] = ends[first + i];
+                s_val[i] = vals[first + i];
             }
-            out[r] = s_val[lo];
+            __syncthreads();
+            if (r0 < t1) {
+                uint32_t lo = 0, hi = (uint32_t)cnt - 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) / 2;
+                    if (s_end[mid] > r0) hi = mid;
+                    else lo = mid + 1;
+                }
+#pragma unroll
+                for (int k = 0; k < PER; ++k) {
+                    while (lo + 1 < cnt && s_end[lo] <= r0 + k) ++lo;
+                    v[k] = s_val[lo];
+                }
+                rle_store<T, PER>(out, r0, t1, v);
+            }
+            __syncthreads();  // the LDS is the next tile's
+            continue;
         }
-        row = covered;
-        first += cnt;
-        __syncthreads();
+        // more runs than the window (not produced by DuckDB's writer): windows of runs in turn
+        uint64_t f = first, row = t0;
+        while (row < t1 && f < n_runs) {
+            const uint64_t c = n_runs - f < (uint64_t)WIN ? n_runs - f : (uint64_t)WIN;
+            for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+                s_end[i] = ends[f + i];
+                s_val[i] = vals[f + i];
+            }
+            __syncthreads();
+            const uint64_t covered = s_end[c - 1] < t1 ? s_end[c - 1] : t1;
+            for (uint64_t r = row + threadIdx.x; r < covered; r += blockDim.x) {
+                uint32_t lo = 0, hi = (uint32_t)c - 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) / 2;
+                    if (s_end[mid] > r) hi = mid;
+                    else lo = mid + 1;
+                }
+                out[r] = s_val[lo];
+            }
+            row = covered;
+            f += c;
+            __syncthreads();
+        }
     }
 }
 
 hipError_t launch_rle_expand(const void* vals, const uint64_t* ends, uint64_t n_runs, uint64_t n_rows, int type,
-                             void* out, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+                             uint64_t* tile_first, void* out, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
     if (n_rows == 0) return hipSuccess;
     const uint64_t tiles = (n_rows + 2047) / 2048;
     if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+    // timed from the first kernel's start to the second's end
+    hipExtLaunchKernelGGL(rle_tile_first_kernel, dim3((unsigned)((tiles + 1 + 255) / 256)), dim3(256), 0, stream, start,
+                          nullptr, 0, ends, n_runs, tiles, tile_first);
+    const unsigned grid = (unsigned)std::min<uint64_t>(tiles, 256 * 16);  // 16 workgroups per CU, tiles in turn
     if (type == 0)
-        hipExtLaunchKernelGGL(rle_expand_kernel<int32_t>, dim3((unsigned)tiles), dim3(256), 0, stream, start, stop, 0,
-                              static_cast<const int32_t*>(vals), ends, n_runs, n_rows, static_cast<int32_t*>(out));
+        hipExtLaunchKernelGGL(rle_expand_kernel<int32_t>, dim3(grid), dim3(256), 0, stream, nullptr, stop, 0,
+                              static_cast<const int32_t*>(vals), ends, tile_first, n_runs, n_rows,
+                              static_cast<int32_t*>(out));
     else
-        hipExtLaunchKernelGGL(rle_expand_kernel<int64_t>, dim3((unsigned)tiles), dim3(256), 0, stream, start, stop, 0,
-                              static_cast<const int64_t*>(vals), ends, n_runs, n_rows, static_cast<int64_t*>(out));
+        hipExtLaunchKernelGGL(rle_expand_kernel<int64_t>, dim3(grid), dim3(256), 0, stream, nullptr, stop, 0,
+                              static_cast<const int64_t*>(vals), ends, tile_first, n_runs, n_rows,
+                              static_cast<int64_t*>(out));
     return hipGetLastError();
 }
 
