@@ -90,11 +90,22 @@ def round_(ctx, seed, n, with_updates):
         valid = rng.random(n) > (0.12 if c != 1 else 0.0)
         vw = validity_from_mask(valid) if c != 1 else None
         if c == 3:
-            # any integral type DuckDB holds, registered plain (widened on the device) or as
-            # BITPACKING segments under a random forced mode, the packed filter on or off
+            # any integral type DuckDB holds, registered plain (widened on the device), as
+            # BITPACKING segments under a random forced mode (the packed filter on or off), or as
+            # RLE segments
             dt = np.dtype(rng.choice(["int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64"]))
             typed = d.astype(dt)
-            if rng.random() < 0.5:
+            codec = rng.random()
+            if codec < 0.25:
+                # RLE segments (the restated compressor over runs of 1-15 rows; runs long enough to
+                # matter), expanded on the device
+                m = n // 4 + 1
+                typed = np.repeat(rng.integers(0, 50, m), rng.integers(1, 16, m))[:n].astype(dt)
+                if len(typed) < n:
+                    typed = np.concatenate([typed, np.zeros(n - len(typed), dt)])
+                data_b, offs, rows = O.rle_compress(typed, valid)
+                t.add_rle_column(c, data_b, offs, rows, dt, validity=vw)
+            elif codec < 0.6:
                 c3 = O.bp_compress(typed, valid.astype(np.uint8), str(rng.choice(["auto", "for", "delta_for"])))
                 if c3 is None:
                     c3 = O.bp_compress(typed, valid.astype(np.uint8), "auto")
