@@ -119,6 +119,31 @@ def main():
             {"after": "con1 COMMIT", "expect": {"con1": 2, "con2": 1}},
         ],
     }
+    # test/sql/storage/compression/rle/*.test: tables whose INTEGER columns DuckDB stores as RLE
+    # segments after the CHECKPOINT, as (value, repeat) runs in row order (null = NULL), a pushed
+    # filter per query ([column, op, constant] or null) and its aggregates as the files state them
+    # (sum / min / max / count of the integer column, count_star, min_id / max_id)
+    rle = {
+        "rle_filter_pushdown": {
+            "source": "test/sql/storage/compression/rle/rle_filter_pushdown.test:12-33",
+            "id": "VARCHAR", "col": [[1, 5000], [2, 5000]],
+            "queries": [{"where": ["col", "=", 2], "expect": {"sum": 10000, "min": 2, "max": 2, "count_star": 5000}},
+                        {"where": ["id", "=", "5000"],
+                         "expect": {"min_id": "5000", "max_id": "5000", "sum": 2, "min": 2, "max": 2, "count_star": 1}}]},
+        "rle_index_fetch": {
+            "source": "test/sql/storage/compression/rle/rle_index_fetch.test:12-31",
+            "id": "INTEGER", "col": [[1, 5000], [2, 5000]],
+            "queries": [{"where": ["id", "=", 5000],
+                         "expect": {"min_id": 5000, "max_id": 5000, "sum": 2, "min": 2, "max": 2, "count_star": 1}}]},
+        "rle_medium": {
+            "source": "test/sql/storage/compression/rle/rle_medium.test:13-33",
+            "id": None, "col": [[k, 1000] for k in range(1, 7)],
+            "queries": [{"where": None, "expect": {"sum": 21000, "min": 1, "max": 6, "count_star": 6000}}]},
+        "rle_nulls_edge_case": {
+            "source": "test/sql/storage/compression/rle/rle_nulls_edge_case.test:21-44",
+            "id": None, "col": [[None, 65535], [1, 1], [2, 1], [3, 1]],
+            "queries": [{"where": None, "expect": {"min": 1, "max": 3, "count_star": 65538, "count": 3}}]},
+    }
     # test/optimizer/pushdown/timestamp_to_date_pushdown.test: t1(ts TIMESTAMP, i INT) as runs of
     # (timestamp, i from generate_series(lo, hi)); `ts::date == d` is pushed to the scan as the
     # TIMESTAMP range [d 00:00, d + 1 day) (the file checks the plan keeps a SEQ_SCAN filter and no
@@ -398,7 +423,7 @@ def main():
         "test/sql/update/test_string_update_many_strings.test", "test/sql/update/test_repeated_string_update.test",
         "test/sql/update/test_update_same_string_value.test")}
     (OUT / "reference_cases.json").write_text(json.dumps({"null_updates": nu, "mvcc_scripts": mvcc, "string_mvcc_scripts": smvcc, "transitive_filters": tf, "zonemap_segment": zm, "interleaved_versions": iv,
-                                                          "timestamp_date_pushdown": tsd,
+                                                          "timestamp_date_pushdown": tsd, "rle_cases": rle,
                                                           "table_or_pushdown": orp, "update": upd,
                                                           "table_filter_pushdown": tfp, "multi_version": mv,
                                                           "concurrent_reads_while_updating": cr,

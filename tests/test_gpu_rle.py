@@ -110,3 +110,43 @@ def test_malformed_segments_are_refused(ctx):
     t.add_rle_column(0, data, offs, rows, np.int64)
     assert np.array_equal(t.download_column(0), v)
     t.close()
+
+
+@pytest.mark.parametrize("encoding", [None, L.INDEX_RANGE, L.INDEX_EQUALITY])
+def test_reference_rle_cases(ctx, encoding):
+    """The reference's RLE .test cases (rle_filter_pushdown, rle_index_fetch, rle_medium,
+    rle_nulls_edge_case): the INTEGER column registered from RLE segments, the id column beside it
+    (INTEGER, or VARCHAR as dictionary codes), every query's pushed filter on the GPU and its
+    aggregates over the probed values = the file's results."""
+    from test_oracle_rle import rle_case_aggregates, rle_case_filters, rle_case_table
+
+    cases = json.loads((Path(__file__).resolve().parent / "golden" / "reference_cases.json").read_text())["rle_cases"]
+    for name, case in cases.items():
+        vals, ok, ids = rle_case_table(case)
+        data, offs, rows = O.rle_compress(vals, ok)
+        t = CubitTable(ctx, len(vals))
+        t.add_rle_column(0, data, offs, rows, np.int32, None if ok.all() else validity_from_mask(ok))
+        id_is_str = case["id"] == "VARCHAR"
+        d = None
+        if ids is not None:
+            if id_is_str:
+                d = t.add_string_column(1, ids)
+            else:
+                t.add_column(1, ids)
+        if encoding is not None:
+            t.build_index(0, encoding)
+        for q in case["queries"]:
+            fl = rle_case_filters(q, id_is_str)
+            fs = F.TableFilterSet({c: F.ConstantFilter(op, k) for c, (op, k) in (fl or {}).items()})
+            got = t.scan(fs)
+            v, vok = t.fetch(0, got)
+            gv = np.zeros(len(vals), np.int32)
+            gok = np.zeros(len(vals), bool)
+            gv[got], gok[got] = v, vok
+            gid = None
+            if ids is not None:
+                iv, _ = t.fetch(1, got)
+                gid = {r: (d.entry(c) if id_is_str else int(c)) for r, c in zip(got.tolist(), iv.tolist())}
+            agg = rle_case_aggregates(got, gv, gok, gid, id_is_str)
+            assert {k: agg.get(k) for k in q["expect"]} == q["expect"], (name, q, encoding)
+        t.close()

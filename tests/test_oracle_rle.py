@@ -83,3 +83,78 @@ def test_zero_length_entries_and_segment_splits():
     data, offs, rows = O.rle_compress(w, block_size=8 + 10 * 100)  # 100 entries per segment
     assert len(offs) == 10 and rows.tolist() == [100] * 10
     assert np.array_equal(O.rle_decode(data, offs, rows, np.int64), w)
+
+
+# ---- the reference's RLE .test cases (tests/golden/reference_cases.json "rle_cases") ------------
+def rle_case_table(case):
+    """(col INT32 values, col valid, id values or None): the case's runs; id as the inserts make it
+    (range(10,000) as INTEGER or as VARCHAR strings)."""
+    vals = np.concatenate([np.full(k, 0 if v is None else v, np.int32) for v, k in case["col"]])
+    ok = np.concatenate([np.full(k, v is not None) for v, k in case["col"]])
+    ids = None
+    if case["id"] == "INTEGER":
+        ids = np.arange(len(vals), dtype=np.int32)
+    elif case["id"] == "VARCHAR":
+        ids = [str(i).encode() for i in range(len(vals))]
+    return vals, ok, ids
+
+
+def rle_case_aggregates(rows, vals, ok, ids, id_is_str):
+    """The aggregates the files select, over the rows a query kept."""
+    out = {"count_star": len(rows)}
+    v = vals[rows][ok[rows]]
+    if len(v):
+        out.update(sum=int(v.astype(np.int64).sum()), min=int(v.min()), max=int(v.max()))
+    out["count"] = len(v)
+    if ids is not None and len(rows):
+        sel = [ids[r] for r in rows.tolist()]
+        lo, hi = min(sel), max(sel)
+        out.update(min_id=lo.decode() if id_is_str else int(lo), max_id=hi.decode() if id_is_str else int(hi))
+    return out
+
+
+def rle_case_filters(q, id_is_str):
+    """The query's pushed filter over (col = column 0, id = column 1)."""
+    if q["where"] is None:
+        return None
+    name, op, c = q["where"]
+    if name == "id" and id_is_str:
+        c = str(c).encode()
+    return {0 if name == "col" else 1: ("=", c) if op == "=" else (op, c)}
+
+
+@pytest.fixture(scope="module")
+def rle_cases():
+    g = json.loads((Path(__file__).resolve().parent / "golden" / "reference_cases.json").read_text())
+    return g["rle_cases"]
+
+
+def test_reference_rle_cases_on_the_oracle(rle_cases):
+    """Each case's INTEGER column written as RLE segments by the restated compressor and read back
+    by the restated decoder, then every query's pushed filter and aggregates against the file's
+    results (rle_nulls_edge_case: 65,535 leading NULLs — the run-length limit — then 1, 2, 3)."""
+    from cubit_amd import filters as F
+    from cubit_amd.datagen import validity_from_mask
+
+    for name, case in rle_cases.items():
+        vals, ok, ids = rle_case_table(case)
+        data, offs, rows = O.rle_compress(vals, ok)
+        dec = O.rle_decode(data, offs, rows, np.int32)
+        assert np.array_equal(dec[ok], vals[ok]), name
+        id_is_str = case["id"] == "VARCHAR"
+        cols = [O.Column(dec, None if ok.all() else validity_from_mask(ok))]
+        if ids is not None:
+            cols.append(O.StringColumn(ids) if id_is_str else O.Column(ids))
+        for q in case["queries"]:
+            fl = rle_case_filters(q, id_is_str)
+            fs = F.TableFilterSet({c: F.ConstantFilter(op, k) for c, (op, k) in (fl or {}).items()})
+            got_rows = O.table_scan(cols, F.serialize(fs), len(vals))
+            agg = rle_case_aggregates(got_rows, dec, ok, ids, id_is_str)
+            assert {k: agg.get(k) for k in q["expect"]} == q["expect"], (name, q)
+    # the edge case's segment: the NULL run at the limit, then one entry per value
+    vals, ok, _ = rle_case_table(rle_cases["rle_nulls_edge_case"])
+    data, offs, rows = O.rle_compress(vals, ok)
+    b = data.tobytes()
+    off = int.from_bytes(b[:8], "little")
+    assert np.frombuffer(b[off:], "<u2").tolist() == [65535, 1, 1, 1]
+    assert np.frombuffer(b[8:8 + 16], "<i4").tolist() == [np.iinfo(np.int32).min, 1, 2, 3]
