@@ -1764,6 +1764,65 @@ bool seg_type_of(int type, SegType& st) {
     }
 }
 
+// The groups of one BITPACKING segment (at byte `base`, `rows` rows from partition row `row`):
+// each group's mode, header fields and packed words, bounds-checked; packed runs off the 4-byte
+// alignment are copied behind the bytes (`moved`, at bytes_padded + …).
+int parse_bp_segment(const uint8_t* bytes, uint64_t n_bytes, uint64_t base, uint64_t rows, uint64_t row,
+                     const SegType& st, uint64_t bytes_padded, std::vector<BpGroup>& groups,
+                     std::vector<uint8_t>& moved, uint32_t sg) {
+    const uint64_t tsz = st.tsz;
+    if (base % 8 || base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
+    uint64_t meta_end;
+    std::memcpy(&meta_end, bytes + base, 8);
+    const uint64_t n_groups = (rows + 2047) / 2048;
+    if (meta_end > n_bytes - base || meta_end < 8 + 4 * n_groups)
+        return fail(CUBIT_ERR_INVALID, "segment %u: bad metadata offset", sg);
+    for (uint64_t g = 0; g < n_groups; ++g) {
+        uint32_t enc;
+        std::memcpy(&enc, bytes + base + meta_end - 4 * (g + 1), 4);
+        BpGroup bg{};
+        const uint32_t mode = enc >> 24;
+        const uint64_t data_off = base + (enc & 0x00ffffffu);
+        bg.mode = (uint8_t)mode;
+        bg.tnorm = st.tnorm;
+        bg.row_start = row + g * 2048;
+        bg.count = (uint32_t)std::min<uint64_t>(2048, rows - g * 2048);
+        // header fields (BitpackingScanState::LoadNextGroup, bitpacking.cpp:620-690)
+        const uint64_t n_fields = mode == 2 ? 1 : (mode == 3 || mode == 5) ? 2 : mode == 4 ? 3 : 0;
+        if (n_fields == 0)
+            return fail(CUBIT_ERR_INVALID, "segment %u group %llu: mode %u", sg, (unsigned long long)g, mode);
+        if (data_off < base + 8 || data_off + n_fields * tsz > n_bytes)
+            return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
+        auto field = [&](uint64_t i) {
+            uint64_t v = 0;  // T's bits, zero-extended (the kernels work mod 2^bits: bp_norm)
+            std::memcpy(&v, bytes + data_off + i * tsz, tsz);
+            return v;
+        };
+        bg.base = field(0);
+        uint64_t packed = 0;
+        if (mode == 3) {
+            bg.aux = field(1);
+        } else if (mode == 4 || mode == 5) {
+            const uint64_t w = field(1) & 0xff;  // the reference reads the width as a T, uses its low byte
+            if (w > 8 * tsz) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: width %u", sg, (unsigned long long)g, (unsigned)w);
+            bg.width = (uint16_t)w;
+            if (mode == 4) bg.aux = field(2);
+            packed = ((uint64_t)bg.count + 31) / 32 * 32 * w / 8;
+        }
+        bg.words_off = data_off + n_fields * tsz;
+        if (bg.words_off + packed > n_bytes)
+            return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
+        if (packed && bg.words_off % 4) {
+            const uint64_t at = moved.size();
+            moved.resize(at + (packed + 15) / 16 * 16, 0);
+            std::memcpy(moved.data() + at, bytes + bg.words_off, packed);
+            bg.words_off = bytes_padded + at;
+        }
+        groups.push_back(bg);
+    }
+    return CUBIT_OK;
+}
+
 // DuckDB BITPACKING segments → device column (K5). The host walks each segment's metadata
 // (header = end of the metadata words, one word per 2,048-row group, highest address first:
 // BitpackingScanState / LoadNextGroup, bitpacking.cpp:620-690), checks every group's bounds,
@@ -1790,63 +1849,15 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     }
     if (!bytes || !seg_offsets || !seg_rows || n_segments == 0) return fail(CUBIT_ERR_INVALID, "null argument");
     if (int rc = set_device(t->ctx)) return rc;
-    const uint64_t tsz = st.tsz;
     const uint64_t esz = st.col_type == CUBIT_TYPE_INT32 ? 4 : 8;
     const uint64_t bytes_padded = (n_bytes + 15) / 16 * 16;
     std::vector<BpGroup> groups;
     std::vector<uint8_t> moved;  // packed runs copied to 16-aligned offsets behind the bytes
     uint64_t row = 0;
     for (uint32_t sg = 0; sg < n_segments; ++sg) {
-        const uint64_t base = seg_offsets[sg];
-        if (base % 8 || base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
-        uint64_t meta_end;
-        std::memcpy(&meta_end, bytes + base, 8);
-        const uint64_t n_groups = (seg_rows[sg] + 2047) / 2048;
-        if (meta_end > n_bytes - base || meta_end < 8 + 4 * n_groups)
-            return fail(CUBIT_ERR_INVALID, "segment %u: bad metadata offset", sg);
-        for (uint64_t g = 0; g < n_groups; ++g) {
-            uint32_t enc;
-            std::memcpy(&enc, bytes + base + meta_end - 4 * (g + 1), 4);
-            BpGroup bg{};
-            const uint32_t mode = enc >> 24;
-            const uint64_t data_off = base + (enc & 0x00ffffffu);
-            bg.mode = (uint8_t)mode;
-            bg.tnorm = st.tnorm;
-            bg.row_start = row + g * 2048;
-            bg.count = (uint32_t)std::min<uint64_t>(2048, seg_rows[sg] - g * 2048);
-            // header fields (BitpackingScanState::LoadNextGroup, bitpacking.cpp:620-690)
-            const uint64_t n_fields = mode == 2 ? 1 : (mode == 3 || mode == 5) ? 2 : mode == 4 ? 3 : 0;
-            if (n_fields == 0)
-                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: mode %u", sg, (unsigned long long)g, mode);
-            if (data_off < base + 8 || data_off + n_fields * tsz > n_bytes)
-                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
-            auto field = [&](uint64_t i) {
-                uint64_t v = 0;  // T's bits, zero-extended (the kernels work mod 2^bits: bp_norm)
-                std::memcpy(&v, bytes + data_off + i * tsz, tsz);
-                return v;
-            };
-            bg.base = field(0);
-            uint64_t packed = 0;
-            if (mode == 3) {
-                bg.aux = field(1);
-            } else if (mode == 4 || mode == 5) {
-                const uint64_t w = field(1) & 0xff;  // the reference reads the width as a T, uses its low byte
-                if (w > 8 * tsz) return fail(CUBIT_ERR_INVALID, "segment %u group %llu: width %u", sg, (unsigned long long)g, (unsigned)w);
-                bg.width = (uint16_t)w;
-                if (mode == 4) bg.aux = field(2);
-                packed = ((uint64_t)bg.count + 31) / 32 * 32 * w / 8;
-            }
-            bg.words_off = data_off + n_fields * tsz;
-            if (bg.words_off + packed > n_bytes)
-                return fail(CUBIT_ERR_INVALID, "segment %u group %llu: out of bounds", sg, (unsigned long long)g);
-            if (packed && bg.words_off % 4) {
-                const uint64_t at = moved.size();
-                moved.resize(at + (packed + 15) / 16 * 16, 0);
-                std::memcpy(moved.data() + at, bytes + bg.words_off, packed);
-                bg.words_off = bytes_padded + at;
-            }
-            groups.push_back(bg);
-        }
+        if (int rc = parse_bp_segment(bytes, n_bytes, seg_offsets[sg], seg_rows[sg], row, st, bytes_padded, groups,
+                                      moved, sg))
+            return rc;
         row += seg_rows[sg];
     }
     if (row != t->n_rows)
@@ -1911,6 +1922,34 @@ extern "C" int cubit_table_add_bitpacked_column(cubit_table* t, int col, int typ
     return CUBIT_OK;
 }
 
+// The runs of one RLE segment (at byte `base`, `rows` rows from partition row `row`): values as
+// T widened to int64 (T's sign), each run's end row appended to `ends`.
+int parse_rle_segment(const uint8_t* bytes, uint64_t n_bytes, uint64_t base, uint64_t rows, uint64_t row,
+                      const SegType& st, std::vector<int64_t>& vals, std::vector<uint64_t>& ends, uint32_t sg) {
+    const uint64_t tsz = st.tsz;
+    if (base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
+    uint64_t off;
+    std::memcpy(&off, bytes + base, 8);
+    if (off < 8 || off > n_bytes - base) return fail(CUBIT_ERR_INVALID, "segment %u: bad run-length offset", sg);
+    uint64_t covered = 0;
+    for (uint64_t k = 0; covered < rows; ++k) {
+        if (8 + (k + 1) * tsz > off || off + 2 * (k + 1) > n_bytes - base)
+            return fail(CUBIT_ERR_INVALID, "segment %u: runs cover %llu of %llu rows", sg, (unsigned long long)covered,
+                        (unsigned long long)rows);
+        uint16_t len;
+        std::memcpy(&len, bytes + base + off + 2 * k, 2);
+        uint64_t raw = 0;  // T's bits, zero-extended, then widened as T
+        std::memcpy(&raw, bytes + base + 8 + k * tsz, tsz);
+        int64_t v = (int64_t)raw;
+        if (st.sgn && tsz < 8) v = (int64_t)(raw << (64 - 8 * tsz)) >> (64 - 8 * tsz);
+        covered += len;
+        if (covered > rows) return fail(CUBIT_ERR_INVALID, "segment %u: runs overrun its rows", sg);
+        vals.push_back(v);
+        ends.push_back(row + covered);
+    }
+    return CUBIT_OK;
+}
+
 // DuckDB RLE segments → device column. Each segment (rle.cpp RLECompressState::FlushSegment,
 // :190-205: 8-byte header = offset of the uint16 run lengths, the run values as T from byte 8,
 // the lengths after them) is walked on the host: run lengths are read until they cover the
@@ -1926,33 +1965,12 @@ extern "C" int cubit_table_add_rle_column(cubit_table* t, int col, int type, con
     if (!seg_type_of(type, st)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
     if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
     if (n_segments && (!bytes || !seg_offsets || !seg_rows)) return fail(CUBIT_ERR_INVALID, "null argument");
-    const uint64_t tsz = st.tsz;
     const bool wide = st.col_type != CUBIT_TYPE_INT32;
     std::vector<int64_t> vals;
     std::vector<uint64_t> ends;
     uint64_t row = 0;
     for (uint32_t sg = 0; sg < n_segments; ++sg) {
-        const uint64_t base = seg_offsets[sg];
-        if (base + 8 > n_bytes) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
-        uint64_t off;
-        std::memcpy(&off, bytes + base, 8);
-        if (off < 8 || off > n_bytes - base) return fail(CUBIT_ERR_INVALID, "segment %u: bad run-length offset", sg);
-        uint64_t covered = 0;
-        for (uint64_t k = 0; covered < seg_rows[sg]; ++k) {
-            if (8 + (k + 1) * tsz > off || off + 2 * (k + 1) > n_bytes - base)
-                return fail(CUBIT_ERR_INVALID, "segment %u: runs cover %llu of %llu rows", sg, (unsigned long long)covered,
-                            (unsigned long long)seg_rows[sg]);
-            uint16_t len;
-            std::memcpy(&len, bytes + base + off + 2 * k, 2);
-            uint64_t raw = 0;  // T's bits, zero-extended, then widened as T
-            std::memcpy(&raw, bytes + base + 8 + k * tsz, tsz);
-            int64_t v = (int64_t)raw;
-            if (st.sgn && tsz < 8) v = (int64_t)(raw << (64 - 8 * tsz)) >> (64 - 8 * tsz);
-            covered += len;
-            if (covered > seg_rows[sg]) return fail(CUBIT_ERR_INVALID, "segment %u: runs overrun its rows", sg);
-            vals.push_back(v);
-            ends.push_back(row + covered);
-        }
+        if (int rc = parse_rle_segment(bytes, n_bytes, seg_offsets[sg], seg_rows[sg], row, st, vals, ends, sg)) return rc;
         row += seg_rows[sg];
     }
     if (row != t->n_rows)
@@ -1980,6 +1998,130 @@ extern "C" int cubit_table_add_rle_column(cubit_table* t, int col, int type, con
     if (int rc = timing_events(t->ctx, e0, e1)) return rc;
     HIP_CHECK(launch_rle_expand(d_vals.p, static_cast<const uint64_t*>(d_ends.p), ends.size(), t->n_rows, wide ? 1 : 0,
                                 static_cast<uint64_t*>(d_tiles.p), out->p, s, e0, e1));
+    HIP_CHECK(hipStreamSynchronize(s));
+    Column c;
+    c.type = st.col_type;
+    c.data = out->p;
+    c.cap_rows = t->n_rows;
+    c.owned.push_back(std::move(out));
+    if (validity) {
+        if (int rc = copy_validity(t, c, validity, 0)) return rc;
+        HIP_CHECK(hipStreamSynchronize(s));
+    }
+    t->cols[col] = std::move(c);
+    drop_patches(t, col);
+    t->idx.erase(col);
+    t->bins.erase(col);
+    return CUBIT_OK;
+}
+
+// A column given as DuckDB segments of mixed codecs, one per row group as DuckDB's checkpoint chose
+// (UNCOMPRESSED, CONSTANT, RLE, BITPACKING). One run list covers every row: CONSTANT segments
+// are one run of their value, RLE segments their runs, the others a placeholder run; the GPU
+// expands it (rle_expand_kernel), then unpacks the BITPACKING groups over their rows
+// (bitunpack_kernel) and copies / widens the UNCOMPRESSED values over theirs, in stream order.
+extern "C" int cubit_table_add_segment_column(cubit_table* t, int col, int type, const uint8_t* bytes, uint64_t n_bytes,
+                                              const uint64_t* seg_offsets, const uint64_t* seg_rows,
+                                              const int32_t* seg_codecs, const int64_t* seg_constants,
+                                              uint32_t n_segments, const uint64_t* validity) {
+    if (!t) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(t->ctx);
+    SegType st;
+    if (!seg_type_of(type, st)) return fail(CUBIT_ERR_UNSUPPORTED, "type %d", type);
+    if (col < 0) return fail(CUBIT_ERR_INVALID, "column %d", col);
+    if (n_segments && (!seg_offsets || !seg_rows || !seg_codecs)) return fail(CUBIT_ERR_INVALID, "null argument");
+    const bool wide = st.col_type != CUBIT_TYPE_INT32;
+    const uint64_t esz = wide ? 8 : 4;
+    const uint64_t bytes_padded = (n_bytes + 15) / 16 * 16;
+    std::vector<int64_t> vals;
+    std::vector<uint64_t> ends;
+    std::vector<BpGroup> groups;
+    std::vector<uint8_t> moved;
+    struct Plain {
+        uint64_t off, rows, row;
+    };
+    std::vector<Plain> plain;
+    uint64_t row = 0;
+    for (uint32_t sg = 0; sg < n_segments; ++sg) {
+        const uint64_t rows = seg_rows[sg];
+        const int codec = seg_codecs[sg];
+        const bool needs_bytes = codec != CUBIT_CODEC_CONSTANT;
+        if (needs_bytes && (!bytes || seg_offsets[sg] > n_bytes)) return fail(CUBIT_ERR_INVALID, "segment %u: bad offset", sg);
+        switch (codec) {
+        case CUBIT_CODEC_CONSTANT:
+            if (!seg_constants) return fail(CUBIT_ERR_INVALID, "segment %u: CONSTANT without a value", sg);
+            vals.push_back(seg_constants[sg]);
+            ends.push_back(row + rows);
+            break;
+        case CUBIT_CODEC_RLE:
+            if (int rc = parse_rle_segment(bytes, n_bytes, seg_offsets[sg], rows, row, st, vals, ends, sg)) return rc;
+            break;
+        case CUBIT_CODEC_BITPACKING:
+            if (int rc = parse_bp_segment(bytes, n_bytes, seg_offsets[sg], rows, row, st, bytes_padded, groups, moved, sg))
+                return rc;
+            vals.push_back(0);  // placeholder, unpacked over below
+            ends.push_back(row + rows);
+            break;
+        case CUBIT_CODEC_UNCOMPRESSED:
+            if (seg_offsets[sg] % st.tsz || rows * st.tsz > n_bytes - seg_offsets[sg])
+                return fail(CUBIT_ERR_INVALID, "segment %u: %llu values past the bytes", sg, (unsigned long long)rows);
+            plain.push_back({seg_offsets[sg], rows, row});
+            vals.push_back(0);  // placeholder, copied over below
+            ends.push_back(row + rows);
+            break;
+        default:
+            return fail(CUBIT_ERR_UNSUPPORTED, "segment %u: codec %d", sg, codec);
+        }
+        row += rows;
+    }
+    if (row != t->n_rows)
+        return fail(CUBIT_ERR_INVALID, "segments hold %llu rows, partition has %llu", (unsigned long long)row,
+                    (unsigned long long)t->n_rows);
+    if (int rc = set_device(t->ctx)) return rc;
+    hipStream_t s = t->ctx->stream;
+    std::vector<int32_t> narrow;
+    if (!wide) narrow.assign(vals.begin(), vals.end());
+    const bool has_bytes = !groups.empty() || !plain.empty();
+    DevBuf d_vals, d_ends, d_tiles, d_bytes, d_groups;
+    auto out = std::make_unique<DevBuf>();
+    const uint64_t n_tiles = (t->n_rows + 2047) / 2048;
+    if (hipMalloc(&d_vals.p, std::max<uint64_t>(vals.size() * esz, 16)) != hipSuccess ||
+        hipMalloc(&d_ends.p, std::max<uint64_t>(ends.size() * 8, 16)) != hipSuccess ||
+        hipMalloc(&d_tiles.p, (n_tiles + 1) * 8) != hipSuccess ||
+        hipMalloc(&out->p, std::max<uint64_t>(t->n_rows * esz, 16)) != hipSuccess ||
+        (has_bytes && hipMalloc(&d_bytes.p, bytes_padded + moved.size() + 16) != hipSuccess) ||
+        (!groups.empty() && hipMalloc(&d_groups.p, groups.size() * sizeof(BpGroup)) != hipSuccess))
+        return fail(CUBIT_ERR_OOM, "segment column allocation failed");
+    if (!vals.empty()) {
+        HIP_CHECK(hipMemcpyAsync(d_vals.p, wide ? (const void*)vals.data() : (const void*)narrow.data(),
+                                 vals.size() * esz, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(d_ends.p, ends.data(), ends.size() * 8, hipMemcpyHostToDevice, s));
+    }
+    if (has_bytes) {
+        HIP_CHECK(hipMemcpyAsync(d_bytes.p, bytes, n_bytes, hipMemcpyHostToDevice, s));
+        if (!moved.empty())
+            HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(d_bytes.p) + bytes_padded, moved.data(), moved.size(),
+                                     hipMemcpyHostToDevice, s));
+    }
+    hipEvent_t e0, e1;
+    if (int rc = timing_events(t->ctx, e0, e1)) return rc;
+    HIP_CHECK(launch_rle_expand(d_vals.p, static_cast<const uint64_t*>(d_ends.p), ends.size(), t->n_rows, wide ? 1 : 0,
+                                static_cast<uint64_t*>(d_tiles.p), out->p, s, e0, groups.empty() && plain.empty() ? e1 : nullptr));
+    if (!groups.empty()) {
+        HIP_CHECK(hipMemcpyAsync(d_groups.p, groups.data(), groups.size() * sizeof(BpGroup), hipMemcpyHostToDevice, s));
+        HIP_CHECK(launch_bitunpack(static_cast<const uint8_t*>(d_bytes.p), static_cast<const BpGroup*>(d_groups.p),
+                                   groups.size(), st.col_type, out->p, s, nullptr, plain.empty() ? e1 : nullptr));
+    }
+    for (size_t i = 0; i < plain.size(); ++i) {
+        const Plain& pl = plain[i];
+        const uint8_t* src = static_cast<const uint8_t*>(d_bytes.p) + pl.off;
+        uint8_t* dst = static_cast<uint8_t*>(out->p) + pl.row * esz;
+        if (st.tsz == esz)  // INT32, INT64, UINT64: the values as held
+            HIP_CHECK(hipMemcpyAsync(dst, src, pl.rows * esz, hipMemcpyDeviceToDevice, s));
+        else
+            HIP_CHECK(launch_widen(src, type, pl.rows, dst, s));
+    }
+    if (e1 && !plain.empty()) HIP_CHECK(hipEventRecord(e1, s));
     HIP_CHECK(hipStreamSynchronize(s));
     Column c;
     c.type = st.col_type;

@@ -34,6 +34,8 @@ TYPE_VARCHAR = 10
 # HUGEINT / UHUGEINT columns are dictionary columns over the values' 16-byte order keys
 # (cubit_key128 / filters.key128): the type codes name the key encoding
 TYPE_INT128, TYPE_UINT128 = 11, 12
+# per-segment codecs of cubit_table_add_segment_column
+CODEC_UNCOMPRESSED, CODEC_CONSTANT, CODEC_RLE, CODEC_BITPACKING = 0, 1, 2, 3
 COLUMN_TYPES = dict(SEGMENT_TYPES, float32=TYPE_FLOAT, float64=TYPE_DOUBLE)
 
 
@@ -150,6 +152,7 @@ GPU_SIGNATURES = {
     "cubit_table_add_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _P, C.c_int]),
     "cubit_table_add_bitpacked_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _U64, _P, _P, _U32, _P]),
     "cubit_table_add_rle_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _U64, _P, _P, _U32, _P]),
+    "cubit_table_add_segment_column": (C.c_int, [_P, C.c_int, C.c_int, _P, _U64, _P, _P, _P, _P, _U32, _P]),
     "cubit_table_build_index": (C.c_int, [_P, C.c_int, C.c_int, _P, _U32]),
     "cubit_table_index_info": (C.c_int, [_P, C.c_int, C.POINTER(_U32), C.POINTER(_U64)]),
     "cubit_table_set_deletes": (C.c_int, [_P, _P, _P, _U64]),

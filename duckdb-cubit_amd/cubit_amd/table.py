@@ -288,6 +288,35 @@ class CubitTable:
                                                     vw.ctypes.data if vw is not None else None))
         self.types[col] = self.column_data(col)[1]
 
+    def add_segment_column(self, col: int, segments, dtype, validity: Optional[np.ndarray] = None) -> None:
+        """A column given as DuckDB segments of mixed codecs, in row order: a list of
+        (codec, payload, rows) — CODEC_CONSTANT with the value as payload, the other codecs with the
+        segment's bytes (UNCOMPRESSED: rows x T)."""
+        buf = bytearray()
+        offs, rows, codecs, consts = [], [], [], []
+        for codec, payload, n in segments:
+            buf += bytes((-len(buf)) % 16)
+            offs.append(len(buf))
+            if codec == L.CODEC_CONSTANT:
+                consts.append(int(payload))
+            else:
+                consts.append(0)
+                buf += bytes(np.asarray(payload, dtype=np.uint8) if not isinstance(payload, (bytes, bytearray))
+                             else payload)
+            rows.append(n)
+            codecs.append(codec)
+        data = np.frombuffer(bytes(buf) or b"\0", dtype=np.uint8).copy()
+        so = np.array(offs, np.uint64)
+        sr = np.array(rows, np.uint64)
+        sc = np.array(codecs, np.int32)
+        cv = np.array([c - (1 << 64) if c >= 1 << 63 else c for c in consts], np.int64)
+        vw = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint64)
+        typ = L.SEGMENT_TYPES[np.dtype(dtype).name]
+        L.check(self.lib.cubit_table_add_segment_column(self.handle, col, typ, data.ctypes.data, len(buf), so.ctypes.data,
+                                                        sr.ctypes.data, sc.ctypes.data, cv.ctypes.data, len(so),
+                                                        vw.ctypes.data if vw is not None else None))
+        self.types[col] = self.column_data(col)[1]
+
     def add_string_column(self, col: int, values, dictionary: Optional[Dictionary] = None) -> Dictionary:
         """Register a VARCHAR column from a list of str / bytes / None (NULL): encoded against
         `dictionary` (default: one built from the values) and held as int32 codes."""

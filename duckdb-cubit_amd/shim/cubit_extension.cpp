@@ -1322,12 +1322,14 @@ static int SegmentType(PhysicalType t) {
 // BlockManager::RegisterBlock, block_manager.hpp:83; BufferManager::Pin, buffer_manager.hpp:41)
 // at their block offset. A BITPACKING segment's first 8 bytes are the end of its metadata, i.e.
 // its size (BitpackingCompressState::FlushSegment); an RLE segment's are the offset of its run
-// lengths, which end it (RLECompressState::FlushSegment, rle.cpp:190-205). A column whose
-// segments are all BITPACKING or all RLE is taken from them; mixed codecs (or CONSTANT
-// segments) use the snapshot's values. Deleted rows stay in the segments (visibility is the
-// partition's delete list); updates make has_updates true and keep this path off.
+// lengths, which end it (RLECompressState::FlushSegment, rle.cpp:190-205); an UNCOMPRESSED one
+// is its values; a CONSTANT one has no bytes, its value is its statistics' minimum. A column
+// whose segments all use those codecs is taken from them (one codec: that codec's entry point;
+// mixed: cubit_table_add_segment_column); any other codec (DICTIONARY, FSST, ALP, …) uses the
+// snapshot's values. Deleted rows stay in the segments (visibility is the partition's delete
+// list); updates make has_updates true and keep this path off.
 static bool AttachSegmentColumn(DuckTableEntry &entry, column_t col, PhysicalType ptype, uint64_t n_rows,
-                                  cubit_table *t, const uint64_t *validity) {
+                                cubit_table *t, const uint64_t *validity) {
     const int seg_type = SegmentType(ptype);
     if (seg_type < 0 || n_rows == 0) {
         return false;
@@ -1345,35 +1347,89 @@ static bool AttachSegmentColumn(DuckTableEntry &entry, column_t col, PhysicalTyp
     std::sort(segs.begin(), segs.end(), [](const ColumnSegmentInfo &a, const ColumnSegmentInfo &b) {
         return a.segment_start < b.segment_start;
     });
-    // every segment of one codec: BITPACKING (unpacked on the GPU) or RLE (runs expanded on the GPU)
-    const string codec = segs.empty() ? bitpacking : segs[0].compression_type;
-    if (codec != bitpacking && codec != rle) {
-        return false;
-    }
+    // the codecs the GPU reads: BITPACKING (unpacked), RLE (runs expanded), CONSTANT (one value,
+    // from the segment's statistics), UNCOMPRESSED (the values); one codec for every segment keeps
+    // its own entry point (a BITPACKING column keeps its segments for the packed filter)
+    const string constant = CompressionTypeToString(CompressionType::COMPRESSION_CONSTANT);
+    const string uncompressed = CompressionTypeToString(CompressionType::COMPRESSION_UNCOMPRESSED);
+    const auto &ltype = entry.GetColumn(LogicalIndex(col)).GetType();
+    vector<int32_t> codecs;
+    vector<int64_t> constants;
     uint64_t next = 0;
     for (auto &sg : segs) {
-        if (!sg.persistent || sg.has_updates || sg.compression_type != codec || sg.segment_start != next) {
+        if (sg.has_updates || sg.segment_start != next) {
             return false;
         }
+        const string &c = sg.compression_type;
+        int32_t codec = -1;
+        int64_t value = 0;
+        if (c == bitpacking) {
+            codec = CUBIT_CODEC_BITPACKING;
+        } else if (c == rle) {
+            codec = CUBIT_CODEC_RLE;
+        } else if (c == uncompressed) {
+            codec = CUBIT_CODEC_UNCOMPRESSED;
+        } else if (c == constant) {
+            // ConstantScanFunction reads NumericStats::Min (compression/numeric_constant.cpp); the
+            // public ColumnSegmentInfo carries it as text ("[Min: v, Max: v][Has Null: …]"),
+            // parsed back through the column's type (DATE, DECIMAL and BOOL print as literals)
+            const string &st = sg.segment_stats;
+            const auto a = st.find("[Min: "), b = st.find(", Max: ");
+            if (a != 0 || b == string::npos) {
+                return false;
+            }
+            const string lit = st.substr(6, b - 6);
+            if (lit != "NULL") {  // an all-NULL segment: any value
+                try {
+                    value = ConstantAsInt64(Value(lit).DefaultCastAs(ltype));
+                } catch (std::exception &) {
+                    return false;
+                }
+            }
+            codec = CUBIT_CODEC_CONSTANT;
+        }
+        if (codec < 0 || (codec != CUBIT_CODEC_CONSTANT && !sg.persistent)) {
+            return false;
+        }
+        codecs.push_back(codec);
+        constants.push_back(value);
         next += sg.segment_count;
     }
-    if (next != n_rows) {
+    if (next != n_rows || segs.empty()) {
         return false;
     }
+    const int tsz = ptype == PhysicalType::BOOL || ptype == PhysicalType::INT8 || ptype == PhysicalType::UINT8 ? 1
+                    : ptype == PhysicalType::INT16 || ptype == PhysicalType::UINT16                        ? 2
+                    : ptype == PhysicalType::INT32 || ptype == PhysicalType::UINT32                        ? 4
+                                                                                                           : 8;
     auto &block_manager = TableIOManager::Get(storage).GetBlockManagerForRowData();
     vector<uint8_t> bytes;
     vector<uint64_t> offsets, rows;
-    for (auto &sg : segs) {
+    for (size_t i = 0; i < segs.size(); i++) {
+        auto &sg = segs[i];
+        const uint64_t at = (bytes.size() + 15) / 16 * 16;
+        offsets.push_back(at);
+        rows.push_back(sg.segment_count);
+        if (codecs[i] == CUBIT_CODEC_CONSTANT) {
+            continue;  // no bytes
+        }
         auto handle = block_manager.RegisterBlock(sg.block_id);
         auto pin = block_manager.buffer_manager.Pin(handle);
         const_data_ptr_t p = pin.Ptr() + sg.block_offset;
         const uint64_t room = block_manager.GetBlockSize() - sg.block_offset;
         uint64_t size = 0;
-        memcpy(&size, p, sizeof(size));  // BITPACKING: the segment's size; RLE: where its run lengths start
-        if (size < 8 || size > room) {
-            return false;  // not a segment header
+        if (codecs[i] == CUBIT_CODEC_UNCOMPRESSED) {
+            size = sg.segment_count * tsz;  // the values from the segment's start (FixedSizeScan)
+            if (size > room) {
+                return false;
+            }
+        } else {
+            memcpy(&size, p, sizeof(size));  // BITPACKING: the segment's size; RLE: where its run lengths start
+            if (size < 8 || size > room) {
+                return false;  // not a segment header
+            }
         }
-        if (codec == rle) {  // the run lengths end the segment: read them until they cover its rows
+        if (codecs[i] == CUBIT_CODEC_RLE) {  // the run lengths end the segment: read them until they cover its rows
             uint64_t covered = 0, k = 0;
             while (covered < sg.segment_count) {
                 if (size + 2 * (k + 1) > room) {
@@ -1385,15 +1441,18 @@ static bool AttachSegmentColumn(DuckTableEntry &entry, column_t col, PhysicalTyp
             }
             size += 2 * k;
         }
-        const uint64_t at = (bytes.size() + 7) / 8 * 8;
         bytes.resize(at + size, 0);
         memcpy(bytes.data() + at, p, size);
-        offsets.push_back(at);
-        rows.push_back(sg.segment_count);
     }
-    auto add = codec == rle ? cubit_table_add_rle_column : cubit_table_add_bitpacked_column;
-    return add(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(), rows.data(), (uint32_t)segs.size(),
-               validity) == CUBIT_OK;
+    const bool all_bp = std::all_of(codecs.begin(), codecs.end(), [](int32_t c) { return c == CUBIT_CODEC_BITPACKING; });
+    const bool all_rle = std::all_of(codecs.begin(), codecs.end(), [](int32_t c) { return c == CUBIT_CODEC_RLE; });
+    if (all_bp || all_rle) {
+        auto add = all_rle ? cubit_table_add_rle_column : cubit_table_add_bitpacked_column;
+        return add(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(), rows.data(), (uint32_t)segs.size(),
+                   validity) == CUBIT_OK;
+    }
+    return cubit_table_add_segment_column(t, (int)col, seg_type, bytes.data(), bytes.size(), offsets.data(), rows.data(),
+                                          codecs.data(), constants.data(), (uint32_t)segs.size(), validity) == CUBIT_OK;
 }
 
 // The column as registered against the snapshot's values on a sample (the valid rows of a

@@ -437,6 +437,22 @@ int cubit_table_add_bitpacked_column(cubit_table *t, int col, int type, const ui
 int cubit_table_add_rle_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
                                const uint64_t *seg_offsets, const uint64_t *seg_rows, uint32_t n_segments,
                                const uint64_t *validity);
+/* Register a column given as DuckDB segments whose codecs differ from row group to row group, as
+ * DuckDB's checkpoint picks one per segment (ColumnDataCheckpointer): seg_codecs[i] is
+ * CUBIT_CODEC_UNCOMPRESSED (rows × T, the segment as FixedSizeAppend writes it),
+ * CUBIT_CODEC_CONSTANT (no bytes; every row is seg_constants[i], the value as T widened to int64 —
+ * a CONSTANT segment's value lives in its statistics), CUBIT_CODEC_RLE or CUBIT_CODEC_BITPACKING
+ * (the layouts above); seg_offsets[i] is ignored for CONSTANT segments and seg_constants may be
+ * NULL when there are none. The GPU writes every segment's rows; `type`, the column held and
+ * `validity` as for cubit_table_add_bitpacked_column (the packed segments are not kept: the
+ * packed filter does not apply). */
+#define CUBIT_CODEC_UNCOMPRESSED 0
+#define CUBIT_CODEC_CONSTANT 1
+#define CUBIT_CODEC_RLE 2
+#define CUBIT_CODEC_BITPACKING 3
+int cubit_table_add_segment_column(cubit_table *t, int col, int type, const uint8_t *bytes, uint64_t n_bytes,
+                                   const uint64_t *seg_offsets, const uint64_t *seg_rows, const int32_t *seg_codecs,
+                                   const int64_t *seg_constants, uint32_t n_segments, const uint64_t *validity);
 /* A column registered with cubit_table_add_bitpacked_column keeps its segments on the device:
  * a constant comparison the index cannot answer (K0) then unpacks and compares in one pass over
  * the packed bytes (w/8 bytes per row — the reference's ColumnSegment::Scan →
