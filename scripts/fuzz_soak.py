@@ -91,12 +91,20 @@ def round_(ctx, seed, n, with_updates):
         vw = validity_from_mask(valid) if c != 1 else None
         if c == 3:
             # any integral type DuckDB holds, registered plain (widened on the device), as
-            # BITPACKING segments under a random forced mode (the packed filter on or off), or as
-            # RLE segments
+            # BITPACKING segments under a random forced mode (the packed filter on or off), as
+            # RLE segments, or as row groups of mixed codecs
             dt = np.dtype(rng.choice(["int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64"]))
             typed = d.astype(dt)
             codec = rng.random()
-            if codec < 0.25:
+            if codec < 0.15:
+                # row groups of mixed codecs (UNCOMPRESSED, CONSTANT, RLE, BITPACKING) as DuckDB's
+                # checkpoint picks them, through cubit_table_add_segment_column
+                from test_gpu_segments import mixed_column
+
+                typed, valid, segs = mixed_column(rng, dt, n // 122_880, n % 122_880)
+                vw = validity_from_mask(valid)
+                t.add_segment_column(c, segs, dt, vw)
+            elif codec < 0.35:
                 # RLE segments (the restated compressor over runs of 1-15 rows; runs long enough to
                 # matter), expanded on the device
                 m = n // 4 + 1

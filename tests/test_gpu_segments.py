@@ -28,6 +28,7 @@ def ctx():
 
 def mixed_column(rng, dt, n_groups, tail):
     """Values, validity and segments: row group g written with codec g mod 4 (shuffled)."""
+    dt = np.dtype(dt)
     info = np.iinfo(dt)
     n = n_groups * RG + tail
     vals = np.empty(n, dtype=dt)
@@ -39,7 +40,7 @@ def mixed_column(rng, dt, n_groups, tail):
         lo, hi = g * RG, min(n, (g + 1) * RG)
         m = hi - lo
         if codec == L.CODEC_CONSTANT:
-            c = dt(rng.choice([info.min, info.max, 0, 7]))
+            c = dt.type([info.min, info.max, 0, 7][int(rng.integers(0, 4))])
             vals[lo:hi] = c
             ok[lo:hi] = True  # a CONSTANT segment's rows are all valid and equal
             segs.append((codec, int(c), m))
