@@ -1695,6 +1695,35 @@ extern "C" int cubit_dict_encode(const cubit_dict* d, const char* bytes, const u
     return CUBIT_OK;
 }
 
+// cubit_dict_encode on the device: the dictionary's entries are copied to the context's device
+// for the call, one lane per string searches them (dict_encode_kernel).
+extern "C" int cubit_dict_encode_device(cubit_ctx* ctx, const cubit_dict* d, const char* d_bytes,
+                                        const uint64_t* d_offsets, uint64_t n, const uint64_t* d_validity,
+                                        int32_t* d_codes) {
+    if (!ctx || !d || (n && (!d_offsets || !d_codes))) return fail(CUBIT_ERR_INVALID, "null argument");
+    CUBIT_LOCK(ctx);
+    if (n == 0) return CUBIT_OK;
+    if (int rc = set_device(ctx)) return rc;
+    const DictData& dd = *d->d;
+    hipStream_t s = ctx->stream;
+    DevBuf db, doffs, miss;
+    if (hipMalloc(&db.p, std::max<uint64_t>(dd.bytes.size(), 16)) != hipSuccess ||
+        hipMalloc(&doffs.p, dd.offs.size() * 8) != hipSuccess || hipMalloc(&miss.p, 8) != hipSuccess)
+        return fail(CUBIT_ERR_OOM, "dictionary upload failed");
+    if (!dd.bytes.empty()) HIP_CHECK(hipMemcpyAsync(db.p, dd.bytes.data(), dd.bytes.size(), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(doffs.p, dd.offs.data(), dd.offs.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemsetAsync(miss.p, 0, 8, s));
+    HIP_CHECK(launch_dict_encode(reinterpret_cast<const uint8_t*>(d_bytes), d_offsets, n, d_validity,
+                                 static_cast<const uint8_t*>(db.p), static_cast<const uint64_t*>(doffs.p), dd.size(),
+                                 d_codes, static_cast<unsigned long long*>(miss.p), s));
+    unsigned long long missing = 0;
+    HIP_CHECK(hipMemcpyAsync(&missing, miss.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (missing)
+        return fail(CUBIT_ERR_UNSUPPORTED, "%llu strings are not in the dictionary (their codes are -1)", missing);
+    return CUBIT_OK;
+}
+
 extern "C" int cubit_dict_lookup(const cubit_dict* d, const char* data, uint64_t size, uint64_t* lower_bound,
                                  int* present) {
     if (!d || !lower_bound || (size && !data)) return fail(CUBIT_ERR_INVALID, "null argument");

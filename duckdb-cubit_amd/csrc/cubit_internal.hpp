@@ -224,6 +224,11 @@ struct BpGroup {
 };
 hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_t n_groups, int type, void* out,
                             hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// strings → codes of a sorted dictionary, all on the device (NULL rows 0; a missing string -1,
+// counted into *missing)
+hipError_t launch_dict_encode(const uint8_t* bytes, const uint64_t* offs, uint64_t n, const uint64_t* validity,
+                              const uint8_t* dbytes, const uint64_t* doffs, uint64_t dn, int32_t* codes,
+                              unsigned long long* missing, hipStream_t stream);
 // DuckDB RLE segments parsed into runs (values of the column's type, cumulative exclusive run
 // ends) expanded into the column (type 0: INT32, else INT64); tile_first: scratch of
 // (n_rows + 2047) / 2048 + 1 words

@@ -3702,6 +3702,59 @@ hipError_t launch_bitunpack(const uint8_t* bytes, const BpGroup* groups, uint64_
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ dictionary encode
+// Strings (bytes + offsets, in device memory) → codes of an order-preserving dictionary (its
+// entries sorted, bytes + offsets on the device): one lane per string, a binary search comparing
+// bytes as unsigned then lengths (string_t's order, the host dictionary's). A NULL row gets code
+// 0; a valid string the dictionary lacks gets -1 and counts into *missing.
+__device__ __forceinline__ int dict_cmp(const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb) {
+    const uint64_t m = na < nb ? na : nb;
+    for (uint64_t i = 0; i < m; ++i)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return na < nb ? -1 : na > nb ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void dict_encode_kernel(const uint8_t* __restrict__ bytes,
+                                                          const uint64_t* __restrict__ offs, uint64_t n,
+                                                          const uint64_t* __restrict__ validity,
+                                                          const uint8_t* __restrict__ dbytes,
+                                                          const uint64_t* __restrict__ doffs, uint64_t dn,
+                                                          int32_t* __restrict__ codes,
+                                                          unsigned long long* __restrict__ missing) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t miss = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (validity && !((validity[i >> 6] >> (i & 63)) & 1ull)) {
+            codes[i] = 0;
+            continue;
+        }
+        const uint8_t* s = bytes + offs[i];
+        const uint64_t ns = offs[i + 1] - offs[i];
+        uint64_t lo = 0, hi = dn;  // first entry >= s
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (dict_cmp(dbytes + doffs[mid], doffs[mid + 1] - doffs[mid], s, ns) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        const bool found = lo < dn && dict_cmp(dbytes + doffs[lo], doffs[lo + 1] - doffs[lo], s, ns) == 0;
+        codes[i] = found ? (int32_t)lo : -1;
+        miss += found ? 0u : 1u;
+    }
+    // one add per wave that saw a miss
+    for (int o = 32; o > 0; o >>= 1) miss += __shfl_down(miss, o, 64);
+    if ((threadIdx.x & 63) == 0 && miss) atomicAdd(missing, (unsigned long long)miss);
+}
+
+hipError_t launch_dict_encode(const uint8_t* bytes, const uint64_t* offs, uint64_t n, const uint64_t* validity,
+                              const uint8_t* dbytes, const uint64_t* doffs, uint64_t dn, int32_t* codes,
+                              unsigned long long* missing, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(dict_encode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, bytes, offs, n, validity, dbytes,
+                       doffs, dn, codes, missing);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ RLE expand
 // DuckDB RLE segments (src/storage/compression/rle.cpp) expanded into a plain column. The host
 // has parsed every segment into runs — the run values (already widened to the column's type) and

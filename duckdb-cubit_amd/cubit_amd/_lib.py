@@ -136,6 +136,7 @@ GPU_SIGNATURES = {
     "cubit_dict_entry": (C.c_int, [_P, _U64, C.POINTER(_P), C.POINTER(_U64)]),
     "cubit_dict_encode": (C.c_int, [_P, _P, _P, _U64, _P, _P]),
     "cubit_dict_lookup": (C.c_int, [_P, _P, _U64, C.POINTER(_U64), C.POINTER(C.c_int)]),
+    "cubit_dict_encode_device": (C.c_int, [_P, _P, _P, _P, _U64, _P, _P]),
     "cubit_table_add_dict_column": (C.c_int, [_P, C.c_int, _P, _P, _P, C.c_int]),
     "cubit_bitvector_eval": (
         C.c_int,

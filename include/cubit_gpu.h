@@ -401,6 +401,12 @@ int cubit_dict_encode(const cubit_dict *d, const char *bytes, const uint64_t *of
                       const uint64_t *validity, int32_t *codes);
 /* *lower_bound = the first code whose string is >= s (the size when none), *present = s is in it */
 int cubit_dict_lookup(const cubit_dict *d, const char *data, uint64_t size, uint64_t *lower_bound, int *present);
+/* cubit_dict_encode with every array in the context's device memory (the strings, their offsets,
+ * the validity, the codes): one GPU lane per string searches the dictionary's entries (copied to
+ * the device for the call). A valid string the dictionary lacks gets code -1 and makes the call
+ * return CUBIT_ERR_UNSUPPORTED after the launch. */
+int cubit_dict_encode_device(cubit_ctx *ctx, const cubit_dict *d, const char *d_bytes, const uint64_t *d_offsets,
+                             uint64_t n, const uint64_t *d_validity, int32_t *d_codes);
 /* Register a VARCHAR column: codes (host, or device with on_device = 1 as cubit_table_add_column)
  * of the table's rows against `d`, validity as for cubit_table_add_column. Every valid code must
  * lie in [0, size of d) (CUBIT_ERR_INVALID otherwise). The column holds a reference to d. */

@@ -321,3 +321,54 @@ def test_equality_index_plans_intervals_as_one_union(ctx):
         fs = F.TableFilterSet({0: flt})
         assert np.array_equal(t.scan(fs, txn=txn), O.table_scan([ucol], F.serialize(fs), n, 0, tx)), terms
     t.close()
+
+
+def test_device_dictionary_encode_equals_host(ctx):
+    """cubit_dict_encode_device (one GPU lane per string, a search of the dictionary's entries in
+    unsigned-byte-then-length order) gives the host encoder's codes — strings with NUL and high
+    bytes, the empty string, prefixes, NULL rows — and refuses strings the dictionary lacks,
+    marking them -1. Device buffers through the C ABI's own allocator."""
+    import ctypes as C
+
+    from cubit_amd.datagen import validity_from_mask
+    from cubit_amd.table import pack_strings
+
+    lib, h = ctx.lib, ctx.handle
+    bufs = []
+
+    def dev(a):
+        a = np.ascontiguousarray(a)
+        p = C.c_void_p()
+        L.check(lib.cubit_dev_alloc(h, max(a.nbytes, 16), C.byref(p)))
+        L.check(lib.cubit_memcpy_h2d(h, p, a.ctypes.data, a.nbytes))
+        bufs.append(p)
+        return p
+
+    def back(p, n):
+        out = np.empty(n, np.int32)
+        L.check(lib.cubit_memcpy_d2h(h, out.ctypes.data, p, out.nbytes))
+        return out
+
+    rng = np.random.default_rng(51)
+    vals, pool = random_strings(rng, 400_003, pool=300)
+    vals = [None if rng.random() < 0.03 else v for v in vals]
+    d = Dictionary(pool)
+    want, wvalid = d.encode(vals)
+    buf, offs, valid = pack_strings(vals)
+    d_codes = dev(np.full(len(vals), 7, np.int32))
+    L.check(lib.cubit_dict_encode_device(h, d.handle, dev(buf), dev(offs), len(vals), dev(validity_from_mask(valid)),
+                                         d_codes))
+    got = back(d_codes, len(vals))
+    assert np.array_equal(got[wvalid], want[wvalid]) and (got[~wvalid] == 0).all()
+    # two strings the dictionary lacks: refused, their codes -1, the others still encoded
+    extra = list(vals[:1000]) + [b"not there", b"\xff" * 40]
+    buf, offs, valid = pack_strings(extra)
+    d_codes = dev(np.zeros(len(extra), np.int32))
+    rc = lib.cubit_dict_encode_device(h, d.handle, dev(buf), dev(offs), len(extra), None, d_codes)
+    assert rc == L.ERR_UNSUPPORTED
+    got = back(d_codes, len(extra))
+    assert got[-2:].tolist() == [-1, -1]
+    w2, v2 = d.encode(extra[:1000])
+    assert np.array_equal(got[:1000][v2], w2[v2])
+    for p in bufs:
+        L.check(lib.cubit_dev_free(h, p))
