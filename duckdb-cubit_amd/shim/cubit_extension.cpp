@@ -1227,7 +1227,37 @@ static void PackStrings(const vector<string> &strs, vector<char> &bytes, vector<
 
 // A VARCHAR column of a snapshot as its table-wide dictionary (its valid strings) and every row's
 // code (NULL rows: 0); the caller owns the dictionary.
-static cubit_dict *EncodeStrings(const vector<string> &strs, const vector<uint64_t> &validity, vector<int32_t> &codes) {
+// The codes of packed strings on the GPU (cubit_dict_encode_device): the bytes, offsets and
+// validity copied to `ctx`'s device, the codes copied back. False when a device step fails (the
+// caller encodes on the host).
+static bool EncodeOnDevice(cubit_ctx *ctx, cubit_dict *d, const vector<char> &bytes, const vector<uint64_t> &offsets,
+                           const vector<uint64_t> &validity, vector<int32_t> &codes) {
+    const uint64_t n = codes.size();
+    void *db = nullptr, *doff = nullptr, *dv = nullptr, *dc = nullptr;
+    bool ok = cubit_dev_alloc(ctx, std::max<uint64_t>(bytes.size(), 16), &db) == CUBIT_OK &&
+              cubit_dev_alloc(ctx, offsets.size() * 8, &doff) == CUBIT_OK &&
+              cubit_dev_alloc(ctx, std::max<uint64_t>(validity.size() * 8, 16), &dv) == CUBIT_OK &&
+              cubit_dev_alloc(ctx, n * 4, &dc) == CUBIT_OK;
+    ok = ok && (bytes.empty() || cubit_memcpy_h2d(ctx, db, bytes.data(), bytes.size()) == CUBIT_OK) &&
+         cubit_memcpy_h2d(ctx, doff, offsets.data(), offsets.size() * 8) == CUBIT_OK &&
+         cubit_memcpy_h2d(ctx, dv, validity.data(), validity.size() * 8) == CUBIT_OK &&
+         cubit_dict_encode_device(ctx, d, static_cast<const char *>(db), static_cast<const uint64_t *>(doff), n,
+                                  static_cast<const uint64_t *>(dv), static_cast<int32_t *>(dc)) == CUBIT_OK &&
+         cubit_memcpy_d2h(ctx, codes.data(), dc, n * 4) == CUBIT_OK;
+    for (void *p : {db, doff, dv, dc}) {
+        if (p) {
+            cubit_dev_free(ctx, p);
+        }
+    }
+    return ok;
+}
+
+// Columns of at least this many rows are encoded on the GPU (a lane per string) when a context is
+// at hand; smaller ones on the host.
+static constexpr uint64_t kDeviceEncodeRows = 1 << 20;
+
+static cubit_dict *EncodeStrings(const vector<string> &strs, const vector<uint64_t> &validity, vector<int32_t> &codes,
+                                 cubit_ctx *ctx = nullptr) {
     vector<string> valid_strs;
     for (idx_t r = 0; r < strs.size(); r++) {
         if ((validity[r >> 6] >> (r & 63)) & 1) {
@@ -1241,6 +1271,9 @@ static cubit_dict *EncodeStrings(const vector<string> &strs, const vector<uint64
     Check(cubit_dict_create(bytes.data(), offsets.data(), valid_strs.size(), &d));
     PackStrings(strs, bytes, offsets);
     codes.assign(strs.size(), 0);
+    if (ctx && strs.size() >= kDeviceEncodeRows && EncodeOnDevice(ctx, d, bytes, offsets, validity, codes)) {
+        return d;  // every valid string is in d (it was built from them): the device encode cannot miss
+    }
     const int rc = cubit_dict_encode(d, bytes.data(), offsets.data(), strs.size(), validity.data(), codes.data());
     if (rc != CUBIT_OK) {
         cubit_dict_destroy(d);
@@ -1516,7 +1549,7 @@ static std::shared_ptr<CubitPartitionSet> BuildPartition(CubitAttached &attached
     for (idx_t c = 0; c < attached.column_order.size(); c++) {
         const column_t col = attached.column_order[c];
         if (DictPhysical(attached.columns[col])) {
-            cubit_dict *d = EncodeStrings(snap.strings[c], snap.validity[c], codes[c]);
+            cubit_dict *d = EncodeStrings(snap.strings[c], snap.validity[c], codes[c], ctxs[0]);
             set->dicts[col] = d;  // the set owns it from here (its destructor frees it)
             uint64_t size = 0;
             cubit_dict_size(d, &size);
